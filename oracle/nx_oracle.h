@@ -1,0 +1,98 @@
+/*
+ * nx_oracle.h -- TEST INFRASTRUCTURE ONLY.
+ *
+ * A scalar CPU restatement of netidx's Pack codec for the publisher->subscriber update stream
+ * (reference: netidx-core/src/pack.rs, netidx-value/src/{lib,array,pbuf,abstract_type}.rs,
+ * netidx-netproto/src/publisher.rs + netidx-derive/src/lib.rs, netidx/src/channel.rs).
+ *
+ * It is the CHECKER for the HIP codec in netidx_amd/: only tests/, __graft_entry__.smoke() and
+ * bench.py's cpu_baseline leg may load it. The product never links or calls it.
+ *
+ * Parity pinning: the reference is Rust-only and cannot be built or run in this image (no
+ * cargo/rustc, no network). This oracle is pinned by (1) the reference's
+ * own tests restated (varint sweep netidx-core/src/test.rs:16-63, encoded_len/round-trip
+ * properties netidx-netproto/src/test.rs:15-21, decode-never-crashes fuzz test.rs:449-456) and
+ * (2) hand-derived known-answer vectors (tests/golden/). Byte-level parity
+ * against the executing reference is therefore "parity partially pinned"; see DESIGN.md.
+ *
+ * Columnar contract (identical to include/nxg_codec.h, restated here independently):
+ *   rows     : one per From::Update            id u64, tag u8, fixed u64, aux u32
+ *   children : elements of Array/Map/Error     tag u8, fixed u64, aux u32
+ *   ctl      : every other From message        row u64, off u64, len u32, variant u8
+ */
+#ifndef NX_ORACLE_H
+#define NX_ORACLE_H
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* PackError, netidx-core/src/pack.rs:89-95 (+ codec-level kinds) */
+enum {
+    NXO_OK = 0,
+    NXO_UNKNOWN_TAG = 1,
+    NXO_TOO_BIG = 2,
+    NXO_INVALID_FORMAT = 3,
+    NXO_BUFFER_SHORT = 4,
+    NXO_DEPTH = 6,     /* nesting deeper than NXO_MAX_DEPTH (documented deviation) */
+    NXO_CAPACITY = 7,  /* output columns too small */
+};
+
+#define NXO_MAX_DEPTH 32
+
+typedef struct NxoCols {
+    /* capacities (in) */
+    uint64_t cap_rows, cap_children, cap_ctl;
+    /* counts (out) */
+    uint64_t n_rows, n_children, n_ctl, n_heartbeat;
+    /* rows */
+    uint64_t* id;
+    uint8_t* tag;
+    uint64_t* fixed;
+    uint32_t* aux;
+    /* children */
+    uint8_t* ctag;
+    uint64_t* cfixed;
+    uint32_t* caux;
+    /* control messages */
+    uint64_t* ctl_row;
+    uint64_t* ctl_off;
+    uint32_t* ctl_len;
+    uint8_t* ctl_variant;
+    /* status (out) */
+    int32_t err_kind;
+    uint64_t err_offset;
+} NxoCols;
+
+/* primitives: pack.rs:472-520 */
+uint32_t nxo_varint_len(uint64_t v);
+uint32_t nxo_encode_varint(uint64_t v, uint8_t* out);
+int nxo_decode_varint(const uint8_t* p, uint64_t avail, uint64_t* v, uint32_t* nread);
+uint32_t nxo_len_wrapped_len(uint64_t inner);
+/* restatement of netidx-core/src/test.rs:16-63 over d in [lo, hi); returns failures */
+uint64_t nxo_varint_sweep(uint64_t lo, uint64_t hi, int short_buf);
+
+/* frame decode: the receive_batch_fn loop (channel.rs:504-521) over From::decode. This is
+ * also the timed cpu_baseline of bench.py (1 core, as one tokio decode task per connection). */
+int nxo_decode_frame(const uint8_t* w, uint64_t len, NxoCols* c);
+
+/* encode: queue_send loop (channel.rs:177-202) over From::encode; heap = bytes referenced by
+ * string/bytes/decimal/abstract offsets and ctl spans. Returns bytes written or -errkind. */
+int64_t nxo_encoded_len(const NxoCols* c, const uint8_t* heap);
+int64_t nxo_encode(const NxoCols* c, const uint8_t* heap, uint8_t* out, uint64_t cap);
+
+/* f64 batch encode from id/val columns (config 4) */
+int64_t nxo_encode_f64(const uint64_t* id, const uint64_t* val, uint64_t n, uint8_t* out,
+                       uint64_t cap);
+
+/* chrono DateTime::from_timestamp validity (pack.rs:1567-1575; chrono 0.4.35+ rules) */
+int nxo_datetime_valid(int64_t secs, uint32_t nsecs);
+/* std str::from_utf8 validity (pack.rs:462) */
+int nxo_utf8_valid(const uint8_t* p, uint64_t n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,131 @@
+"""ctypes binding of the CPU oracle (oracle/build/libnx_oracle.so) -- TEST INFRASTRUCTURE.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import this module. It is
+the checker, never the thing measured or shipped.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(ROOT, "oracle", "build", "libnx_oracle.so")
+
+U64P = C.POINTER(C.c_uint64)
+U32P = C.POINTER(C.c_uint32)
+U8P = C.POINTER(C.c_uint8)
+
+
+class NxoCols(C.Structure):
+    _fields_ = [
+        ("cap_rows", C.c_uint64), ("cap_children", C.c_uint64), ("cap_ctl", C.c_uint64),
+        ("n_rows", C.c_uint64), ("n_children", C.c_uint64), ("n_ctl", C.c_uint64),
+        ("n_heartbeat", C.c_uint64),
+        ("id", U64P), ("tag", U8P), ("fixed", U64P), ("aux", U32P),
+        ("ctag", U8P), ("cfixed", U64P), ("caux", U32P),
+        ("ctl_row", U64P), ("ctl_off", U64P), ("ctl_len", U32P), ("ctl_variant", U8P),
+        ("err_kind", C.c_int32), ("err_offset", C.c_uint64),
+    ]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"oracle not built: {LIB_PATH} (run make -C oracle)")
+        L = C.CDLL(LIB_PATH)
+        L.nxo_varint_len.restype = C.c_uint32
+        L.nxo_varint_len.argtypes = [C.c_uint64]
+        L.nxo_encode_varint.restype = C.c_uint32
+        L.nxo_encode_varint.argtypes = [C.c_uint64, U8P]
+        L.nxo_decode_varint.restype = C.c_int
+        L.nxo_decode_varint.argtypes = [U8P, C.c_uint64, U64P, U32P]
+        L.nxo_varint_sweep.restype = C.c_uint64
+        L.nxo_varint_sweep.argtypes = [C.c_uint64, C.c_uint64, C.c_int]
+        L.nxo_decode_frame.restype = C.c_int
+        L.nxo_decode_frame.argtypes = [C.c_void_p, C.c_uint64, C.POINTER(NxoCols)]
+        L.nxo_encoded_len.restype = C.c_int64
+        L.nxo_encoded_len.argtypes = [C.POINTER(NxoCols), C.c_void_p]
+        L.nxo_encode.restype = C.c_int64
+        L.nxo_encode.argtypes = [C.POINTER(NxoCols), C.c_void_p, C.c_void_p, C.c_uint64]
+        L.nxo_encode_f64.restype = C.c_int64
+        L.nxo_encode_f64.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64]
+        L.nxo_datetime_valid.restype = C.c_int
+        L.nxo_datetime_valid.argtypes = [C.c_int64, C.c_uint32]
+        L.nxo_utf8_valid.restype = C.c_int
+        L.nxo_utf8_valid.argtypes = [C.c_void_p, C.c_uint64]
+        _lib = L
+    return _lib
+
+
+def _p(a, t):
+    return a.ctypes.data_as(t)
+
+
+class Decoded:
+    """Numpy view of an oracle decode (same columnar contract as include/nxg_codec.h)."""
+
+    def __init__(self, cap_rows, cap_children, cap_ctl):
+        self.id = np.zeros(cap_rows, np.uint64)
+        self.tag = np.zeros(cap_rows, np.uint8)
+        self.fixed = np.zeros(cap_rows, np.uint64)
+        self.aux = np.zeros(cap_rows, np.uint32)
+        self.ctag = np.zeros(cap_children, np.uint8)
+        self.cfixed = np.zeros(cap_children, np.uint64)
+        self.caux = np.zeros(cap_children, np.uint32)
+        self.ctl_row = np.zeros(cap_ctl, np.uint64)
+        self.ctl_off = np.zeros(cap_ctl, np.uint64)
+        self.ctl_len = np.zeros(cap_ctl, np.uint32)
+        self.ctl_variant = np.zeros(cap_ctl, np.uint8)
+        self.s = NxoCols(cap_rows, cap_children, cap_ctl, 0, 0, 0, 0,
+                         _p(self.id, U64P), _p(self.tag, U8P), _p(self.fixed, U64P),
+                         _p(self.aux, U32P), _p(self.ctag, U8P), _p(self.cfixed, U64P),
+                         _p(self.caux, U32P), _p(self.ctl_row, U64P), _p(self.ctl_off, U64P),
+                         _p(self.ctl_len, U32P), _p(self.ctl_variant, U8P), 0, 0)
+
+    def trim(self):
+        s = self.s
+        n, c, k = s.n_rows, s.n_children, s.n_ctl
+        return {
+            "id": self.id[:n], "tag": self.tag[:n], "fixed": self.fixed[:n], "aux": self.aux[:n],
+            "ctag": self.ctag[:c], "cfixed": self.cfixed[:c], "caux": self.caux[:c],
+            "ctl_row": self.ctl_row[:k], "ctl_off": self.ctl_off[:k],
+            "ctl_len": self.ctl_len[:k], "ctl_variant": self.ctl_variant[:k],
+            "n_heartbeat": s.n_heartbeat, "err_kind": s.err_kind, "err_offset": s.err_offset,
+        }
+
+
+def decode(wire, cap_rows=None, cap_children=None, cap_ctl=None):
+    wire = np.frombuffer(bytes(wire), np.uint8) if not isinstance(wire, np.ndarray) else wire
+    n = len(wire)
+    d = Decoded(cap_rows if cap_rows is not None else n // 4 + 1,
+                cap_children if cap_children is not None else n + 1,
+                cap_ctl if cap_ctl is not None else n // 2 + 1)
+    lib().nxo_decode_frame(wire.ctypes.data, n, C.byref(d.s))
+    d.wire = wire
+    return d
+
+
+def encode(d, heap):
+    heap = np.frombuffer(bytes(heap), np.uint8) if not isinstance(heap, np.ndarray) else heap
+    n = lib().nxo_encoded_len(C.byref(d.s), heap.ctypes.data)
+    if n < 0:
+        raise ValueError(f"encode error {-n}")
+    out = np.zeros(max(n, 1), np.uint8)
+    m = lib().nxo_encode(C.byref(d.s), heap.ctypes.data, out.ctypes.data, n)
+    assert m == n, (m, n)
+    return out[:n].tobytes()
+
+
+def encode_f64(ids, vals):
+    ids = np.ascontiguousarray(ids, np.uint64)
+    vals = np.ascontiguousarray(vals, np.uint64)
+    cap = 21 * len(ids) + 16
+    out = np.zeros(cap, np.uint8)
+    n = lib().nxo_encode_f64(ids.ctypes.data, vals.ctypes.data, len(ids), out.ctypes.data, cap)
+    if n < 0:
+        raise ValueError(f"encode error {-n}")
+    return out[:n]
