@@ -1,0 +1,318 @@
+#!/usr/bin/env python3
+"""bench.py -- BASELINE.json metric: device-resident Value-batch decode throughput on MI355X.
+
+A "step" decodes one batch: a frame payload of From::Update(Id, F64) messages (configs[1],
+10^7 records, 147,886,336 wire bytes), from HBM-resident wire bytes into HBM-resident id/f64
+columns, through the C ABI (nxg_decode_updates_async). With --gpus N each rank decodes its own
+10^7-record shard; the ids are disjoint and there is no data-path collective ("weak" scaling).
+`value` is the whole-job aggregate in M updates/s, over all ranks.
+
+Each step is verified bit-exact against the columns it was encoded from. The inputs come from
+the product encoder (config 4); the CPU oracle is only used in the cpu_baseline leg.
+
+Also reported on the same JSON line:
+  roofline       the decode kernel's algorithmic bytes (W + 16 N) / mean launch time (HIP
+                 events on the codec stream) vs the 8 TB/s HBM3E peak;
+  cpu_baseline   the C restatement of the reference decoder (oracle/, 1 core) on this host;
+  extras         10^8-record decode (north-star size), mixed-tag decode (config 3), f64 encode
+                 (config 4); with N>1, the config-5 sharded encode + RCCL all-gather.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+KERNEL_DEC_F64 = "nxg_dec_f64_kernel"
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def dist_setup():
+    import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return world, rank, local
+
+
+def barrier(world):
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+
+
+def max_over_ranks(x, world):
+    if world == 1:
+        return x
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def make_f64_wire(codec, n, rank):
+    import netidx_amd
+    from netidx_amd import synth
+    ids, vals = synth.f64_columns(n, synth.SEED_F64, id_offset=rank * n)
+    cols = netidx_amd.columns_from_arrays(ids, vals)
+    wire = codec.encode_batch(cols)
+    return cols, wire
+
+
+def time_decode(codec, wire, out, n, steps, warmup, world, stream, flags=0):
+    """Returns (wall seconds max over ranks, mean kernel ms, last status)."""
+    import torch
+    nbytes = wire.numel()
+    for _ in range(warmup):
+        codec.decode_async(wire.data_ptr(), nbytes, out, flags)
+        codec.sync()
+    barrier(world)
+    torch.cuda.synchronize()
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for i in range(steps):
+        codec.decode_async(wire.data_ptr(), nbytes, out, flags)
+        if (i + 1) % 100 == 0:
+            codec.sync()
+    e1.record(stream)
+    st = codec.sync()
+    torch.cuda.synchronize()
+    barrier(world)
+    wall = max_over_ranks(time.perf_counter() - t0, world)
+    return wall, e0.elapsed_time(e1) / steps, st
+
+
+def cpu_baseline(wire_host, n, seconds):
+    """The oracle (C restatement of the reference's sequential decoder) on one host core."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import nxo
+    reps, t_total = 0, 0.0
+    while t_total < seconds or reps == 0:
+        t0 = time.perf_counter()
+        d = nxo.decode(wire_host, cap_rows=n + 1, cap_children=1, cap_ctl=1)
+        t_total += time.perf_counter() - t0
+        reps += 1
+        assert d.s.err_kind == 0 and d.s.n_rows == n
+    return n * reps / t_total, reps, t_total
+
+
+def read_traffic(records):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary, if it matches."""
+    p = os.path.join(ROOT, "profiles", "pmc_dec_f64.json")
+    try:
+        j = json.load(open(p))
+        if j.get("records") == records and j.get("kernel") == KERNEL_DEC_F64:
+            return j.get("hbm_bytes_per_launch")
+    except Exception:
+        pass
+    return None
+
+
+def extras_single_gpu(codec, stream, steps, warmup):
+    import netidx_amd
+    import numpy as np
+    import torch
+    from netidx_amd import synth
+    from netidx_amd.codec import Columns
+    ex = {}
+    # (a) north-star size: 10^8 f64 records on one GPU
+    try:
+        n = 100_000_000
+        cols, wire = make_f64_wire(codec, n, 0)
+        out = Columns(n, 0, 0, netidx_amd.LAYOUT_F64, "cuda")
+        wall, kms, st = time_decode(codec, wire, out, n, max(3, steps // 4), 2, 1, stream)
+        assert st.path == 1 and st.n_rows == n
+        assert torch.equal(out.fixed[:n], cols.fixed[:n]) and torch.equal(out.id[:n], cols.id[:n])
+        b = wire.numel() + 16 * n
+        ex["decode_f64_1e8"] = {"records": n, "wire_bytes": wire.numel(),
+                                "M_updates_s": round(n / (kms / 1e3) / 1e6, 1),
+                                "kernel_ms": round(kms, 4),
+                                "hbm_frac": round(b / (kms / 1e3) / 1e9 / HBM_PEAK_GBS, 4)}
+        del cols, wire, out
+        torch.cuda.empty_cache()
+    except Exception as e:  # report, never hide
+        ex["decode_f64_1e8"] = {"error": repr(e)}
+    # (b) config 3: mixed-tag decode (general kernel)
+    try:
+        n = 10_000_000
+        m = synth.mixed_columns(n)
+        mc = netidx_amd.columns_from_arrays(m.id, m.fixed, m.tag, m.aux, m.ctag, m.cfixed, m.caux)
+        heap = torch.from_numpy(m.heap.copy()).cuda()
+        wire = codec.encode_batch(mc, heap)
+        out = Columns(n + 1, len(m.ctag) + 1, 1, netidx_amd.LAYOUT_MIXED, "cuda")
+        wall, kms, st = time_decode(codec, wire, out, n, max(3, steps // 4), 1, 1, stream,
+                                    flags=netidx_amd.HINT_MIXED)
+        assert st.path == 2 and st.n_rows == n and st.err_kind == 0
+        assert torch.equal(out.id[:n], mc.id[:n]) and torch.equal(out.tag[:n], mc.tag[:n])
+        nd = int((m.tag == 10).sum())
+        ns = int((m.tag == 12).sum())
+        na = int((m.tag == 19).sum())
+        b = wire.numel() + n * (8 + 1 + 8 + 4) + 13 * len(m.ctag)
+        ex["decode_mixed_1e7"] = {"records": n, "wire_bytes": wire.numel(),
+                                  "M_updates_s": round(n / (kms / 1e3) / 1e6, 1),
+                                  "kernel_ms": round(kms, 4),
+                                  "hbm_frac": round(b / (kms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                                  "n_datetime": nd, "n_string": ns, "n_array": na,
+                                  "n_children": len(m.ctag)}
+        del mc, heap, wire, out
+        torch.cuda.empty_cache()
+    except Exception as e:
+        ex["decode_mixed_1e7"] = {"error": repr(e)}
+    # (c) config 4: f64 encode from device columns, byte-identical round trip
+    try:
+        n = 10_000_000
+        cols, wire = make_f64_wire(codec, n, 0)
+        dout = torch.empty(wire.numel() + 64, dtype=torch.uint8, device="cuda")
+        for _ in range(2):
+            codec.encode_async(cols, None, dout.data_ptr(), dout.numel())
+            codec.sync()
+        torch.cuda.synchronize()
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        k = max(3, steps // 2)
+        e0.record(stream)
+        for _ in range(k):
+            codec.encode_async(cols, None, dout.data_ptr(), dout.numel())
+        e1.record(stream)
+        codec.sync()
+        torch.cuda.synchronize()
+        kms = e0.elapsed_time(e1) / k
+        assert torch.equal(dout[: wire.numel()], wire)
+        b = wire.numel() + 16 * n
+        ex["encode_f64_1e7"] = {"records": n, "M_updates_s": round(n / (kms / 1e3) / 1e6, 1),
+                                "kernel_ms": round(kms, 4),
+                                "hbm_frac": round(b / (kms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                                "roundtrip_identical": True}
+    except Exception as e:
+        ex["encode_f64_1e7"] = {"error": repr(e)}
+    return ex
+
+
+def extras_multi_gpu(codec, world, rank, stream):
+    """Config 5: 10^8 records sharded by record; each rank encodes its shard, then an RCCL
+    all-gather (padded to the largest shard) assembles the full wire on every GPU."""
+    import netidx_amd
+    import torch
+    import torch.distributed as dist
+    from netidx_amd import synth
+    total = 100_000_000
+    n = total // world
+    ids, vals = synth.f64_columns(n, synth.SEED_8GPU, id_offset=rank * n)
+    cols = netidx_amd.columns_from_arrays(ids, vals)
+    dout = torch.empty(21 * n + 64, dtype=torch.uint8, device="cuda")
+    lens = torch.zeros(world, dtype=torch.int64, device="cuda")
+    times = []
+    for it in range(3):
+        barrier(world)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ln = codec.encode_async(cols, None, dout.data_ptr(), dout.numel())
+        codec.sync()
+        mine = torch.tensor([ln.value], dtype=torch.int64, device="cuda")
+        dist.all_gather_into_tensor(lens, mine)
+        mx = int(lens.max().item())
+        gathered = torch.empty(world * mx, dtype=torch.uint8, device="cuda")
+        dist.all_gather_into_tensor(gathered, dout[:mx])
+        torch.cuda.synchronize()
+        times.append(time.perf_counter() - t0)
+    t = max_over_ranks(min(times), world)
+    wire_total = int(lens.sum().item())
+    return {"records": total, "wire_bytes": wire_total, "world": world,
+            "encode_allgather_ms": round(t * 1e3, 3),
+            "M_updates_s": round(total / t / 1e6, 1)}
+
+
+def main():
+    ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--records", type=int, default=10_000_000)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-extras", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import netidx_amd
+    from netidx_amd.codec import Columns
+
+    world, rank, local = dist_setup()
+    codec = netidx_amd.Codec(local)
+    stream = torch.cuda.Stream()
+    codec.set_stream(stream.cuda_stream)
+    n = args.records
+
+    cols, wire = make_f64_wire(codec, n, rank)
+    nbytes = wire.numel()
+    out = Columns(n, 0, 0, netidx_amd.LAYOUT_F64, "cuda")
+    wall, kms, st = time_decode(codec, wire, out, n, args.steps, args.warmup, world, stream)
+    assert st.err_kind == 0 and st.path == 1 and st.n_rows == n, st
+    assert torch.equal(out.id[:n], cols.id[:n]) and torch.equal(out.fixed[:n], cols.fixed[:n]), \
+        "decode is not bit-exact"
+
+    value = world * n * args.steps / wall / 1e6
+    alg_bytes = nbytes + 16 * n
+    achieved = alg_bytes / (kms / 1e3) / 1e9
+    line = {
+        "metric": "Value-batch decode: M updates/s/GPU + GiB/s (device-resident) vs HBM roofline",
+        "value": round(value, 2),
+        "unit": "M updates/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(wall / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (SplitMix64 f64 values, sequential ids; wire made by the product "
+                "encoder)",
+        "config": {"workload": "decode 10^7-record all-f64 From::Update batch per GPU "
+                               "(BASELINE configs[1])",
+                   "records_per_gpu": n, "wire_bytes_per_gpu": nbytes,
+                   "parallelism": f"shard-per-gpu x{world} (no data-path collective)"},
+        "per_gpu_M_updates_s": round(value / world, 2),
+        "gib_per_s": round(world * alg_bytes * args.steps / wall / 2**30, 2),
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": read_traffic(n), "kernel": KERNEL_DEC_F64,
+                     "kernel_ms": round(kms, 4), "algorithmic_bytes_per_launch": alg_bytes},
+    }
+    if rank == 0 and world == 1:
+        host = wire.cpu().numpy()
+        ups, reps, secs = cpu_baseline(host, n, args.cpu_seconds)
+        line["cpu_baseline"] = {"value": round(ups / 1e6, 3), "unit": "M updates/s", "cores": 1,
+                                "kind": "port",
+                                "sample": f"full {n}-record f64 frame decoded {reps}x "
+                                          f"({secs:.1f} s) by oracle/nx_oracle.c"}
+        if not args.no_extras:
+            line["extras"] = extras_single_gpu(codec, stream, args.steps, args.warmup)
+    elif world > 1 and not args.no_extras:
+        ex = extras_multi_gpu(codec, world, rank, stream)
+        if rank == 0:
+            line["extras"] = {"encode_allgather_1e8": ex}
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    codec.close()
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

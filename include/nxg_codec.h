@@ -1,0 +1,180 @@
+/*
+ * nxg_codec.h -- C ABI of the MI355X-native netidx batch-update codec.
+ *
+ * The reference codec is the generic Rust `trait Pack` (netidx-core/src/pack.rs:149-165). It is
+ * called once per message at two seams:
+ *
+ *   encode: ClientCtx::handle_updates   netidx/src/publisher/server.rs:604-629
+ *           -> WriteChannel::queue_send netidx/src/channel.rs:177-202
+ *           -> <From as Pack>::encode   (netidx-derive/src/lib.rs:289-381)
+ *   decode: decode_task                 netidx/src/subscriber/connection.rs:209-242
+ *           -> ReadChannel::receive_batch_fn   netidx/src/channel.rs:504-521
+ *           -> <From as Pack>::decode   (netidx-derive/src/lib.rs:482-601)
+ *
+ * This ABI replaces each of those per-message loops with ONE batch call. Each call covers all
+ * the messages of one frame payload, executed by hand-written gfx950 HIP kernels. The wire bytes
+ * are identical to the reference.
+ *
+ * Conventions follow netidx-ffi (netidx-ffi/netidx.h, netidx-ffi/src/error.rs:19-29):
+ * - fallible calls return `bool`;
+ * - on failure they fill a caller-provided `NetidxError*` whose `msg` must be released with
+ *   nxg_error_free;
+ * - handles are opaque.
+ *
+ * Threading: an NxgCtx is not internally synchronised. Use one ctx per connection/thread. Each ctx
+ * owns one HIP stream (or a caller-provided one).
+ *
+ * Columnar layout (the decode output and the encode input):
+ *
+ *   rows (one per From::Update, in wire order):
+ *     id    u64  publisher::Id (netidx-netproto/src/publisher.rs:7)
+ *     tag   u8   Value wire tag (netidx-value/src/lib.rs:361-468); 17 is normalised to 16, and
+ *                Error(String) is always 18
+ *     fixed u64  scalar payload: integers (signed values sign-extended), f32/f64 bit patterns,
+ *                DateTime/Duration seconds, bool as 1/0; for String/Bytes/Error(String)/Decimal/
+ *                Abstract: byte offset of the payload in the heap (decode: the frame itself);
+ *                for Array/Map/Error(Value): index of the first child slot
+ *     aux   u32  DateTime/Duration nanoseconds; byte length of String/Bytes/Decimal/Abstract;
+ *                element count of Array, entry count of Map, 1 for Error(Value)
+ *   children (elements of Array, key/value pairs of Map, inner of Error(Value)): ctag/cfixed/
+ *     caux with the same meaning. Each container's elements are contiguous, allocated
+ *     depth-first.
+ *   ctl (every other From message, with Heartbeat included, kept as validated raw spans):
+ *     ctl_row     index of the first Update row that follows it
+ *     ctl_off     byte offset of the message in the frame
+ *     ctl_len     byte length of the message
+ *     ctl_variant From variant (0 NoSuchValue, 1 Denied, 2 Unsubscribed, 3 Subscribed,
+ *                 5 Heartbeat, 6 WriteResult)
+ *
+ * NXG_LAYOUT_F64 is the homogeneous fast path. It is valid only when every message is
+ * From::Update with an F64 value. Only id and fixed (the f64 bits) are meaningful; tag is
+ * implicitly 9.
+ */
+#ifndef NXG_CODEC_H
+#define NXG_CODEC_H
+#include <stdbool.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* netidx-ffi/netidx.h:162-164 */
+typedef struct NetidxError {
+    char* msg;
+} NetidxError;
+
+typedef struct NxgCtx NxgCtx;
+
+/* PackError (netidx-core/src/pack.rs:89-95) plus codec-level kinds */
+enum NxgErrKind {
+    NXG_OK = 0,
+    NXG_UNKNOWN_TAG = 1,
+    NXG_TOO_BIG = 2,
+    NXG_INVALID_FORMAT = 3,
+    NXG_BUFFER_SHORT = 4,
+    NXG_DEPTH = 6,    /* Value nesting deeper than NXG_MAX_DEPTH (documented deviation) */
+    NXG_CAPACITY = 7, /* output columns too small */
+    NXG_NOT_F64 = 8,  /* valid batch, but F64-only columns were supplied for mixed content */
+    NXG_TIMEOUT = 9,  /* device-side progress watchdog fired (should never happen) */
+};
+
+#define NXG_MAX_DEPTH 32
+
+enum NxgLayout { NXG_LAYOUT_F64 = 1, NXG_LAYOUT_MIXED = 2 };
+enum NxgMem { NXG_MEM_DEVICE = 0, NXG_MEM_HOST = 1 /* pinned host */ };
+enum NxgDecodeFlags {
+    NXG_DECODE_DEFAULT = 0,
+    NXG_DECODE_HINT_MIXED = 1, /* skip the homogeneous-f64 attempt */
+};
+
+typedef struct NxgColumns {
+    uint32_t layout; /* NxgLayout: alloc-time capability; after decode, what was written */
+    uint32_t mem;    /* NxgMem */
+    uint64_t cap_rows, cap_children, cap_ctl;
+    uint64_t n_rows, n_children, n_ctl, n_heartbeat;
+    uint64_t* id;
+    uint8_t* tag;
+    uint64_t* fixed;
+    uint32_t* aux;
+    uint8_t* ctag;
+    uint64_t* cfixed;
+    uint32_t* caux;
+    uint64_t* ctl_row;
+    uint64_t* ctl_off;
+    uint32_t* ctl_len;
+    uint8_t* ctl_variant;
+} NxgColumns;
+
+typedef struct NxgStatus {
+    uint64_t n_rows, n_children, n_ctl, n_heartbeat;
+    int32_t err_kind;    /* NxgErrKind of the FIRST failing message (reference is sequential) */
+    uint32_t path;       /* 1 = homogeneous-f64 kernel, 2 = general kernel */
+    uint64_t err_offset; /* byte offset of the first failing message */
+} NxgStatus;
+
+/* ---- lifetime -------------------------------------------------------------------------- */
+NxgCtx* nxg_ctx_new(int device, NetidxError* err);
+void nxg_ctx_destroy(NxgCtx* ctx);
+/* Use `hip_stream` (a hipStream_t) instead of the ctx's own stream; NULL restores it. */
+bool nxg_ctx_set_stream(NxgCtx* ctx, void* hip_stream, NetidxError* err);
+void* nxg_ctx_stream(NxgCtx* ctx);
+void nxg_error_free(NetidxError* err);
+/* library version string, e.g. "nxg 0.1.0 gfx950" */
+const char* nxg_version(void);
+
+/* ---- columns ------------------------------------------------------------------------------
+ * layout F64 allocates id+fixed only; MIXED allocates every array. mem: device or pinned host.
+ * Capacity bounds for a frame of W bytes: rows <= W/4 (the smallest Update, `04 04 00 10`),
+ * children <= W, ctl <= W/2 (`02 05`). */
+bool nxg_columns_alloc(NxgCtx* ctx, uint32_t layout, uint64_t cap_rows, uint64_t cap_children,
+                       uint64_t cap_ctl, uint32_t mem, NxgColumns* out, NetidxError* err);
+void nxg_columns_free(NxgCtx* ctx, NxgColumns* cols);
+
+/* ---- decode: replaces decode_task's receive_batch_fn loop (connection.rs:209-242) ---------
+ * `frame` is one frame payload (no u32 header; channel.rs:379-443 strips it), host or device
+ * memory. `out` must come from nxg_columns_alloc. Synchronous. Returns false only on API
+ * misuse or a HIP failure. A malformed frame returns true with st->err_kind != 0, and the whole
+ * frame is rejected, as in connection.rs:228-231. */
+bool nxg_decode_updates(NxgCtx* ctx, const uint8_t* frame, uint64_t len, NxgColumns* out,
+                        uint32_t flags, NxgStatus* st, NetidxError* err);
+/* Asynchronous device-resident variant: enqueue on the ctx stream; no host sync. Only the
+ * path selected up front runs (flags). nxg_ctx_sync completes it, runs the general fallback if
+ * the homogeneous path rejected the frame, and fills the status. */
+bool nxg_decode_updates_async(NxgCtx* ctx, const uint8_t* dframe, uint64_t len, NxgColumns* dout,
+                              uint32_t flags, NetidxError* err);
+bool nxg_ctx_sync(NxgCtx* ctx, NxgStatus* st, NetidxError* err);
+
+/* ---- encode: replaces handle_updates' queue_send loop (server.rs:610-612) ----------------
+ * `heap` holds the bytes that string/bytes/decimal/abstract offsets and ctl spans refer to.
+ * It may be NULL for pure fixed-width columns. in/heap/out must all be device memory, or all
+ * host memory. */
+bool nxg_encoded_len(NxgCtx* ctx, const NxgColumns* in, const uint8_t* heap, uint64_t* len_out,
+                     NetidxError* err);
+bool nxg_encode_updates(NxgCtx* ctx, const NxgColumns* in, const uint8_t* heap, uint8_t* out,
+                        uint64_t cap, uint64_t* len_out, NetidxError* err);
+/* Async device-resident variant (len_out is written at nxg_ctx_sync time). */
+bool nxg_encode_updates_async(NxgCtx* ctx, const NxgColumns* din, const uint8_t* dheap,
+                              uint8_t* dout, uint64_t cap, uint64_t* len_out, NetidxError* err);
+
+/* ---- host framing (netidx/src/channel.rs) ------------------------------------------------
+ * Frame boundaries exactly as WriteChannel::queue_send/try_flush split the buffer. The split
+ * happens at MAX_BATCH = 0x3FFFFFFF (channel.rs:34, 187-191) and is recorded between messages.
+ * `msg_len` holds the encoded length of each message, in order. `chunk_len_out` receives the
+ * length of each frame payload. Returns the number of frames, or -1 if cap_chunks is too small
+ * or a message exceeds MAX_BATCH. */
+int64_t nxg_frame_split(const uint64_t* msg_len, uint64_t n_msgs, uint64_t* chunk_len_out,
+                        uint64_t cap_chunks);
+/* flush_buf (channel.rs:107-126): the u32 big-endian header, with bit 31 set when the frame is
+ * encrypted. */
+void nxg_frame_header(uint32_t payload_len, bool encrypted, uint8_t out[4]);
+/* read_task (channel.rs:379-443): parse one header from `buf`. Returns the header size (4), or
+ * 0 if fewer than 4 bytes are present. */
+uint32_t nxg_frame_parse_header(const uint8_t* buf, uint64_t avail, uint32_t* payload_len,
+                                bool* encrypted);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

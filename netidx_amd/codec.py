@@ -1,0 +1,362 @@
+"""ctypes binding of the C ABI in include/nxg_codec.h (netidx_amd/lib/libnxg_codec.so).
+
+The Python surface mirrors the two seams that the codec replaces in the reference:
+
+* ``Codec.decode_batch(frame)`` replaces the ``decode_task`` -> ``receive_batch_fn`` loop
+  (netidx/src/subscriber/connection.rs:209-242, netidx/src/channel.rs:504-521). A malformed
+  frame raises ``PackError`` with the reference's kind and the offset of the first failing
+  message, and the whole frame is rejected, as in connection.rs:228-231.
+* ``Codec.encode_batch(cols)`` replaces the ``handle_updates`` -> ``queue_send`` loop
+  (netidx/src/publisher/server.rs:610-612, netidx/src/channel.rs:177-202).
+
+The product path is the HIP library. There is no CPU fallback: if the shared library or a GPU
+is missing, the calls raise.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libnxg_codec.so")
+
+# NxgErrKind (include/nxg_codec.h) = PackError (netidx-core/src/pack.rs:89-95) + codec kinds
+OK, UNKNOWN_TAG, TOO_BIG, INVALID_FORMAT, BUFFER_SHORT = 0, 1, 2, 3, 4
+DEPTH, CAPACITY, NOT_F64, TIMEOUT = 6, 7, 8, 9
+ERR_NAMES = {1: "UnknownTag", 2: "TooBig", 3: "InvalidFormat", 4: "BufferShort", 6: "Depth",
+             7: "Capacity", 8: "NotF64", 9: "Timeout"}
+LAYOUT_F64, LAYOUT_MIXED = 1, 2
+MEM_DEVICE, MEM_HOST = 0, 1
+HINT_MIXED = 1
+
+
+class PackError(Exception):
+    """A frame the reference would reject (netidx-core/src/pack.rs:89-95)."""
+
+    def __init__(self, kind, offset):
+        self.kind = kind
+        self.offset = offset
+        super().__init__(f"{ERR_NAMES.get(kind, kind)} at message offset {offset}")
+
+
+class CodecError(RuntimeError):
+    """API misuse or a HIP failure (NetidxError)."""
+
+
+class NetidxError(C.Structure):
+    _fields_ = [("msg", C.c_char_p)]
+
+
+U64P, U32P, U8P = C.c_void_p, C.c_void_p, C.c_void_p
+
+
+class NxgColumns(C.Structure):
+    _fields_ = [
+        ("layout", C.c_uint32), ("mem", C.c_uint32),
+        ("cap_rows", C.c_uint64), ("cap_children", C.c_uint64), ("cap_ctl", C.c_uint64),
+        ("n_rows", C.c_uint64), ("n_children", C.c_uint64), ("n_ctl", C.c_uint64),
+        ("n_heartbeat", C.c_uint64),
+        ("id", C.c_void_p), ("tag", C.c_void_p), ("fixed", C.c_void_p), ("aux", C.c_void_p),
+        ("ctag", C.c_void_p), ("cfixed", C.c_void_p), ("caux", C.c_void_p),
+        ("ctl_row", C.c_void_p), ("ctl_off", C.c_void_p), ("ctl_len", C.c_void_p),
+        ("ctl_variant", C.c_void_p),
+    ]
+
+
+class NxgStatus(C.Structure):
+    _fields_ = [
+        ("n_rows", C.c_uint64), ("n_children", C.c_uint64), ("n_ctl", C.c_uint64),
+        ("n_heartbeat", C.c_uint64), ("err_kind", C.c_int32), ("path", C.c_uint32),
+        ("err_offset", C.c_uint64),
+    ]
+
+
+# every symbol include/nxg_codec.h declares, with its ctypes signature
+SIGNATURES = {
+    "nxg_ctx_new": (C.c_void_p, [C.c_int, C.POINTER(NetidxError)]),
+    "nxg_ctx_destroy": (None, [C.c_void_p]),
+    "nxg_ctx_set_stream": (C.c_bool, [C.c_void_p, C.c_void_p, C.POINTER(NetidxError)]),
+    "nxg_ctx_stream": (C.c_void_p, [C.c_void_p]),
+    "nxg_error_free": (None, [C.POINTER(NetidxError)]),
+    "nxg_version": (C.c_char_p, []),
+    "nxg_columns_alloc": (C.c_bool, [C.c_void_p, C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint64,
+                                     C.c_uint32, C.POINTER(NxgColumns), C.POINTER(NetidxError)]),
+    "nxg_columns_free": (None, [C.c_void_p, C.POINTER(NxgColumns)]),
+    "nxg_decode_updates": (C.c_bool, [C.c_void_p, C.c_void_p, C.c_uint64, C.POINTER(NxgColumns),
+                                      C.c_uint32, C.POINTER(NxgStatus), C.POINTER(NetidxError)]),
+    "nxg_decode_updates_async": (C.c_bool, [C.c_void_p, C.c_void_p, C.c_uint64,
+                                            C.POINTER(NxgColumns), C.c_uint32,
+                                            C.POINTER(NetidxError)]),
+    "nxg_ctx_sync": (C.c_bool, [C.c_void_p, C.POINTER(NxgStatus), C.POINTER(NetidxError)]),
+    "nxg_encoded_len": (C.c_bool, [C.c_void_p, C.POINTER(NxgColumns), C.c_void_p,
+                                   C.POINTER(C.c_uint64), C.POINTER(NetidxError)]),
+    "nxg_encode_updates": (C.c_bool, [C.c_void_p, C.POINTER(NxgColumns), C.c_void_p, C.c_void_p,
+                                      C.c_uint64, C.POINTER(C.c_uint64), C.POINTER(NetidxError)]),
+    "nxg_encode_updates_async": (C.c_bool, [C.c_void_p, C.POINTER(NxgColumns), C.c_void_p,
+                                            C.c_void_p, C.c_uint64, C.POINTER(C.c_uint64),
+                                            C.POINTER(NetidxError)]),
+    "nxg_frame_split": (C.c_int64, [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64]),
+    "nxg_frame_header": (None, [C.c_uint32, C.c_bool, C.c_void_p]),
+    "nxg_frame_parse_header": (C.c_uint32, [C.c_void_p, C.c_uint64, C.POINTER(C.c_uint32),
+                                            C.POINTER(C.c_bool)]),
+}
+
+_lib = None
+
+
+def lib():
+    """Load libnxg_codec.so (loud failure if it was not built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise CodecError(f"{LIB_PATH} missing: build it (python -c 'import __graft_entry__ as g; g.build()')")
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _check(ok, err):
+    if not ok:
+        msg = err.msg.decode() if err.msg else "unknown error"
+        lib().nxg_error_free(C.byref(err))
+        raise CodecError(msg)
+
+
+def _ptr(t):
+    return C.c_void_p(t.data_ptr()) if t is not None else C.c_void_p(0)
+
+
+class Columns:
+    """Columnar batch (include/nxg_codec.h). Arrays are torch tensors on `device` (or pinned
+    host numpy-backed tensors when device is 'cpu')."""
+
+    FIELDS = [("id", "torch.int64", "rows"), ("fixed", "torch.int64", "rows"),
+              ("tag", "torch.uint8", "rows"), ("aux", "torch.int32", "rows"),
+              ("ctag", "torch.uint8", "children"), ("cfixed", "torch.int64", "children"),
+              ("caux", "torch.int32", "children"), ("ctl_row", "torch.int64", "ctl"),
+              ("ctl_off", "torch.int64", "ctl"), ("ctl_len", "torch.int32", "ctl"),
+              ("ctl_variant", "torch.uint8", "ctl")]
+
+    def __init__(self, cap_rows, cap_children=0, cap_ctl=0, layout=LAYOUT_MIXED, device="cuda"):
+        import torch
+        self.device = torch.device(device)
+        self.layout = layout
+        self.caps = {"rows": max(cap_rows, 1), "children": max(cap_children, 1),
+                     "ctl": max(cap_ctl, 1)}
+        self.t = {}
+        dt = {"torch.int64": torch.int64, "torch.int32": torch.int32, "torch.uint8": torch.uint8}
+        for name, d, kind in self.FIELDS:
+            if layout == LAYOUT_F64 and name not in ("id", "fixed"):
+                self.t[name] = None
+                continue
+            x = torch.zeros(self.caps[kind], dtype=dt[d], device=self.device)
+            if self.device.type == "cpu":
+                x = x.pin_memory()
+            self.t[name] = x
+        self.s = NxgColumns()
+        self.s.layout = layout
+        self.s.mem = MEM_DEVICE if self.device.type == "cuda" else MEM_HOST
+        self.s.cap_rows, self.s.cap_children, self.s.cap_ctl = (
+            self.caps["rows"], self.caps["children"], self.caps["ctl"])
+        for name, _, _ in self.FIELDS:
+            setattr(self.s, name, _ptr(self.t[name]).value)
+
+    @classmethod
+    def for_frame(cls, nbytes, layout=LAYOUT_MIXED, device="cuda"):
+        """Capacity bounds of include/nxg_codec.h for a frame of `nbytes`."""
+        return cls(nbytes // 4 + 1, nbytes + 1, nbytes // 2 + 1, layout, device)
+
+    def __getattr__(self, k):
+        t = self.__dict__.get("t", {})
+        if k in t:
+            return t[k]
+        raise AttributeError(k)
+
+    @property
+    def n_rows(self):
+        return self.s.n_rows
+
+    def numpy(self):
+        """Trimmed host copy: {field: ndarray} (unsigned views)."""
+        n = {"rows": self.s.n_rows, "children": self.s.n_children, "ctl": self.s.n_ctl}
+        out = {}
+        u = {"torch.int64": np.uint64, "torch.int32": np.uint32, "torch.uint8": np.uint8}
+        for name, d, kind in self.FIELDS:
+            x = self.t[name]
+            if x is None:
+                continue
+            out[name] = x[: n[kind]].cpu().numpy().view(u[d])
+        if self.s.layout == LAYOUT_F64:  # homogeneous result: tag 9 implied, aux unused
+            out["tag"] = np.full(n["rows"], 9, np.uint8)
+            if "aux" in out:
+                out["aux"] = np.zeros(n["rows"], np.uint32)
+        out["n_heartbeat"] = self.s.n_heartbeat
+        out["layout"] = self.s.layout
+        return out
+
+
+class Codec:
+    """One codec context per connection/thread (NxgCtx)."""
+
+    def __init__(self, device=0):
+        err = NetidxError()
+        self.ctx = lib().nxg_ctx_new(device, C.byref(err))
+        _check(self.ctx is not None, err)
+        self.device = device
+
+    def close(self):
+        if self.ctx:
+            lib().nxg_ctx_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_stream(self, stream_ptr):
+        err = NetidxError()
+        _check(lib().nxg_ctx_set_stream(self.ctx, C.c_void_p(stream_ptr), C.byref(err)), err)
+
+    def decode_into(self, frame, nbytes, cols, flags=0, check=True):
+        """frame: device pointer (int), torch tensor or bytes. Returns NxgStatus."""
+        keep = None
+        if isinstance(frame, (bytes, bytearray, memoryview)):
+            keep = np.frombuffer(bytes(frame), np.uint8)
+            ptr = keep.ctypes.data
+        elif isinstance(frame, np.ndarray):
+            keep = np.ascontiguousarray(frame)
+            ptr = keep.ctypes.data
+        elif hasattr(frame, "data_ptr"):
+            ptr = frame.data_ptr()
+        else:
+            ptr = int(frame)
+        st, err = NxgStatus(), NetidxError()
+        ok = lib().nxg_decode_updates(self.ctx, C.c_void_p(ptr), nbytes, C.byref(cols.s), flags,
+                                      C.byref(st), C.byref(err))
+        _check(ok, err)
+        if check and st.err_kind:
+            raise PackError(st.err_kind, st.err_offset)
+        return st
+
+    def decode_batch(self, frame, layout=LAYOUT_MIXED, flags=0, device="cuda"):
+        """Decode one frame payload; returns (Columns, NxgStatus)."""
+        n = len(frame) if not hasattr(frame, "numel") else frame.numel()
+        cols = Columns.for_frame(n, layout, device)
+        st = self.decode_into(frame, n, cols, flags)
+        return cols, st
+
+    def decode_async(self, dframe_ptr, nbytes, cols, flags=0):
+        err = NetidxError()
+        _check(lib().nxg_decode_updates_async(self.ctx, C.c_void_p(dframe_ptr), nbytes,
+                                              C.byref(cols.s), flags, C.byref(err)), err)
+
+    def sync(self, check=True):
+        st, err = NxgStatus(), NetidxError()
+        ok = lib().nxg_ctx_sync(self.ctx, C.byref(st), C.byref(err))
+        self.__dict__["_pending_len"] = []
+        _check(ok, err)
+        if check and st.err_kind:
+            raise PackError(st.err_kind, st.err_offset)
+        return st
+
+    def encoded_len(self, cols, heap=None):
+        n, err = C.c_uint64(0), NetidxError()
+        _check(lib().nxg_encoded_len(self.ctx, C.byref(cols.s), _heap_ptr(heap), C.byref(n),
+                                     C.byref(err)), err)
+        return n.value
+
+    def encode_into(self, cols, heap, out_ptr, cap):
+        n, err = C.c_uint64(0), NetidxError()
+        _check(lib().nxg_encode_updates(self.ctx, C.byref(cols.s), _heap_ptr(heap),
+                                        C.c_void_p(out_ptr), cap, C.byref(n), C.byref(err)), err)
+        return n.value
+
+    def encode_batch(self, cols, heap=None):
+        """Encode columns to one frame payload (torch uint8 tensor on the columns' device)."""
+        import torch
+        n = self.encoded_len(cols, heap)
+        out = torch.empty(max(n, 16), dtype=torch.uint8, device=cols.device)
+        m = self.encode_into(cols, heap, out.data_ptr(), n)
+        assert m == n
+        return out[:n]
+
+    def encode_async(self, cols, heap, out_ptr, cap):
+        """Enqueue an encode; the returned c_uint64 holds the length after sync()."""
+        n, err = C.c_uint64(0), NetidxError()
+        self.__dict__.setdefault("_pending_len", []).append(n)  # written by the C side at sync
+        _check(lib().nxg_encode_updates_async(self.ctx, C.byref(cols.s), _heap_ptr(heap),
+                                              C.c_void_p(out_ptr), cap, C.byref(n),
+                                              C.byref(err)), err)
+        return n
+
+
+def _heap_ptr(heap):
+    if heap is None:
+        return C.c_void_p(0)
+    if hasattr(heap, "data_ptr"):
+        return C.c_void_p(heap.data_ptr())
+    if isinstance(heap, np.ndarray):
+        return C.c_void_p(heap.ctypes.data)
+    return C.c_void_p(int(heap))
+
+
+# ---- host framing (netidx/src/channel.rs) ----------------------------------------------------
+def frame_split(msg_lens):
+    """Frame payload lengths for a queue of encoded messages (WriteChannel::queue_send)."""
+    a = np.ascontiguousarray(msg_lens, np.uint64)
+    out = np.zeros(len(a) + 1, np.uint64)
+    n = lib().nxg_frame_split(a.ctypes.data, len(a), out.ctypes.data, len(out))
+    if n < 0:
+        raise CodecError("message exceeds MAX_BATCH")
+    return out[:n]
+
+
+def frame_header(payload_len, encrypted=False):
+    b = (C.c_uint8 * 4)()
+    lib().nxg_frame_header(payload_len, encrypted, b)
+    return bytes(b)
+
+
+def frame_parse_header(buf):
+    ln, enc = C.c_uint32(0), C.c_bool(False)
+    a = np.frombuffer(bytes(buf), np.uint8)
+    n = lib().nxg_frame_parse_header(a.ctypes.data, len(a), C.byref(ln), C.byref(enc))
+    return (None if n == 0 else (ln.value, bool(enc.value)))
+
+
+def columns_from_arrays(id, fixed, tag=None, aux=None, ctag=None, cfixed=None, caux=None,
+                        ctl_row=None, ctl_off=None, ctl_len=None, ctl_variant=None,
+                        device="cuda"):
+    """Build encode-input Columns from host numpy arrays (uploaded to `device`)."""
+    import torch
+    n = len(id)
+    nc = 0 if ctag is None else len(ctag)
+    nk = 0 if ctl_row is None else len(ctl_row)
+    layout = LAYOUT_F64 if tag is None else LAYOUT_MIXED
+    cols = Columns(n, nc, nk, layout, device)
+
+    def put(name, arr, dt):
+        if arr is None or len(arr) == 0:
+            return
+        src = torch.from_numpy(np.ascontiguousarray(arr).view(dt))
+        cols.t[name][: len(arr)].copy_(src)
+
+    put("id", id, np.int64)
+    put("fixed", fixed, np.int64)
+    put("tag", tag, np.uint8)
+    put("aux", aux, np.int32)
+    put("ctag", ctag, np.uint8)
+    put("cfixed", cfixed, np.int64)
+    put("caux", caux, np.int32)
+    put("ctl_row", ctl_row, np.int64)
+    put("ctl_off", ctl_off, np.int64)
+    put("ctl_len", ctl_len, np.int32)
+    put("ctl_variant", ctl_variant, np.uint8)
+    cols.s.n_rows, cols.s.n_children, cols.s.n_ctl = n, nc, nk
+    return cols

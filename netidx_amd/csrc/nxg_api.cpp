@@ -1,0 +1,808 @@
+// nxg_api.cpp -- the C ABI (include/nxg_codec.h): contexts, column allocation, dispatch of the
+// gfx950 kernels, host staging for host-resident frames/columns, and host framing.
+//
+// Error convention follows netidx-ffi (netidx-ffi/src/error.rs:19-29): fallible calls return
+// bool and fill NetidxError.msg with a heap string released by nxg_error_free.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/nxg_codec.h"
+#include "nxg_internal.h"
+
+namespace {
+
+void set_err(NetidxError* err, const char* fmt, ...) {
+    if (!err) return;
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    free(err->msg);
+    err->msg = strdup(buf);
+}
+
+#define HIPCHK(expr)                                                                       \
+    do {                                                                                   \
+        hipError_t e_ = (expr);                                                            \
+        if (e_ != hipSuccess) {                                                            \
+            set_err(err, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__,  \
+                    __LINE__);                                                             \
+            return false;                                                                  \
+        }                                                                                  \
+    } while (0)
+
+constexpr int kStatusRing = 256;
+
+}  // namespace
+
+thread_local DevStatus* nxg_zero_slot = nullptr;
+
+struct NxgCtx {
+    int device = 0;
+    hipStream_t own = nullptr;
+    hipStream_t stream = nullptr;
+    int ncu = 0;
+    int grid_dec_f64 = 0, grid_dec_gen = 0, grid_enc_f64 = 0, grid_enc_gen = 0;
+    // status ring: one DevStatus per call, the whole ring re-zeroed once per lap
+    DevStatus* dst = nullptr;
+    DevStatus* hst = nullptr;  // pinned mirror
+    uint32_t calls = 0;
+    uint32_t epoch = 0;
+    uint64_t* tstat = nullptr;
+    size_t tstat_words = 0;
+    uint8_t* dframe = nullptr;
+    size_t dframe_cap = 0;
+    uint64_t* escratch = nullptr;
+    size_t escratch_words = 0;
+    NxgColumns dcols{};  // device staging columns for host-resident outputs/inputs
+    bool dcols_valid = false;
+    uint8_t* dheap = nullptr;
+    size_t dheap_cap = 0;
+    // in-flight async operations (completed in order by nxg_ctx_sync)
+    struct Pending {
+        int kind;  // 1 decode, 2 encode
+        int fast;
+        const uint8_t* frame;
+        uint64_t len;
+        NxgColumns* cols;
+        uint64_t* len_out;
+        DevStatus* st;
+        uint32_t slot;
+    };
+    std::vector<Pending> pending;
+};
+
+namespace {
+
+bool set_device(NxgCtx* c, NetidxError* err) {
+    HIPCHK(hipSetDevice(c->device));
+    return true;
+}
+
+// Next status slot + epoch for one call. Slot k is zeroed by block 0 of the call that used
+// slot k-128 (nxg_zero_slot), so at most kStatusRing/2 calls may be in flight.
+bool begin_call(NxgCtx* c, DevStatus** st, uint32_t* slot, NetidxError* err) {
+    *slot = c->calls % kStatusRing;
+    *st = c->dst + *slot;
+    nxg_zero_slot = c->dst + (c->calls + kStatusRing / 2) % kStatusRing;
+    c->calls++;
+    c->epoch++;
+    if (c->epoch > kEpochMax) {  // wrap: stale words could alias epoch 1 again
+        c->epoch = 1;
+        if (c->tstat) HIPCHK(hipMemsetAsync(c->tstat, 0, c->tstat_words * 8, c->stream));
+    }
+    return true;
+}
+
+bool ensure_tstat(NxgCtx* c, size_t words, NetidxError* err) {
+    if (words <= c->tstat_words) return true;
+    size_t n = std::max(words, c->tstat_words * 2);
+    n = std::max<size_t>(n, 4096);
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (c->tstat) HIPCHK(hipFree(c->tstat));
+    c->tstat = nullptr;
+    HIPCHK(hipMalloc(&c->tstat, n * 8));
+    HIPCHK(hipMemsetAsync(c->tstat, 0, n * 8, c->stream));
+    c->tstat_words = n;
+    return true;
+}
+
+bool ensure_escratch(NxgCtx* c, size_t words, NetidxError* err) {
+    if (words <= c->escratch_words) return true;
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (c->escratch) HIPCHK(hipFree(c->escratch));
+    c->escratch = nullptr;
+    size_t n = std::max<size_t>(words, 1024);
+    HIPCHK(hipMalloc(&c->escratch, n * 8));
+    c->escratch_words = n;
+    return true;
+}
+
+bool is_device_ptr(const void* p) {
+    if (!p) return false;
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeDevice;
+}
+
+ColsDesc desc_of(const NxgColumns* c) {
+    ColsDesc d{};
+    d.cap_rows = c->cap_rows;
+    d.cap_children = c->cap_children;
+    d.cap_ctl = c->cap_ctl;
+    d.n_rows = c->n_rows;
+    d.n_children = c->n_children;
+    d.n_ctl = c->n_ctl;
+    d.id = c->id;
+    d.tag = c->tag;
+    d.fixed = c->fixed;
+    d.aux = c->aux;
+    d.ctag = c->ctag;
+    d.cfixed = c->cfixed;
+    d.caux = c->caux;
+    d.ctl_row = c->ctl_row;
+    d.ctl_off = c->ctl_off;
+    d.ctl_len = c->ctl_len;
+    d.ctl_variant = c->ctl_variant;
+    return d;
+}
+
+bool cols_alloc_impl(uint32_t layout, uint64_t cr, uint64_t cc, uint64_t ck, uint32_t mem,
+                     NxgColumns* o, NetidxError* err) {
+    memset(o, 0, sizeof *o);
+    o->layout = layout;
+    o->mem = mem;
+    o->cap_rows = cr;
+    o->cap_children = cc;
+    o->cap_ctl = ck;
+    auto alloc = [&](void** p, size_t bytes) -> bool {
+        bytes = std::max<size_t>(bytes, 16);
+        hipError_t e = mem == NXG_MEM_DEVICE ? hipMalloc(p, bytes)
+                                             : hipHostMalloc(p, bytes, hipHostMallocDefault);
+        if (e != hipSuccess) {
+            set_err(err, "column allocation of %zu bytes failed: %s", bytes, hipGetErrorString(e));
+            return false;
+        }
+        return true;
+    };
+    if (!alloc((void**)&o->id, cr * 8) || !alloc((void**)&o->fixed, cr * 8)) return false;
+    if (layout == NXG_LAYOUT_MIXED) {
+        if (!alloc((void**)&o->tag, cr) || !alloc((void**)&o->aux, cr * 4) ||
+            !alloc((void**)&o->ctag, cc) || !alloc((void**)&o->cfixed, cc * 8) ||
+            !alloc((void**)&o->caux, cc * 4) || !alloc((void**)&o->ctl_row, ck * 8) ||
+            !alloc((void**)&o->ctl_off, ck * 8) || !alloc((void**)&o->ctl_len, ck * 4) ||
+            !alloc((void**)&o->ctl_variant, ck))
+            return false;
+    }
+    return true;
+}
+
+void cols_free_impl(NxgColumns* c) {
+    void* ps[] = {c->id, c->tag, c->fixed, c->aux, c->ctag, c->cfixed, c->caux,
+                  c->ctl_row, c->ctl_off, c->ctl_len, c->ctl_variant};
+    for (void* p : ps) {
+        if (!p) continue;
+        if (c->mem == NXG_MEM_DEVICE) (void)hipFree(p);
+        else (void)hipHostFree(p);
+    }
+    memset(c, 0, sizeof *c);
+}
+
+// device staging columns shaped like `like` (grown on demand)
+bool mixed_capable(const NxgColumns* c) {
+    return c->tag && c->aux && c->ctag && c->cfixed && c->caux && c->ctl_row && c->ctl_off &&
+           c->ctl_len && c->ctl_variant;
+}
+
+bool ensure_dcols(NxgCtx* c, const NxgColumns* like, NetidxError* err) {
+    const bool mixed = mixed_capable(like);
+    if (c->dcols_valid && c->dcols.cap_rows >= like->cap_rows &&
+        c->dcols.cap_children >= like->cap_children && c->dcols.cap_ctl >= like->cap_ctl &&
+        (c->dcols.layout == NXG_LAYOUT_MIXED || !mixed))
+        return true;
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (c->dcols_valid) cols_free_impl(&c->dcols);
+    c->dcols_valid = false;
+    if (!cols_alloc_impl(mixed ? NXG_LAYOUT_MIXED : NXG_LAYOUT_F64, like->cap_rows,
+                         like->cap_children, like->cap_ctl, NXG_MEM_DEVICE, &c->dcols, err))
+        return false;
+    c->dcols_valid = true;
+    return true;
+}
+
+// view of the device staging columns restricted to `like`'s layout and capacities
+NxgColumns staged_view(NxgCtx* c, const NxgColumns* like) {
+    NxgColumns v = c->dcols;
+    v.layout = like->layout;
+    v.cap_rows = like->cap_rows;
+    v.cap_children = like->cap_children;
+    v.cap_ctl = like->cap_ctl;
+    if (!mixed_capable(like)) {
+        v.tag = nullptr;
+        v.aux = nullptr;
+        v.ctag = nullptr;
+        v.cfixed = nullptr;
+        v.caux = nullptr;
+        v.ctl_row = nullptr;
+        v.ctl_off = nullptr;
+        v.ctl_len = nullptr;
+        v.ctl_variant = nullptr;
+    }
+    return v;
+}
+
+bool enqueue_dec_fast(NxgCtx* c, const uint8_t* f, uint64_t len, NxgColumns* out, DevStatus* st,
+                      NetidxError* err) {
+    const uint64_t nt = (len + f64dec::TILE - 1) / f64dec::TILE;
+    if (!ensure_tstat(c, nt, err)) return false;
+    HIPCHK(nxg_launch_dec_f64(f, len, out->id, out->fixed, out->cap_rows, c->tstat, c->epoch, st,
+                              c->grid_dec_f64, c->stream));
+    return true;
+}
+
+bool enqueue_dec_general(NxgCtx* c, const uint8_t* f, uint64_t len, NxgColumns* out,
+                         DevStatus* st, NetidxError* err) {
+    const uint64_t nt = (len + gdec::TILE - 1) / gdec::TILE;
+    if (!ensure_tstat(c, nt * gdec::SLOT_WORDS, err)) return false;
+    const ColsDesc d = desc_of(out);
+    HIPCHK(nxg_launch_dec_general(f, len, d, c->tstat, c->epoch, st, 1, c->grid_dec_gen,
+                                  c->stream));
+    return true;
+}
+
+// finish a device decode: read status, fall back to the general kernel if the f64 kernel
+// rejected the frame, fill the user-visible status
+bool finish_decode(NxgCtx* c, const uint8_t* f, uint64_t len, NxgColumns* out, int tried_fast,
+                   DevStatus* st, uint32_t slot, NxgStatus* ust, NetidxError* err) {
+    HIPCHK(hipMemcpyAsync(c->hst + slot, st, sizeof(DevStatus), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    DevStatus h = c->hst[slot];
+    if (tried_fast && len > 0 && h.fast_fail) {
+        DevStatus* st2;
+        uint32_t slot2;
+        if (!begin_call(c, &st2, &slot2, err)) return false;
+        if (!enqueue_dec_general(c, f, len, out, st2, err)) return false;
+        HIPCHK(hipMemcpyAsync(c->hst + slot2, st2, sizeof(DevStatus), hipMemcpyDeviceToHost,
+                              c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        h = c->hst[slot2];
+    }
+    if (h.timeout) {
+        set_err(err, "device look-back watchdog expired");
+        return false;
+    }
+    NxgStatus s{};
+    s.n_rows = h.n_rows;
+    s.n_children = h.n_children;
+    s.n_ctl = h.n_ctl;
+    s.n_heartbeat = h.n_heartbeat;
+    s.err_kind = (int32_t)h.err_kind;
+    s.err_offset = h.err_offset;
+    s.path = len == 0 ? 1 : h.path;
+    if (!s.err_kind && h.capacity) s.err_kind = NXG_CAPACITY;
+    if (!s.err_kind && !mixed_capable(out) && (h.nonf64 || s.n_ctl || s.n_children))
+        s.err_kind = NXG_NOT_F64;
+    if (ust) *ust = s;
+    out->n_rows = s.n_rows;
+    out->n_children = s.n_children;
+    out->n_ctl = s.n_ctl;
+    out->n_heartbeat = s.n_heartbeat;
+    return true;
+}
+
+bool copy_cols_d2h(NxgCtx* c, const NxgColumns* d, NxgColumns* h, NetidxError* err) {
+    const uint64_t nr = std::min(d->n_rows, h->cap_rows);
+    HIPCHK(hipMemcpyAsync(h->id, d->id, nr * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(h->fixed, d->fixed, nr * 8, hipMemcpyDeviceToHost, c->stream));
+    if (mixed_capable(h) && d->tag) {
+        const uint64_t nc = std::min(d->n_children, h->cap_children);
+        const uint64_t nk = std::min(d->n_ctl, h->cap_ctl);
+        HIPCHK(hipMemcpyAsync(h->tag, d->tag, nr, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipMemcpyAsync(h->aux, d->aux, nr * 4, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipMemcpyAsync(h->ctag, d->ctag, nc, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipMemcpyAsync(h->cfixed, d->cfixed, nc * 8, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipMemcpyAsync(h->caux, d->caux, nc * 4, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipMemcpyAsync(h->ctl_row, d->ctl_row, nk * 8, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipMemcpyAsync(h->ctl_off, d->ctl_off, nk * 8, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipMemcpyAsync(h->ctl_len, d->ctl_len, nk * 4, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipMemcpyAsync(h->ctl_variant, d->ctl_variant, nk, hipMemcpyDeviceToHost,
+                              c->stream));
+    }
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return true;
+}
+
+bool copy_cols_h2d(NxgCtx* c, const NxgColumns* h, NxgColumns* d, NetidxError* err) {
+    const uint64_t nr = h->n_rows, nc = h->n_children, nk = h->n_ctl;
+    HIPCHK(hipMemcpyAsync(d->id, h->id, nr * 8, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(d->fixed, h->fixed, nr * 8, hipMemcpyHostToDevice, c->stream));
+    if (h->layout == NXG_LAYOUT_MIXED) {
+        HIPCHK(hipMemcpyAsync(d->tag, h->tag, nr, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(hipMemcpyAsync(d->aux, h->aux, nr * 4, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(hipMemcpyAsync(d->ctag, h->ctag, nc, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(hipMemcpyAsync(d->cfixed, h->cfixed, nc * 8, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(hipMemcpyAsync(d->caux, h->caux, nc * 4, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(hipMemcpyAsync(d->ctl_row, h->ctl_row, nk * 8, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(hipMemcpyAsync(d->ctl_off, h->ctl_off, nk * 8, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(hipMemcpyAsync(d->ctl_len, h->ctl_len, nk * 4, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(hipMemcpyAsync(d->ctl_variant, h->ctl_variant, nk, hipMemcpyHostToDevice,
+                              c->stream));
+    }
+    d->n_rows = nr;
+    d->n_children = nc;
+    d->n_ctl = nk;
+    return true;
+}
+
+bool frame_to_device(NxgCtx* c, const uint8_t* frame, uint64_t len, const uint8_t** df,
+                     NetidxError* err) {
+    const bool dev = is_device_ptr(frame);
+    if (dev && ((uintptr_t)frame & 15) == 0) {
+        *df = frame;
+        return true;
+    }
+    if (c->dframe_cap < len + 16) {
+        HIPCHK(hipStreamSynchronize(c->stream));
+        if (c->dframe) HIPCHK(hipFree(c->dframe));
+        c->dframe = nullptr;
+        size_t n = std::max<size_t>(len + 16, 1 << 20);
+        HIPCHK(hipMalloc(&c->dframe, n));
+        c->dframe_cap = n;
+    }
+    if (len)
+        HIPCHK(hipMemcpyAsync(c->dframe, frame, len,
+                              dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, c->stream));
+    *df = c->dframe;
+    return true;
+}
+
+bool enqueue_encode(NxgCtx* c, const NxgColumns* in, const uint8_t* heap, uint8_t* out,
+                    uint64_t cap, DevStatus* st, NetidxError* err) {
+    if (in->layout == NXG_LAYOUT_F64) {
+        const uint64_t nt = (in->n_rows + f64enc::TILE - 1) / f64enc::TILE;
+        if (!ensure_tstat(c, nt, err)) return false;
+        HIPCHK(nxg_launch_enc_f64(in->id, in->fixed, in->n_rows, out, cap, c->tstat, c->epoch, st,
+                                  c->grid_enc_f64, c->stream));
+        return true;
+    }
+    const uint64_t nt = (in->n_rows + 255) / 256;
+    if (!ensure_tstat(c, nt, err)) return false;
+    if (!ensure_escratch(c, in->n_ctl ? in->n_ctl + 1 + in->n_rows : 1, err)) return false;
+    const ColsDesc d = desc_of(in);
+    HIPCHK(nxg_launch_enc_general(d, heap, out, cap, c->escratch, c->tstat, c->epoch, st,
+                                  c->grid_enc_gen, c->stream));
+    return true;
+}
+
+bool finish_encode(NxgCtx* c, const NxgColumns* in, DevStatus* st, uint32_t slot,
+                   uint64_t* len_out, uint64_t cap, bool wrote, NetidxError* err) {
+    HIPCHK(hipMemcpyAsync(c->hst + slot, st, sizeof(DevStatus), hipMemcpyDeviceToHost, c->stream));
+    uint64_t ctl_total = 0;
+    if (in->layout == NXG_LAYOUT_MIXED && in->n_ctl)
+        HIPCHK(hipMemcpyAsync(&ctl_total, c->escratch + in->n_ctl, 8, hipMemcpyDeviceToHost,
+                              c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    const DevStatus& h = c->hst[slot];
+    if (h.timeout) {
+        set_err(err, "device look-back watchdog expired");
+        return false;
+    }
+    if (h.err_kind) {
+        set_err(err, "encode failed: PackError kind %u", h.err_kind);
+        return false;
+    }
+    const uint64_t total = h.total_bytes + ctl_total;
+    if (len_out) *len_out = total;
+    if (wrote && (h.capacity || total > cap)) {
+        set_err(err, "output buffer too small: need %llu bytes, have %llu",
+                (unsigned long long)total, (unsigned long long)cap);
+        return false;
+    }
+    return true;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* nxg_version(void) { return "nxg 0.1.0 gfx950"; }
+
+void nxg_error_free(NetidxError* err) {
+    if (!err) return;
+    free(err->msg);
+    err->msg = nullptr;
+}
+
+NxgCtx* nxg_ctx_new(int device, NetidxError* err) {
+    NxgCtx* c = new NxgCtx();
+    c->device = device;
+    auto fail = [&](const char* what, hipError_t e) -> NxgCtx* {
+        set_err(err, "%s: %s", what, hipGetErrorString(e));
+        delete c;
+        return nullptr;
+    };
+    hipError_t e;
+    if ((e = hipSetDevice(device)) != hipSuccess) return fail("hipSetDevice", e);
+    hipDeviceProp_t prop;
+    if ((e = hipGetDeviceProperties(&prop, device)) != hipSuccess)
+        return fail("hipGetDeviceProperties", e);
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+        set_err(err, "nxg codec is built for gfx950 (MI355X); device %d is %s", device,
+                prop.gcnArchName);
+        delete c;
+        return nullptr;
+    }
+    c->ncu = prop.multiProcessorCount;
+    if ((e = hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking)) != hipSuccess)
+        return fail("hipStreamCreate", e);
+    c->stream = c->own;
+    // persistent grids: every workgroup must be co-resident (look-back progress); keep one
+    // block of margin under the occupancy answer (MI355X_MICROARCH.md residency notes)
+    auto grid = [&](int occ) { return c->ncu * std::max(1, occ > 2 ? occ - 1 : occ); };
+    c->grid_dec_f64 = grid(nxg_occupancy_dec_f64());
+    c->grid_dec_gen = grid(nxg_occupancy_dec_general());
+    c->grid_enc_f64 = grid(nxg_occupancy_enc_f64());
+    c->grid_enc_gen = grid(nxg_occupancy_enc_general());
+    if ((e = hipMalloc(&c->dst, sizeof(DevStatus) * kStatusRing)) != hipSuccess)
+        return fail("hipMalloc(status)", e);
+    if ((e = hipMemset(c->dst, 0, sizeof(DevStatus) * kStatusRing)) != hipSuccess)
+        return fail("hipMemset(status)", e);
+    if ((e = hipHostMalloc(&c->hst, sizeof(DevStatus) * kStatusRing, hipHostMallocDefault)) !=
+        hipSuccess)
+        return fail("hipHostMalloc(status)", e);
+    return c;
+}
+
+void nxg_ctx_destroy(NxgCtx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->dcols_valid) cols_free_impl(&c->dcols);
+    if (c->tstat) (void)hipFree(c->tstat);
+    if (c->dframe) (void)hipFree(c->dframe);
+    if (c->escratch) (void)hipFree(c->escratch);
+    if (c->dheap) (void)hipFree(c->dheap);
+    if (c->dst) (void)hipFree(c->dst);
+    if (c->hst) (void)hipHostFree(c->hst);
+    if (c->own) (void)hipStreamDestroy(c->own);
+    delete c;
+}
+
+bool nxg_ctx_set_stream(NxgCtx* c, void* s, NetidxError* err) {
+    if (!c) {
+        set_err(err, "null ctx");
+        return false;
+    }
+    if (!set_device(c, err)) return false;
+    HIPCHK(hipStreamSynchronize(c->stream));
+    c->stream = s ? (hipStream_t)s : c->own;
+    return true;
+}
+
+void* nxg_ctx_stream(NxgCtx* c) { return c ? (void*)c->stream : nullptr; }
+
+bool nxg_columns_alloc(NxgCtx* c, uint32_t layout, uint64_t cap_rows, uint64_t cap_children,
+                       uint64_t cap_ctl, uint32_t mem, NxgColumns* out, NetidxError* err) {
+    if (!c || !out) {
+        set_err(err, "null argument");
+        return false;
+    }
+    if (layout != NXG_LAYOUT_F64 && layout != NXG_LAYOUT_MIXED) {
+        set_err(err, "unknown layout %u", layout);
+        return false;
+    }
+    if (mem != NXG_MEM_DEVICE && mem != NXG_MEM_HOST) {
+        set_err(err, "unknown memory kind %u", mem);
+        return false;
+    }
+    if (!set_device(c, err)) return false;
+    if (!cols_alloc_impl(layout, cap_rows, cap_children, cap_ctl, mem, out, err)) {
+        cols_free_impl(out);
+        return false;
+    }
+    return true;
+}
+
+void nxg_columns_free(NxgCtx* c, NxgColumns* cols) {
+    if (!cols) return;
+    if (c) (void)hipSetDevice(c->device);
+    cols_free_impl(cols);
+}
+
+bool nxg_decode_updates(NxgCtx* c, const uint8_t* frame, uint64_t len, NxgColumns* out,
+                        uint32_t flags, NxgStatus* ust, NetidxError* err) {
+    if (!c || !out || (!frame && len)) {
+        set_err(err, "null argument");
+        return false;
+    }
+    if (!c->pending.empty()) {
+        set_err(err, "an async operation is pending on this ctx; call nxg_ctx_sync first");
+        return false;
+    }
+    if (len >= (1ull << 40)) {
+        set_err(err, "frame too large (%llu bytes)", (unsigned long long)len);
+        return false;
+    }
+    if (!set_device(c, err)) return false;
+    const uint8_t* df;
+    if (!frame_to_device(c, frame, len, &df, err)) return false;
+    NxgColumns* target = out;
+    NxgColumns view;
+    const bool host_out = out->mem == NXG_MEM_HOST;
+    if (host_out) {
+        if (!ensure_dcols(c, out, err)) return false;
+        view = staged_view(c, out);
+        target = &view;
+    }
+    DevStatus* st;
+    uint32_t slot;
+    if (!begin_call(c, &st, &slot, err)) return false;
+    const int fast = !(flags & NXG_DECODE_HINT_MIXED);
+    if (fast) {
+        if (!enqueue_dec_fast(c, df, len, target, st, err)) return false;
+    } else {
+        if (!enqueue_dec_general(c, df, len, target, st, err)) return false;
+    }
+    NxgStatus s;
+    if (!finish_decode(c, df, len, target, fast, st, slot, &s, err)) return false;
+    // result layout: F64 when the homogeneous kernel produced it (tag/aux not written)
+    out->layout = (!mixed_capable(out) || s.path == 1) ? NXG_LAYOUT_F64 : NXG_LAYOUT_MIXED;
+    if (host_out) {
+        target->n_rows = s.n_rows;
+        target->n_children = s.n_children;
+        target->n_ctl = s.n_ctl;
+        if (s.err_kind == 0) {
+            NxgColumns hv = *out;
+            if (s.path == 1) hv.tag = nullptr;  // only id/fixed were produced
+            if (!copy_cols_d2h(c, target, &hv, err)) return false;
+        }
+    }
+    out->n_rows = s.n_rows;
+    out->n_children = s.n_children;
+    out->n_ctl = s.n_ctl;
+    out->n_heartbeat = s.n_heartbeat;
+    if (ust) *ust = s;
+    return true;
+}
+
+bool nxg_decode_updates_async(NxgCtx* c, const uint8_t* dframe, uint64_t len, NxgColumns* dout,
+                              uint32_t flags, NetidxError* err) {
+    if (!c || !dout || (!dframe && len)) {
+        set_err(err, "null argument");
+        return false;
+    }
+    if (c->pending.size() >= kStatusRing / 2) {
+        set_err(err, "too many in-flight async calls (max %d); call nxg_ctx_sync", kStatusRing / 2);
+        return false;
+    }
+    if (dout->mem != NXG_MEM_DEVICE || ((uintptr_t)dframe & 15)) {
+        set_err(err, "async decode needs device columns and a 16-byte aligned device frame");
+        return false;
+    }
+    DevStatus* st;
+    uint32_t slot;
+    if (!begin_call(c, &st, &slot, err)) return false;
+    const int fast = !(flags & NXG_DECODE_HINT_MIXED);
+    if (fast ? !enqueue_dec_fast(c, dframe, len, dout, st, err)
+             : !enqueue_dec_general(c, dframe, len, dout, st, err))
+        return false;
+    c->pending.push_back({1, fast, dframe, len, dout, nullptr, st, slot});
+    return true;
+}
+
+// Completes every in-flight call in order; the status returned is the last call's (the first
+// failing call's, if one failed).
+bool nxg_ctx_sync(NxgCtx* c, NxgStatus* ust, NetidxError* err) {
+    if (!c) {
+        set_err(err, "null ctx");
+        return false;
+    }
+    if (!set_device(c, err)) return false;
+    std::vector<NxgCtx::Pending> ps;
+    ps.swap(c->pending);
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (ust) memset(ust, 0, sizeof *ust);
+    bool reported = false;
+    for (auto& p : ps) {
+        if (p.kind == 1) {
+            NxgStatus s;
+            if (!finish_decode(c, p.frame, p.len, p.cols, p.fast, p.st, p.slot, &s, err))
+                return false;
+            p.cols->layout =
+                (!mixed_capable(p.cols) || s.path == 1) ? NXG_LAYOUT_F64 : NXG_LAYOUT_MIXED;
+            if (ust && !reported) *ust = s;
+            if (s.err_kind) reported = true;
+        } else {
+            NxgColumns dummy{};
+            dummy.layout = NXG_LAYOUT_F64;
+            if (!finish_encode(c, p.cols ? p.cols : &dummy, p.st, p.slot, p.len_out, ~0ull, false,
+                               err))
+                return false;
+        }
+    }
+    return true;
+}
+
+static bool encode_impl(NxgCtx* c, const NxgColumns* in, const uint8_t* heap, uint8_t* out,
+                        uint64_t cap, uint64_t* len_out, NetidxError* err) {
+    if (!c || !in) {
+        set_err(err, "null argument");
+        return false;
+    }
+    if (!c->pending.empty()) {
+        set_err(err, "an async operation is pending on this ctx; call nxg_ctx_sync first");
+        return false;
+    }
+    if (!set_device(c, err)) return false;
+    const bool host = in->mem == NXG_MEM_HOST || !is_device_ptr(in->id);
+    const NxgColumns* din = in;
+    NxgColumns view;
+    const uint8_t* dheap = heap;
+    uint8_t* dout = out;
+    uint64_t heap_len = 0;
+    if (host) {
+        if (!ensure_dcols(c, in, err)) return false;
+        view = staged_view(c, in);
+        if (!copy_cols_h2d(c, in, &view, err)) return false;
+        din = &view;
+        // the heap extent: everything referenced by offsets; callers pass the frame/heap whose
+        // length is not part of the ABI, so stage the maximum referenced byte
+        if (heap && in->layout == NXG_LAYOUT_MIXED) {
+            uint64_t hi = 0;
+            auto upd = [&](uint8_t t, uint64_t f, uint32_t a) {
+                if (t == 12 || t == 13 || t == 18 || t == 27) hi = std::max<uint64_t>(hi, f + a);
+                if (t == 20) hi = std::max<uint64_t>(hi, f + 16);
+            };
+            for (uint64_t i = 0; i < in->n_rows; i++) upd(in->tag[i], in->fixed[i], in->aux[i]);
+            for (uint64_t i = 0; i < in->n_children; i++)
+                upd(in->ctag[i], in->cfixed[i], in->caux[i]);
+            for (uint64_t i = 0; i < in->n_ctl; i++)
+                hi = std::max<uint64_t>(hi, in->ctl_off[i] + in->ctl_len[i]);
+            heap_len = hi;
+            if (c->dheap_cap < heap_len + 16) {
+                HIPCHK(hipStreamSynchronize(c->stream));
+                if (c->dheap) HIPCHK(hipFree(c->dheap));
+                c->dheap = nullptr;
+                size_t n = std::max<size_t>(heap_len + 16, 1 << 20);
+                HIPCHK(hipMalloc(&c->dheap, n));
+                c->dheap_cap = n;
+            }
+            if (heap_len)
+                HIPCHK(hipMemcpyAsync(c->dheap, heap, heap_len, hipMemcpyHostToDevice, c->stream));
+            dheap = c->dheap;
+        }
+        dout = nullptr;
+    }
+    DevStatus* st;
+    uint32_t slot;
+    uint64_t total = 0;
+    // pass 1 (sizing) when writing to a host buffer; a device buffer is written directly
+    if (host && out) {
+        if (!begin_call(c, &st, &slot, err)) return false;
+        if (!enqueue_encode(c, din, dheap, nullptr, 0, st, err)) return false;
+        if (!finish_encode(c, din, st, slot, &total, 0, false, err)) return false;
+        if (total > cap) {
+            set_err(err, "output buffer too small: need %llu bytes, have %llu",
+                    (unsigned long long)total, (unsigned long long)cap);
+            return false;
+        }
+        if (c->dframe_cap < total + 16) {
+            HIPCHK(hipStreamSynchronize(c->stream));
+            if (c->dframe) HIPCHK(hipFree(c->dframe));
+            c->dframe = nullptr;
+            size_t n = std::max<size_t>(total + 16, 1 << 20);
+            HIPCHK(hipMalloc(&c->dframe, n));
+            c->dframe_cap = n;
+        }
+        dout = c->dframe;
+        cap = total;
+    }
+    if (!begin_call(c, &st, &slot, err)) return false;
+    if (!enqueue_encode(c, din, dheap, dout, out ? cap : 0, st, err)) return false;
+    if (!finish_encode(c, din, st, slot, &total, cap, dout != nullptr, err)) return false;
+    if (host && out && total) {
+        HIPCHK(hipMemcpyAsync(out, dout, total, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+    }
+    if (len_out) *len_out = total;
+    return true;
+}
+
+bool nxg_encoded_len(NxgCtx* c, const NxgColumns* in, const uint8_t* heap, uint64_t* len_out,
+                     NetidxError* err) {
+    return encode_impl(c, in, heap, nullptr, 0, len_out, err);
+}
+
+bool nxg_encode_updates(NxgCtx* c, const NxgColumns* in, const uint8_t* heap, uint8_t* out,
+                        uint64_t cap, uint64_t* len_out, NetidxError* err) {
+    if (!out) {
+        set_err(err, "null output buffer");
+        return false;
+    }
+    return encode_impl(c, in, heap, out, cap, len_out, err);
+}
+
+bool nxg_encode_updates_async(NxgCtx* c, const NxgColumns* din, const uint8_t* dheap,
+                              uint8_t* dout, uint64_t cap, uint64_t* len_out, NetidxError* err) {
+    if (!c || !din || !dout) {
+        set_err(err, "null argument");
+        return false;
+    }
+    if (c->pending.size() >= kStatusRing / 2) {
+        set_err(err, "too many in-flight async calls (max %d); call nxg_ctx_sync", kStatusRing / 2);
+        return false;
+    }
+    // the control-span prefix lives in shared ctx scratch: one such encode in flight at a time
+    for (auto& p : c->pending)
+        if (p.kind == 2 && din->layout == NXG_LAYOUT_MIXED && din->n_ctl) {
+            set_err(err, "sync the previous encode before an async encode with control spans");
+            return false;
+        }
+    DevStatus* st;
+    uint32_t slot;
+    if (!begin_call(c, &st, &slot, err)) return false;
+    if (!enqueue_encode(c, din, dheap, dout, cap, st, err)) return false;
+    c->pending.push_back({2, 0, nullptr, 0, const_cast<NxgColumns*>(din), len_out, st, slot});
+    return true;
+}
+
+// ---- host framing ------------------------------------------------------------------------
+
+// WriteChannel::queue_send (channel.rs:177-202) + try_flush (237-257). `boundries` holds chunk
+// LENGTHS. A new boundary is recorded when (buf_len - last boundary length) + len > MAX_BATCH,
+// i.e. the comparison uses the last chunk's length, not the sum (channel.rs:187-190).
+int64_t nxg_frame_split(const uint64_t* msg_len, uint64_t n_msgs, uint64_t* chunk_len_out,
+                        uint64_t cap_chunks) {
+    const uint64_t MAX_BATCH = 0x3FFFFFFF;
+    uint64_t buf_len = 0, sum_b = 0, last_b = 0, nb = 0;
+    for (uint64_t i = 0; i < n_msgs; i++) {
+        const uint64_t len = msg_len[i];
+        if (len > MAX_BATCH) return -1;
+        if ((buf_len - (nb ? last_b : 0)) + len > MAX_BATCH) {
+            const uint64_t b = buf_len - sum_b;
+            if (nb >= cap_chunks) return -1;
+            chunk_len_out[nb++] = b;
+            sum_b += b;
+            last_b = b;
+        }
+        buf_len += len;
+    }
+    if (buf_len > sum_b) {
+        if (nb >= cap_chunks) return -1;
+        chunk_len_out[nb++] = buf_len - sum_b;
+    }
+    return (int64_t)nb;
+}
+
+// flush_buf (channel.rs:107-126)
+void nxg_frame_header(uint32_t payload_len, bool encrypted, uint8_t out[4]) {
+    const uint32_t v = encrypted ? (payload_len | 0x80000000u) : payload_len;
+    out[0] = (uint8_t)(v >> 24);
+    out[1] = (uint8_t)(v >> 16);
+    out[2] = (uint8_t)(v >> 8);
+    out[3] = (uint8_t)v;
+}
+
+// read_task (channel.rs:389-398): hdr > LEN_MASK => encrypted, len = hdr & LEN_MASK
+uint32_t nxg_frame_parse_header(const uint8_t* buf, uint64_t avail, uint32_t* payload_len,
+                                bool* encrypted) {
+    if (avail < 4) return 0;
+    const uint32_t hdr = ((uint32_t)buf[0] << 24) | ((uint32_t)buf[1] << 16) |
+                         ((uint32_t)buf[2] << 8) | buf[3];
+    *encrypted = hdr > 0x7FFFFFFFu;
+    *payload_len = hdr & 0x7FFFFFFFu;
+    return 4;
+}
+
+}  // extern "C"

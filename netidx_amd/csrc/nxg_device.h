@@ -1,0 +1,135 @@
+// nxg_device.h -- device-side primitives shared by the gfx950 codec kernels.
+//
+// These are re-statements of the reference's scalar rules, written for the device:
+//   varint_len            netidx-core/src/pack.rs:472-474
+//   decode_varint         pack.rs:504-520 (reads <= 10 bytes from the Take-limited chunk)
+//   len_wrapped_len       pack.rs:522-525
+//   zigzag                pack.rs:488-502
+//   str::from_utf8        pack.rs:462
+//   DateTime::from_timestamp validity  pack.rs:1572 (chrono >= 0.4.35 rules)
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "nxg_internal.h"
+
+#define NXG_DEV __device__ __forceinline__
+
+// ---- inter-workgroup hand-off (MI355X_MICROARCH.md "Valid forms"): 8-byte granules written
+// with one agent-scope relaxed atomic store (sc1) and polled with agent-scope relaxed loads.
+NXG_DEV uint64_t ld_agent(const uint64_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+NXG_DEV uint32_t ld_agent32(const uint32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+NXG_DEV void st_agent(uint64_t* p, uint64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// drain this wave's outstanding stores before a flag store (guide: asm wait, never builtin)
+NXG_DEV void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// watchdog: 100 MHz s_memrealtime, bound every spin (deadlock => NXG_TIMEOUT, never a hang)
+NXG_DEV uint64_t rt_now() { return __builtin_amdgcn_s_memrealtime(); }
+constexpr uint64_t kSpinTicks = 200ull * 1000 * 1000;  // 2 s at 100 MHz
+
+NXG_DEV uint32_t vl64(uint64_t v) {
+    uint32_t hb = 63u - (uint32_t)__clzll((long long)(v | 1ull));
+    return (hb * 9u + 73u) >> 6;
+}
+NXG_DEV uint64_t lwlen(uint64_t n) { return n + vl64(n + vl64(n)); }
+NXG_DEV uint32_t zz32(int32_t n) { return ((uint32_t)n << 1) ^ (uint32_t)(n >> 31); }
+NXG_DEV uint64_t zz64(int64_t n) { return ((uint64_t)n << 1) ^ (uint64_t)(n >> 63); }
+
+NXG_DEV uint32_t alignbyte(uint32_t hi, uint32_t lo, uint32_t s) {
+    return __builtin_amdgcn_alignbyte(hi, lo, s);
+}
+NXG_DEV uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
+
+// ---- wave/block scans (wave64) -----------------------------------------------------------
+NXG_DEV uint32_t lane_id() { return __lane_id(); }
+
+template <typename T>
+NXG_DEV T wave_incl_scan(T v) {
+    const uint32_t l = lane_id();
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        T o = __shfl_up(v, d, 64);
+        if (l >= (uint32_t)d) v += o;
+    }
+    return v;
+}
+
+template <typename T>
+NXG_DEV T wave_sum(T v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+    return v;
+}
+
+// exclusive scan over a 256-thread block; `tmp` = 4 (or more) T in LDS. Returns the exclusive
+// prefix, sets *total. Contains __syncthreads().
+template <typename T, int NT>
+NXG_DEV T block_excl_scan(T v, T* tmp, T* total) {
+    const uint32_t tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+    T inc = wave_incl_scan(v);
+    if (l == 63) tmp[w] = inc;
+    __syncthreads();
+    T wbase = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < NT / 64; i++) {
+        T x = tmp[i];
+        if ((uint32_t)i < w) wbase += x;
+        tot += x;
+    }
+    __syncthreads();
+    *total = tot;
+    return wbase + inc - v;
+}
+
+// ---- UTF-8 (std::str::from_utf8) over an arbitrary byte source -----------------------------
+template <typename Src>
+NXG_DEV bool utf8_valid(const Src& s, uint64_t p, uint64_t n) {
+    uint64_t i = 0;
+    while (i < n) {
+        uint32_t c = s.byte(p + i);
+        if (c < 0x80) {
+            i++;
+            continue;
+        }
+        uint32_t lo = 0x80, hi = 0xBF, need;
+        if (c >= 0xC2 && c <= 0xDF) need = 1;
+        else if (c == 0xE0) { need = 2; lo = 0xA0; }
+        else if ((c >= 0xE1 && c <= 0xEC) || c == 0xEE || c == 0xEF) need = 2;
+        else if (c == 0xED) { need = 2; hi = 0x9F; }
+        else if (c == 0xF0) { need = 3; lo = 0x90; }
+        else if (c >= 0xF1 && c <= 0xF3) need = 3;
+        else if (c == 0xF4) { need = 3; hi = 0x8F; }
+        else return false;
+        if (i + need >= n) return false;
+        uint32_t c1 = s.byte(p + i + 1);
+        if (c1 < lo || c1 > hi) return false;
+        for (uint32_t k = 2; k <= need; k++)
+            if ((s.byte(p + i + k) & 0xC0) != 0x80) return false;
+        i += need + 1;
+    }
+    return true;
+}
+
+// ---- chrono DateTime::from_timestamp validity ----------------------------------------------
+// days-from-CE bounds of NaiveDate::MIN (-262143-01-01) and MAX (262142-12-31)
+constexpr int64_t kMinDaysCE = -95746129;  // days_from_civil(-262143,1,1) + 719163
+constexpr int64_t kMaxDaysCE = 95745399;   // days_from_civil(262142,12,31) + 719163
+NXG_DEV bool datetime_valid(int64_t secs, uint32_t ns) {
+    int64_t days = secs / 86400;
+    int64_t sod = secs % 86400;
+    if (sod < 0) {
+        sod += 86400;
+        days -= 1;
+    }
+    int64_t dce = days + 719163;
+    if (dce < kMinDaysCE || dce > kMaxDaysCE) return false;
+    if (ns >= 2000000000u) return false;
+    if (ns >= 1000000000u && (sod % 60) != 59) return false;
+    return true;
+}

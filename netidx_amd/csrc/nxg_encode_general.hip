@@ -1,0 +1,307 @@
+// nxg_encode_general.hip -- encode arbitrary columns (rows + children + control spans) to wire.
+//
+// Replaces handle_updates -> queue_send (netidx/src/publisher/server.rs:610-612,
+// netidx/src/channel.rs:177-202). Each row becomes
+//     varint(L) 04 varint(id) Value            L = lw(1 + vl(id) + |Value|)
+// with Value::encode (netidx-value/src/lib.rs:361-468), ValArray (array.rs:583-593), Map
+// (pack.rs:1212-1223) and Abstract (abstract_type.rs:272-278). Control messages (ctl) are
+// copied verbatim from the heap and placed before row ctl_row[k], in order.
+//
+// Three launches:
+// 1. ctl_scan: prefix of the control spans' lengths. One workgroup; skipped when there are no
+//    control messages.
+// 2. rows: each lane encodes one row. The launch does a block scan plus a decoupled look-back
+//    over byte counts. Each row's position is its rows-prefix plus the ctl bytes that precede
+//    it; the latter is found by binary search over ctl_row. The row is then written straight
+//    to the output.
+// 3. ctl_write: copies each control span to its position.
+#include "nxg_device.h"
+
+namespace {
+
+constexpr int TPB = 256;
+constexpr uint64_t kMaxVec = 2ull * 1024 * 1024 * 1024;
+
+struct Slot {
+    uint32_t tag;
+    uint64_t fixed;
+    uint32_t aux;
+};
+
+NXG_DEV Slot get_slot(const ColsDesc& c, bool row, uint64_t i) {
+    if (row) return Slot{c.tag[i], c.fixed[i], c.aux[i]};
+    return Slot{c.ctag[i], c.cfixed[i], c.caux[i]};
+}
+
+// |Value| for the value in (row?, slot), children included; 0 => error (*err set)
+NXG_DEV uint64_t value_len(const ColsDesc& c, bool row, uint64_t slot, uint32_t* err) {
+    uint64_t frem[NXG_MAX_DEPTH + 2], fslot[NXG_MAX_DEPTH + 2];
+    int top = -1, depth = 0;
+    bool is_row = row;
+    uint64_t cur = slot, total = 0;
+    for (;;) {
+        if (depth > NXG_MAX_DEPTH) {
+            *err = 6;
+            return 0;
+        }
+        const Slot s = get_slot(c, is_row, cur);
+        uint64_t kids = 0;
+        switch (s.tag) {
+        case 0: case 2: case 8: total += 5; break;
+        case 1: total += 1 + vl64((uint32_t)s.fixed); break;
+        case 3: total += 1 + vl64(zz32((int32_t)(uint32_t)s.fixed)); break;
+        case 4: case 6: case 9: total += 9; break;
+        case 5: total += 1 + vl64(s.fixed); break;
+        case 7: total += 1 + vl64(zz64((int64_t)s.fixed)); break;
+        case 10: case 11: total += 13; break;
+        case 12: case 13: case 18: total += 1 + vl64(s.aux) + s.aux; break;
+        case 14: case 15: case 16: total += 1; break;
+        case 19:
+        case 21:
+            if ((uint64_t)s.aux * (s.tag == 19 ? 16 : 32) > kMaxVec) {  // encode guard
+                *err = 2;
+                return 0;
+            }
+            total += 1 + vl64(s.aux);
+            kids = s.tag == 19 ? s.aux : 2ull * s.aux;
+            break;
+        case 20: total += 17; break;
+        case 22: total += 1; kids = 1; break;
+        case 23: case 24: total += 2; break;
+        case 25: case 26: total += 3; break;
+        case 27: total += 1 + lwlen(s.aux); break;
+        default:
+            *err = 1;
+            return 0;
+        }
+        if (kids) {
+            ++top;
+            frem[top] = kids;
+            fslot[top] = s.fixed;
+        }
+        while (top >= 0 && frem[top] == 0) top--;
+        if (top < 0) return total;
+        frem[top]--;
+        cur = fslot[top]++;
+        is_row = false;
+        depth = top + 1;
+    }
+}
+
+struct Out {
+    uint8_t* o;
+    uint64_t p;
+    NXG_DEV void b(uint32_t x) { o[p++] = (uint8_t)x; }
+    NXG_DEV void be(uint64_t v, int n) {
+        for (int i = n - 1; i >= 0; i--) o[p++] = (uint8_t)(v >> (8 * i));
+    }
+    NXG_DEV void var(uint64_t v) {
+        while (v >= 0x80) {
+            o[p++] = (uint8_t)((v & 0x7f) | 0x80);
+            v >>= 7;
+        }
+        o[p++] = (uint8_t)v;
+    }
+    NXG_DEV void copy(const uint8_t* src, uint64_t n) {
+        for (uint64_t i = 0; i < n; i++) o[p++] = src[i];
+    }
+};
+
+NXG_DEV void value_write(const ColsDesc& c, const uint8_t* heap, bool row, uint64_t slot, Out& w) {
+    uint64_t frem[NXG_MAX_DEPTH + 2], fslot[NXG_MAX_DEPTH + 2];
+    int top = -1;
+    bool is_row = row;
+    uint64_t cur = slot;
+    for (;;) {
+        const Slot s = get_slot(c, is_row, cur);
+        uint64_t kids = 0;
+        w.b(s.tag);
+        switch (s.tag) {
+        case 0: case 2: case 8: w.be(s.fixed, 4); break;
+        case 1: w.var((uint32_t)s.fixed); break;
+        case 3: w.var(zz32((int32_t)(uint32_t)s.fixed)); break;
+        case 4: case 6: case 9: w.be(s.fixed, 8); break;
+        case 5: w.var(s.fixed); break;
+        case 7: w.var(zz64((int64_t)s.fixed)); break;
+        case 10: case 11: w.be(s.fixed, 8); w.be(s.aux, 4); break;
+        case 12: case 13: case 18: w.var(s.aux); w.copy(heap + s.fixed, s.aux); break;
+        case 19: case 21:
+            w.var(s.aux);
+            kids = s.tag == 19 ? s.aux : 2ull * s.aux;
+            break;
+        case 20: w.copy(heap + s.fixed, 16); break;
+        case 22: kids = 1; break;
+        case 23: case 24: w.be(s.fixed, 1); break;
+        case 25: case 26: w.be(s.fixed, 2); break;
+        case 27: w.var(lwlen(s.aux)); w.copy(heap + s.fixed, s.aux); break;
+        default: break;
+        }
+        if (kids) {
+            ++top;
+            frem[top] = kids;
+            fslot[top] = s.fixed;
+        }
+        while (top >= 0 && frem[top] == 0) top--;
+        if (top < 0) return;
+        frem[top]--;
+        cur = fslot[top]++;
+        is_row = false;
+    }
+}
+
+// number of ctl entries with ctl_row <= r (ctl_row is non-decreasing)
+NXG_DEV uint64_t ctl_upto(const uint64_t* ctl_row, uint64_t n_ctl, uint64_t r) {
+    uint64_t lo = 0, hi = n_ctl;
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (ctl_row[mid] <= r) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+}  // namespace
+
+// exclusive prefix of ctl_len into ctl_pre[0..n_ctl] (one workgroup)
+__global__ __launch_bounds__(TPB) void nxg_enc_ctl_scan_kernel(ColsDesc c, uint64_t* ctl_pre) {
+    __shared__ uint64_t tmp[4];
+    uint64_t carry = 0;
+    for (uint64_t b = 0; b < c.n_ctl; b += TPB) {
+        const uint64_t i = b + threadIdx.x;
+        const uint64_t v = i < c.n_ctl ? c.ctl_len[i] : 0;
+        uint64_t tot;
+        const uint64_t ex = block_excl_scan<uint64_t, TPB>(v, tmp, &tot);
+        if (i < c.n_ctl) ctl_pre[i] = carry + ex;
+        carry += tot;
+    }
+    if (threadIdx.x == 0) ctl_pre[c.n_ctl] = carry;
+}
+
+__global__ __launch_bounds__(TPB) void nxg_enc_rows_kernel(
+    ColsDesc c, const uint8_t* __restrict__ heap, uint8_t* __restrict__ out, uint64_t cap,
+    const uint64_t* __restrict__ ctl_pre, uint64_t* __restrict__ row_off,
+    uint64_t* __restrict__ tstat, uint32_t ntiles, uint32_t epoch, DevStatus* __restrict__ st,
+    DevStatus* zst) {
+    zero_status(zst);
+    __shared__ uint64_t tmp[4];
+    __shared__ uint64_t sh_base;
+    const uint32_t tid = threadIdx.x, lane = tid & 63;
+    const uint64_t n = c.n_rows;
+    for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const uint64_t r = (uint64_t)tile * TPB + tid;
+        uint64_t L = 0;
+        uint32_t err = 0;
+        if (r < n) {
+            const uint64_t vlen = value_len(c, true, r, &err);
+            L = err ? 0 : lwlen(1 + vl64(c.id[r]) + vlen);
+        }
+        if (err) atomicMax(&st->err_kind, err);
+        uint64_t tot;
+        const uint64_t off = block_excl_scan<uint64_t, TPB>(L, tmp, &tot);
+        if (tid == 0) st_agent(&tstat[tile], lb_word(tile == 0 ? kFlagInc : kFlagAgg, epoch, tot));
+        if (tid < 64) {
+            uint64_t base = 0;
+            if (tile != 0) {
+                int64_t pred = (int64_t)tile - 1;
+                const uint64_t t_start = rt_now();
+                bool give_up = false;
+                for (;;) {
+                    const int64_t idx = pred - (int64_t)lane;
+                    uint64_t s = idx >= 0 ? ld_agent(&tstat[idx]) : lb_word(kFlagInc, epoch, 0);
+                    while (!__all(lb_flag(s, epoch) != 0)) {
+                        __builtin_amdgcn_s_sleep(1);
+                        if (lb_flag(s, epoch) == 0) s = ld_agent(&tstat[idx]);
+                        if (rt_now() - t_start > kSpinTicks) {
+                            give_up = true;
+                            break;
+                        }
+                    }
+                    if (give_up) break;
+                    const uint64_t inc = __ballot(lb_flag(s, epoch) == kFlagInc);
+                    if (inc) {
+                        const uint32_t first = (uint32_t)__builtin_ctzll(inc);
+                        base += wave_sum<uint64_t>(lane <= first ? (s & kValMask) : 0ull);
+                        break;
+                    }
+                    base += wave_sum<uint64_t>(s & kValMask);
+                    pred -= 64;
+                }
+                if (give_up && lane == 0) atomicOr(&st->timeout, 1u);
+                if (lane == 0) st_agent(&tstat[tile], lb_word(kFlagInc, epoch, base + tot));
+            }
+            if (lane == 0) sh_base = base;
+        }
+        __syncthreads();
+        const uint64_t rpos = sh_base + off;  // rows-only prefix
+        if (r < n && !err) {
+            if (row_off) row_off[r] = rpos;
+            uint64_t pos = rpos;
+            if (c.n_ctl) pos += ctl_pre[ctl_upto(c.ctl_row, c.n_ctl, r)];
+            if (out) {
+                if (pos + L > cap) {
+                    atomicOr(&st->capacity, 1u);
+                } else {
+                    Out w{out, pos};
+                    w.var(L);
+                    w.b(4);
+                    w.var(c.id[r]);
+                    value_write(c, heap, true, r, w);
+                }
+            }
+        }
+        if (tile == ntiles - 1 && tid == 0) {
+            st->total_bytes = sh_base + tot;  // rows only; ctl bytes added by the host
+            st->n_rows = n;
+        }
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(TPB) void nxg_enc_ctl_write_kernel(
+    ColsDesc c, const uint8_t* __restrict__ heap, uint8_t* __restrict__ out, uint64_t cap,
+    const uint64_t* __restrict__ ctl_pre, const uint64_t* __restrict__ row_off,
+    const DevStatus* __restrict__ st, DevStatus* stw) {
+    const uint64_t rows_total = st->total_bytes;
+    for (uint64_t k = (uint64_t)blockIdx.x * TPB + threadIdx.x; k < c.n_ctl;
+         k += (uint64_t)gridDim.x * TPB) {
+        const uint64_t r = c.ctl_row[k];
+        const uint64_t rb = r < c.n_rows ? row_off[r] : rows_total;
+        const uint64_t pos = rb + ctl_pre[k];
+        const uint64_t len = c.ctl_len[k];
+        if (pos + len > cap) {
+            atomicOr(&stw->capacity, 1u);
+            continue;
+        }
+        const uint8_t* src = heap + c.ctl_off[k];
+        for (uint64_t i = 0; i < len; i++) out[pos + i] = src[i];
+    }
+}
+
+hipError_t nxg_launch_enc_general(const ColsDesc& cd, const uint8_t* heap, uint8_t* out,
+                                  uint64_t cap, uint64_t* scratch, uint64_t* tstat,
+                                  uint32_t epoch, DevStatus* st, int grid, hipStream_t s) {
+    // scratch layout: ctl_pre[n_ctl + 1] | row_off[n_rows]  (only when n_ctl > 0)
+    uint64_t* ctl_pre = scratch;
+    uint64_t* row_off = cd.n_ctl ? scratch + cd.n_ctl + 1 : nullptr;
+    if (cd.n_ctl) hipLaunchKernelGGL(nxg_enc_ctl_scan_kernel, dim3(1), dim3(TPB), 0, s, cd, ctl_pre);
+    const uint64_t nt = (cd.n_rows + TPB - 1) / TPB;
+    if (nt) {
+        const int g = (int)(nt < (uint64_t)grid ? nt : (uint64_t)grid);
+        hipLaunchKernelGGL(nxg_enc_rows_kernel, dim3(g), dim3(TPB), 0, s, cd, heap, out, cap,
+                           cd.n_ctl ? ctl_pre : nullptr, row_off, tstat, (uint32_t)nt, epoch, st, nxg_zero_slot);
+    }
+    if (cd.n_ctl && out) {
+        const uint64_t nb = (cd.n_ctl + TPB - 1) / TPB;
+        hipLaunchKernelGGL(nxg_enc_ctl_write_kernel, dim3((unsigned)(nb < 1024 ? nb : 1024)),
+                           dim3(TPB), 0, s, cd, heap, out, cap, ctl_pre, row_off, st, st);
+    }
+    return hipGetLastError();
+}
+
+int nxg_occupancy_enc_general() {
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, nxg_enc_rows_kernel, TPB, 0) !=
+        hipSuccess)
+        return 1;
+    return n;
+}

@@ -1,0 +1,109 @@
+// nxg_internal.h -- structures shared by the kernels and the host dispatch layer (not ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/nxg_codec.h"
+
+// Per-call device status block (zeroed by hipMemsetAsync before every call).
+struct DevStatus {
+    uint64_t n_rows, n_children, n_ctl, n_heartbeat;  // totals written by the last tile
+    uint32_t err_kind;                                 // first error in wire order
+    uint32_t path;
+    uint64_t err_offset;
+    uint32_t fast_fail;  // homogeneous-f64 kernel rejected the frame (=> general path)
+    uint32_t timeout;    // a bounded spin expired (protocol bug); reported as NXG_TIMEOUT
+    uint32_t capacity;   // a column overflowed its capacity
+    uint32_t done;       // number of tiles completed (diagnostics)
+    uint64_t total_bytes;  // encode: bytes written
+    uint32_t nonf64;       // general path ran into content that F64-only columns cannot hold
+    uint32_t pad0;
+    uint64_t pad[2];
+};
+static_assert(sizeof(DevStatus) == 96, "DevStatus layout");
+
+// Look-back status granule (one 8-byte word, written with one sc1 store):
+//   bits 63:62 flag (1 aggregate, 2 inclusive), 61:44 call epoch, 43:0 value.
+// A word whose epoch differs from the current call's reads as "not ready", so the status
+// arrays need no per-call memset (they are zeroed only when the 18-bit epoch wraps).
+constexpr uint64_t kFlagAgg = 1ull << 62;
+constexpr uint64_t kFlagInc = 2ull << 62;
+constexpr uint64_t kFlagMask = 3ull << 62;
+constexpr int kEpochShift = 44;
+constexpr uint64_t kEpochMax = (1ull << 18) - 1;
+constexpr uint64_t kValMask = (1ull << kEpochShift) - 1;
+__host__ __device__ inline uint64_t lb_word(uint64_t flag, uint32_t epoch, uint64_t v) {
+    return flag | ((uint64_t)epoch << kEpochShift) | (v & kValMask);
+}
+__host__ __device__ inline uint64_t lb_flag(uint64_t w, uint32_t epoch) {
+    return ((w >> kEpochShift) & kEpochMax) == epoch ? (w & kFlagMask) : 0ull;
+}
+
+// ---- f64 decode geometry (nxg_decode_f64.hip) ----
+namespace f64dec {
+constexpr int TPB = 256;
+constexpr int CHUNK = 64;                // bytes per lane
+constexpr int TILE = TPB * CHUNK;        // 16 KiB per tile
+constexpr int HALO = 128;                // look-ahead bytes loaded past the tile
+constexpr int WIN = 64;                  // merge-point search bound (bits of the walk mask)
+constexpr int MAXREC = TILE / 12 + 16;   // staging slots (records are >= 12 bytes)
+}  // namespace f64dec
+
+// ---- general decode geometry (nxg_decode_general.hip) ----
+namespace gdec {
+constexpr int TPB = 256;
+constexpr int CHUNK = 32;
+constexpr int TILE = TPB * CHUNK;  // 8 KiB per tile
+constexpr int HALO = 256;
+constexpr int SLOT_WORDS = 16;     // per-tile look-back descriptor (agg 8 words + inc 8 words)
+}  // namespace gdec
+
+// ---- f64 encode geometry ----
+namespace f64enc {
+constexpr int TPB = 256;
+constexpr int RPT = 4;                 // records per thread
+constexpr int TILE = TPB * RPT;        // records per tile
+constexpr int MAXB = TILE * 15 + 32;   // staging bytes (f64 records <= 15 B for ids < 2^28)
+}  // namespace f64enc
+
+// launchers (each defined next to its kernel)
+struct ColsDesc;
+// Every launcher takes the call's status slot `st` and `zst`, the slot that the call 128 calls
+// later will use. Block 0 zeroes `zst` on entry, so the ring needs no per-call memset.
+__device__ inline void zero_status(DevStatus* zst) {
+    if (zst && blockIdx.x == 0 && threadIdx.x == 0) *zst = DevStatus{};
+}
+extern thread_local DevStatus* nxg_zero_slot;  // host side: passed through to the kernels
+hipError_t nxg_launch_dec_f64(const uint8_t* wire, uint64_t W, uint64_t* oid, uint64_t* oval,
+                              uint64_t cap, uint64_t* tstat, uint32_t epoch, DevStatus* st,
+                              int grid, hipStream_t s);
+hipError_t nxg_launch_dec_general(const uint8_t* wire, uint64_t W, const ColsDesc& cols,
+                                  uint64_t* tslots, uint32_t epoch, DevStatus* st, int emit,
+                                  int grid, hipStream_t s);
+hipError_t nxg_launch_enc_f64(const uint64_t* id, const uint64_t* val, uint64_t n, uint8_t* out,
+                              uint64_t cap, uint64_t* tstat, uint32_t epoch, DevStatus* st,
+                              int grid, hipStream_t s);
+hipError_t nxg_launch_enc_general(const ColsDesc& cols, const uint8_t* heap, uint8_t* out,
+                                  uint64_t cap, uint64_t* scratch, uint64_t* tstat,
+                                  uint32_t epoch, DevStatus* st, int grid, hipStream_t s);
+int nxg_occupancy_dec_f64();
+int nxg_occupancy_dec_general();
+int nxg_occupancy_enc_f64();
+int nxg_occupancy_enc_general();
+
+// Device-side copy of the column pointers (passed by value to kernels).
+struct ColsDesc {
+    uint64_t cap_rows, cap_children, cap_ctl;
+    uint64_t n_rows, n_children, n_ctl;  // encode input counts
+    uint64_t* id;
+    uint8_t* tag;
+    uint64_t* fixed;
+    uint32_t* aux;
+    uint8_t* ctag;
+    uint64_t* cfixed;
+    uint32_t* caux;
+    uint64_t* ctl_row;
+    uint64_t* ctl_off;
+    uint32_t* ctl_len;
+    uint8_t* ctl_variant;
+};

@@ -1,0 +1,334 @@
+// nxg_msg.h -- device-side decoder of one publisher::From message (general path).
+//
+// A per-lane restatement of:
+//   len_wrapped_decode         netidx-core/src/pack.rs:537-555
+//   derived enum decode        netidx-derive/src/lib.rs:482-601 (From, publisher.rs:73-96;
+//                              #[pack(default)] WriteId per lib.rs:392-401)
+//   Value::decode              netidx-value/src/lib.rs:470-506
+//   ValArray / Map / PBytes / ArcStr / DateTime / Duration / Decimal / Abstract decoders
+//                              array.rs:595-612, pack.rs:1225-1239, pbuf.rs:139-147,
+//                              pack.rs:457-469, 1567-1575, 1591-1595, 614-622,
+//                              abstract_type.rs:280-298
+// Nested values are walked iteratively with an explicit stack. Children are allocated
+// depth-first, the same order as the recursive reference decoder, which produces them as it
+// goes.
+#pragma once
+#include "nxg_device.h"
+
+namespace nxgmsg {
+
+constexpr uint32_t E_OK = 0, E_UNKNOWN_TAG = 1, E_TOO_BIG = 2, E_INVALID = 3, E_SHORT = 4,
+                   E_DEPTH = 6, E_BUDGET = 100;  // E_BUDGET: speculation gave up (not an error)
+constexpr uint64_t kMaxVec = 2ull * 1024 * 1024 * 1024;  // pack.rs:917
+
+// Bytes of the frame: [t0, t0+nlds) come from LDS, everything else from global memory.
+struct Src {
+    const uint8_t* lds;
+    uint64_t t0;
+    uint32_t nlds;
+    const uint8_t* __restrict__ g;
+    uint64_t W;
+    NXG_DEV uint32_t byte(uint64_t p) const {
+        const uint64_t r = p - t0;
+        return r < nlds ? (uint32_t)lds[r] : (uint32_t)g[p];
+    }
+};
+
+// Where a decoded value goes. EMIT=false only counts children.
+struct Sink {
+    ColsDesc c;
+    uint32_t* cap_flag;
+    uint32_t* nonf64;  // F64-only columns (tag == nullptr) met a value they cannot hold
+};
+
+NXG_DEV uint32_t dvar(const Src& s, uint64_t& p, uint64_t lim, uint64_t& v) {
+    uint64_t val = 0;
+#pragma unroll 1
+    for (uint32_t i = 0; i < 10; i++) {
+        if (p + i >= lim) return E_SHORT;
+        const uint32_t b = s.byte(p + i);
+        val |= (uint64_t)(b & 0x7fu) << (7 * i);
+        if (b < 0x80u) {
+            p += i + 1;
+            v = val;
+            return E_OK;
+        }
+    }
+    return E_INVALID;
+}
+
+NXG_DEV uint32_t dfix(const Src& s, uint64_t& p, uint64_t lim, uint32_t n, uint64_t& v) {
+    if (lim - p < n) return E_SHORT;
+    uint64_t x = 0;
+    for (uint32_t i = 0; i < n; i++) x = (x << 8) | s.byte(p + i);
+    p += n;
+    v = x;
+    return E_OK;
+}
+
+template <bool EMIT>
+NXG_DEV void put(const Sink* k, bool row, uint64_t slot, uint32_t tag, uint64_t fixed, uint32_t aux) {
+    if (!EMIT) return;
+    if (row) {
+        if (!k->c.tag) {  // F64-only columns
+            if (tag != 9) atomicOr(k->nonf64, 1u);
+            else if (slot < k->c.cap_rows) k->c.fixed[slot] = fixed;
+        } else if (slot < k->c.cap_rows) {
+            k->c.tag[slot] = (uint8_t)tag;
+            k->c.fixed[slot] = fixed;
+            k->c.aux[slot] = aux;
+        }
+    } else {
+        if (!k->c.ctag) {
+            atomicOr(k->nonf64, 1u);
+        } else if (slot < k->c.cap_children) {
+            k->c.ctag[slot] = (uint8_t)tag;
+            k->c.cfixed[slot] = fixed;
+            k->c.caux[slot] = aux;
+        } else {
+            atomicOr(k->cap_flag, 1u);
+        }
+    }
+}
+
+// string/bytes payload: varint len; TooBig if len > remaining; UTF-8 unless !utf8 or !check
+NXG_DEV uint32_t dstr(const Src& s, uint64_t& p, uint64_t lim, bool utf8, uint64_t& off,
+                      uint64_t& len) {
+    uint64_t n;
+    uint32_t e = dvar(s, p, lim, n);
+    if (e) return e;
+    if (n > lim - p) return E_TOO_BIG;
+    if (utf8 && !utf8_valid(s, p, n)) return E_INVALID;
+    off = p;
+    len = n;
+    p += n;
+    return E_OK;
+}
+
+// Decode one Value at p (limit lim) into (row?, slot), children from `child_next`.
+// SPEC=true: plausibility only (no UTF-8 scan, bounded work -> E_BUDGET).
+template <bool EMIT, bool SPEC>
+NXG_DEV uint32_t dvalue(const Src& s, uint64_t& p, uint64_t lim, const Sink* k, bool row,
+                        uint64_t slot, uint64_t& child_next) {
+    uint64_t frem[NXG_MAX_DEPTH + 2];
+    uint64_t fslot[NXG_MAX_DEPTH + 2];
+    int top = -1;
+    int depth = 0;
+    bool is_row = row;
+    uint64_t cur = slot;
+    uint32_t budget = 0;
+#pragma unroll 1
+    for (;;) {
+        if (depth > NXG_MAX_DEPTH) return E_DEPTH;
+        if (SPEC && ++budget > 256) return E_BUDGET;
+        if (p >= lim) return E_SHORT;
+        const uint32_t t = s.byte(p++);
+        uint64_t v, v2, off, len;
+        uint32_t e = E_OK;
+        uint64_t kids = 0;  // values to push for containers
+        switch (t) {
+        case 0:
+            if (!(e = dfix(s, p, lim, 4, v))) put<EMIT>(k, is_row, cur, 0, v, 0);
+            break;
+        case 1:
+            if (!(e = dvar(s, p, lim, v))) put<EMIT>(k, is_row, cur, 1, (uint32_t)v, 0);
+            break;
+        case 2:
+            if (!(e = dfix(s, p, lim, 4, v)))
+                put<EMIT>(k, is_row, cur, 2, (uint64_t)(int64_t)(int32_t)(uint32_t)v, 0);
+            break;
+        case 3:
+            if (!(e = dvar(s, p, lim, v))) {
+                const uint32_t n = (uint32_t)v;
+                const int32_t r = (int32_t)(n >> 1) ^ (int32_t)(0u - (n & 1u));
+                put<EMIT>(k, is_row, cur, 3, (uint64_t)(int64_t)r, 0);
+            }
+            break;
+        case 4:
+        case 6:
+        case 9:
+            if (!(e = dfix(s, p, lim, 8, v))) put<EMIT>(k, is_row, cur, t, v, 0);
+            break;
+        case 5:
+            if (!(e = dvar(s, p, lim, v))) put<EMIT>(k, is_row, cur, 5, v, 0);
+            break;
+        case 7:
+            if (!(e = dvar(s, p, lim, v))) put<EMIT>(k, is_row, cur, 7, (v >> 1) ^ (0ull - (v & 1ull)), 0);
+            break;
+        case 8:
+            if (!(e = dfix(s, p, lim, 4, v))) put<EMIT>(k, is_row, cur, 8, v, 0);
+            break;
+        case 10:
+            if ((e = dfix(s, p, lim, 8, v))) break;
+            if ((e = dfix(s, p, lim, 4, v2))) break;
+            if (!datetime_valid((int64_t)v, (uint32_t)v2)) {
+                e = E_INVALID;
+                break;
+            }
+            put<EMIT>(k, is_row, cur, 10, v, (uint32_t)v2);
+            break;
+        case 11: {
+            if ((e = dfix(s, p, lim, 8, v))) break;
+            if ((e = dfix(s, p, lim, 4, v2))) break;
+            uint64_t secs = v;
+            uint32_t ns = (uint32_t)v2;
+            if (ns >= 1000000000u) {
+                const uint64_t add = ns / 1000000000u;
+                if (secs + add < secs) {
+                    e = E_INVALID;  // Duration::new overflow panics in the reference
+                    break;
+                }
+                secs += add;
+                ns %= 1000000000u;
+            }
+            put<EMIT>(k, is_row, cur, 11, secs, ns);
+            break;
+        }
+        case 12:
+        case 18:
+            if (!(e = dstr(s, p, lim, !SPEC, off, len))) put<EMIT>(k, is_row, cur, t, off, (uint32_t)len);
+            break;
+        case 13:
+            if (!(e = dstr(s, p, lim, false, off, len))) put<EMIT>(k, is_row, cur, 13, off, (uint32_t)len);
+            break;
+        case 14:
+            put<EMIT>(k, is_row, cur, 14, 1, 0);
+            break;
+        case 15:
+            put<EMIT>(k, is_row, cur, 15, 0, 0);
+            break;
+        case 16:
+        case 17:
+            put<EMIT>(k, is_row, cur, 16, 0, 0);
+            break;
+        case 19:
+        case 21: {
+            if ((e = dvar(s, p, lim, v))) break;
+            const uint64_t maxe = t == 19 ? (kMaxVec / 16) : (kMaxVec / 32);
+            const uint64_t unit = t == 19 ? 16 : 32;
+            if (v > maxe || v * unit > ((lim - p) << 8)) {
+                e = E_TOO_BIG;
+                break;
+            }
+            kids = t == 19 ? v : 2 * v;
+            put<EMIT>(k, is_row, cur, t, child_next, (uint32_t)v);
+            break;
+        }
+        case 20:
+            if (lim - p < 16) {
+                e = E_SHORT;
+                break;
+            }
+            put<EMIT>(k, is_row, cur, 20, p, 16);
+            p += 16;
+            break;
+        case 22:
+            // Error(Value) whose inner value is a String is Error(String) = wire tag 18
+            if (p < lim && s.byte(p) == 12u) {
+                p++;
+                if (!(e = dstr(s, p, lim, !SPEC, off, len))) put<EMIT>(k, is_row, cur, 18, off, (uint32_t)len);
+                break;
+            }
+            kids = 1;
+            put<EMIT>(k, is_row, cur, 22, child_next, 1);
+            break;
+        case 23:
+            if (!(e = dfix(s, p, lim, 1, v))) put<EMIT>(k, is_row, cur, 23, v, 0);
+            break;
+        case 24:
+            if (!(e = dfix(s, p, lim, 1, v)))
+                put<EMIT>(k, is_row, cur, 24, (uint64_t)(int64_t)(int8_t)(uint8_t)v, 0);
+            break;
+        case 25:
+            if (!(e = dfix(s, p, lim, 2, v))) put<EMIT>(k, is_row, cur, 25, v, 0);
+            break;
+        case 26:
+            if (!(e = dfix(s, p, lim, 2, v)))
+                put<EMIT>(k, is_row, cur, 26, (uint64_t)(int64_t)(int16_t)(uint16_t)v, 0);
+            break;
+        case 27: {
+            if ((e = dvar(s, p, lim, v))) break;
+            if (v < 1) {
+                e = E_SHORT;
+                break;
+            }
+            const uint64_t take = v - vl64(v);
+            const uint64_t l2 = take < lim - p ? p + take : lim;
+            if (l2 - p < 16) {
+                e = E_SHORT;
+                break;
+            }
+            put<EMIT>(k, is_row, cur, 27, p, (uint32_t)(l2 - p));
+            p = l2;
+            break;
+        }
+        default:
+            e = E_UNKNOWN_TAG;
+        }
+        if (e) return e;
+        if (kids) {
+            const uint64_t base = child_next;
+            child_next += kids;
+            ++top;
+            frem[top] = kids;
+            fslot[top] = base;
+        }
+        while (top >= 0 && frem[top] == 0) top--;
+        if (top < 0) return E_OK;
+        frem[top]--;
+        cur = fslot[top]++;
+        is_row = false;
+        depth = top + 1;
+    }
+}
+
+struct MsgInfo {
+    uint64_t next;
+    uint32_t variant;
+    uint64_t id;
+};
+
+// Decode the message starting at `pos`. On success, info.next is the position after the
+// length-wrapped region (trailing bytes skipped, pack.rs:551-553). Update values are written
+// to row `row` (EMIT); children are allocated from child_next.
+template <bool EMIT, bool SPEC>
+NXG_DEV uint32_t decode_msg(const Src& s, uint64_t pos, MsgInfo& info, const Sink* k,
+                            uint64_t row, uint64_t& child_next) {
+    uint64_t p = pos, L;
+    uint32_t e = dvar(s, p, s.W, L);
+    if (e) return e;
+    if (L < 1) return E_SHORT;
+    const uint64_t take = L - vl64(L);
+    const uint64_t lim = take < s.W - p ? p + take : s.W;
+    info.next = lim;
+    if (p >= lim) return E_SHORT;
+    const uint32_t variant = s.byte(p++);
+    info.variant = variant;
+    uint64_t v, off, len, dummy = 0;
+    switch (variant) {
+    case 0:
+    case 1:
+        return dstr(s, p, lim, !SPEC, off, len);
+    case 2:
+        return dvar(s, p, lim, v);
+    case 3:
+        if ((e = dstr(s, p, lim, !SPEC, off, len))) return e;
+        if ((e = dvar(s, p, lim, v))) return e;
+        return dvalue<false, SPEC>(s, p, lim, k, false, 0, dummy);
+    case 4:
+        if ((e = dvar(s, p, lim, v))) return e;
+        info.id = v;
+        return dvalue<EMIT, SPEC>(s, p, lim, k, true, row, child_next);
+    case 5:
+        return E_OK;
+    case 6:
+        if ((e = dvar(s, p, lim, v))) return e;
+        if ((e = dvalue<false, SPEC>(s, p, lim, k, false, 0, dummy))) return e;
+        e = dvar(s, p, lim, v);
+        return e == E_SHORT ? E_OK : e;  // #[pack(default)] WriteId
+    default:
+        return E_UNKNOWN_TAG;
+    }
+}
+
+}  // namespace nxgmsg
