@@ -51,6 +51,7 @@ struct NxgCtx {
     hipStream_t stream = nullptr;
     int ncu = 0;
     int grid_dec_f64 = 0, grid_dec_gen = 0, grid_enc_f64 = 0, grid_enc_gen = 0;
+    int grid_dec_f64_persistent = 0;
     // status ring: one DevStatus per call, the whole ring re-zeroed once per lap
     DevStatus* dst = nullptr;
     DevStatus* hst = nullptr;  // pinned mirror
@@ -78,6 +79,7 @@ struct NxgCtx {
         uint32_t slot;
     };
     std::vector<Pending> pending;
+    DevStatus last{};  // last completed decode's device status (diagnostics)
 };
 
 namespace {
@@ -268,6 +270,11 @@ bool finish_decode(NxgCtx* c, const uint8_t* f, uint64_t len, NxgColumns* out, i
     HIPCHK(hipMemcpyAsync(c->hst + slot, st, sizeof(DevStatus), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     DevStatus h = c->hst[slot];
+    if (tried_fast && h.timeout && c->grid_dec_f64 <= 0) {
+        // the one-tile-per-workgroup schedule relies on in-order dispatch; if the watchdog
+        // ever fires, this ctx switches to the persistent co-resident schedule for good
+        c->grid_dec_f64 = c->grid_dec_f64_persistent;
+    }
     if (tried_fast && len > 0 && h.fast_fail) {
         DevStatus* st2;
         uint32_t slot2;
@@ -278,6 +285,7 @@ bool finish_decode(NxgCtx* c, const uint8_t* f, uint64_t len, NxgColumns* out, i
         HIPCHK(hipStreamSynchronize(c->stream));
         h = c->hst[slot2];
     }
+    c->last = h;
     if (h.timeout) {
         set_err(err, "device look-back watchdog expired");
         return false;
@@ -418,6 +426,11 @@ extern "C" {
 
 const char* nxg_version(void) { return "nxg 0.1.0 gfx950"; }
 
+// Not part of the ABI: the last decode's kernel diagnostics (DevStatus::diag), for profiling.
+void nxg_debug_diag(NxgCtx* c, unsigned long long out[8]) {
+    for (int i = 0; i < 8; i++) out[i] = c ? c->last.diag[i] : 0;
+}
+
 void nxg_error_free(NetidxError* err) {
     if (!err) return;
     free(err->msg);
@@ -447,13 +460,18 @@ NxgCtx* nxg_ctx_new(int device, NetidxError* err) {
     if ((e = hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking)) != hipSuccess)
         return fail("hipStreamCreate", e);
     c->stream = c->own;
-    // persistent grids: every workgroup must be co-resident (look-back progress); keep one
-    // block of margin under the occupancy answer (MI355X_MICROARCH.md residency notes)
+    // Default schedule: one workgroup per tile in blockIdx order (grid 0). The decoupled
+    // look-back then always finds recent inclusive prefixes. Persistent fallback: every
+    // workgroup co-resident, with one block of margin under the occupancy answer
+    // (MI355X_MICROARCH.md residency notes). NXG_PERSISTENT=1 forces it.
     auto grid = [&](int occ) { return c->ncu * std::max(1, occ > 2 ? occ - 1 : occ); };
-    c->grid_dec_f64 = grid(nxg_occupancy_dec_f64());
-    c->grid_dec_gen = grid(nxg_occupancy_dec_general());
-    c->grid_enc_f64 = grid(nxg_occupancy_enc_f64());
-    c->grid_enc_gen = grid(nxg_occupancy_enc_general());
+    c->grid_dec_f64_persistent = grid(nxg_occupancy_dec_f64());
+    const char* pe = getenv("NXG_PERSISTENT");
+    const bool persist = pe && pe[0] == '1';
+    c->grid_dec_f64 = persist ? c->grid_dec_f64_persistent : 0;
+    c->grid_dec_gen = persist ? grid(nxg_occupancy_dec_general()) : 0;
+    c->grid_enc_f64 = persist ? grid(nxg_occupancy_enc_f64()) : 0;
+    c->grid_enc_gen = persist ? grid(nxg_occupancy_enc_general()) : 0;
     if ((e = hipMalloc(&c->dst, sizeof(DevStatus) * kStatusRing)) != hipSuccess)
         return fail("hipMalloc(status)", e);
     if ((e = hipMemset(c->dst, 0, sizeof(DevStatus) * kStatusRing)) != hipSuccess)

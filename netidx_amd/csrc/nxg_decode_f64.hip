@@ -141,7 +141,9 @@ NXG_DEV uint4 ld16_guard(const uint8_t* __restrict__ wire, uint64_t off, uint64_
 }
 
 }  // namespace
-
+// One wave per workgroup, one 4 KiB tile per wave iteration. All exchanges between lanes are
+// wave-local (shuffles, ballots, the wave's own LDS), so no phase waits for other waves. Many
+// waves per CU hide each other's look-back latency.
 __global__ __launch_bounds__(TPB) void nxg_dec_f64_kernel(
     const uint8_t* __restrict__ wire, uint64_t W, uint64_t* __restrict__ oid,
     uint64_t* __restrict__ oval, uint64_t cap, uint64_t* __restrict__ tstat, uint32_t ntiles,
@@ -150,61 +152,50 @@ __global__ __launch_bounds__(TPB) void nxg_dec_f64_kernel(
     __shared__ __attribute__((aligned(16))) uint8_t buf[TILE + HALO];
     __shared__ __attribute__((aligned(16))) uint64_t sid[MAXREC];
     __shared__ __attribute__((aligned(16))) uint64_t sval[MAXREC];
-    __shared__ uint32_t xs[TPB + 1];
-    __shared__ uint32_t scan_tmp[4];
-    __shared__ uint32_t sh_fail, sh_abort;
-    __shared__ uint64_t sh_base;
 
-    const uint32_t tid = threadIdx.x;
-    const uint32_t lane = tid & 63;
+    const uint32_t lane = threadIdx.x;
     uint32_t tile = blockIdx.x;
     if (tile >= ntiles) return;
 
-    // register prefetch of the first tile (4 x 16 B per thread + the halo)
+    // register prefetch of the first tile: 4 x 16 B per lane + the halo (8 lanes x 16 B)
     uint4 pre[4], preh = make_uint4(0, 0, 0, 0);
     {
         const uint64_t t0 = (uint64_t)tile * TILE;
 #pragma unroll
-        for (int i = 0; i < 4; i++) pre[i] = ld16_guard(wire, t0 + i * 4096 + tid * 16, W);
-        if (tid < HALO / 16) preh = ld16_guard(wire, t0 + TILE + tid * 16, W);
+        for (int i = 0; i < 4; i++) pre[i] = ld16_guard(wire, t0 + i * 1024 + lane * 16, W);
+        if (lane < HALO / 16) preh = ld16_guard(wire, t0 + TILE + lane * 16, W);
     }
 
     for (; tile < ntiles; tile += gridDim.x) {
         const uint64_t t0 = (uint64_t)tile * TILE;
 #pragma unroll
-        for (int i = 0; i < 4; i++) *reinterpret_cast<uint4*>(buf + i * 4096 + tid * 16) = pre[i];
-        if (tid < HALO / 16) *reinterpret_cast<uint4*>(buf + TILE + tid * 16) = preh;
-        if (tid == 0) {
-            sh_fail = 0;
-            sh_abort = ld_agent32(&st->fast_fail);
-        }
-        __syncthreads();
-        if (sh_abort) break;  // another tile already rejected the frame
+        for (int i = 0; i < 4; i++) *reinterpret_cast<uint4*>(buf + i * 1024 + lane * 16) = pre[i];
+        if (lane < HALO / 16) *reinterpret_cast<uint4*>(buf + TILE + lane * 16) = preh;
+        __syncthreads();  // single-wave workgroup: orders the LDS writes before the reads
+        if (ld_agent32(&st->fast_fail)) break;  // another tile already rejected the frame
 
         // prefetch the next tile while this one is parsed
         const uint32_t nxt = tile + gridDim.x;
         if (nxt < ntiles) {
             const uint64_t n0 = (uint64_t)nxt * TILE;
 #pragma unroll
-            for (int i = 0; i < 4; i++) pre[i] = ld16_guard(wire, n0 + i * 4096 + tid * 16, W);
-            if (tid < HALO / 16) preh = ld16_guard(wire, n0 + TILE + tid * 16, W);
+            for (int i = 0; i < 4; i++) pre[i] = ld16_guard(wire, n0 + i * 1024 + lane * 16, W);
+            if (lane < HALO / 16) preh = ld16_guard(wire, n0 + TILE + lane * 16, W);
         }
 
-        // 1. merge points: one per chunk start, plus the next tile's first chunk
-        uint32_t x;
-        if (tile == 0 && tid == 0) {
+        // 1. merge points of this lane's chunk start and of the next chunk start
+        uint32_t xa;
+        if (tile == 0 && lane == 0) {
             uint32_t e0, e1, e2, e3;
             load16(buf, 0, e0, e1, e2, e3);
-            x = (W == 0 || rec_check(e0, e1, W)) ? 0u : FAIL;
+            xa = (W == 0 || rec_check(e0, e1, W)) ? 0u : FAIL;
         } else {
-            x = merge_point(buf, tid * CHUNK, t0, W);
+            xa = merge_point(buf, lane * CHUNK, t0, W);
         }
-        xs[tid] = x;
-        if (tid == TPB - 1) xs[TPB] = merge_point(buf, TILE, t0, W);
-        __syncthreads();
+        uint32_t xb = __shfl_down(xa, 1, 64);
+        if (lane == TPB - 1) xb = merge_point(buf, TILE, t0, W);
 
         // 2. count walk over [X_j, X_{j+1})
-        const uint32_t xa = xs[tid], xb = xs[tid + 1];
         uint32_t n = 0;
         bool bad = (xa == FAIL) | (xb == FAIL) | (xa > xb);
         if (!bad) {
@@ -221,11 +212,12 @@ __global__ __launch_bounds__(TPB) void nxg_dec_f64_kernel(
             bad |= (pos != xb);
         }
         if (bad) n = 0;
-        uint32_t ntile;
-        const uint32_t off = block_excl_scan<uint32_t, TPB>(n, scan_tmp, &ntile);
+        const uint32_t inc = wave_incl_scan(n);
+        const uint32_t off = inc - n;
+        const uint32_t ntile = __shfl(inc, TPB - 1, 64);
 
         // 3. publish this tile's aggregate as early as possible
-        if (tid == 0) st_agent(&tstat[tile], lb_word(tile == 0 ? kFlagInc : kFlagAgg, epoch, ntile));
+        if (lane == 0) st_agent(&tstat[tile], lb_word(tile == 0 ? kFlagInc : kFlagAgg, epoch, ntile));
 
         // 4. validate + decode into the LDS staging buffer
         if (!bad) {
@@ -245,62 +237,58 @@ __global__ __launch_bounds__(TPB) void nxg_dec_f64_kernel(
                 pos += L;
             }
         }
-        if (bad) atomicOr(&sh_fail, 1u);
+        bool fail = __any(bad);
 
-        // 5. decoupled look-back (wave 0) for the tile's first record index
-        if (tid < 64) {
-            uint64_t base = 0;
-            if (tile != 0) {
-                int64_t pred = (int64_t)tile - 1;
-                const uint64_t t_start = rt_now();
-                bool give_up = false;
-                for (;;) {
-                    const int64_t idx = pred - (int64_t)lane;
-                    uint64_t s = idx >= 0 ? ld_agent(&tstat[idx]) : lb_word(kFlagInc, epoch, 0);
-                    while (!__all(lb_flag(s, epoch) != 0)) {
-                        __builtin_amdgcn_s_sleep(1);
-                        if (lb_flag(s, epoch) == 0) s = ld_agent(&tstat[idx]);
-                        if (ld_agent32(&st->fast_fail) || rt_now() - t_start > kSpinTicks) {
-                            give_up = true;
-                            break;
-                        }
-                    }
-                    if (give_up) break;
-                    const uint64_t inc = __ballot(lb_flag(s, epoch) == kFlagInc);
-                    if (inc) {
-                        const uint32_t first = (uint32_t)__builtin_ctzll(inc);
-                        base += wave_sum<uint64_t>(lane <= first ? (s & kValMask) : 0ull);
+        // 5. decoupled look-back for the tile's first record index
+        uint64_t base = 0;
+        if (tile != 0) {
+            int64_t pred = (int64_t)tile - 1;
+            const uint64_t t_start = rt_now();
+            bool give_up = false;
+            for (;;) {
+                const int64_t idx = pred - (int64_t)lane;
+                uint64_t s = idx >= 0 ? ld_agent(&tstat[idx]) : lb_word(kFlagInc, epoch, 0);
+                while (!__all(lb_flag(s, epoch) != 0)) {
+                    __builtin_amdgcn_s_sleep(1);
+                    if (lb_flag(s, epoch) == 0) s = ld_agent(&tstat[idx]);
+                    if (ld_agent32(&st->fast_fail) || rt_now() - t_start > kSpinTicks) {
+                        give_up = true;
                         break;
                     }
-                    base += wave_sum<uint64_t>(s & kValMask);
-                    pred -= 64;
                 }
-                if (give_up && lane == 0) {
-                    if (!ld_agent32(&st->fast_fail)) atomicOr(&st->timeout, 1u);
-                    atomicOr(&sh_fail, 1u);
+                if (give_up) break;
+                const uint64_t incm = __ballot(lb_flag(s, epoch) == kFlagInc);
+                if (incm) {
+                    const uint32_t first = (uint32_t)__builtin_ctzll(incm);
+                    base += wave_sum<uint64_t>(lane <= first ? (s & kValMask) : 0ull);
+                    break;
                 }
-                if (lane == 0) st_agent(&tstat[tile], lb_word(kFlagInc, epoch, base + ntile));
+                base += wave_sum<uint64_t>(s & kValMask);
+                pred -= 64;
             }
-            if (lane == 0) sh_base = base;
+            if (give_up) {
+                if (lane == 0 && !ld_agent32(&st->fast_fail)) atomicOr(&st->timeout, 1u);
+                fail = true;
+            }
+            if (lane == 0) st_agent(&tstat[tile], lb_word(kFlagInc, epoch, base + ntile));
         }
-        __syncthreads();
-        if (sh_fail) {
-            if (tid == 0) atomicOr(&st->fast_fail, 1u);
+        if (fail) {
+            if (lane == 0) atomicOr(&st->fast_fail, 1u);
             break;
         }
+        __syncthreads();  // staging writes before the cross-lane reads below
 
         // 6. coalesced stores of the staged records
-        const uint64_t base = sh_base;
         uint32_t lim = ntile;
         if (base + ntile > cap) {
             lim = base < cap ? (uint32_t)(cap - base) : 0u;
-            if (tid == 0) atomicOr(&st->capacity, 1u);
+            if (lane == 0) atomicOr(&st->capacity, 1u);
         }
-        for (uint32_t i = tid; i < lim; i += TPB) {
+        for (uint32_t i = lane; i < lim; i += TPB) {
             oid[base + i] = sid[i];
             oval[base + i] = sval[i];
         }
-        if (tile == ntiles - 1 && tid == 0) {
+        if (tile == ntiles - 1 && lane == 0) {
             st->n_rows = base + ntile;
             st->path = 1;
         }
@@ -313,7 +301,11 @@ hipError_t nxg_launch_dec_f64(const uint8_t* wire, uint64_t W, uint64_t* oid, ui
                               int grid, hipStream_t s) {
     const uint64_t nt = (W + TILE - 1) / TILE;
     if (nt == 0) return hipSuccess;
-    const int g = (int)(nt < (uint64_t)grid ? nt : (uint64_t)grid);
+    // grid <= 0: one workgroup per tile in blockIdx order. Each XCD dispatches its blocks in
+    // increasing order, so the lowest unfinished tile is always resident and its predecessor is
+    // done (progress). grid > 0: persistent grid of `grid` co-resident workgroups striding over
+    // the tiles (the fallback if the watchdog ever fires).
+    const uint64_t g = grid <= 0 ? nt : (nt < (uint64_t)grid ? nt : (uint64_t)grid);
     hipLaunchKernelGGL(nxg_dec_f64_kernel, dim3(g), dim3(TPB), 0, s, wire, W, oid, oval, cap,
                        tstat, (uint32_t)nt, epoch, st, nxg_zero_slot);
     return hipGetLastError();

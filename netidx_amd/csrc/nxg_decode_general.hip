@@ -6,18 +6,20 @@
 // may be arbitrarily long. They are resolved in parallel by speculation with exact repair:
 //
 //  * lane: each lane owns a 32-byte chunk. It guesses its first message start: the first
-//    position from which two consecutive messages decode plausibly. From that guess it walks the
-//    messages that START inside its chunk with the full validating decoder, and records its
-//    exit (the first message start past its chunk) and its counts.
+//    position from which two consecutive messages decode plausibly. From that guess it walks
+//    the messages that START inside its chunk with the full validating decoder. This walk has a
+//    work budget: a wrong guess must not wander through megabytes. The lane records its exit
+//    (the first message start past its chunk) and its counts.
 //  * block repair: a lane whose guess differs from its predecessor's exit re-walks from that
-//    exit. Iterating to a fixed point makes every lane exact relative to the tile's entry.
+//    exit. Iterating to a fixed point makes every lane consistent with the tile's entry.
 //  * tile: descriptors {speculated entry, exit, counts, first error} are published as
 //    aggregates, and later as inclusive prefixes, through a decoupled look-back. A tile
 //    composes its predecessors' aggregates only when each aggregate's entry equals the exit of
-//    the tile before it. Otherwise it waits for its predecessor's inclusive prefix. If its own
-//    guess proves wrong, the tile re-runs the block repair from the true entry.
-//  * emit: with exact lane entries and global bases, every lane decodes its messages again and
-//    writes the columns.
+//    the tile before it. Otherwise it waits for its predecessor's inclusive prefix.
+//  * exact phase: once the true entry is known, the tile re-runs the repair from it if its
+//    guess was wrong or a walk ran out of budget. Walks in this phase are unbounded and start
+//    only at true message starts, so their cost is proportional to the real data.
+//  * emit: every lane decodes its messages again and writes the columns at global bases.
 //
 // The first error on the true chain is carried forward through the inclusive prefixes. The
 // frame is rejected with that (kind, message offset), just as the sequential reference stops at
@@ -34,7 +36,7 @@ constexpr uint64_t POSM = (1ull << 56) - 1;
 
 // descriptor word indices (SLOT_WORDS = 16 u64 per tile)
 enum {
-    W_FLAG = 0,   // flag(63:62) | rows (aggregate) or rows prefix (inclusive)
+    W_FLAG = 0,   // flag(63:62) | epoch | rows (aggregate) or rows prefix (inclusive)
     A_CHILD = 1,
     A_CTLHB = 2,  // ctl (lo 32) | heartbeats (hi 32)
     A_SPEC = 3,   // speculated entry; NONE => not composable
@@ -46,30 +48,42 @@ enum {
     I_ERR = 11,
 };
 
+// lane states (LDS word: state << 8 | error kind)
+enum { S_NONE = 0, S_EXH = 1, S_OK = 2, S_ERR = 3 };
+
 struct LaneRes {
     uint64_t x;  // exit (first message start at/after the chunk end), or error position
     uint32_t rows, ctl, hb;
     uint64_t children;
-    uint32_t ek;  // error kind, 0 = none
+    uint32_t st;  // S_*
+    uint32_t ek;  // error kind when S_ERR
 };
 
-NXG_DEV void lane_clear(LaneRes& r, uint64_t x) {
+NXG_DEV void lane_set(LaneRes& r, uint32_t state, uint64_t x) {
     r.x = x;
     r.rows = r.ctl = r.hb = 0;
     r.children = 0;
+    r.st = state;
     r.ek = 0;
 }
 
-// full validating walk of the messages starting in [e, end)
+// validating walk of the messages starting in [e, end)
+template <int MODE>
 NXG_DEV void walk(const Src& s, uint64_t e, uint64_t end, LaneRes& r) {
-    lane_clear(r, e);
+    lane_set(r, S_OK, e);
     uint64_t pos = e;
     const uint64_t stop = end < s.W ? end : s.W;
+    uint32_t work = 0;
     while (pos < stop) {
         MsgInfo mi;
         uint64_t ch = 0;
-        const uint32_t err = decode_msg<false, false>(s, pos, mi, nullptr, 0, ch);
+        const uint32_t err = decode_msg<false, MODE>(s, pos, mi, nullptr, 0, ch, work);
+        if (err == E_BUDGET) {
+            r.st = S_EXH;
+            return;
+        }
         if (err) {
+            r.st = S_ERR;
             r.ek = err;
             break;
         }
@@ -82,54 +96,148 @@ NXG_DEV void walk(const Src& s, uint64_t e, uint64_t end, LaneRes& r) {
     r.x = pos;  // on error: the failing message's start
 }
 
-// first position in [c, end) from which two messages decode plausibly (cheap checks only)
-NXG_DEV uint64_t speculate(const Src& s, uint64_t c, uint64_t end) {
+// First position in [c, end) where an Update message decodes plausibly and is followed by
+// another Update (or the frame end). Only Updates are guessed: a Heartbeat (`L 05 ...`) or
+// Unsubscribed accepts almost any bytes inside its length, so those would be false starts.
+// A chunk whose first messages are control messages simply guesses later (or nothing), and
+// the repair resolves it exactly.
+NXG_DEV uint64_t speculate(const Src& s, uint64_t c, uint64_t end, uint32_t& tries) {
     const uint64_t stop = end < s.W ? end : s.W;
     for (uint64_t p = c; p < stop; p++) {
         MsgInfo mi;
         uint64_t ch = 0;
-        if (decode_msg<false, true>(s, p, mi, nullptr, 0, ch)) continue;
+        uint32_t work = 0;
+        tries++;
+        if (decode_msg<false, M_SPEC>(s, p, mi, nullptr, 0, ch, work) || mi.variant != 4)
+            continue;
         if (mi.next >= s.W) return p;
         MsgInfo m2;
-        if (decode_msg<false, true>(s, mi.next, m2, nullptr, 0, ch) == E_OK) return p;
+        work = 0;
+        if (decode_msg<false, M_SPEC>(s, mi.next, m2, nullptr, 0, ch, work) == E_OK &&
+            m2.variant == 4)
+            return p;
     }
     return NONE;
 }
 
-// Block repair: every lane's entry becomes its predecessor's exit (lane 0 is fixed). A lane
-// whose predecessor died inherits the error. Lanes before the first definite entry stay NONE.
-NXG_DEV void repair(const Src& s, uint64_t cend, uint64_t& e, LaneRes& r, uint64_t* sx,
-                    uint32_t* sek, uint32_t* sflag) {
-    const uint32_t tid = threadIdx.x;
-    for (;;) {
-        sx[tid] = r.x;
-        sek[tid] = r.ek | (e == NONE ? 0x80000000u : 0u);
-        if (tid == 0) *sflag = 0;
-        __syncthreads();
-        bool ch = false;
-        if (tid > 0) {
-            const uint32_t pk = sek[tid - 1];
-            const uint64_t px = sx[tid - 1];
-            const bool pnone = (pk & 0x80000000u) && (pk & 0x7fffffffu) == 0;
-            const uint32_t perr = pk & 0x7fffffffu;
-            if (perr) {  // chain dies before this lane: no messages, inherit the error
-                if (!(r.ek == perr && r.x == px && e == NONE)) {
-                    e = NONE;
-                    lane_clear(r, px);
-                    r.ek = perr;
-                    ch = true;
-                }
-            } else if (!pnone && px != e) {
-                e = px;
-                walk(s, e, cend, r);
-                ch = true;
+// Index of the nearest lane below this one whose state is not S_NONE, or -1. Lanes in S_NONE
+// have no message start in their chunk: the chain passes straight through them.
+NXG_DEV int nearest_def(bool def, uint32_t* wtop) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const uint64_t m = __ballot(def);
+    if (lane == 0) wtop[wv] = m ? wv * 64 + 63 - (uint32_t)__builtin_clzll(m) : 0xffffffffu;
+    __syncthreads();
+    const uint64_t below = m & ((1ull << lane) - 1);
+    int src = -1;
+    if (below) {
+        src = (int)(wv * 64 + 63 - (uint32_t)__builtin_clzll(below));
+    } else {
+        for (int i = (int)wv - 1; i >= 0; i--)
+            if (wtop[i] != 0xffffffffu) {
+                src = (int)wtop[i];
+                break;
             }
+    }
+    return src;
+}
+
+// Block repair from an anchor lane. A lane is VERIFIED when every lane from the anchor up to it
+// is consistent: a lane with an entry starts exactly at the exit of the nearest lane below it
+// that has an entry; a lane without one (S_NONE) lies wholly before that exit (pass-through).
+// Each round, the first unverified lane (the "break") is fixed from its verified predecessor:
+// - lanes whose whole chunk lies before the predecessor's exit become pass-through;
+// - the lane whose chunk contains that exit re-walks from it;
+// - after a dead predecessor, every remaining lane inherits the error.
+// An unverified exit is never propagated, so a wrong guess cannot corrupt correct lanes.
+// Rounds = number of breaks + 1. In M_BOUNDED mode the repair stops at a predecessor whose walk
+// ran out of budget; `complete` stays false and the tile is then not composable. On completion,
+// *texit / *tek receive the tile's exit (the effective exit of the last lane).
+template <int MODE>
+NXG_DEV uint32_t repair(const Src& s, uint64_t cend, uint32_t anchor, uint64_t& e, LaneRes& r,
+                        uint64_t* sx, uint32_t* sst, uint32_t* wtop, uint32_t* wbreak,
+                        uint64_t* bx, uint32_t* nwalks, bool& complete, uint64_t* texit,
+                        uint32_t* tek) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    // messages can start in [cend - CHUNK, stop): the chunk, clipped to the frame
+    const uint64_t stop = cend < s.W ? cend : s.W;
+    uint32_t rounds = 0;
+    complete = false;
+    for (;;) {
+        // every round fixes the first break and breaks only move forward: TPB + 1 rounds
+        // suffice. The cap turns a logic error into a reported failure, never a hang.
+        if (++rounds > 2 * TPB + 4) {
+            __syncthreads();
+            return rounds;  // complete == false
         }
-        if (ch) atomicOr(sflag, 1u);
+        sx[tid] = r.x;
+        sst[tid] = (r.st << 8) | r.ek;
+        const int src = nearest_def(r.st != S_NONE, wtop);  // contains the barrier
+        uint32_t pst = S_NONE, pek = 0;
+        uint64_t px = 0;
+        if (src >= 0) {
+            pst = sst[src] >> 8;
+            pek = sst[src] & 0xff;
+            px = sx[src];
+        }
+        bool cons = true;
+        if (tid > anchor) {
+            if (pst == S_ERR) cons = r.st == S_ERR && e == NONE && r.x == px;
+            else if (pst == S_OK)
+                cons = r.st == S_NONE ? px >= stop
+                                      : (e == px && (MODE != M_EXACT || r.st != S_EXH));
+            else cons = false;  // behind an exhausted walk: unverifiable here
+        } else if (tid == anchor) {
+            cons = MODE != M_EXACT || r.st != S_EXH;
+        }
+        const uint64_t bad = __ballot(!cons);
+        if (lane == 0) wbreak[wv] = bad ? wv * 64 + (uint32_t)__builtin_ctzll(bad) : TPB;
         __syncthreads();
-        const bool any = *sflag != 0;
+        uint32_t brk = TPB;
+        for (int i = 0; i < 4; i++) brk = min(brk, wbreak[i]);
+        if (brk >= TPB) {
+            complete = true;
+            if (tid == TPB - 1) {
+                *texit = r.st != S_NONE ? r.x : px;
+                *tek = r.st == S_ERR ? r.ek : (r.st == S_NONE && pst == S_ERR ? pek : 0u);
+            }
+            __syncthreads();
+            return rounds;
+        }
+        if (tid == brk) {  // broadcast the break's predecessor
+            bx[0] = px;
+            bx[1] = ((uint64_t)pst << 8) | pek;
+        }
         __syncthreads();
-        if (!any) return;
+        const uint64_t X = bx[0];
+        const uint32_t xst = (uint32_t)(bx[1] >> 8), xek = (uint32_t)(bx[1] & 0xff);
+        bool progressed = true;
+        if (brk == anchor) {  // anchor exhausted in exact mode: walk it unbounded
+            if (tid == anchor) {
+                walk<MODE>(s, e, cend, r);
+                atomicAdd(nwalks, 1u);
+            }
+        } else if (xst == S_ERR) {
+            if (tid >= brk) {
+                e = NONE;
+                lane_set(r, S_ERR, X);
+                r.ek = xek;
+            }
+        } else if (xst == S_OK) {
+            if (tid >= brk) {
+                if (stop <= X) {  // pass-through (including chunks past the frame end)
+                    e = NONE;
+                    lane_set(r, S_NONE, NONE);
+                } else if (cend - CHUNK <= X) {  // this chunk contains X
+                    e = X;
+                    walk<MODE>(s, e, cend, r);
+                    atomicAdd(nwalks, 1u);
+                }
+            }
+        } else {
+            progressed = false;
+        }
+        __syncthreads();
+        if (!progressed) return rounds;
     }
 }
 
@@ -165,14 +273,19 @@ __global__ __launch_bounds__(TPB) void nxg_dec_general_kernel(
     zero_status(zst);
     __shared__ __attribute__((aligned(16))) uint8_t buf[TILE + HALO];
     __shared__ uint64_t sx[TPB];
-    __shared__ uint32_t sek[TPB];
+    __shared__ uint32_t sst[TPB];
     __shared__ uint64_t se[TPB];
     __shared__ uint64_t scan64[4];
     __shared__ uint32_t scan32[4];
     __shared__ uint32_t wfirst[4];
-    __shared__ uint32_t sh_flag;
+    __shared__ uint32_t wtop[4];
+    __shared__ uint64_t bx[2];
+    __shared__ uint64_t sh_texit;
+    __shared__ uint32_t sh_tek;
+    __shared__ uint32_t sh_flag, sh_bad;
     __shared__ uint64_t sh_E, sh_rows, sh_ch, sh_ctl, sh_hb;
-    __shared__ uint32_t sh_ek, sh_timeout;
+    __shared__ uint32_t sh_ek, sh_timeout, sh_fallback;
+    __shared__ uint32_t dg_walks, dg_tries, dg_exh;
 
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const Sink sink{cols, &st->capacity, &st->nonf64};
@@ -181,6 +294,12 @@ __global__ __launch_bounds__(TPB) void nxg_dec_general_kernel(
         const uint64_t t0 = (uint64_t)tile * TILE;
         const uint64_t navail = W - t0;
         const uint32_t nlds = (uint32_t)(navail < (uint64_t)(TILE + HALO) ? navail : (TILE + HALO));
+        if (tid == 0) {
+            dg_walks = 0;
+            dg_tries = 0;
+            dg_exh = 0;
+            sh_bad = 0;
+        }
         for (uint32_t i = tid; i < (TILE + HALO) / 16; i += TPB) {
             const uint64_t o = t0 + 16ull * i;
             uint4 v = make_uint4(0, 0, 0, 0);
@@ -199,35 +318,54 @@ __global__ __launch_bounds__(TPB) void nxg_dec_general_kernel(
         const uint64_t c = t0 + (uint64_t)tid * CHUNK;
         const uint64_t cend = c + CHUNK;
 
-        // 1. speculate + walk + block repair
-        uint64_t e = (tile == 0 && tid == 0) ? 0 : speculate(s, c, cend);
+        // 1. speculate + bounded walk + block repair
+        uint32_t tries = 0;
+        uint64_t e = (tile == 0 && tid == 0) ? 0 : speculate(s, c, cend, tries);
         LaneRes r;
-        if (e != NONE) walk(s, e, cend, r);
-        else lane_clear(r, NONE);
-        repair(s, cend, e, r, sx, sek, &sh_flag);
-
-        // 2. tile aggregate: entry = first definite lane's entry, exit = last lane's exit
+        if (e != NONE) walk<M_BOUNDED>(s, e, cend, r);
+        else lane_set(r, S_NONE, NONE);
+        atomicAdd(&dg_tries, tries);
+        if (e != NONE) atomicAdd(&dg_walks, 1u);
         {
             const uint64_t m = __ballot(e != NONE);
             if (lane == 0) wfirst[wv] = m ? wv * 64 + (uint32_t)__builtin_ctzll(m) : 0xffffu;
-            se[tid] = e;
         }
+        __syncthreads();
+        uint32_t jstar = 0xffffu;
+        for (int i = 0; i < 4; i++) jstar = min(jstar, wfirst[i]);
+        __syncthreads();
+        // the tile's guess = the first lane with a guess; repair the chain from there
+        bool complete = false;
+        uint32_t rounds1 = 0;
+        if (tid == 0) {
+            sh_texit = NONE;
+            sh_tek = 0;
+        }
+        if (jstar < TPB)
+            rounds1 = repair<M_BOUNDED>(s, cend, jstar, e, r, sx, sst, wtop, wfirst, bx,
+                                        &dg_walks, complete, &sh_texit, &sh_tek);
+        if (r.st == S_EXH) atomicAdd(&dg_exh, 1u);
+
+        // 2. tile aggregate: entry = the anchor's guess, exit = last lane's exit; composable
+        // only if the repair verified every lane from the anchor on
         uint32_t trows, tctl, thb;
         uint64_t tch;
         block_excl_scan<uint32_t, TPB>(r.rows, scan32, &trows);
         block_excl_scan<uint32_t, TPB>(r.ctl, scan32, &tctl);
         block_excl_scan<uint32_t, TPB>(r.hb, scan32, &thb);
         block_excl_scan<uint64_t, TPB>(r.children, scan64, &tch);
-        uint32_t jstar = 0xffffu;
-        for (int i = 0; i < 4; i++) jstar = min(jstar, wfirst[i]);
-        const uint64_t tspec = jstar < TPB ? se[jstar] : NONE;
-        const uint64_t texit = sx[TPB - 1];
-        const uint32_t tek = sek[TPB - 1] & 0x7fffffffu;
+        if (tid == jstar) se[0] = e;
+        __syncthreads();
+        const bool composable = jstar < TPB && complete;
+        const uint64_t tspec = jstar < TPB ? se[0] : NONE;
+        const uint64_t texit = sh_texit;
+        const uint32_t tek = sh_tek;
+        __syncthreads();
         uint64_t* d = slots + (uint64_t)tile * SLOT_WORDS;
         if (tid == 0 && tile != 0) {
             st_agent(d + A_CHILD, tch);
             st_agent(d + A_CTLHB, (uint64_t)tctl | ((uint64_t)thb << 32));
-            st_agent(d + A_SPEC, tek ? tspec : (tspec == NONE ? NONE : tspec));
+            st_agent(d + A_SPEC, composable ? tspec : NONE);
             st_agent(d + A_EXIT, texit);
             st_agent(d + A_ERR, tek ? (((uint64_t)tek << 56) | (texit & POSM)) : 0ull);
             drain_stores();
@@ -238,12 +376,13 @@ __global__ __launch_bounds__(TPB) void nxg_dec_general_kernel(
         if (wv == 0) {
             Seg acc{false, true, NONE, 0, 0, 0, 0, 0, 0};
             uint32_t timeout = 0;
+            bool fallback = false;
             if (tile == 0) {
                 acc = Seg{true, true, 0, 0, 0, 0, 0, 0, 0};
             } else {
                 const uint64_t t_start = rt_now();
                 int64_t pred = (int64_t)tile - 1;
-                bool fallback = false, done = false;
+                bool done = false;
                 while (!done) {
                     const int64_t idx = pred - (int64_t)lane;
                     const uint64_t* q = slots + (uint64_t)(idx < 0 ? 0 : idx) * SLOT_WORDS;
@@ -276,7 +415,6 @@ __global__ __launch_bounds__(TPB) void nxg_dec_general_kernel(
                     const uint64_t incm = __ballot(isinc);
                     const int fi = incm ? __builtin_ctzll(incm) : 64;  // youngest inclusive
                     const int hi = fi - 1;                              // aggregate lanes [0, hi]
-                    // window summary of the aggregate lanes (young part of this window)
                     Seg w{hi >= 0, true, NONE, 0, 0, 0, 0, 0, 0};
                     if (hi >= 0) {
                         const uint64_t errm = __ballot((int)lane <= hi && xerr != 0);
@@ -317,8 +455,6 @@ __global__ __launch_bounds__(TPB) void nxg_dec_general_kernel(
                         const uint64_t er = __shfl(xerr, fi, 64);
                         inc.ek = (uint32_t)(er >> 56);
                         inc.out = inc.ek ? (er & POSM) : __shfl(xexit, fi, 64);
-                        if (idx < 0 && fi == (int)lane) {
-                        }
                         acc = compose(inc, acc);
                         if (!acc.ok) fallback = true;
                         done = true;
@@ -358,6 +494,7 @@ __global__ __launch_bounds__(TPB) void nxg_dec_general_kernel(
                 sh_ctl = acc.ctl;
                 sh_hb = acc.hb;
                 sh_timeout = timeout;
+                sh_fallback = fallback;
                 if (timeout) atomicOr(&st->timeout, 1u);
             }
         }
@@ -365,30 +502,32 @@ __global__ __launch_bounds__(TPB) void nxg_dec_general_kernel(
         const uint64_t E = sh_E;
         const bool dead = sh_ek != 0 || sh_timeout != 0;
 
-        // 4. redo from the true entry when the speculation was wrong
-        if (!dead && tile != 0 && E != tspec) {
+        // 4. exact phase from the true entry when the guess was wrong or a walk gave up
+        const bool redo = !dead && (E != tspec || !composable);
+        uint32_t rounds2 = 0;
+        if (redo) {
             if (tid == 0) {
                 e = E;
-                walk(s, e, cend, r);
+                walk<M_EXACT>(s, e, cend, r);
+                atomicAdd(&dg_walks, 1u);
             }
-            repair(s, cend, e, r, sx, sek, &sh_flag);
+            bool done;
+            rounds2 = repair<M_EXACT>(s, cend, 0, e, r, sx, sst, wtop, wfirst, bx, &dg_walks,
+                                      done, &sh_texit, &sh_tek);
+            if (!done && tid == 0) atomicOr(&st->timeout, 1u);  // unreachable by design
         }
 
         // 5. per-lane bases; tile exit
-        const bool live = !dead && e != NONE;
+        const bool live = !dead && e != NONE && r.st == S_OK;
         uint32_t r_tot, c_tot, h_tot;
         uint64_t ch_tot;
         const uint32_t rb = block_excl_scan<uint32_t, TPB>(live ? r.rows : 0u, scan32, &r_tot);
         const uint32_t cb = block_excl_scan<uint32_t, TPB>(live ? r.ctl : 0u, scan32, &c_tot);
         block_excl_scan<uint32_t, TPB>(live ? r.hb : 0u, scan32, &h_tot);
-        const uint64_t chb = block_excl_scan<uint64_t, TPB>(live ? r.children : 0ull, scan64, &ch_tot);
-        if (tid == TPB - 1) {
-            sx[0] = r.x;
-            sek[0] = r.ek;
-        }
-        __syncthreads();
-        uint64_t out_x = sx[0];
-        uint32_t out_ek = sek[0];
+        const uint64_t chb =
+            block_excl_scan<uint64_t, TPB>(live ? r.children : 0ull, scan64, &ch_tot);
+        uint64_t out_x = sh_texit;  // from the last completed repair
+        uint32_t out_ek = sh_tek;
         if (dead) {
             out_x = E;
             out_ek = sh_ek;
@@ -413,6 +552,13 @@ __global__ __launch_bounds__(TPB) void nxg_dec_general_kernel(
                 st->err_offset = out_ek ? out_x : 0;
                 st->path = 2;
             }
+            atomicAdd(&st->diag[0], redo ? 1ull : 0ull);
+            atomicAdd(&st->diag[1], sh_fallback ? 1ull : 0ull);
+            atomicAdd(&st->diag[2], (unsigned long long)(rounds1 + rounds2));
+            atomicAdd(&st->diag[3], (unsigned long long)dg_walks);
+            atomicAdd(&st->diag[4], (unsigned long long)dg_tries);
+            atomicAdd(&st->diag[5], jstar < TPB ? 0ull : 1ull);
+            atomicAdd(&st->diag[6], (unsigned long long)dg_exh);
         }
 
         // 7. emit: decode again, writing the columns (skipped once the frame is rejected)
@@ -420,9 +566,11 @@ __global__ __launch_bounds__(TPB) void nxg_dec_general_kernel(
             uint64_t row = row0 + rb, ctl = ctl0 + cb, child = ch0 + chb;
             uint64_t pos = e;
             const uint64_t stop = cend < W ? cend : W;
+            uint32_t work = 0;
             while (pos < stop) {
                 MsgInfo mi;
-                const uint32_t err = decode_msg<true, false>(s, pos, mi, &sink, row, child);
+                const uint32_t err =
+                    decode_msg<true, M_EXACT>(s, pos, mi, &sink, row, child, work);
                 if (err) break;  // unreachable: the walk validated this chain
                 if (mi.variant == 4) {
                     if (row < cols.cap_rows) cols.id[row] = mi.id;
@@ -430,6 +578,7 @@ __global__ __launch_bounds__(TPB) void nxg_dec_general_kernel(
                     row++;
                 } else if (!cols.ctl_row) {
                     atomicOr(&st->nonf64, 1u);
+                    ctl++;
                 } else {
                     if (ctl < cols.cap_ctl) {
                         cols.ctl_row[ctl] = row;
@@ -453,7 +602,7 @@ hipError_t nxg_launch_dec_general(const uint8_t* wire, uint64_t W, const ColsDes
                                   int grid, hipStream_t s) {
     const uint64_t nt = (W + TILE - 1) / TILE;
     if (nt == 0) return hipSuccess;
-    const int g = (int)(nt < (uint64_t)grid ? nt : (uint64_t)grid);
+    const uint64_t g = grid <= 0 ? nt : (nt < (uint64_t)grid ? nt : (uint64_t)grid);
     hipLaunchKernelGGL(nxg_dec_general_kernel, dim3(g), dim3(TPB), 0, s, wire, W, cd, tslots,
                        (uint32_t)nt, epoch, st, emit, nxg_zero_slot);
     return hipGetLastError();

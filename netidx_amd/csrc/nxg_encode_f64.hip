@@ -147,7 +147,7 @@ hipError_t nxg_launch_enc_f64(const uint64_t* id, const uint64_t* val, uint64_t 
                               int grid, hipStream_t s) {
     const uint64_t nt = (n + TILE - 1) / TILE;
     if (nt == 0) return hipSuccess;
-    const int g = (int)(nt < (uint64_t)grid ? nt : (uint64_t)grid);
+    const uint64_t g = grid <= 0 ? nt : (nt < (uint64_t)grid ? nt : (uint64_t)grid);
     hipLaunchKernelGGL(nxg_enc_f64_kernel, dim3(g), dim3(TPB), 0, s, id, val, n, out, cap, tstat,
                        (uint32_t)nt, epoch, st, nxg_zero_slot);
     return hipGetLastError();

@@ -286,7 +286,7 @@ hipError_t nxg_launch_enc_general(const ColsDesc& cd, const uint8_t* heap, uint8
     if (cd.n_ctl) hipLaunchKernelGGL(nxg_enc_ctl_scan_kernel, dim3(1), dim3(TPB), 0, s, cd, ctl_pre);
     const uint64_t nt = (cd.n_rows + TPB - 1) / TPB;
     if (nt) {
-        const int g = (int)(nt < (uint64_t)grid ? nt : (uint64_t)grid);
+        const uint64_t g = grid <= 0 ? nt : (nt < (uint64_t)grid ? nt : (uint64_t)grid);
         hipLaunchKernelGGL(nxg_enc_rows_kernel, dim3(g), dim3(TPB), 0, s, cd, heap, out, cap,
                            cd.n_ctl ? ctl_pre : nullptr, row_off, tstat, (uint32_t)nt, epoch, st, nxg_zero_slot);
     }

@@ -19,8 +19,12 @@ struct DevStatus {
     uint32_t nonf64;       // general path ran into content that F64-only columns cannot hold
     uint32_t pad0;
     uint64_t pad[2];
+    // diagnostics (general decode): 0 redo tiles, 1 look-back fallbacks, 2 repair rounds,
+    // 3 lane walks, 4 speculation attempts, 5 tiles without a speculated entry,
+    // 6 exhausted (budgeted) walks, 7 unused
+    unsigned long long diag[8];
 };
-static_assert(sizeof(DevStatus) == 96, "DevStatus layout");
+static_assert(sizeof(DevStatus) == 160, "DevStatus layout");
 
 // Look-back status granule (one 8-byte word, written with one sc1 store):
 //   bits 63:62 flag (1 aggregate, 2 inclusive), 61:44 call epoch, 43:0 value.
@@ -41,9 +45,9 @@ __host__ __device__ inline uint64_t lb_flag(uint64_t w, uint32_t epoch) {
 
 // ---- f64 decode geometry (nxg_decode_f64.hip) ----
 namespace f64dec {
-constexpr int TPB = 256;
+constexpr int TPB = 64;                  // one wave per workgroup: no cross-wave barriers
 constexpr int CHUNK = 64;                // bytes per lane
-constexpr int TILE = TPB * CHUNK;        // 16 KiB per tile
+constexpr int TILE = TPB * CHUNK;        // 4 KiB per tile
 constexpr int HALO = 128;                // look-ahead bytes loaded past the tile
 constexpr int WIN = 64;                  // merge-point search bound (bits of the walk mask)
 constexpr int MAXREC = TILE / 12 + 16;   // staging slots (records are >= 12 bytes)

@@ -12,14 +12,23 @@
 // Nested values are walked iteratively with an explicit stack. Children are allocated
 // depth-first, the same order as the recursive reference decoder, which produces them as it
 // goes.
+//
+// Modes:
+//   M_SPEC    plausibility only (no UTF-8 scan), small work budget: used to GUESS a start
+//   M_BOUNDED full validation with a work budget (E_BUDGET when exceeded): speculative walks,
+//             which may start from a wrong position and must not wander through megabytes
+//   M_EXACT   full validation, unbounded: walks from positions known to be message starts
 #pragma once
 #include "nxg_device.h"
 
 namespace nxgmsg {
 
 constexpr uint32_t E_OK = 0, E_UNKNOWN_TAG = 1, E_TOO_BIG = 2, E_INVALID = 3, E_SHORT = 4,
-                   E_DEPTH = 6, E_BUDGET = 100;  // E_BUDGET: speculation gave up (not an error)
+                   E_DEPTH = 6, E_BUDGET = 100;  // E_BUDGET: gave up, not a decode error
 constexpr uint64_t kMaxVec = 2ull * 1024 * 1024 * 1024;  // pack.rs:917
+enum Mode { M_SPEC = 0, M_BOUNDED = 1, M_EXACT = 2 };
+constexpr uint32_t kSpecBudget = 256;     // value headers per speculative decode
+constexpr uint32_t kWalkBudget = 2048;    // work units per bounded walk (headers + 16 B of text)
 
 // Bytes of the frame: [t0, t0+nlds) come from LDS, everything else from global memory.
 struct Src {
@@ -91,14 +100,22 @@ NXG_DEV void put(const Sink* k, bool row, uint64_t slot, uint32_t tag, uint64_t 
     }
 }
 
-// string/bytes payload: varint len; TooBig if len > remaining; UTF-8 unless !utf8 or !check
+// string/bytes payload: varint len; TooBig if len > remaining; UTF-8 for strings (not in
+// M_SPEC). In M_BOUNDED a long text spends work, one unit per 16 bytes.
+template <int MODE>
 NXG_DEV uint32_t dstr(const Src& s, uint64_t& p, uint64_t lim, bool utf8, uint64_t& off,
-                      uint64_t& len) {
+                      uint64_t& len, uint32_t& work) {
     uint64_t n;
     uint32_t e = dvar(s, p, lim, n);
     if (e) return e;
     if (n > lim - p) return E_TOO_BIG;
-    if (utf8 && !utf8_valid(s, p, n)) return E_INVALID;
+    if (utf8 && MODE != M_SPEC) {
+        if (MODE == M_BOUNDED) {
+            work += (uint32_t)min<uint64_t>(n >> 4, kWalkBudget);
+            if (work > kWalkBudget) return E_BUDGET;
+        }
+        if (!utf8_valid(s, p, n)) return E_INVALID;
+    }
     off = p;
     len = n;
     p += n;
@@ -106,21 +123,20 @@ NXG_DEV uint32_t dstr(const Src& s, uint64_t& p, uint64_t lim, bool utf8, uint64
 }
 
 // Decode one Value at p (limit lim) into (row?, slot), children from `child_next`.
-// SPEC=true: plausibility only (no UTF-8 scan, bounded work -> E_BUDGET).
-template <bool EMIT, bool SPEC>
+template <bool EMIT, int MODE>
 NXG_DEV uint32_t dvalue(const Src& s, uint64_t& p, uint64_t lim, const Sink* k, bool row,
-                        uint64_t slot, uint64_t& child_next) {
+                        uint64_t slot, uint64_t& child_next, uint32_t& work) {
     uint64_t frem[NXG_MAX_DEPTH + 2];
     uint64_t fslot[NXG_MAX_DEPTH + 2];
     int top = -1;
     int depth = 0;
     bool is_row = row;
     uint64_t cur = slot;
-    uint32_t budget = 0;
 #pragma unroll 1
     for (;;) {
         if (depth > NXG_MAX_DEPTH) return E_DEPTH;
-        if (SPEC && ++budget > 256) return E_BUDGET;
+        if (MODE == M_SPEC && ++work > kSpecBudget) return E_BUDGET;
+        if (MODE == M_BOUNDED && ++work > kWalkBudget) return E_BUDGET;
         if (p >= lim) return E_SHORT;
         const uint32_t t = s.byte(p++);
         uint64_t v, v2, off, len;
@@ -153,7 +169,8 @@ NXG_DEV uint32_t dvalue(const Src& s, uint64_t& p, uint64_t lim, const Sink* k, 
             if (!(e = dvar(s, p, lim, v))) put<EMIT>(k, is_row, cur, 5, v, 0);
             break;
         case 7:
-            if (!(e = dvar(s, p, lim, v))) put<EMIT>(k, is_row, cur, 7, (v >> 1) ^ (0ull - (v & 1ull)), 0);
+            if (!(e = dvar(s, p, lim, v)))
+                put<EMIT>(k, is_row, cur, 7, (v >> 1) ^ (0ull - (v & 1ull)), 0);
             break;
         case 8:
             if (!(e = dfix(s, p, lim, 4, v))) put<EMIT>(k, is_row, cur, 8, v, 0);
@@ -186,10 +203,12 @@ NXG_DEV uint32_t dvalue(const Src& s, uint64_t& p, uint64_t lim, const Sink* k, 
         }
         case 12:
         case 18:
-            if (!(e = dstr(s, p, lim, !SPEC, off, len))) put<EMIT>(k, is_row, cur, t, off, (uint32_t)len);
+            if (!(e = dstr<MODE>(s, p, lim, true, off, len, work)))
+                put<EMIT>(k, is_row, cur, t, off, (uint32_t)len);
             break;
         case 13:
-            if (!(e = dstr(s, p, lim, false, off, len))) put<EMIT>(k, is_row, cur, 13, off, (uint32_t)len);
+            if (!(e = dstr<MODE>(s, p, lim, false, off, len, work)))
+                put<EMIT>(k, is_row, cur, 13, off, (uint32_t)len);
             break;
         case 14:
             put<EMIT>(k, is_row, cur, 14, 1, 0);
@@ -226,7 +245,8 @@ NXG_DEV uint32_t dvalue(const Src& s, uint64_t& p, uint64_t lim, const Sink* k, 
             // Error(Value) whose inner value is a String is Error(String) = wire tag 18
             if (p < lim && s.byte(p) == 12u) {
                 p++;
-                if (!(e = dstr(s, p, lim, !SPEC, off, len))) put<EMIT>(k, is_row, cur, 18, off, (uint32_t)len);
+                if (!(e = dstr<MODE>(s, p, lim, true, off, len, work)))
+                    put<EMIT>(k, is_row, cur, 18, off, (uint32_t)len);
                 break;
             }
             kids = 1;
@@ -291,13 +311,17 @@ struct MsgInfo {
 // Decode the message starting at `pos`. On success, info.next is the position after the
 // length-wrapped region (trailing bytes skipped, pack.rs:551-553). Update values are written
 // to row `row` (EMIT); children are allocated from child_next.
-template <bool EMIT, bool SPEC>
+template <bool EMIT, int MODE>
 NXG_DEV uint32_t decode_msg(const Src& s, uint64_t pos, MsgInfo& info, const Sink* k,
-                            uint64_t row, uint64_t& child_next) {
+                            uint64_t row, uint64_t& child_next, uint32_t& work) {
     uint64_t p = pos, L;
     uint32_t e = dvar(s, p, s.W, L);
     if (e) return e;
     if (L < 1) return E_SHORT;
+    // a guess must look like encoder output: minimal length varint (and, below, content that
+    // fills the length-wrapped region exactly). Otherwise a payload byte >= 0x80 just before a
+    // true start makes a "shadow" message with a huge length and skipped trailing bytes.
+    if (MODE == M_SPEC && p - pos != vl64(L)) return E_INVALID;
     const uint64_t take = L - vl64(L);
     const uint64_t lim = take < s.W - p ? p + take : s.W;
     info.next = lim;
@@ -308,22 +332,24 @@ NXG_DEV uint32_t decode_msg(const Src& s, uint64_t pos, MsgInfo& info, const Sin
     switch (variant) {
     case 0:
     case 1:
-        return dstr(s, p, lim, !SPEC, off, len);
+        return dstr<MODE>(s, p, lim, true, off, len, work);
     case 2:
         return dvar(s, p, lim, v);
     case 3:
-        if ((e = dstr(s, p, lim, !SPEC, off, len))) return e;
+        if ((e = dstr<MODE>(s, p, lim, true, off, len, work))) return e;
         if ((e = dvar(s, p, lim, v))) return e;
-        return dvalue<false, SPEC>(s, p, lim, k, false, 0, dummy);
+        return dvalue<false, MODE>(s, p, lim, k, false, 0, dummy, work);
     case 4:
         if ((e = dvar(s, p, lim, v))) return e;
         info.id = v;
-        return dvalue<EMIT, SPEC>(s, p, lim, k, true, row, child_next);
+        e = dvalue<EMIT, MODE>(s, p, lim, k, true, row, child_next, work);
+        if (MODE == M_SPEC && !e && p != lim) return E_INVALID;  // exact fit (see above)
+        return e;
     case 5:
         return E_OK;
     case 6:
         if ((e = dvar(s, p, lim, v))) return e;
-        if ((e = dvalue<false, SPEC>(s, p, lim, k, false, 0, dummy))) return e;
+        if ((e = dvalue<false, MODE>(s, p, lim, k, false, 0, dummy, work))) return e;
         e = dvar(s, p, lim, v);
         return e == E_SHORT ? E_OK : e;  // #[pack(default)] WriteId
     default:
