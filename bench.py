@@ -11,7 +11,7 @@ Each step is verified bit-exact against the columns it was encoded from. The inp
 the product encoder (config 4); the CPU oracle is only used in the cpu_baseline leg.
 
 Also reported on the same JSON line:
-  roofline       the decode kernel's algorithmic bytes (W + 16 N) / mean launch time (HIP
+  roofline       the decode's algorithmic bytes (W + 16 N) / mean time of one decode (HIP
                  events on the codec stream) vs the 8 TB/s HBM3E peak;
   cpu_baseline   the C restatement of the reference decoder (oracle/, 1 core) on this host;
   extras         10^8-record decode (north-star size), mixed-tag decode (config 3), f64 encode
@@ -27,7 +27,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-KERNEL_DEC_F64 = "nxg_dec_f64_kernel"
+KERNEL_DEC_F64 = "nxg_f64_count_kernel+nxg_f64_emit_kernel"
 
 
 def log(*a):

@@ -50,8 +50,7 @@ struct NxgCtx {
     hipStream_t own = nullptr;
     hipStream_t stream = nullptr;
     int ncu = 0;
-    int grid_dec_f64 = 0, grid_dec_gen = 0, grid_enc_f64 = 0, grid_enc_gen = 0;
-    int grid_dec_f64_persistent = 0;
+    int grid_dec_gen = 0, grid_enc_f64 = 0, grid_enc_gen = 0;
     // status ring: one DevStatus per call, the whole ring re-zeroed once per lap
     DevStatus* dst = nullptr;
     DevStatus* hst = nullptr;  // pinned mirror
@@ -59,6 +58,8 @@ struct NxgCtx {
     uint32_t epoch = 0;
     uint64_t* tstat = nullptr;
     size_t tstat_words = 0;
+    uint64_t* fscratch = nullptr;  // f64 decode: per-run counts / first indices (+ ticket)
+    int wgs_dec_f64 = 0;
     uint8_t* dframe = nullptr;
     size_t dframe_cap = 0;
     uint64_t* escratch = nullptr;
@@ -246,10 +247,9 @@ NxgColumns staged_view(NxgCtx* c, const NxgColumns* like) {
 
 bool enqueue_dec_fast(NxgCtx* c, const uint8_t* f, uint64_t len, NxgColumns* out, DevStatus* st,
                       NetidxError* err) {
-    const uint64_t nt = (len + f64dec::TILE - 1) / f64dec::TILE;
-    if (!ensure_tstat(c, nt, err)) return false;
-    HIPCHK(nxg_launch_dec_f64(f, len, out->id, out->fixed, out->cap_rows, c->tstat, c->epoch, st,
-                              c->grid_dec_f64, c->stream));
+    HIPCHK(nxg_launch_dec_f64(f, len, out->id, out->fixed, out->cap_rows, c->fscratch,
+                              reinterpret_cast<uint32_t*>(c->fscratch + f64dec::SCRATCH_WORDS),
+                              c->wgs_dec_f64, st, c->stream));
     return true;
 }
 
@@ -270,11 +270,6 @@ bool finish_decode(NxgCtx* c, const uint8_t* f, uint64_t len, NxgColumns* out, i
     HIPCHK(hipMemcpyAsync(c->hst + slot, st, sizeof(DevStatus), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     DevStatus h = c->hst[slot];
-    if (tried_fast && h.timeout && c->grid_dec_f64 <= 0) {
-        // the one-tile-per-workgroup schedule relies on in-order dispatch; if the watchdog
-        // ever fires, this ctx switches to the persistent co-resident schedule for good
-        c->grid_dec_f64 = c->grid_dec_f64_persistent;
-    }
     if (tried_fast && len > 0 && h.fast_fail) {
         DevStatus* st2;
         uint32_t slot2;
@@ -460,15 +455,13 @@ NxgCtx* nxg_ctx_new(int device, NetidxError* err) {
     if ((e = hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking)) != hipSuccess)
         return fail("hipStreamCreate", e);
     c->stream = c->own;
-    // Default schedule: one workgroup per tile in blockIdx order (grid 0). The decoupled
-    // look-back then always finds recent inclusive prefixes. Persistent fallback: every
-    // workgroup co-resident, with one block of margin under the occupancy answer
-    // (MI355X_MICROARCH.md residency notes). NXG_PERSISTENT=1 forces it.
+    // Default schedule for the look-back kernels: one workgroup per tile in blockIdx order
+    // (grid 0), so the look-back always finds recent inclusive prefixes. NXG_PERSISTENT=1
+    // selects a persistent grid instead: every workgroup co-resident, with one block of margin
+    // under the occupancy answer (MI355X_MICROARCH.md residency notes).
     auto grid = [&](int occ) { return c->ncu * std::max(1, occ > 2 ? occ - 1 : occ); };
-    c->grid_dec_f64_persistent = grid(nxg_occupancy_dec_f64());
     const char* pe = getenv("NXG_PERSISTENT");
     const bool persist = pe && pe[0] == '1';
-    c->grid_dec_f64 = persist ? c->grid_dec_f64_persistent : 0;
     c->grid_dec_gen = persist ? grid(nxg_occupancy_dec_general()) : 0;
     c->grid_enc_f64 = persist ? grid(nxg_occupancy_enc_f64()) : 0;
     c->grid_enc_gen = persist ? grid(nxg_occupancy_enc_general()) : 0;
@@ -479,6 +472,12 @@ NxgCtx* nxg_ctx_new(int device, NetidxError* err) {
     if ((e = hipHostMalloc(&c->hst, sizeof(DevStatus) * kStatusRing, hipHostMallocDefault)) !=
         hipSuccess)
         return fail("hipHostMalloc(status)", e);
+    // f64 decode scratch: run counts, run first indices, running total, then the ticket word;
+    // the kernels leave the running total and the ticket zeroed after every call
+    const size_t fw = f64dec::SCRATCH_WORDS + 1;
+    if ((e = hipMalloc(&c->fscratch, fw * 8)) != hipSuccess) return fail("hipMalloc(fscratch)", e);
+    if ((e = hipMemset(c->fscratch, 0, fw * 8)) != hipSuccess) return fail("hipMemset(fscratch)", e);
+    c->wgs_dec_f64 = nxg_dec_f64_wgs(c->ncu);
     return c;
 }
 
@@ -488,6 +487,7 @@ void nxg_ctx_destroy(NxgCtx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->dcols_valid) cols_free_impl(&c->dcols);
     if (c->tstat) (void)hipFree(c->tstat);
+    if (c->fscratch) (void)hipFree(c->fscratch);
     if (c->dframe) (void)hipFree(c->dframe);
     if (c->escratch) (void)hipFree(c->escratch);
     if (c->dheap) (void)hipFree(c->dheap);

@@ -282,7 +282,7 @@ __global__ __launch_bounds__(TPB) void nxg_dec_general_kernel(
     __shared__ uint64_t bx[2];
     __shared__ uint64_t sh_texit;
     __shared__ uint32_t sh_tek;
-    __shared__ uint32_t sh_flag, sh_bad;
+    __shared__ uint32_t sh_flag;
     __shared__ uint64_t sh_E, sh_rows, sh_ch, sh_ctl, sh_hb;
     __shared__ uint32_t sh_ek, sh_timeout, sh_fallback;
     __shared__ uint32_t dg_walks, dg_tries, dg_exh;
@@ -298,7 +298,6 @@ __global__ __launch_bounds__(TPB) void nxg_dec_general_kernel(
             dg_walks = 0;
             dg_tries = 0;
             dg_exh = 0;
-            sh_bad = 0;
         }
         for (uint32_t i = tid; i < (TILE + HALO) / 16; i += TPB) {
             const uint64_t o = t0 + 16ull * i;

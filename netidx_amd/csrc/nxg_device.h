@@ -67,6 +67,72 @@ NXG_DEV T wave_sum(T v) {
     return v;
 }
 
+// ---- decoupled look-back with a wide window ---------------------------------------------------
+// Exclusive prefix of `tile` over the epoch-tagged tile words tstat[0..tile). Called by one full
+// wave. The first poll covers the 64 nearest predecessors (lane l owns tile-1-l); when none of
+// them is inclusive yet, later polls cover 64*U predecessors at once (word tile-1-64u-l for
+// u = 0..U-1, each load instruction still one contiguous 512-byte run), so the inclusive front
+// advances 64*U tiles per memory round trip instead of 64. Sets `give_up` on the watchdog or when
+// *abort becomes non-zero (abort may be null).
+template <int U>
+NXG_DEV uint64_t lookback_prefix(const uint64_t* tstat, uint32_t tile, uint32_t epoch,
+                                 const uint32_t* abort, bool& give_up) {
+    const uint32_t lane = lane_id();
+    uint64_t base = 0;
+    int64_t pred = (int64_t)tile - 1;
+    const uint64_t t_start = rt_now();
+    give_up = false;
+    int nu = 1;  // rows of 64 words polled in this step
+    while (pred >= 0) {
+        uint64_t s[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int64_t idx = pred - 64 * u - (int64_t)lane;
+            s[u] = (u < nu && idx >= 0) ? ld_agent(&tstat[idx]) : lb_word(kFlagInc, epoch, 0);
+        }
+        int uf;          // row of the nearest inclusive word (nu: none)
+        uint32_t lf;     // its lane
+        for (;;) {
+            uf = nu;
+            lf = 64;
+            bool hole = false;
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                if (u >= nu || uf < nu) break;
+                const uint64_t f = lb_flag(s[u], epoch);
+                const uint64_t m = __ballot(f == kFlagInc);
+                if (m) {
+                    uf = u;
+                    lf = (uint32_t)__builtin_ctzll(m);
+                    hole |= (f == 0) && lane < lf;
+                } else {
+                    hole |= (f == 0);
+                }
+            }
+            if (!__any(hole)) break;
+            __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const int64_t idx = pred - 64 * u - (int64_t)lane;
+                if (u < nu && lb_flag(s[u], epoch) == 0) s[u] = ld_agent(&tstat[idx]);
+            }
+            if ((abort && ld_agent32(abort)) || rt_now() - t_start > kSpinTicks) {
+                give_up = true;
+                return 0;
+            }
+        }
+        uint64_t part = 0;
+#pragma unroll
+        for (int u = 0; u < U; u++)
+            if (u < uf || (u == uf && lane <= lf)) part += s[u] & kValMask;
+        base += wave_sum<uint64_t>(part);
+        if (uf < nu) break;
+        pred -= 64 * nu;
+        nu = U;
+    }
+    return base;
+}
+
 // exclusive scan over a 256-thread block; `tmp` = 4 (or more) T in LDS. Returns the exclusive
 // prefix, sets *total. Contains __syncthreads().
 template <typename T, int NT>

@@ -77,30 +77,8 @@ __global__ __launch_bounds__(TPB) void nxg_enc_f64_kernel(
         if (tid < 64) {
             uint64_t base = 0;
             if (tile != 0) {
-                int64_t pred = (int64_t)tile - 1;
-                const uint64_t t_start = rt_now();
-                bool give_up = false;
-                for (;;) {
-                    const int64_t idx = pred - (int64_t)lane;
-                    uint64_t s = idx >= 0 ? ld_agent(&tstat[idx]) : lb_word(kFlagInc, epoch, 0);
-                    while (!__all(lb_flag(s, epoch) != 0)) {
-                        __builtin_amdgcn_s_sleep(1);
-                        if (lb_flag(s, epoch) == 0) s = ld_agent(&tstat[idx]);
-                        if (rt_now() - t_start > kSpinTicks) {
-                            give_up = true;
-                            break;
-                        }
-                    }
-                    if (give_up) break;
-                    const uint64_t inc = __ballot(lb_flag(s, epoch) == kFlagInc);
-                    if (inc) {
-                        const uint32_t first = (uint32_t)__builtin_ctzll(inc);
-                        base += wave_sum<uint64_t>(lane <= first ? (s & kValMask) : 0ull);
-                        break;
-                    }
-                    base += wave_sum<uint64_t>(s & kValMask);
-                    pred -= 64;
-                }
+                bool give_up;
+                base = lookback_prefix<LB_U>(tstat, tile, epoch, nullptr, give_up);
                 if (give_up && lane == 0) atomicOr(&st->timeout, 1u);
                 if (lane == 0) st_agent(&tstat[tile], lb_word(kFlagInc, epoch, base + tbytes));
             }

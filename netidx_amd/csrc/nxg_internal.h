@@ -5,7 +5,7 @@
 
 #include "../../include/nxg_codec.h"
 
-// Per-call device status block (zeroed by hipMemsetAsync before every call).
+// Per-call device status block (a ring slot, zeroed in-kernel 128 calls ahead: zero_status).
 struct DevStatus {
     uint64_t n_rows, n_children, n_ctl, n_heartbeat;  // totals written by the last tile
     uint32_t err_kind;                                 // first error in wire order
@@ -45,12 +45,16 @@ __host__ __device__ inline uint64_t lb_flag(uint64_t w, uint32_t epoch) {
 
 // ---- f64 decode geometry (nxg_decode_f64.hip) ----
 namespace f64dec {
-constexpr int TPB = 64;                  // one wave per workgroup: no cross-wave barriers
+constexpr int TPB = 256;                 // 4 independent waves per workgroup
+constexpr int WAVES = TPB / 64;
 constexpr int CHUNK = 64;                // bytes per lane
-constexpr int TILE = TPB * CHUNK;        // 4 KiB per tile
+constexpr int TILE = 64 * CHUNK;         // 4 KiB per tile (one wave walks one tile at a time)
 constexpr int HALO = 128;                // look-ahead bytes loaded past the tile
 constexpr int WIN = 64;                  // merge-point search bound (bits of the walk mask)
-constexpr int MAXREC = TILE / 12 + 16;   // staging slots (records are >= 12 bytes)
+constexpr int MAXREC = TILE / 12 + 16;   // record slots per tile (records are >= 12 bytes)
+constexpr int SEG_TILES = 1 << 24;         // tiles per segment: count, then emit (one segment measured fastest)
+constexpr int MAX_WGS = 2048;            // workgroups per pass (one run per wave)
+constexpr int SCRATCH_WORDS = MAX_WGS * WAVES / 2 + MAX_WGS / 2 + MAX_WGS + 1;
 }  // namespace f64dec
 
 // ---- general decode geometry (nxg_decode_general.hip) ----
@@ -64,6 +68,7 @@ constexpr int SLOT_WORDS = 16;     // per-tile look-back descriptor (agg 8 words
 
 // ---- f64 encode geometry ----
 namespace f64enc {
+constexpr int LB_U = 1;                 // look-back window rows (64 tiles each); wider measured slower
 constexpr int TPB = 256;
 constexpr int RPT = 4;                 // records per thread
 constexpr int TILE = TPB * RPT;        // records per tile
@@ -78,9 +83,13 @@ __device__ inline void zero_status(DevStatus* zst) {
     if (zst && blockIdx.x == 0 && threadIdx.x == 0) *zst = DevStatus{};
 }
 extern thread_local DevStatus* nxg_zero_slot;  // host side: passed through to the kernels
+// f64 decode: count pass + emit pass per segment, `wgs` workgroups each (nxg_dec_f64_wgs).
+// `scratch` holds f64dec::SCRATCH_WORDS words (no initialisation needed); `ticket` one zeroed
+// word (left zeroed on return).
 hipError_t nxg_launch_dec_f64(const uint8_t* wire, uint64_t W, uint64_t* oid, uint64_t* oval,
-                              uint64_t cap, uint64_t* tstat, uint32_t epoch, DevStatus* st,
-                              int grid, hipStream_t s);
+                              uint64_t cap, uint64_t* scratch, uint32_t* ticket, int wgs,
+                              DevStatus* st, hipStream_t s);
+int nxg_dec_f64_wgs(int ncu);
 hipError_t nxg_launch_dec_general(const uint8_t* wire, uint64_t W, const ColsDesc& cols,
                                   uint64_t* tslots, uint32_t epoch, DevStatus* st, int emit,
                                   int grid, hipStream_t s);
@@ -90,7 +99,6 @@ hipError_t nxg_launch_enc_f64(const uint64_t* id, const uint64_t* val, uint64_t 
 hipError_t nxg_launch_enc_general(const ColsDesc& cols, const uint8_t* heap, uint8_t* out,
                                   uint64_t cap, uint64_t* scratch, uint64_t* tstat,
                                   uint32_t epoch, DevStatus* st, int grid, hipStream_t s);
-int nxg_occupancy_dec_f64();
 int nxg_occupancy_dec_general();
 int nxg_occupancy_enc_f64();
 int nxg_occupancy_enc_general();
