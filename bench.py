@@ -54,13 +54,8 @@ def barrier(world):
 
 
 def max_over_ranks(x, world):
-    if world == 1:
-        return x
-    import torch
-    import torch.distributed as dist
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item())
+    from netidx_amd import shard
+    return shard.max_over_ranks(x, world, device="cuda")
 
 
 def make_f64_wire(codec, n, rank):
@@ -205,17 +200,17 @@ def extras_single_gpu(codec, stream, steps, warmup):
 
 def extras_multi_gpu(codec, world, rank, stream):
     """Config 5: 10^8 records sharded by record; each rank encodes its shard, then an RCCL
-    all-gather (padded to the largest shard) assembles the full wire on every GPU."""
+    all-gather (padded to the longest shard, netidx_amd/shard.py) assembles the full frame on
+    every GPU. This is the path's only collective."""
     import netidx_amd
     import torch
-    import torch.distributed as dist
-    from netidx_amd import synth
+    from netidx_amd import shard, synth
     total = 100_000_000
-    n = total // world
-    ids, vals = synth.f64_columns(n, synth.SEED_8GPU, id_offset=rank * n)
+    b, e = shard.shard_range(total, world, rank)
+    n = e - b
+    ids, vals = synth.f64_columns(n, synth.SEED_8GPU, id_offset=b)
     cols = netidx_amd.columns_from_arrays(ids, vals)
     dout = torch.empty(21 * n + 64, dtype=torch.uint8, device="cuda")
-    lens = torch.zeros(world, dtype=torch.int64, device="cuda")
     times = []
     for it in range(3):
         barrier(world)
@@ -223,16 +218,11 @@ def extras_multi_gpu(codec, world, rank, stream):
         t0 = time.perf_counter()
         ln = codec.encode_async(cols, None, dout.data_ptr(), dout.numel())
         codec.sync()
-        mine = torch.tensor([ln.value], dtype=torch.int64, device="cuda")
-        dist.all_gather_into_tensor(lens, mine)
-        mx = int(lens.max().item())
-        gathered = torch.empty(world * mx, dtype=torch.uint8, device="cuda")
-        dist.all_gather_into_tensor(gathered, dout[:mx])
+        full, lengths = shard.gather_frames(dout, ln.value, world)
         torch.cuda.synchronize()
         times.append(time.perf_counter() - t0)
     t = max_over_ranks(min(times), world)
-    wire_total = int(lens.sum().item())
-    return {"records": total, "wire_bytes": wire_total, "world": world,
+    return {"records": total, "wire_bytes": int(full.numel()), "world": world,
             "encode_allgather_ms": round(t * 1e3, 3),
             "M_updates_s": round(total / t / 1e6, 1)}
 
