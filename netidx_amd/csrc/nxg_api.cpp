@@ -58,8 +58,10 @@ struct NxgCtx {
     uint32_t epoch = 0;
     uint64_t* tstat = nullptr;
     size_t tstat_words = 0;
-    uint64_t* fscratch = nullptr;  // f64 decode: per-run counts / first indices (+ ticket)
+    uint64_t* fscratch = nullptr;  // f64 decode: per-run / per-workgroup record counts
     int wgs_dec_f64 = 0;
+    uint8_t* fmoff = nullptr;      // f64 decode: merge-point offsets, 64 B per tile
+    size_t fmoff_cap = 0;
     uint8_t* dframe = nullptr;
     size_t dframe_cap = 0;
     uint64_t* escratch = nullptr;
@@ -115,6 +117,18 @@ bool ensure_tstat(NxgCtx* c, size_t words, NetidxError* err) {
     HIPCHK(hipMalloc(&c->tstat, n * 8));
     HIPCHK(hipMemsetAsync(c->tstat, 0, n * 8, c->stream));
     c->tstat_words = n;
+    return true;
+}
+
+bool ensure_fmoff(NxgCtx* c, size_t bytes, NetidxError* err) {
+    if (bytes <= c->fmoff_cap) return true;
+    size_t n = std::max(bytes, c->fmoff_cap * 2);
+    n = std::max<size_t>(n, 1 << 16);
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (c->fmoff) HIPCHK(hipFree(c->fmoff));
+    c->fmoff = nullptr;
+    HIPCHK(hipMalloc(&c->fmoff, n));
+    c->fmoff_cap = n;
     return true;
 }
 
@@ -247,8 +261,8 @@ NxgColumns staged_view(NxgCtx* c, const NxgColumns* like) {
 
 bool enqueue_dec_fast(NxgCtx* c, const uint8_t* f, uint64_t len, NxgColumns* out, DevStatus* st,
                       NetidxError* err) {
-    HIPCHK(nxg_launch_dec_f64(f, len, out->id, out->fixed, out->cap_rows, c->fscratch,
-                              reinterpret_cast<uint32_t*>(c->fscratch + f64dec::SCRATCH_WORDS),
+    if (!ensure_fmoff(c, 64 * nxg_dec_f64_tiles(len), err)) return false;
+    HIPCHK(nxg_launch_dec_f64(f, len, out->id, out->fixed, out->cap_rows, c->fscratch, c->fmoff,
                               c->wgs_dec_f64, st, c->stream));
     return true;
 }
@@ -472,9 +486,8 @@ NxgCtx* nxg_ctx_new(int device, NetidxError* err) {
     if ((e = hipHostMalloc(&c->hst, sizeof(DevStatus) * kStatusRing, hipHostMallocDefault)) !=
         hipSuccess)
         return fail("hipHostMalloc(status)", e);
-    // f64 decode scratch: run counts, run first indices, running total, then the ticket word;
-    // the kernels leave the running total and the ticket zeroed after every call
-    const size_t fw = f64dec::SCRATCH_WORDS + 1;
+    // f64 decode scratch: per-run and per-workgroup record counts
+    const size_t fw = f64dec::SCRATCH_WORDS;
     if ((e = hipMalloc(&c->fscratch, fw * 8)) != hipSuccess) return fail("hipMalloc(fscratch)", e);
     if ((e = hipMemset(c->fscratch, 0, fw * 8)) != hipSuccess) return fail("hipMemset(fscratch)", e);
     c->wgs_dec_f64 = nxg_dec_f64_wgs(c->ncu);
@@ -488,6 +501,7 @@ void nxg_ctx_destroy(NxgCtx* c) {
     if (c->dcols_valid) cols_free_impl(&c->dcols);
     if (c->tstat) (void)hipFree(c->tstat);
     if (c->fscratch) (void)hipFree(c->fscratch);
+    if (c->fmoff) (void)hipFree(c->fmoff);
     if (c->dframe) (void)hipFree(c->dframe);
     if (c->escratch) (void)hipFree(c->escratch);
     if (c->dheap) (void)hipFree(c->dheap);

@@ -28,6 +28,7 @@ using namespace f64dec;
 namespace {
 
 constexpr uint32_t FAIL = 0xffffffffu;
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));  // first-class vector: no memcpy
 
 // 16 bytes at tile-relative byte `rel` (any alignment) as four little-endian dwords.
 NXG_DEV void load16(const uint8_t* buf, uint32_t rel, uint32_t& e0, uint32_t& e1, uint32_t& e2,
@@ -82,8 +83,9 @@ NXG_DEV uint32_t merge_point(const uint8_t* buf, uint32_t r, uint64_t t0, uint64
     const uint64_t abs_r = t0 + r;
     if (abs_r >= W) return (uint32_t)(W - t0);  // chunk past the end: the END position
     const uint64_t remr = W - abs_r;
-    const uint32_t* w = reinterpret_cast<const uint32_t*>(buf + r);
-    const uint32_t d0 = w[0], d1 = w[1], d2 = w[2], d3 = w[3], d4 = w[4];
+    const u32x4 q = *reinterpret_cast<const u32x4*>(buf + r);  // r is 64-byte aligned
+    const uint32_t d0 = q.x, d1 = q.y, d2 = q.z, d3 = q.w;
+    const uint32_t d4 = *reinterpret_cast<const uint32_t*>(buf + r + 16);
     // candidate starts: byte in 12..15 followed by 0x04
     const uint32_t a = nib(zero_bytes((d0 & 0xfcfcfcfcu) ^ 0x0c0c0c0cu)) |
                        (nib(zero_bytes((d1 & 0xfcfcfcfcu) ^ 0x0c0c0c0cu)) << 4) |
@@ -135,26 +137,29 @@ NXG_DEV uint4 ld16_guard(const uint8_t* __restrict__ wire, uint64_t off, uint64_
 
 // One 4 KiB tile plus HALO look-ahead bytes in registers: lane owns the 16-byte pieces
 // i*1024 + lane*16 (coalesced); lanes < HALO/16 also own one halo piece.
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));  // first-class vector: no memcpy
 struct TileRegs {
     u32x4 v[4];
     u32x4 h;
+    uint32_t m;  // this lane's merge-point offset from the count pass (emit pass only)
 };
 NXG_DEV void tile_load(TileRegs& r, const uint8_t* __restrict__ wire, uint64_t t0, uint64_t W,
-                       uint32_t lane) {
+                       uint32_t lane, const uint8_t* moff) {
+    if (moff) r.m = moff[lane];
 #pragma unroll
     for (int i = 0; i < 4; i++) {
         const uint4 x = ld16_guard(wire, t0 + i * 1024 + lane * 16, W);
         r.v[i] = u32x4{x.x, x.y, x.z, x.w};
     }
-    const uint4 x = ld16_guard(wire, t0 + TILE + (lane & (HALO / 16 - 1)) * 16, W);
+    const uint4 x = ld16_guard(wire, t0 + IMG + (lane & (HALO / 16 - 1)) * 16, W);
     r.h = u32x4{x.x, x.y, x.z, x.w};
 }
 // The same for a tile whose bytes and halo lie inside the frame: straight-line loads only, so
 // the compiler can wait for exactly the oldest tile in flight (vmcnt(N), not vmcnt(0)). Lanes
 // past the halo re-read its lines instead of branching.
+template <bool MOFF>
 NXG_DEV void tile_load_full(TileRegs& r, const uint8_t* __restrict__ wire, uint64_t t0,
-                            uint32_t lane) {
+                            uint32_t lane, const uint8_t* moff) {
+    if (MOFF) r.m = moff[lane];
     const u32x4* p = reinterpret_cast<const u32x4*>(wire + t0);
 #pragma unroll
     for (int i = 0; i < 4; i++) r.v[i] = p[i * 64 + lane];
@@ -165,7 +170,7 @@ NXG_DEV void tile_store(uint8_t* buf, const TileRegs& r, uint32_t lane) {
     for (int i = 0; i < 4; i++) *reinterpret_cast<u32x4*>(buf + i * 1024 + lane * 16) = r.v[i];
     // every lane stores its halo piece; lanes that share a piece write identical bytes (no
     // branch, so the compiler can keep later tiles' loads in flight across this store)
-    *reinterpret_cast<u32x4*>(buf + TILE + (lane & (HALO / 16 - 1)) * 16) = r.h;
+    *reinterpret_cast<u32x4*>(buf + IMG + (lane & (HALO / 16 - 1)) * 16) = r.h;
 }
 // A wave's LDS image is private to it and LDS operations of one wave complete in order, so only
 // the compiler has to be kept from moving accesses across this point.
@@ -175,26 +180,32 @@ NXG_DEV void wave_lds_order() {
     asm volatile("" ::: "memory");
 }
 
-// Records of this lane's chunk [X_lane, X_lane+1) of `tile` (buf = the tile's LDS image).
-// Sets `bad` if the chunk is not a chain of valid f64 records from merge point to merge point.
-// With POS, the tile-relative record starts go to pslot[lane*SLOTS + k].
-constexpr int SLOTS = 12;  // records a lane can own: span < CHUNK + WIN bytes, >= 12 B each
-template <bool POS>
-NXG_DEV uint32_t chunk_walk(const uint8_t* buf, uint64_t tile, uint64_t W, uint32_t lane,
-                            uint16_t* pslot, bool& bad) {
-    const uint64_t t0 = tile * TILE;
-    uint32_t xa;
-    if (tile == 0 && lane == 0) {
+// Merge point X_lane of this lane's chunk [64*lane, 64*lane+64) of `tile` (buf = the tile's
+// LDS image): FAIL if the walks starting there do not merge. Lane 63's chunk starts at STRIDE,
+// so its merge point is the next tile's X_0 and the tiles join without a gap or overlap.
+NXG_DEV uint32_t chunk_merge(const uint8_t* buf, uint64_t tile, uint64_t W, uint32_t lane) {
+    if (tile == 0 && lane == 0) {  // the frame's first record starts at byte 0
         uint32_t e0, e1, e2, e3;
         load16(buf, 0, e0, e1, e2, e3);
-        xa = (W == 0 || rec_check(e0, e1, W)) ? 0u : FAIL;
-    } else {
-        xa = merge_point(buf, lane * CHUNK, t0, W);
+        return (W == 0 || rec_check(e0, e1, W)) ? 0u : FAIL;
     }
-    uint32_t xb = __shfl_down(xa, 1, 64);
-    if (lane == 63) xb = merge_point(buf, TILE, t0, W);
-    uint32_t n = 0;
+    return merge_point(buf, lane * CHUNK, tile * STRIDE, W);
+}
+
+// Records of this lane's chunk [xa, X_lane+1) (lane 63 owns none). Sets `bad` if the chunk is
+// not a chain of valid f64 records from merge point to merge point. With POS, the tile-relative
+// record starts go to pslot[lane*SLOTS + k].
+constexpr int SLOTS = 12;  // records a lane can own: span < CHUNK + WIN bytes, >= 12 B each
+template <bool POS>
+NXG_DEV uint32_t chunk_walk(const uint8_t* buf, uint32_t xa, uint32_t lane, uint16_t* pslot,
+                            bool& bad) {
+    const uint32_t xb = __shfl_down(xa, 1, 64);
     bad = (xa == FAIL) | (xb == FAIL) | (xa > xb);
+    if (lane == 63) {
+        bad = xa == FAIL;
+        return 0;
+    }
+    uint32_t n = 0;
     if (!bad) {
         uint32_t pos = xa;
         while (pos < xb) {
@@ -225,31 +236,37 @@ NXG_DEV uint64_t run_begin(uint64_t first, uint64_t nt, uint32_t R, uint32_t r) 
 // each stage is an exact vmcnt(5): the set's own loads (and fn's earlier stores), never the
 // other set's. Tiles reaching past the frame's end (at most the last two) are loaded with
 // guards after the pipelined loop.
-template <typename Stage, typename Fn>
+// With MOFF, each tile's 64 merge-point offsets (moff + 64*tile, from the count pass) are
+// loaded with its bytes, one per lane, into TileRegs::m.
+template <bool MOFF, typename Stage, typename Fn>
 NXG_DEV void for_run_tiles(const uint8_t* __restrict__ wire, uint64_t W, uint64_t b, uint64_t e,
-                           uint32_t lane, Stage&& stage, Fn&& fn) {
-    const uint64_t nfull = W >= TILE + HALO ? (W - HALO) / TILE : 0;  // tile t full iff t < nfull
+                           uint32_t lane, const uint8_t* moff, Stage&& stage, Fn&& fn) {
+    // tile t is full (image and halo inside the frame) iff t < nfull
+    const uint64_t nfull = W >= IMG + HALO ? (W - IMG - HALO) / STRIDE + 1 : 0;
     const uint64_t ef = e < nfull ? e : (b > nfull ? b : nfull);
     if (b < ef) {
         const uint64_t tl = ef - 1;
         TileRegs A, B;
-        tile_load_full(A, wire, b * TILE, lane);
-        tile_load_full(B, wire, (b + 1 < ef ? b + 1 : tl) * TILE, lane);
+        tile_load_full<MOFF>(A, wire, b * STRIDE, lane, moff + 64 * b);
+        tile_load_full<MOFF>(B, wire, (b + 1 < ef ? b + 1 : tl) * STRIDE, lane,
+                             moff + 64 * (b + 1 < ef ? b + 1 : tl));
         for (uint64_t t = b; t < ef; t += 2) {
             stage(A, t);
             fn(t);
-            tile_load_full(A, wire, (t + 2 < ef ? t + 2 : tl) * TILE, lane);
+            tile_load_full<MOFF>(A, wire, (t + 2 < ef ? t + 2 : tl) * STRIDE, lane,
+                                 moff + 64 * (t + 2 < ef ? t + 2 : tl));
             asm volatile("" ::: "memory");  // keep the refill here (not sunk into the next step)
             if (t + 1 >= ef) break;
             stage(B, t + 1);
             fn(t + 1);
-            tile_load_full(B, wire, (t + 3 < ef ? t + 3 : tl) * TILE, lane);
+            tile_load_full<MOFF>(B, wire, (t + 3 < ef ? t + 3 : tl) * STRIDE, lane,
+                                 moff + 64 * (t + 3 < ef ? t + 3 : tl));
             asm volatile("" ::: "memory");
         }
     }
     for (uint64_t t = ef; t < e; t++) {
         TileRegs A;
-        tile_load(A, wire, t * TILE, W, lane);
+        tile_load(A, wire, t * STRIDE, W, lane, MOFF ? moff + 64 * t : nullptr);
         stage(A, t);
         fn(t);
     }

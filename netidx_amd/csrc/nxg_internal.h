@@ -48,13 +48,15 @@ namespace f64dec {
 constexpr int TPB = 256;                 // 4 independent waves per workgroup
 constexpr int WAVES = TPB / 64;
 constexpr int CHUNK = 64;                // bytes per lane
-constexpr int TILE = 64 * CHUNK;         // 4 KiB per tile (one wave walks one tile at a time)
-constexpr int HALO = 128;                // look-ahead bytes loaded past the tile
+constexpr int IMG = 64 * CHUNK;          // 4 KiB tile image per wave (16 B x 64 lanes x 4)
+constexpr int STRIDE = IMG - CHUNK;      // tiles start 4032 B apart: lanes 0..62 own the records,
+                                         // lane 63's merge point is the next tile's first
+constexpr int TILE = IMG;                // (image size; kept for LDS sizing)
+constexpr int HALO = 128;                // look-ahead bytes loaded past the image
 constexpr int WIN = 64;                  // merge-point search bound (bits of the walk mask)
 constexpr int MAXREC = TILE / 12 + 16;   // record slots per tile (records are >= 12 bytes)
-constexpr int SEG_TILES = 1 << 24;         // tiles per segment: count, then emit (one segment measured fastest)
 constexpr int MAX_WGS = 2048;            // workgroups per pass (one run per wave)
-constexpr int SCRATCH_WORDS = MAX_WGS * WAVES / 2 + MAX_WGS / 2 + MAX_WGS + 1;
+constexpr int SCRATCH_WORDS = MAX_WGS * WAVES / 2 + MAX_WGS / 2;  // wcnt + gcnt (u32)
 }  // namespace f64dec
 
 // ---- general decode geometry (nxg_decode_general.hip) ----
@@ -83,11 +85,12 @@ __device__ inline void zero_status(DevStatus* zst) {
     if (zst && blockIdx.x == 0 && threadIdx.x == 0) *zst = DevStatus{};
 }
 extern thread_local DevStatus* nxg_zero_slot;  // host side: passed through to the kernels
-// f64 decode: count pass + emit pass per segment, `wgs` workgroups each (nxg_dec_f64_wgs).
-// `scratch` holds f64dec::SCRATCH_WORDS words (no initialisation needed); `ticket` one zeroed
-// word (left zeroed on return).
+// f64 decode: count pass + emit pass, `wgs` workgroups each (nxg_dec_f64_wgs). `scratch`
+// holds f64dec::SCRATCH_WORDS words and `moff` 64 bytes per tile (nxg_dec_f64_tiles(W) tiles);
+// neither needs initialisation.
+uint64_t nxg_dec_f64_tiles(uint64_t W);
 hipError_t nxg_launch_dec_f64(const uint8_t* wire, uint64_t W, uint64_t* oid, uint64_t* oval,
-                              uint64_t cap, uint64_t* scratch, uint32_t* ticket, int wgs,
+                              uint64_t cap, uint64_t* scratch, uint8_t* moff, int wgs,
                               DevStatus* st, hipStream_t s);
 int nxg_dec_f64_wgs(int ncu);
 hipError_t nxg_launch_dec_general(const uint8_t* wire, uint64_t W, const ColsDesc& cols,

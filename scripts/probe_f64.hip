@@ -1,7 +1,7 @@
 // probe_f64.hip -- standalone timing probe for the f64 decode (diagnostics, not product).
 // Builds an all-f64 frame on the host, then times with HIP events:
 //   dec       the product decode (count + emit per segment); outputs are checked on the host
-//   dec_*     the same with one knob changed: seg1 one segment, seg48 48 MiB segments
+//   dec_sc    the experimental single-pass scanner variant (nxg_decode_f64_sc.hip)
 //   stream    a plain kernel reading W bytes and writing 16N bytes (practical HBM ceiling)
 //   d2d       hipMemcpyDeviceToDevice of the frame
 // Usage: probe_f64 [records] [reps]
@@ -13,16 +13,6 @@
 
 namespace prod {
 #include "../netidx_amd/csrc/nxg_decode_f64.hip"
-}
-namespace seg1 {
-#define SEG_TILES (1 << 24)
-#include "../netidx_amd/csrc/nxg_decode_f64.hip"
-#undef SEG_TILES
-}
-namespace seg48 {
-#define SEG_TILES 12288
-#include "../netidx_amd/csrc/nxg_decode_f64.hip"
-#undef SEG_TILES
 }
 namespace sc {
 #include "../netidx_amd/csrc/nxg_decode_f64_sc.hip"
@@ -131,6 +121,8 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&tstat, 2 * ntiles * 8 + 64));
     CK(hipMemset(tstat, 0, 2 * ntiles * 8 + 64));
     uint32_t epoch = 0;
+    uint8_t* moff;
+    CK(hipMalloc(&moff, 64 * (W / 4032 + 2)));
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
@@ -160,15 +152,13 @@ int main(int argc, char** argv) {
                h.timeout, h.capacity, bad);
         fflush(stdout);
     };
-#define LAUNCH(NS) CK(NS::nxg_launch_dec_f64(dw, W, oid, oval, N, scratch, tickets, \
+#define LAUNCH(NS) CK(NS::nxg_launch_dec_f64(dw, W, oid, oval, N, scratch, moff, \
                                             NS::nxg_dec_f64_wgs(ncu), st, 0))
     auto dec = [&](int v) {
         return [&, v]() {
             CK(hipMemsetAsync(st, 0, sizeof(DevStatus), 0));
             CK(hipMemsetAsync(oid, 0, 8, 0));
             if (v == 0) LAUNCH(prod);
-            if (v == 1) LAUNCH(seg1);
-            if (v == 2) LAUNCH(seg48);
             if (v == 5) {
                 epoch++;
                 CK(sc::nxg_launch_dec_f64_sc(dw, W, oid, oval, N, tstat, epoch,
@@ -180,8 +170,6 @@ int main(int argc, char** argv) {
     printf("records=%llu wire=%llu bytes tiles=%llu\n", (unsigned long long)N,
            (unsigned long long)W, (unsigned long long)((W + 4095) / 4096));
     timeit("dec", dec(0), true);
-    timeit("dec_seg1", dec(1), true);
-    timeit("dec_seg48", dec(2), true);
     printf("sc wgs=%d\n", sc::nxg_dec_f64_sc_wgs(ncu));
     timeit("dec_sc", dec(5), true);
     {
