@@ -62,6 +62,11 @@ struct NxgCtx {
     int wgs_dec_f64 = 0;
     uint8_t* fmoff = nullptr;      // f64 decode: merge-point offsets, 64 B per tile
     size_t fmoff_cap = 0;
+    uint32_t* glws = nullptr;      // general decode: lane words, 256 B per tile
+    size_t glws_cap = 0;
+    uint64_t* gruns = nullptr;     // general decode: run summaries + bases
+    int wgs_dec_gen = 0;
+    bool gen_v1 = false;           // NXG_GEN_V1=1: the single-pass look-back decoder instead
     uint8_t* dframe = nullptr;
     size_t dframe_cap = 0;
     uint64_t* escratch = nullptr;
@@ -267,8 +272,28 @@ bool enqueue_dec_fast(NxgCtx* c, const uint8_t* f, uint64_t len, NxgColumns* out
     return true;
 }
 
+bool ensure_glws(NxgCtx* c, size_t bytes, NetidxError* err) {
+    if (bytes <= c->glws_cap) return true;
+    size_t n = std::max(bytes, c->glws_cap * 2);
+    n = std::max<size_t>(n, 1 << 16);
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (c->glws) HIPCHK(hipFree(c->glws));
+    c->glws = nullptr;
+    HIPCHK(hipMalloc(&c->glws, n));
+    c->glws_cap = n;
+    return true;
+}
+
 bool enqueue_dec_general(NxgCtx* c, const uint8_t* f, uint64_t len, NxgColumns* out,
                          DevStatus* st, NetidxError* err) {
+    if (!c->gen_v1) {
+        if (!ensure_glws(c, 256 * nxg_dec_gen_tiles(len), err)) return false;
+        const ColsDesc d = desc_of(out);
+        HIPCHK(nxg_launch_dec_gen(f, len, d, c->glws, c->gruns,
+                                  c->gruns + (size_t)gdec2::MAX_RUNS * gdec2::RUN_WORDS,
+                                  c->wgs_dec_gen, st, c->stream));
+        return true;
+    }
     const uint64_t nt = (len + gdec::TILE - 1) / gdec::TILE;
     if (!ensure_tstat(c, nt * gdec::SLOT_WORDS, err)) return false;
     const ColsDesc d = desc_of(out);
@@ -491,6 +516,12 @@ NxgCtx* nxg_ctx_new(int device, NetidxError* err) {
     if ((e = hipMalloc(&c->fscratch, fw * 8)) != hipSuccess) return fail("hipMalloc(fscratch)", e);
     if ((e = hipMemset(c->fscratch, 0, fw * 8)) != hipSuccess) return fail("hipMemset(fscratch)", e);
     c->wgs_dec_f64 = nxg_dec_f64_wgs(c->ncu);
+    // general decode: run summaries + bases (no initialisation needed)
+    const size_t gw = (size_t)gdec2::MAX_RUNS * (gdec2::RUN_WORDS + 4);
+    if ((e = hipMalloc(&c->gruns, gw * 8)) != hipSuccess) return fail("hipMalloc(gruns)", e);
+    c->wgs_dec_gen = nxg_dec_gen_wgs(c->ncu);
+    const char* g1 = getenv("NXG_GEN_V1");
+    c->gen_v1 = g1 && g1[0] == '1';
     return c;
 }
 
@@ -502,6 +533,8 @@ void nxg_ctx_destroy(NxgCtx* c) {
     if (c->tstat) (void)hipFree(c->tstat);
     if (c->fscratch) (void)hipFree(c->fscratch);
     if (c->fmoff) (void)hipFree(c->fmoff);
+    if (c->glws) (void)hipFree(c->glws);
+    if (c->gruns) (void)hipFree(c->gruns);
     if (c->dframe) (void)hipFree(c->dframe);
     if (c->escratch) (void)hipFree(c->escratch);
     if (c->dheap) (void)hipFree(c->dheap);

@@ -1,0 +1,664 @@
+// nxg_decode_gen.hip -- general From-stream decode for gfx950: every From variant, every Value
+// tag, nesting, errors. Replaces the receive_batch_fn loop (netidx/src/channel.rs:504-521) for
+// frames the homogeneous-f64 kernels do not take.
+//
+// Message boundaries form a pointer chain (len_wrapped_decode, pack.rs:537-555): a message's
+// length prefix says where the next one starts. The chain is followed in parallel, with the
+// same run structure as the f64 decoder (nxg_decode_f64.hip):
+//
+//   count    wave v owns a contiguous run of 4 KiB tiles. In each tile, lane j owns the 64-byte
+//            chunk j. Every lane guesses the first message start in its chunk, walks and
+//            validates the messages that start there, and the wave then checks that lane j's
+//            start is exactly the exit of the nearest lane below it that has a start; a lane
+//            that disagrees re-walks from that exit (exact repair, one lane per round). The
+//            first tile of a run has a guessed entry; each later tile's entry is the previous
+//            tile's exit, so only a run's first entry is ever speculative. Per tile and lane the
+//            wave stores one word (start offset, rows, control messages, children); per run, a
+//            summary (guessed entry, exit, totals, first error).
+//   resolve  one workgroup: checks that each run's guessed entry is the previous run's exit and
+//            re-walks, in order, any run whose guess was wrong (its per-lane words are
+//            rewritten); finds the first error on the true chain; prefix sums of the run totals.
+//   emit     the same runs again: each lane decodes its messages from the stored start and
+//            writes the columns at the bases from the prefix sums.
+//
+// The frame fails with the first error on the true chain, (PackError kind, offset of the
+// failing message), as the sequential reference stops at its first error
+// (netidx/src/subscriber/connection.rs:228-231).
+#include "nxg_msg.h"
+
+using namespace nxgmsg;
+
+namespace {
+
+constexpr int TPB = gdec2::TPB;
+constexpr int WAVES = TPB / 64;
+constexpr int CH = gdec2::CH;
+constexpr uint32_t TILE = gdec2::TILE;
+constexpr uint32_t IMG = gdec2::IMG;
+constexpr uint64_t NONE = ~0ull;
+constexpr uint32_t NOSTART = 127u;  // lane word: no message starts in the chunk
+constexpr uint32_t CH_ESC = 8191u;  // lane word: children count did not fit (recount in emit)
+
+// lane word: start offset (7 bits) | rows (6) | control messages (6) | children (13)
+NXG_DEV uint32_t lw_pack(uint32_t off, uint32_t rows, uint32_t ctl, uint64_t ch) {
+    return off | (rows << 7) | (ctl << 13) | ((uint32_t)(ch < CH_ESC ? ch : CH_ESC) << 19);
+}
+NXG_DEV uint32_t lw_off(uint32_t w) { return w & 127u; }
+NXG_DEV uint32_t lw_rows(uint32_t w) { return (w >> 7) & 63u; }
+NXG_DEV uint32_t lw_ctl(uint32_t w) { return (w >> 13) & 63u; }
+NXG_DEV uint32_t lw_ch(uint32_t w) { return w >> 19; }
+
+// run summary words
+enum { R_SPEC = 0, R_EXIT, R_ROWS, R_CH, R_CTL, R_HB, R_ERR, R_FIXED, R_WORDS };
+static_assert(R_WORDS == gdec2::RUN_WORDS, "run summary");
+// R_ERR: kind << 56 | offset (0 = none). R_SPEC: NONE when the run holds no message start.
+
+constexpr uint64_t POSM = (1ull << 56) - 1;
+
+// lane states
+enum { S_NONE = 0, S_EXH = 1, S_OK = 2, S_ERR = 3 };
+
+struct LaneRes {
+    uint64_t x;  // exit (first message start at/after the chunk end), or the failing message
+    uint32_t rows, ctl, hb;
+    uint64_t children;
+    uint32_t st;
+    uint32_t ek;
+};
+
+// Validating walk of the messages that start in [e, end).
+template <int MODE>
+NXG_DEV void walk(const Src& s, uint64_t e, uint64_t end, LaneRes& r) {
+    r.x = e;
+    r.rows = r.ctl = r.hb = 0;
+    r.children = 0;
+    r.st = S_OK;
+    r.ek = 0;
+    uint64_t pos = e;
+    const uint64_t stop = end < s.W ? end : s.W;
+    uint32_t work = 0;
+#pragma unroll 1
+    while (pos < stop) {
+        MsgInfo mi;
+        uint64_t ch = 0;
+        const uint32_t err = decode_msg<false, MODE>(s, pos, mi, nullptr, 0, ch, work);
+        if (err == E_BUDGET) {
+            r.st = S_EXH;
+            return;
+        }
+        if (err) {
+            r.st = S_ERR;
+            r.ek = err;
+            r.x = pos;
+            return;
+        }
+        if (mi.variant == 4) r.rows++;
+        else r.ctl++;
+        r.hb += mi.variant == 5;
+        r.children += ch;
+        pos = mi.next;
+    }
+    r.x = pos;
+}
+
+// First position in [c, stop) where an Update decodes plausibly (minimal length varint, value
+// filling the length exactly) and is followed by a plausible message (or the frame end).
+// Candidates come from a SWAR scan for the Update variant byte (4) one or two bytes after a
+// 1- or 2-byte length varint. Only Updates are guessed: a Heartbeat or Unsubscribed accepts
+// almost any bytes; a chunk that starts with one is resolved by the repair.
+NXG_DEV uint64_t speculate(const Src& s, uint64_t c, uint64_t stop, uint32_t& tries) {
+    if (c >= stop) return NONE;
+    const uint64_t rc = c - s.t0;  // 64-aligned, inside the image with 68 bytes to spare
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(s.lds + rc);
+    uint64_t e4 = 0;  // bit q: byte c+1+q == 4, q in [0, 64)
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const uint32_t x = alignbyte(w[k + 1], w[k], 1);  // bytes c+4k+1 .. c+4k+4
+        e4 |= (uint64_t)nib(zero_bytes(x ^ 0x04040404u)) << (4 * k);
+    }
+    const uint32_t x16 = alignbyte(w[17], w[16], 1);  // byte c+65 (for 2-byte-length starts)
+    bool e4_64 = (x16 & 0xffu) == 4u;
+#pragma unroll 1
+    while (e4 || e4_64) {
+        uint32_t q;  // variant byte at c+1+q
+        if (e4) {
+            q = (uint32_t)__builtin_ctzll(e4);
+            e4 &= e4 - 1;
+        } else {
+            q = 64;
+            e4_64 = false;
+        }
+        // p = c+q: 1-byte length (4..127) then the variant; p = c+q-1: 2-byte length
+        for (int form = 0; form < 2; form++) {
+            const int64_t pr = form == 0 ? (int64_t)q - 1 : (int64_t)q;
+            if (pr < 0) continue;
+            const uint64_t p = c + (uint64_t)pr;
+            if (p >= stop) continue;
+            const uint32_t b0 = s.byte(p);
+            if (form == 0) {  // 2-byte length: b0 >= 128, next byte 1..127, then 4
+                const uint32_t b1 = s.byte(p + 1);
+                if (b0 < 0x80u || b1 == 0u || b1 >= 0x80u) continue;
+            } else if (b0 < 4u || b0 >= 0x80u) {
+                continue;
+            }
+            MsgInfo mi;
+            uint64_t ch = 0;
+            uint32_t work = 0;
+            tries++;
+            if (decode_msg<false, M_SPEC>(s, p, mi, nullptr, 0, ch, work) || mi.variant != 4)
+                continue;
+            if (mi.next >= s.W) return p;
+            MsgInfo m2;
+            work = 0;
+            if (decode_msg<false, M_SPEC>(s, mi.next, m2, nullptr, 0, ch, work) == E_OK) return p;
+        }
+    }
+    return NONE;
+}
+
+struct TileOut {
+    uint64_t anchor;  // entry the tile assumed: the given entry, or the first guess (NONE: none)
+    uint64_t exit;    // first message start at/after the tile end (error: the failing message)
+    uint32_t ek;      // error kind on the chain, 0 = none
+    uint64_t rows, ch, ctl, hb;
+    uint32_t rounds;
+};
+
+// Resolve one tile (its bytes are in the wave's LDS image `s`). `entry` is the exact first
+// message start at/after the tile start, or NONE (guess it). Sets this lane's word (lwo)
+// and returns the tile's totals. Wave-level: no block barriers.
+NXG_DEV TileOut process_tile(const Src& s, uint64_t t0, uint64_t entry, uint32_t& lwo,
+                             uint32_t& tries) {
+    const uint32_t lane = __lane_id();
+    const uint64_t W = s.W;
+    TileOut to{entry, entry, 0, 0, 0, 0, 0, 0};
+    if (entry != NONE && (entry >= t0 + TILE || entry >= s.W)) {  // inside one message, or done
+        lwo = NOSTART;
+        return to;
+    }
+    const uint64_t c = t0 + (uint64_t)lane * CH, cend = c + CH;
+    const uint64_t stop = cend < W ? cend : W;  // message starts are positions < W
+    bool has = false;
+    uint64_t e = NONE;
+    if (entry != NONE && entry >= c) {
+        has = entry < stop;  // the anchor lane (lanes before it: no start)
+        e = has ? entry : NONE;
+    } else {
+        e = speculate(s, c, stop, tries);
+        has = e != NONE;
+    }
+    // anchor = the lane holding the entry, else the first lane with a guess
+    uint32_t a;
+    if (entry != NONE) {
+        a = (uint32_t)((entry - t0) / CH);
+    } else {
+        const uint64_t m = __ballot(has);
+        if (!m) {  // no guess anywhere: assume the tile lies inside one message
+            lwo = NOSTART;
+            to.anchor = NONE;
+            to.exit = NONE;
+            return to;
+        }
+        a = (uint32_t)__builtin_ctzll(m);
+    }
+    if (lane < a) has = false;
+    to.anchor = __shfl(e, (int)a, 64);
+    LaneRes r{e, 0, 0, 0, 0, S_NONE, 0};
+    if (has) {
+        if (lane == a && entry != NONE) walk<M_EXACT>(s, e, cend, r);
+        else walk<M_BOUNDED>(s, e, cend, r);
+    }
+    // Exact repair, one lane per round in lane order. Lane j > a is consistent when, with x the
+    // exit of the nearest lane below it that has a start: x < stop_j and j starts exactly at x,
+    // or x >= stop_j and j has no start. Events: the first inconsistent lane (re-walked from x,
+    // or cleared), a consistent lane whose bounded walk ran out of budget (re-walked exactly),
+    // a consistent lane whose walk failed (the tile's error: everything after it is moot).
+    const uint64_t lt = (1ull << lane) - 1;
+    const uint64_t from_a = ~0ull << a;
+    int errlane = -1;
+    uint32_t rounds = 0;
+#pragma unroll 1
+    for (;;) {
+        if (++rounds > 2 * 64 + 4) {
+            errlane = -2;  // logic error guard: reported as a timeout, never a hang
+            break;
+        }
+        const uint64_t m = __ballot(has);
+        const uint64_t below = m & lt;
+        const int pi = below ? 63 - __builtin_clzll(below) : (int)lane;
+        const uint64_t px = __shfl(r.x, pi, 64);
+        const uint32_t pst = __shfl(r.st, pi, 64);
+        bool cons = true;
+        if (lane > a && below && pst == S_OK) cons = px < stop ? (has && e == px) : !has;
+        const bool ev_exh = cons && has && r.st == S_EXH;
+        const bool ev_err = cons && has && r.st == S_ERR;
+        const uint64_t fm = __ballot((!cons) || ev_exh || ev_err) & from_a;
+        if (!fm) break;
+        const int bl = __builtin_ctzll(fm);
+        if (__shfl((uint32_t)ev_err, bl, 64)) {
+            errlane = bl;
+            break;
+        }
+        if ((int)lane == bl) {
+            if (ev_exh) {
+                walk<M_EXACT>(s, e, cend, r);
+            } else if (px < stop) {
+                has = true;
+                e = px;
+                walk<M_EXACT>(s, e, cend, r);
+            } else {
+                has = false;
+                e = NONE;
+                r.st = S_NONE;
+            }
+        }
+    }
+    to.rounds = rounds;
+    if (errlane == -2) {
+        to.ek = NXG_TIMEOUT;
+        to.exit = 0;
+        lwo = NOSTART;
+        return to;
+    }
+    bool live = has;
+    if (errlane >= 0) {
+        live = has && (int)lane < errlane;
+        to.ek = __shfl(r.ek, errlane, 64);
+        to.exit = __shfl(r.x, errlane, 64);
+    } else {
+        const uint64_t m = __ballot(has);
+        const int z = 63 - __builtin_clzll(m);  // lane a at least
+        to.exit = __shfl(r.x, z, 64);
+    }
+    lwo = live ? lw_pack((uint32_t)(e - c), r.rows, r.ctl, r.children) : NOSTART;
+    to.rows = wave_sum<uint64_t>(live ? r.rows : 0u);
+    to.ctl = wave_sum<uint64_t>(live ? r.ctl : 0u);
+    to.hb = wave_sum<uint64_t>(live ? r.hb : 0u);
+    to.ch = wave_sum<uint64_t>(live ? r.children : 0ull);
+    return to;
+}
+
+// ---- tile staging: 4 KiB + 1 KiB look-ahead per wave, 5 x 16 B per lane, zero past the end --
+struct GRegs {
+    uint4 v[5];
+};
+NXG_DEV uint4 ld16z(const uint8_t* __restrict__ wire, uint64_t off, uint64_t W) {
+    if (off + 16 <= W) return *reinterpret_cast<const uint4*>(wire + off);
+    uint32_t v[4] = {0, 0, 0, 0};
+    for (int k = 0; k < 16; k++)
+        if (off + k < W) v[k >> 2] |= (uint32_t)wire[off + k] << (8 * (k & 3));
+    return make_uint4(v[0], v[1], v[2], v[3]);
+}
+NXG_DEV void g_load(GRegs& g, const uint8_t* __restrict__ wire, uint64_t t0, uint64_t W,
+                    uint32_t lane) {
+    if (t0 + IMG <= W) {
+        const uint4* p = reinterpret_cast<const uint4*>(wire + t0);
+#pragma unroll
+        for (int i = 0; i < 5; i++) g.v[i] = p[i * 64 + lane];
+    } else {
+#pragma unroll
+        for (int i = 0; i < 5; i++) g.v[i] = ld16z(wire, t0 + i * 1024 + lane * 16, W);
+    }
+}
+NXG_DEV void g_stage(uint8_t* buf, const GRegs& g, uint32_t lane) {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int i = 0; i < 5; i++) *reinterpret_cast<uint4*>(buf + i * 1024 + lane * 16) = g.v[i];
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+}
+NXG_DEV Src g_src(const uint8_t* buf, const uint8_t* wire, uint64_t t0, uint64_t W) {
+    const uint64_t n = W - t0;
+    return Src{buf, t0, (uint32_t)(n < IMG ? n : IMG), wire, W};
+}
+
+NXG_DEV uint64_t run_begin(uint64_t nt, uint32_t R, uint32_t r) { return nt * r / R; }
+
+// Re-walk / first walk of the tiles [b, e) of a run from `entry` (NONE: guessed). Lane words go
+// to lws + 64*tile. Fills the run summary (in registers; lane 0 stores it).
+struct RunSum {
+    uint64_t spec, exit, rows, ch, ctl, hb, err;
+    uint32_t rounds, tries;
+};
+NXG_DEV RunSum run_tiles(const uint8_t* __restrict__ wire, uint64_t W, uint64_t b, uint64_t e,
+                         uint64_t entry, uint32_t* __restrict__ lws, uint8_t* buf) {
+    const uint32_t lane = __lane_id();
+    RunSum rs{NONE, entry, 0, 0, 0, 0, 0, 0, 0};
+    bool have_spec = entry != NONE;
+    if (have_spec) rs.spec = entry;
+    GRegs g;
+    if (b < e) g_load(g, wire, b * TILE, W, lane);
+    uint64_t cur = entry;
+#pragma unroll 1
+    for (uint64_t t = b; t < e; t++) {
+        const uint64_t t0 = t * TILE;
+        g_stage(buf, g, lane);
+        if (t + 1 < e) g_load(g, wire, (t + 1) * TILE, W, lane);
+        const Src s = g_src(buf, wire, t0, W);
+        uint32_t tries = 0;
+        uint32_t lwv;
+        const TileOut to = process_tile(s, t0, cur, lwv, tries);
+        lws[t * 64 + lane] = lwv;
+        rs.tries += wave_sum<uint32_t>(tries);
+        rs.rounds += to.rounds;
+        if (!have_spec && to.anchor != NONE) {
+            rs.spec = to.anchor;
+            have_spec = true;
+        }
+        rs.rows += to.rows;
+        rs.ch += to.ch;
+        rs.ctl += to.ctl;
+        rs.hb += to.hb;
+        if (to.ek) {
+            rs.err = ((uint64_t)to.ek << 56) | (to.exit & POSM);
+            rs.exit = to.exit;
+            return rs;
+        }
+        cur = to.exit;
+        rs.exit = cur;
+    }
+    return rs;
+}
+
+}  // namespace
+
+// ---- pass 1: count ---------------------------------------------------------------------------
+__global__ __launch_bounds__(TPB) void nxg_gen_count_kernel(
+    const uint8_t* __restrict__ wire, uint64_t W, uint64_t nt, uint32_t* __restrict__ lws,
+    uint64_t* __restrict__ runs, DevStatus* __restrict__ st, DevStatus* zst) {
+    zero_status(zst);
+    __shared__ __attribute__((aligned(16))) uint8_t bufs[WAVES][IMG];
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint32_t R = gridDim.x * WAVES, r = blockIdx.x * WAVES + w;
+    const uint64_t b = run_begin(nt, R, r), e = run_begin(nt, R, r + 1);
+    const RunSum rs = run_tiles(wire, W, b, e, b == 0 ? 0ull : NONE, lws, bufs[w]);
+    if (lane < R_WORDS) {
+        const uint64_t v[R_WORDS] = {rs.spec, rs.exit, rs.rows, rs.ch, rs.ctl, rs.hb, rs.err, 0};
+        uint64_t x = v[0];
+#pragma unroll
+        for (int i = 1; i < R_WORDS; i++)
+            if ((int)lane == i) x = v[i];
+        runs[(uint64_t)r * R_WORDS + lane] = x;
+    }
+    if (lane == 0) {
+        atomicAdd(&st->diag[2], (unsigned long long)rs.rounds);
+        atomicAdd(&st->diag[4], (unsigned long long)rs.tries);
+    }
+}
+
+// ---- resolve: one workgroup ------------------------------------------------------------------
+// Thread i owns runs [i*K, (i+1)*K). The exit entering run r is the exit of the latest run before
+// it that holds a message start (run 0 always does: it starts at byte 0). Events, in run order
+// from `from` on: a run whose guessed entry disagrees with its entering exit (wave 0 re-walks it
+// from that exit, rewriting its lane words and summary), or the first run with an error (the
+// frame's error). Then the run totals are prefix-summed into the emit pass's bases.
+constexpr int RES_TPB = 1024;
+constexpr int RES_K = gdec2::MAX_RUNS / RES_TPB;
+static_assert(gdec2::MAX_RUNS % RES_TPB == 0, "resolve geometry");
+
+// exclusive block scan (sum) over RES_TPB threads
+template <typename T>
+NXG_DEV T res_scan(T v, T* tmp, T& total) {
+    const uint32_t tid = threadIdx.x, wv = tid >> 6, l = tid & 63;
+    const T inc = wave_incl_scan(v);
+    if (l == 63) tmp[wv] = inc;
+    __syncthreads();
+    T wb = 0, tot = 0;
+    for (int i = 0; i < RES_TPB / 64; i++) {
+        const T x = tmp[i];
+        if ((uint32_t)i < wv) wb += x;
+        tot += x;
+    }
+    __syncthreads();
+    total = tot;
+    return wb + inc - v;
+}
+// exclusive block scan (max) over RES_TPB threads
+NXG_DEV uint64_t res_scan_max(uint64_t v, uint64_t* tmp) {
+    const uint32_t tid = threadIdx.x, wv = tid >> 6, l = tid & 63;
+    uint64_t inc = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t o = __shfl_up(inc, d, 64);
+        if (l >= (uint32_t)d && o > inc) inc = o;
+    }
+    if (l == 63) tmp[wv] = inc;
+    __syncthreads();
+    uint64_t m = 0;
+    for (uint32_t i = 0; i < wv; i++) m = tmp[i] > m ? tmp[i] : m;
+    __syncthreads();
+    uint64_t ex = __shfl_up(inc, 1, 64);
+    if (l == 0) ex = 0;
+    return ex > m ? ex : m;
+}
+
+__global__ __launch_bounds__(RES_TPB) void nxg_gen_resolve_kernel(
+    const uint8_t* __restrict__ wire, uint64_t W, uint64_t nt, uint32_t R,
+    uint32_t* __restrict__ lws, uint64_t* __restrict__ runs, uint64_t* __restrict__ base,
+    DevStatus* __restrict__ st) {
+    __shared__ __attribute__((aligned(16))) uint8_t buf[IMG];
+    __shared__ uint64_t tmp[RES_TPB / 64];
+    __shared__ uint32_t sh_first;
+    __shared__ uint64_t sh_x;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t r0 = tid * RES_K;
+    uint32_t from = 0, fixes = 0;
+    bool failed = false;
+#pragma unroll 1
+    for (;;) {
+        // latest run (index + 1) with a start among this thread's runs, then across threads
+        uint64_t mine = 0;
+        for (int k = 0; k < RES_K; k++) {
+            const uint32_t r = r0 + k;
+            if (r < R && runs[(uint64_t)r * R_WORDS + R_SPEC] != NONE) mine = r + 1;
+        }
+        const uint64_t before = res_scan_max(mine, tmp);
+        uint64_t X = before ? runs[(before - 1) * R_WORDS + R_EXIT] : 0ull;
+        uint32_t first = 0xffffffffu;
+        uint64_t xfirst = 0;
+        for (int k = 0; k < RES_K; k++) {
+            const uint32_t r = r0 + k;
+            if (r >= R) break;
+            const uint64_t* q = runs + (uint64_t)r * R_WORDS;
+            const uint64_t spec = q[R_SPEC];
+            const uint64_t rend = run_begin(nt, R, r + 1) * TILE;
+            const bool ok = r == 0 || (spec == NONE ? (X >= rend || X >= W) : spec == X);
+            if (r >= from && (!ok || q[R_ERR] != 0)) {
+                first = r;
+                xfirst = X;
+                break;
+            }
+            if (spec != NONE) X = q[R_EXIT];
+        }
+        if (tid == 0) sh_first = 0xffffffffu;
+        __syncthreads();
+        if (first != 0xffffffffu) atomicMin(&sh_first, first);
+        __syncthreads();
+        const uint32_t F = sh_first;
+        if (F != 0xffffffffu && first == F) sh_x = xfirst;
+        __syncthreads();
+        if (F == 0xffffffffu) break;  // every run verified, no error
+        const uint64_t XF = sh_x;
+        const uint64_t* q = runs + (uint64_t)F * R_WORDS;
+        const uint64_t spec = q[R_SPEC];
+        const uint64_t rend = run_begin(nt, R, F + 1) * TILE;
+        const bool ok = F == 0 || (spec == NONE ? (XF >= rend || XF >= W) : spec == XF);
+        if (ok) {  // the first error on the true chain: the frame fails here
+            if (tid == 0) {
+                const uint64_t er = q[R_ERR];
+                st->err_kind = (uint32_t)(er >> 56);
+                st->err_offset = er & POSM;
+            }
+            failed = true;
+            break;
+        }
+        __syncthreads();
+        if (tid < 64) {  // wave 0 re-walks run F from its true entry
+            const uint64_t b = run_begin(nt, R, F), e = run_begin(nt, R, F + 1);
+            const RunSum rs = run_tiles(wire, W, b, e, XF, lws, buf);
+            if (tid < R_WORDS) {
+                const uint64_t v[R_WORDS] = {rs.spec, rs.exit, rs.rows, rs.ch,
+                                             rs.ctl,  rs.hb,   rs.err,  1};
+                uint64_t x = v[0];
+#pragma unroll
+                for (int i = 1; i < R_WORDS; i++)
+                    if ((int)tid == i) x = v[i];
+                runs[(uint64_t)F * R_WORDS + tid] = x;
+            }
+        }
+        fixes++;
+        __threadfence_block();
+        __syncthreads();
+        from = F;  // run F is now on the true chain; an error in it is found next round
+    }
+    if (tid == 0) {
+        st->path = 2;
+        st->diag[0] = fixes;
+    }
+    if (failed) return;
+    // prefix sums of the run totals -> bases
+    uint64_t lr = 0, lc = 0, lk = 0, lh = 0;
+    for (int k = 0; k < RES_K; k++) {
+        const uint32_t r = r0 + k;
+        if (r >= R) break;
+        const uint64_t* q = runs + (uint64_t)r * R_WORDS;
+        lr += q[R_ROWS];
+        lc += q[R_CH];
+        lk += q[R_CTL];
+        lh += q[R_HB];
+    }
+    uint64_t tr, tc, tk, th;
+    uint64_t br = res_scan<uint64_t>(lr, tmp, tr);
+    uint64_t bc = res_scan<uint64_t>(lc, tmp, tc);
+    uint64_t bk = res_scan<uint64_t>(lk, tmp, tk);
+    res_scan<uint64_t>(lh, tmp, th);
+    for (int k = 0; k < RES_K; k++) {
+        const uint32_t r = r0 + k;
+        if (r >= R) break;
+        const uint64_t* q = runs + (uint64_t)r * R_WORDS;
+        base[(uint64_t)r * 4 + 0] = br;
+        base[(uint64_t)r * 4 + 1] = bc;
+        base[(uint64_t)r * 4 + 2] = bk;
+        br += q[R_ROWS];
+        bc += q[R_CH];
+        bk += q[R_CTL];
+    }
+    if (tid == 0) {
+        st->n_rows = tr;
+        st->n_children = tc;
+        st->n_ctl = tk;
+        st->n_heartbeat = th;
+    }
+}
+
+// ---- pass 3: emit ----------------------------------------------------------------------------
+__global__ __launch_bounds__(TPB) void nxg_gen_emit_kernel(
+    const uint8_t* __restrict__ wire, uint64_t W, uint64_t nt, const uint32_t* __restrict__ lws,
+    const uint64_t* __restrict__ base, ColsDesc cols, DevStatus* __restrict__ st) {
+    if (ld_agent32(&st->err_kind)) return;  // the frame failed: no columns
+    __shared__ __attribute__((aligned(16))) uint8_t bufs[WAVES][IMG];
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint32_t R = gridDim.x * WAVES, r = blockIdx.x * WAVES + w;
+    const uint64_t b = run_begin(nt, R, r), e = run_begin(nt, R, r + 1);
+    if (b >= e) return;
+    uint8_t* buf = bufs[w];
+    const Sink sink{cols, &st->capacity, &st->nonf64};
+    uint64_t row = base[(uint64_t)r * 4 + 0];
+    uint64_t child = base[(uint64_t)r * 4 + 1];
+    uint64_t ctl = base[(uint64_t)r * 4 + 2];
+    GRegs g;
+    g_load(g, wire, b * TILE, W, lane);
+    uint32_t lwn = lws[b * 64 + lane];
+#pragma unroll 1
+    for (uint64_t t = b; t < e; t++) {
+        const uint64_t t0 = t * TILE;
+        const uint32_t lw = lwn;
+        g_stage(buf, g, lane);
+        if (t + 1 < e) {
+            g_load(g, wire, (t + 1) * TILE, W, lane);
+            lwn = lws[(t + 1) * 64 + lane];
+        }
+        const Src s = g_src(buf, wire, t0, W);
+        const uint64_t c = t0 + (uint64_t)lane * CH;
+        const uint64_t stop = c + CH < W ? c + CH : W;
+        const bool has = lw_off(lw) != NOSTART;
+        uint32_t nr = has ? lw_rows(lw) : 0u, nk = has ? lw_ctl(lw) : 0u;
+        uint64_t nch = has ? lw_ch(lw) : 0u;
+        if (has && nch == CH_ESC) {  // children count did not fit the lane word: recount
+            LaneRes rr;
+            walk<M_EXACT>(s, c + lw_off(lw), c + CH, rr);
+            nch = rr.children;
+        }
+        const uint32_t rin = wave_incl_scan(nr);
+        const uint32_t kin = wave_incl_scan(nk);
+        const uint64_t cin = wave_incl_scan<uint64_t>(nch);
+        uint64_t myrow = row + rin - nr, myctl = ctl + kin - nk, mych = child + cin - nch;
+        row += __shfl(rin, 63, 64);
+        ctl += __shfl(kin, 63, 64);
+        child += __shfl(cin, 63, 64);
+        uint64_t pos = has ? c + lw_off(lw) : stop;
+        uint32_t work = 0;
+#pragma unroll 1
+        while (pos < stop) {
+            MsgInfo mi;
+            const uint32_t err = decode_msg<true, M_EXACT>(s, pos, mi, &sink, myrow, mych, work);
+            if (err) {  // unreachable: the count pass validated this chain
+                atomicOr(&st->timeout, 2u);
+                break;
+            }
+            if (mi.variant == 4) {
+                if (myrow < cols.cap_rows) cols.id[myrow] = mi.id;
+                else atomicOr(&st->capacity, 1u);
+                myrow++;
+            } else if (!cols.ctl_row) {
+                atomicOr(&st->nonf64, 1u);
+                myctl++;
+            } else {
+                if (myctl < cols.cap_ctl) {
+                    cols.ctl_row[myctl] = myrow;
+                    cols.ctl_off[myctl] = pos;
+                    cols.ctl_len[myctl] = (uint32_t)(mi.next - pos);
+                    cols.ctl_variant[myctl] = (uint8_t)mi.variant;
+                } else {
+                    atomicOr(&st->capacity, 1u);
+                }
+                myctl++;
+            }
+            pos = mi.next;
+        }
+    }
+}
+
+uint64_t nxg_dec_gen_tiles(uint64_t W) { return (W + TILE - 1) / TILE; }
+
+hipError_t nxg_launch_dec_gen(const uint8_t* wire, uint64_t W, const ColsDesc& cd, uint32_t* lws,
+                              uint64_t* runs, uint64_t* base, int wgs, DevStatus* st,
+                              hipStream_t s) {
+    const uint64_t nt = nxg_dec_gen_tiles(W);
+    if (nt == 0) return hipSuccess;
+    if (wgs <= 0 || wgs * WAVES > gdec2::MAX_RUNS) return hipErrorInvalidValue;
+    // no more runs than tiles: empty runs only cost a pass-through in resolve
+    uint64_t g = (nt + WAVES - 1) / WAVES;
+    if (g > (uint64_t)wgs) g = wgs;
+    const uint32_t R = (uint32_t)g * WAVES;
+    hipLaunchKernelGGL(nxg_gen_count_kernel, dim3(g), dim3(TPB), 0, s, wire, W, nt, lws, runs, st,
+                       nxg_zero_slot);
+    hipLaunchKernelGGL(nxg_gen_resolve_kernel, dim3(1), dim3(RES_TPB), 0, s, wire, W, nt, R, lws,
+                       runs, base, st);
+    hipLaunchKernelGGL(nxg_gen_emit_kernel, dim3(g), dim3(TPB), 0, s, wire, W, nt, lws, base, cd,
+                       st);
+    return hipGetLastError();
+}
+
+int nxg_dec_gen_wgs(int ncu) {
+    int a = 0, b = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, nxg_gen_count_kernel, TPB, 0) !=
+            hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, nxg_gen_emit_kernel, TPB, 0) !=
+            hipSuccess)
+        return ncu;
+    const int occ = a < b ? a : b;
+    int g = ncu * (occ > 0 ? occ : 1);
+    return g < gdec2::MAX_RUNS / WAVES ? g : gdec2::MAX_RUNS / WAVES;
+}

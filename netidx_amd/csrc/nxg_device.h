@@ -46,6 +46,13 @@ NXG_DEV uint32_t alignbyte(uint32_t hi, uint32_t lo, uint32_t s) {
 }
 NXG_DEV uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 
+// SWAR: 0x80 in every zero byte of x (exact, no borrow propagation)
+NXG_DEV uint32_t zero_bytes(uint32_t x) {
+    return ~(((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x | 0x7f7f7f7fu);
+}
+// gather the 0x80 flags of a zero_bytes() result into 4 bits
+NXG_DEV uint32_t nib(uint32_t zb) { return (((zb >> 7) & 0x01010101u) * 0x01020408u) >> 24; }
+
 // ---- wave/block scans (wave64) -----------------------------------------------------------
 NXG_DEV uint32_t lane_id() { return __lane_id(); }
 

@@ -71,12 +71,6 @@ NXG_DEV void rec_decode(uint32_t e0, uint32_t e1, uint32_t e2, uint32_t e3, uint
     val = ((uint64_t)bswap32(lo) << 32) | bswap32(hi);  // big-endian f64 (pack.rs:592-598)
 }
 
-// SWAR: 0x80 in every zero byte of x (exact, no borrow propagation)
-NXG_DEV uint32_t zero_bytes(uint32_t x) {
-    return ~(((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x | 0x7f7f7f7fu);
-}
-// gather the 0x80 flags of a zero_bytes() result into 4 bits
-NXG_DEV uint32_t nib(uint32_t zb) { return (((zb >> 7) & 0x01010101u) * 0x01020408u) >> 24; }
 
 // Merge point of all record walks starting in [r, r+15) (tile-relative). r is 4-aligned.
 NXG_DEV uint32_t merge_point(const uint8_t* buf, uint32_t r, uint64_t t0, uint64_t W) {

@@ -68,6 +68,16 @@ constexpr int HALO = 256;
 constexpr int SLOT_WORDS = 16;     // per-tile look-back descriptor (agg 8 words + inc 8 words)
 }  // namespace gdec
 
+// ---- general decode v2 geometry (nxg_decode_gen.hip) ----
+namespace gdec2 {
+constexpr int TPB = 256;            // 4 independent waves per workgroup, one run each
+constexpr int CH = 64;              // bytes per lane
+constexpr uint32_t TILE = 64 * CH;  // 4 KiB per tile
+constexpr uint32_t IMG = TILE + 1024;  // LDS image: tile + 1 KiB look-ahead
+constexpr int MAX_RUNS = 8192;      // runs (waves) per pass
+constexpr int RUN_WORDS = 8;        // per-run summary words
+}  // namespace gdec2
+
 // ---- f64 encode geometry ----
 namespace f64enc {
 constexpr int LB_U = 1;                 // look-back window rows (64 tiles each); wider measured slower
@@ -102,6 +112,13 @@ hipError_t nxg_launch_enc_f64(const uint64_t* id, const uint64_t* val, uint64_t 
 hipError_t nxg_launch_enc_general(const ColsDesc& cols, const uint8_t* heap, uint8_t* out,
                                   uint64_t cap, uint64_t* scratch, uint64_t* tstat,
                                   uint32_t epoch, DevStatus* st, int grid, hipStream_t s);
+// general decode v2: count + resolve + emit. `lws` holds 64 u32 per tile (nxg_dec_gen_tiles),
+// `runs` gdec2::MAX_RUNS * RUN_WORDS u64, `base` gdec2::MAX_RUNS * 4 u64; none needs zeroing.
+uint64_t nxg_dec_gen_tiles(uint64_t W);
+hipError_t nxg_launch_dec_gen(const uint8_t* wire, uint64_t W, const ColsDesc& cols, uint32_t* lws,
+                              uint64_t* runs, uint64_t* base, int wgs, DevStatus* st,
+                              hipStream_t s);
+int nxg_dec_gen_wgs(int ncu);
 int nxg_occupancy_dec_general();
 int nxg_occupancy_enc_f64();
 int nxg_occupancy_enc_general();

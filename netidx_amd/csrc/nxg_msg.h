@@ -9,9 +9,10 @@
 //                              array.rs:595-612, pack.rs:1225-1239, pbuf.rs:139-147,
 //                              pack.rs:457-469, 1567-1575, 1591-1595, 614-622,
 //                              abstract_type.rs:280-298
-// Nested values are walked iteratively with an explicit stack. Children are allocated
-// depth-first, the same order as the recursive reference decoder, which produces them as it
-// goes.
+// A value is decoded without a stack when it is nested at most one level deep (dvalue_flat, the
+// common case); deeper values are walked iteratively with an explicit stack (dvalue_deep).
+// Children are allocated depth-first, the same order as the recursive reference decoder, which
+// produces them as it goes.
 //
 // Modes:
 //   M_SPEC    plausibility only (no UTF-8 scan), small work budget: used to GUESS a start
@@ -42,6 +43,46 @@ struct Src {
         return r < nlds ? (uint32_t)lds[r] : (uint32_t)g[p];
     }
 };
+
+// std::str::from_utf8 (pack.rs:462) over a Src: four ASCII bytes per step while the text lies
+// in the LDS image, the byte-wise state machine (nxg_device.h utf8_valid) otherwise.
+NXG_DEV bool utf8_valid_src(const Src& s, uint64_t p, uint64_t n) {
+    uint64_t i = 0;
+    const uint64_t r0 = p - s.t0;
+#pragma unroll 1
+    while (i < n) {
+        const uint64_t r = r0 + i;
+        if (i + 4 <= n && r + 8 <= s.nlds) {
+            const uint32_t* w = reinterpret_cast<const uint32_t*>(s.lds + (r & ~3ull));
+            const uint32_t x = alignbyte(w[1], w[0], (uint32_t)(r & 3));
+            if (!(x & 0x80808080u)) {
+                i += 4;
+                continue;
+            }
+        }
+        const uint32_t c = s.byte(p + i);
+        if (c < 0x80) {
+            i++;
+            continue;
+        }
+        uint32_t lo = 0x80, hi = 0xBF, need;
+        if (c >= 0xC2 && c <= 0xDF) need = 1;
+        else if (c == 0xE0) { need = 2; lo = 0xA0; }
+        else if ((c >= 0xE1 && c <= 0xEC) || c == 0xEE || c == 0xEF) need = 2;
+        else if (c == 0xED) { need = 2; hi = 0x9F; }
+        else if (c == 0xF0) { need = 3; lo = 0x90; }
+        else if (c >= 0xF1 && c <= 0xF3) need = 3;
+        else if (c == 0xF4) { need = 3; hi = 0x8F; }
+        else return false;
+        if (i + need >= n) return false;
+        const uint32_t c1 = s.byte(p + i + 1);
+        if (c1 < lo || c1 > hi) return false;
+        for (uint32_t k = 2; k <= need; k++)
+            if ((s.byte(p + i + k) & 0xC0) != 0x80) return false;
+        i += need + 1;
+    }
+    return true;
+}
 
 // Where a decoded value goes. EMIT=false only counts children.
 struct Sink {
@@ -114,7 +155,7 @@ NXG_DEV uint32_t dstr(const Src& s, uint64_t& p, uint64_t lim, bool utf8, uint64
             work += (uint32_t)min<uint64_t>(n >> 4, kWalkBudget);
             if (work > kWalkBudget) return E_BUDGET;
         }
-        if (!utf8_valid(s, p, n)) return E_INVALID;
+        if (!utf8_valid_src(s, p, n)) return E_INVALID;
     }
     off = p;
     len = n;
@@ -122,10 +163,204 @@ NXG_DEV uint32_t dstr(const Src& s, uint64_t& p, uint64_t lim, bool utf8, uint64
     return E_OK;
 }
 
-// Decode one Value at p (limit lim) into (row?, slot), children from `child_next`.
+// Payload of one non-container value with wire tag t (the tag byte already consumed) into
+// (row?, slot). Containers (19 Array, 21 Map, 22 Error(Value) whose inner is not a String) are
+// handled by the callers. Tag 22 reaches here only as Error(String).
 template <bool EMIT, int MODE>
-NXG_DEV uint32_t dvalue(const Src& s, uint64_t& p, uint64_t lim, const Sink* k, bool row,
-                        uint64_t slot, uint64_t& child_next, uint32_t& work) {
+NXG_DEV uint32_t dleaf(const Src& s, uint32_t t, uint64_t& p, uint64_t lim, const Sink* k,
+                       bool is_row, uint64_t cur, uint32_t& work) {
+    uint64_t v, v2, off, len;
+    uint32_t e = E_OK;
+    switch (t) {
+    case 0:
+        if (!(e = dfix(s, p, lim, 4, v))) put<EMIT>(k, is_row, cur, 0, v, 0);
+        break;
+    case 1:
+        if (!(e = dvar(s, p, lim, v))) put<EMIT>(k, is_row, cur, 1, (uint32_t)v, 0);
+        break;
+    case 2:
+        if (!(e = dfix(s, p, lim, 4, v)))
+            put<EMIT>(k, is_row, cur, 2, (uint64_t)(int64_t)(int32_t)(uint32_t)v, 0);
+        break;
+    case 3:
+        if (!(e = dvar(s, p, lim, v))) {
+            const uint32_t n = (uint32_t)v;
+            const int32_t r = (int32_t)(n >> 1) ^ (int32_t)(0u - (n & 1u));
+            put<EMIT>(k, is_row, cur, 3, (uint64_t)(int64_t)r, 0);
+        }
+        break;
+    case 4:
+    case 6:
+    case 9:
+        if (!(e = dfix(s, p, lim, 8, v))) put<EMIT>(k, is_row, cur, t, v, 0);
+        break;
+    case 5:
+        if (!(e = dvar(s, p, lim, v))) put<EMIT>(k, is_row, cur, 5, v, 0);
+        break;
+    case 7:
+        if (!(e = dvar(s, p, lim, v)))
+            put<EMIT>(k, is_row, cur, 7, (v >> 1) ^ (0ull - (v & 1ull)), 0);
+        break;
+    case 8:
+        if (!(e = dfix(s, p, lim, 4, v))) put<EMIT>(k, is_row, cur, 8, v, 0);
+        break;
+    case 10:
+        if ((e = dfix(s, p, lim, 8, v))) break;
+        if ((e = dfix(s, p, lim, 4, v2))) break;
+        if (!datetime_valid((int64_t)v, (uint32_t)v2)) {
+            e = E_INVALID;
+            break;
+        }
+        put<EMIT>(k, is_row, cur, 10, v, (uint32_t)v2);
+        break;
+    case 11: {
+        if ((e = dfix(s, p, lim, 8, v))) break;
+        if ((e = dfix(s, p, lim, 4, v2))) break;
+        uint64_t secs = v;
+        uint32_t ns = (uint32_t)v2;
+        if (ns >= 1000000000u) {
+            const uint64_t add = ns / 1000000000u;
+            if (secs + add < secs) {
+                e = E_INVALID;  // Duration::new overflow panics in the reference
+                break;
+            }
+            secs += add;
+            ns %= 1000000000u;
+        }
+        put<EMIT>(k, is_row, cur, 11, secs, ns);
+        break;
+    }
+    case 12:
+    case 18:
+        if (!(e = dstr<MODE>(s, p, lim, true, off, len, work)))
+            put<EMIT>(k, is_row, cur, t, off, (uint32_t)len);
+        break;
+    case 13:
+        if (!(e = dstr<MODE>(s, p, lim, false, off, len, work)))
+            put<EMIT>(k, is_row, cur, 13, off, (uint32_t)len);
+        break;
+    case 14:
+        put<EMIT>(k, is_row, cur, 14, 1, 0);
+        break;
+    case 15:
+        put<EMIT>(k, is_row, cur, 15, 0, 0);
+        break;
+    case 16:
+    case 17:
+        put<EMIT>(k, is_row, cur, 16, 0, 0);
+        break;
+    case 20:
+        if (lim - p < 16) {
+            e = E_SHORT;
+            break;
+        }
+        put<EMIT>(k, is_row, cur, 20, p, 16);
+        p += 16;
+        break;
+    case 22:  // Error(Value) whose inner value is a String: wire tag 18 in the columns
+        p++;  // the inner String tag (12), checked by the caller
+        if (!(e = dstr<MODE>(s, p, lim, true, off, len, work)))
+            put<EMIT>(k, is_row, cur, 18, off, (uint32_t)len);
+        break;
+    case 23:
+        if (!(e = dfix(s, p, lim, 1, v))) put<EMIT>(k, is_row, cur, 23, v, 0);
+        break;
+    case 24:
+        if (!(e = dfix(s, p, lim, 1, v)))
+            put<EMIT>(k, is_row, cur, 24, (uint64_t)(int64_t)(int8_t)(uint8_t)v, 0);
+        break;
+    case 25:
+        if (!(e = dfix(s, p, lim, 2, v))) put<EMIT>(k, is_row, cur, 25, v, 0);
+        break;
+    case 26:
+        if (!(e = dfix(s, p, lim, 2, v)))
+            put<EMIT>(k, is_row, cur, 26, (uint64_t)(int64_t)(int16_t)(uint16_t)v, 0);
+        break;
+    case 27: {
+        if ((e = dvar(s, p, lim, v))) break;
+        if (v < 1) {
+            e = E_SHORT;
+            break;
+        }
+        const uint64_t take = v - vl64(v);
+        const uint64_t l2 = take < lim - p ? p + take : lim;
+        if (l2 - p < 16) {
+            e = E_SHORT;
+            break;
+        }
+        put<EMIT>(k, is_row, cur, 27, p, (uint32_t)(l2 - p));
+        p = l2;
+        break;
+    }
+    default:
+        e = E_UNKNOWN_TAG;
+    }
+    return e;
+}
+
+// Does the value whose tag t was just consumed (next byte at p) contain other values?
+NXG_DEV bool is_container(const Src& s, uint32_t t, uint64_t p, uint64_t lim) {
+    return t == 19 || t == 21 || (t == 22 && !(p < lim && s.byte(p) == 12u));
+}
+
+// Container header at p (tag t consumed): element count -> kids, and the container's own row.
+template <bool EMIT>
+NXG_DEV uint32_t dcontainer(const Src& s, uint32_t t, uint64_t& p, uint64_t lim, const Sink* k,
+                            bool is_row, uint64_t cur, uint64_t child_next, uint64_t& kids) {
+    if (t == 22) {
+        kids = 1;
+        put<EMIT>(k, is_row, cur, 22, child_next, 1);
+        return E_OK;
+    }
+    uint64_t v;
+    const uint32_t e = dvar(s, p, lim, v);
+    if (e) return e;
+    // ValArray / Map guards: array.rs:600-603 (16 B per element), pack.rs:1228-1231 (32 B)
+    const uint64_t maxe = t == 19 ? (kMaxVec / 16) : (kMaxVec / 32);
+    const uint64_t unit = t == 19 ? 16 : 32;
+    if (v > maxe || v * unit > ((lim - p) << 8)) return E_TOO_BIG;
+    kids = t == 19 ? v : 2 * v;
+    put<EMIT>(k, is_row, cur, t, child_next, (uint32_t)v);
+    return E_OK;
+}
+
+constexpr uint32_t E_NESTED = 101;  // internal: flat decoder met a nested container
+
+// One Value at p, for values nested at most one level deep (a container of leaves): no stack,
+// so nothing spills to scratch. A deeper value returns E_NESTED (after the same checks the
+// general decoder would have made up to that point), and the caller re-decodes it with dvalue.
+template <bool EMIT, int MODE>
+NXG_DEV uint32_t dvalue_flat(const Src& s, uint64_t& p, uint64_t lim, const Sink* k, bool row,
+                             uint64_t slot, uint64_t& child_next, uint32_t& work) {
+    if (MODE == M_SPEC && ++work > kSpecBudget) return E_BUDGET;
+    if (MODE == M_BOUNDED && ++work > kWalkBudget) return E_BUDGET;
+    if (p >= lim) return E_SHORT;
+    const uint32_t t = s.byte(p++);
+    if (!is_container(s, t, p, lim)) return dleaf<EMIT, MODE>(s, t, p, lim, k, row, slot, work);
+    uint64_t kids;
+    uint32_t e = dcontainer<EMIT>(s, t, p, lim, k, row, slot, child_next, kids);
+    if (e) return e;
+    const uint64_t base = child_next;
+    child_next += kids;
+#pragma unroll 1
+    for (uint64_t i = 0; i < kids; i++) {
+        if (MODE == M_SPEC && ++work > kSpecBudget) return E_BUDGET;
+        if (MODE == M_BOUNDED && ++work > kWalkBudget) return E_BUDGET;
+        if (p >= lim) return E_SHORT;
+        const uint32_t t2 = s.byte(p++);
+        if (is_container(s, t2, p, lim)) return E_NESTED;
+        if ((e = dleaf<EMIT, MODE>(s, t2, p, lim, k, false, base + i, work))) return e;
+    }
+    return E_OK;
+}
+
+// Any Value at p: iterative depth-first walk with an explicit stack (scratch memory), used only
+// for values nested deeper than dvalue_flat handles. Children are allocated depth-first, the
+// order in which the recursive reference decoder produces them.
+template <bool EMIT, int MODE>
+__device__ __attribute__((noinline)) uint32_t dvalue_deep(const Src& s, uint64_t& p, uint64_t lim,
+                                                          const Sink* k, bool row, uint64_t slot,
+                                                          uint64_t& child_next, uint32_t& work) {
     uint64_t frem[NXG_MAX_DEPTH + 2];
     uint64_t fslot[NXG_MAX_DEPTH + 2];
     int top = -1;
@@ -139,152 +374,10 @@ NXG_DEV uint32_t dvalue(const Src& s, uint64_t& p, uint64_t lim, const Sink* k, 
         if (MODE == M_BOUNDED && ++work > kWalkBudget) return E_BUDGET;
         if (p >= lim) return E_SHORT;
         const uint32_t t = s.byte(p++);
-        uint64_t v, v2, off, len;
-        uint32_t e = E_OK;
-        uint64_t kids = 0;  // values to push for containers
-        switch (t) {
-        case 0:
-            if (!(e = dfix(s, p, lim, 4, v))) put<EMIT>(k, is_row, cur, 0, v, 0);
-            break;
-        case 1:
-            if (!(e = dvar(s, p, lim, v))) put<EMIT>(k, is_row, cur, 1, (uint32_t)v, 0);
-            break;
-        case 2:
-            if (!(e = dfix(s, p, lim, 4, v)))
-                put<EMIT>(k, is_row, cur, 2, (uint64_t)(int64_t)(int32_t)(uint32_t)v, 0);
-            break;
-        case 3:
-            if (!(e = dvar(s, p, lim, v))) {
-                const uint32_t n = (uint32_t)v;
-                const int32_t r = (int32_t)(n >> 1) ^ (int32_t)(0u - (n & 1u));
-                put<EMIT>(k, is_row, cur, 3, (uint64_t)(int64_t)r, 0);
-            }
-            break;
-        case 4:
-        case 6:
-        case 9:
-            if (!(e = dfix(s, p, lim, 8, v))) put<EMIT>(k, is_row, cur, t, v, 0);
-            break;
-        case 5:
-            if (!(e = dvar(s, p, lim, v))) put<EMIT>(k, is_row, cur, 5, v, 0);
-            break;
-        case 7:
-            if (!(e = dvar(s, p, lim, v)))
-                put<EMIT>(k, is_row, cur, 7, (v >> 1) ^ (0ull - (v & 1ull)), 0);
-            break;
-        case 8:
-            if (!(e = dfix(s, p, lim, 4, v))) put<EMIT>(k, is_row, cur, 8, v, 0);
-            break;
-        case 10:
-            if ((e = dfix(s, p, lim, 8, v))) break;
-            if ((e = dfix(s, p, lim, 4, v2))) break;
-            if (!datetime_valid((int64_t)v, (uint32_t)v2)) {
-                e = E_INVALID;
-                break;
-            }
-            put<EMIT>(k, is_row, cur, 10, v, (uint32_t)v2);
-            break;
-        case 11: {
-            if ((e = dfix(s, p, lim, 8, v))) break;
-            if ((e = dfix(s, p, lim, 4, v2))) break;
-            uint64_t secs = v;
-            uint32_t ns = (uint32_t)v2;
-            if (ns >= 1000000000u) {
-                const uint64_t add = ns / 1000000000u;
-                if (secs + add < secs) {
-                    e = E_INVALID;  // Duration::new overflow panics in the reference
-                    break;
-                }
-                secs += add;
-                ns %= 1000000000u;
-            }
-            put<EMIT>(k, is_row, cur, 11, secs, ns);
-            break;
-        }
-        case 12:
-        case 18:
-            if (!(e = dstr<MODE>(s, p, lim, true, off, len, work)))
-                put<EMIT>(k, is_row, cur, t, off, (uint32_t)len);
-            break;
-        case 13:
-            if (!(e = dstr<MODE>(s, p, lim, false, off, len, work)))
-                put<EMIT>(k, is_row, cur, 13, off, (uint32_t)len);
-            break;
-        case 14:
-            put<EMIT>(k, is_row, cur, 14, 1, 0);
-            break;
-        case 15:
-            put<EMIT>(k, is_row, cur, 15, 0, 0);
-            break;
-        case 16:
-        case 17:
-            put<EMIT>(k, is_row, cur, 16, 0, 0);
-            break;
-        case 19:
-        case 21: {
-            if ((e = dvar(s, p, lim, v))) break;
-            const uint64_t maxe = t == 19 ? (kMaxVec / 16) : (kMaxVec / 32);
-            const uint64_t unit = t == 19 ? 16 : 32;
-            if (v > maxe || v * unit > ((lim - p) << 8)) {
-                e = E_TOO_BIG;
-                break;
-            }
-            kids = t == 19 ? v : 2 * v;
-            put<EMIT>(k, is_row, cur, t, child_next, (uint32_t)v);
-            break;
-        }
-        case 20:
-            if (lim - p < 16) {
-                e = E_SHORT;
-                break;
-            }
-            put<EMIT>(k, is_row, cur, 20, p, 16);
-            p += 16;
-            break;
-        case 22:
-            // Error(Value) whose inner value is a String is Error(String) = wire tag 18
-            if (p < lim && s.byte(p) == 12u) {
-                p++;
-                if (!(e = dstr<MODE>(s, p, lim, true, off, len, work)))
-                    put<EMIT>(k, is_row, cur, 18, off, (uint32_t)len);
-                break;
-            }
-            kids = 1;
-            put<EMIT>(k, is_row, cur, 22, child_next, 1);
-            break;
-        case 23:
-            if (!(e = dfix(s, p, lim, 1, v))) put<EMIT>(k, is_row, cur, 23, v, 0);
-            break;
-        case 24:
-            if (!(e = dfix(s, p, lim, 1, v)))
-                put<EMIT>(k, is_row, cur, 24, (uint64_t)(int64_t)(int8_t)(uint8_t)v, 0);
-            break;
-        case 25:
-            if (!(e = dfix(s, p, lim, 2, v))) put<EMIT>(k, is_row, cur, 25, v, 0);
-            break;
-        case 26:
-            if (!(e = dfix(s, p, lim, 2, v)))
-                put<EMIT>(k, is_row, cur, 26, (uint64_t)(int64_t)(int16_t)(uint16_t)v, 0);
-            break;
-        case 27: {
-            if ((e = dvar(s, p, lim, v))) break;
-            if (v < 1) {
-                e = E_SHORT;
-                break;
-            }
-            const uint64_t take = v - vl64(v);
-            const uint64_t l2 = take < lim - p ? p + take : lim;
-            if (l2 - p < 16) {
-                e = E_SHORT;
-                break;
-            }
-            put<EMIT>(k, is_row, cur, 27, p, (uint32_t)(l2 - p));
-            p = l2;
-            break;
-        }
-        default:
-            e = E_UNKNOWN_TAG;
-        }
+        uint32_t e;
+        uint64_t kids = 0;
+        if (is_container(s, t, p, lim)) e = dcontainer<EMIT>(s, t, p, lim, k, is_row, cur, child_next, kids);
+        else e = dleaf<EMIT, MODE>(s, t, p, lim, k, is_row, cur, work);
         if (e) return e;
         if (kids) {
             const uint64_t base = child_next;
@@ -300,6 +393,20 @@ NXG_DEV uint32_t dvalue(const Src& s, uint64_t& p, uint64_t lim, const Sink* k, 
         is_row = false;
         depth = top + 1;
     }
+}
+
+// Decode one Value at p (limit lim) into (row?, slot), children from `child_next`.
+template <bool EMIT, int MODE>
+NXG_DEV uint32_t dvalue(const Src& s, uint64_t& p, uint64_t lim, const Sink* k, bool row,
+                        uint64_t slot, uint64_t& child_next, uint32_t& work) {
+    const uint64_t p0 = p, c0 = child_next;
+    const uint32_t w0 = work;
+    const uint32_t e = dvalue_flat<EMIT, MODE>(s, p, lim, k, row, slot, child_next, work);
+    if (e != E_NESTED) return e;
+    p = p0;
+    child_next = c0;
+    work = w0;
+    return dvalue_deep<EMIT, MODE>(s, p, lim, k, row, slot, child_next, work);
 }
 
 struct MsgInfo {

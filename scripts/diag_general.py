@@ -13,8 +13,7 @@ import netidx_amd
 from netidx_amd import synth
 from netidx_amd.codec import Columns, lib
 
-NAMES = ["redo_tiles", "fallbacks", "repair_rounds", "walks", "spec_tries", "no_spec_tiles",
-         "exhausted", "-"]
+NAMES = ["run_fixes", "-", "repair_rounds", "-", "spec_tries", "-", "-", "-"]
 
 
 def diag(codec):
@@ -39,6 +38,6 @@ for n in [int(x) for x in (sys.argv[1:] or ["100000", "1000000", "10000000"])]:
         st = codec.decode_into(wire, wire.numel(), out, netidx_amd.HINT_MIXED)
         t = time.perf_counter() - t0
     ok = torch.equal(out.id[:n], mc.id[:n]) and torch.equal(out.fixed[:n], mc.fixed[:n])
-    tiles = (wire.numel() + 8191) // 8192
+    tiles = (wire.numel() + 4095) // 4096
     print(f"n={n} W={wire.numel()} tiles={tiles} enc={t_enc*1e3:.1f}ms dec={t*1e3:.2f}ms "
           f"rows={st.n_rows} err={st.err_kind} ok={ok} {diag(codec)}", flush=True)
