@@ -50,7 +50,7 @@ struct NxgCtx {
     hipStream_t own = nullptr;
     hipStream_t stream = nullptr;
     int ncu = 0;
-    int grid_dec_gen = 0, grid_enc_f64 = 0, grid_enc_gen = 0;
+    int grid_enc_f64 = 0, grid_enc_gen = 0;
     // status ring: one DevStatus per call, the whole ring re-zeroed once per lap
     DevStatus* dst = nullptr;
     DevStatus* hst = nullptr;  // pinned mirror
@@ -66,7 +66,6 @@ struct NxgCtx {
     size_t glws_cap = 0;
     uint64_t* gruns = nullptr;     // general decode: run summaries + bases
     int wgs_dec_gen = 0;
-    bool gen_v1 = false;           // NXG_GEN_V1=1: the single-pass look-back decoder instead
     uint8_t* dframe = nullptr;
     size_t dframe_cap = 0;
     uint64_t* escratch = nullptr;
@@ -286,19 +285,11 @@ bool ensure_glws(NxgCtx* c, size_t bytes, NetidxError* err) {
 
 bool enqueue_dec_general(NxgCtx* c, const uint8_t* f, uint64_t len, NxgColumns* out,
                          DevStatus* st, NetidxError* err) {
-    if (!c->gen_v1) {
-        if (!ensure_glws(c, 256 * nxg_dec_gen_tiles(len), err)) return false;
-        const ColsDesc d = desc_of(out);
-        HIPCHK(nxg_launch_dec_gen(f, len, d, c->glws, c->gruns,
-                                  c->gruns + (size_t)gdec2::MAX_RUNS * gdec2::RUN_WORDS,
-                                  c->wgs_dec_gen, st, c->stream));
-        return true;
-    }
-    const uint64_t nt = (len + gdec::TILE - 1) / gdec::TILE;
-    if (!ensure_tstat(c, nt * gdec::SLOT_WORDS, err)) return false;
+    if (!ensure_glws(c, 256 * nxg_dec_gen_tiles(len), err)) return false;
     const ColsDesc d = desc_of(out);
-    HIPCHK(nxg_launch_dec_general(f, len, d, c->tstat, c->epoch, st, 1, c->grid_dec_gen,
-                                  c->stream));
+    HIPCHK(nxg_launch_dec_gen(f, len, d, c->glws, c->gruns,
+                              c->gruns + (size_t)gdec2::MAX_RUNS * gdec2::RUN_WORDS,
+                              c->wgs_dec_gen, st, c->stream));
     return true;
 }
 
@@ -319,8 +310,12 @@ bool finish_decode(NxgCtx* c, const uint8_t* f, uint64_t len, NxgColumns* out, i
         HIPCHK(hipStreamSynchronize(c->stream));
         h = c->hst[slot2];
     }
+    if (h.err_key) {  // general decode: the earliest (offset, kind) on the true chain
+        h.err_kind = (uint32_t)(~h.err_key & 0xffu);
+        h.err_offset = ~h.err_key >> 8;
+    }
     c->last = h;
-    if (h.timeout) {
+    if (h.timeout || h.err_kind == NXG_TIMEOUT) {
         set_err(err, "device look-back watchdog expired");
         return false;
     }
@@ -494,14 +489,13 @@ NxgCtx* nxg_ctx_new(int device, NetidxError* err) {
     if ((e = hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking)) != hipSuccess)
         return fail("hipStreamCreate", e);
     c->stream = c->own;
-    // Default schedule for the look-back kernels: one workgroup per tile in blockIdx order
-    // (grid 0), so the look-back always finds recent inclusive prefixes. NXG_PERSISTENT=1
+    // Default schedule for the look-back (encode) kernels: one workgroup per tile in blockIdx
+    // order (grid 0), so the look-back always finds recent inclusive prefixes. NXG_PERSISTENT=1
     // selects a persistent grid instead: every workgroup co-resident, with one block of margin
     // under the occupancy answer (MI355X_MICROARCH.md residency notes).
     auto grid = [&](int occ) { return c->ncu * std::max(1, occ > 2 ? occ - 1 : occ); };
     const char* pe = getenv("NXG_PERSISTENT");
     const bool persist = pe && pe[0] == '1';
-    c->grid_dec_gen = persist ? grid(nxg_occupancy_dec_general()) : 0;
     c->grid_enc_f64 = persist ? grid(nxg_occupancy_enc_f64()) : 0;
     c->grid_enc_gen = persist ? grid(nxg_occupancy_enc_general()) : 0;
     if ((e = hipMalloc(&c->dst, sizeof(DevStatus) * kStatusRing)) != hipSuccess)
@@ -520,8 +514,6 @@ NxgCtx* nxg_ctx_new(int device, NetidxError* err) {
     const size_t gw = (size_t)gdec2::MAX_RUNS * (gdec2::RUN_WORDS + 4);
     if ((e = hipMalloc(&c->gruns, gw * 8)) != hipSuccess) return fail("hipMalloc(gruns)", e);
     c->wgs_dec_gen = nxg_dec_gen_wgs(c->ncu);
-    const char* g1 = getenv("NXG_GEN_V1");
-    c->gen_v1 = g1 && g1[0] == '1';
     return c;
 }
 

@@ -49,7 +49,7 @@ NXG_DEV uint32_t lw_ctl(uint32_t w) { return (w >> 13) & 63u; }
 NXG_DEV uint32_t lw_ch(uint32_t w) { return w >> 19; }
 
 // run summary words
-enum { R_SPEC = 0, R_EXIT, R_ROWS, R_CH, R_CTL, R_HB, R_ERR, R_FIXED, R_WORDS };
+enum { R_SPEC = 0, R_EXIT, R_ROWS, R_CH, R_CTL, R_ERR, R_FIXED, R_PAD, R_WORDS };
 static_assert(R_WORDS == gdec2::RUN_WORDS, "run summary");
 // R_ERR: kind << 56 | offset (0 = none). R_SPEC: NONE when the run holds no message start.
 
@@ -66,9 +66,9 @@ struct LaneRes {
     uint32_t ek;
 };
 
-// Validating walk of the messages that start in [e, end).
-template <int MODE>
-NXG_DEV void walk(const Src& s, uint64_t e, uint64_t end, LaneRes& r) {
+// Structural walk of the messages that start in [e, end) (skim_msg: lengths, variants, child
+// slots). Only a broken length prefix is an error here; content errors are the emit pass's.
+NXG_DEV void walk(const Src& s, uint64_t e, uint64_t end, LaneRes& r, uint32_t budget) {
     r.x = e;
     r.rows = r.ctl = r.hb = 0;
     r.children = 0;
@@ -81,7 +81,7 @@ NXG_DEV void walk(const Src& s, uint64_t e, uint64_t end, LaneRes& r) {
     while (pos < stop) {
         MsgInfo mi;
         uint64_t ch = 0;
-        const uint32_t err = decode_msg<false, MODE>(s, pos, mi, nullptr, 0, ch, work);
+        const uint32_t err = skim_msg(s, pos, mi, ch, work, budget);
         if (err == E_BUDGET) {
             r.st = S_EXH;
             return;
@@ -101,15 +101,79 @@ NXG_DEV void walk(const Src& s, uint64_t e, uint64_t end, LaneRes& r) {
     r.x = pos;
 }
 
-// First position in [c, stop) where an Update decodes plausibly (minimal length varint, value
-// filling the length exactly) and is followed by a plausible message (or the frame end).
-// Candidates come from a SWAR scan for the Update variant byte (4) one or two bytes after a
-// 1- or 2-byte length varint. Only Updates are guessed: a Heartbeat or Unsubscribed accepts
-// almost any bytes; a chunk that starts with one is resolved by the repair.
+// 1 + payload size of the fixed-size value tags (pack.rs / value lib.rs:361-468), 4 bits per
+// tag; 0 = variable size (varints, text, containers) or not checked (Decimal)
+constexpr uint64_t kFixLo = 0x1100DD9509090505ull;  // tags 0..15
+constexpr uint64_t kFixHi = 0x0000033220000011ull;  // tags 16..27
+NXG_DEV uint32_t fixed_size1(uint32_t t) {
+    return (uint32_t)(((t < 16 ? kFixLo >> (4 * t) : kFixHi >> (4 * (t - 16)))) & 0xfu);
+}
+
+// Structural plausibility of an Update at p with an nb-byte length prefix L (minimal): the
+// Update variant is already matched by the caller. Checks that the id varint and the value tag
+// fit in the message, that a fixed-size value fills it exactly, and that the next position
+// looks like a message start (length >= 2, variant <= 6) or is the frame end. Only the
+// candidate's own bytes are guaranteed to be in the LDS image.
+NXG_DEV bool plausible(const Src& s, uint64_t p, uint32_t nb, uint64_t L) {
+    const uint64_t next = p + L;  // total size = nb + L - vl(L) = L for a minimal prefix
+    if (next > s.W) return false;
+    uint64_t q = p + nb + 1;  // id varint
+    uint32_t k = 0;
+    while (k < 10 && q + k < next && (s.img_byte(q + k) & 0x80u)) k++;
+    const uint64_t tp = q + k + 1;  // value tag
+    if (k == 10 || tp >= next) return false;
+    const uint32_t t = s.img_byte(tp);
+    if (t >= 28u) return false;
+    const uint32_t f1 = fixed_size1(t);
+    if (f1 && tp + f1 != next) return false;
+    const bool vint = t == 1 || t == 3 || t == 5 || t == 7;
+    const bool text = t == 12 || t == 13 || t == 18;
+    if (vint || text) {  // the varint payload, or text length + text, fills the message exactly
+        uint64_t v = 0, a = tp + 1;
+        uint32_t i = 0, b;
+        do {
+            if (a + i >= next || i == 10) return false;
+            b = s.any_byte(a + i);
+            v |= (uint64_t)(b & 0x7fu) << (7 * i);
+            i++;
+        } while (b & 0x80u);
+        if ((vint ? a + i : a + i + v) != next) return false;
+    }
+    if (t == 19) {  // Array: an empty one ends the message, elements fit, the first tag is valid
+        uint64_t v = 0, a = tp + 1;
+        uint32_t i = 0, b;
+        do {
+            if (a + i >= next || i == 10) return false;
+            b = s.any_byte(a + i);
+            v |= (uint64_t)(b & 0x7fu) << (7 * i);
+            i++;
+        } while (b & 0x80u);
+        if (v == 0 ? a + i != next : (a + i + v > next || s.any_byte(a + i) >= 28u)) return false;
+    }
+    if (next == s.W) return true;
+    if (next + 2 > s.W) return false;  // no room for a message (>= 2 bytes)
+    const uint32_t b0 = s.any_byte(next);
+    uint32_t v;
+    if (b0 < 0x80u) {
+        if (b0 < 2u) return false;
+        v = s.any_byte(next + 1);
+    } else {
+        if (next + 3 > s.W) return false;
+        const uint32_t b1 = s.any_byte(next + 1);
+        if (b1 == 0u || b1 >= 0x80u) return false;
+        v = s.any_byte(next + 2);
+    }
+    return v <= 6u;
+}
+
+// First position in [c, stop) that starts a plausible Update (see plausible). Candidates come
+// from a SWAR scan for the Update variant byte (4) one or two bytes after a 1- or 2-byte length
+// varint. Only Updates are guessed: a Heartbeat or Unsubscribed accepts almost any bytes; a
+// chunk that starts with one, or a wrong guess, is resolved exactly by the repair.
 NXG_DEV uint64_t speculate(const Src& s, uint64_t c, uint64_t stop, uint32_t& tries) {
     if (c >= stop) return NONE;
     const uint64_t rc = c - s.t0;  // 64-aligned, inside the image with 68 bytes to spare
-    const uint32_t* w = reinterpret_cast<const uint32_t*>(s.lds + rc);
+    lds_words w = (lds_words)(s.lds + rc);
     uint64_t e4 = 0;  // bit q: byte c+1+q == 4, q in [0, 64)
 #pragma unroll
     for (int k = 0; k < 16; k++) {
@@ -128,29 +192,26 @@ NXG_DEV uint64_t speculate(const Src& s, uint64_t c, uint64_t stop, uint32_t& tr
             q = 64;
             e4_64 = false;
         }
-        // p = c+q: 1-byte length (4..127) then the variant; p = c+q-1: 2-byte length
-        for (int form = 0; form < 2; form++) {
+        // p = c+q: 1-byte length (4..127) then the variant; p = c+q-1: 2-byte length. The
+        // 1-byte form goes first: a 2-byte "shadow" (a payload byte >= 0x80 just before a true
+        // 1-byte length) shares its variant byte, and only one of the two can be a start.
+        for (int form = 1; form >= 0; form--) {
             const int64_t pr = form == 0 ? (int64_t)q - 1 : (int64_t)q;
             if (pr < 0) continue;
             const uint64_t p = c + (uint64_t)pr;
             if (p >= stop) continue;
-            const uint32_t b0 = s.byte(p);
+            const uint32_t b0 = s.img_byte(p);
+            uint64_t L;
             if (form == 0) {  // 2-byte length: b0 >= 128, next byte 1..127, then 4
-                const uint32_t b1 = s.byte(p + 1);
+                const uint32_t b1 = s.img_byte(p + 1);
                 if (b0 < 0x80u || b1 == 0u || b1 >= 0x80u) continue;
-            } else if (b0 < 4u || b0 >= 0x80u) {
-                continue;
+                L = (b0 & 0x7fu) | (b1 << 7);
+            } else {
+                if (b0 < 4u || b0 >= 0x80u) continue;
+                L = b0;
             }
-            MsgInfo mi;
-            uint64_t ch = 0;
-            uint32_t work = 0;
             tries++;
-            if (decode_msg<false, M_SPEC>(s, p, mi, nullptr, 0, ch, work) || mi.variant != 4)
-                continue;
-            if (mi.next >= s.W) return p;
-            MsgInfo m2;
-            work = 0;
-            if (decode_msg<false, M_SPEC>(s, mi.next, m2, nullptr, 0, ch, work) == E_OK) return p;
+            if (plausible(s, p, form == 0 ? 2u : 1u, L)) return p;
         }
     }
     return NONE;
@@ -162,6 +223,7 @@ struct TileOut {
     uint32_t ek;      // error kind on the chain, 0 = none
     uint64_t rows, ch, ctl, hb;
     uint32_t rounds;
+    uint64_t why;  // repairs by cause, 16 bits each: exhausted, wrong guess, missed, spurious
 };
 
 // Resolve one tile (its bytes are in the wave's LDS image `s`). `entry` is the exact first
@@ -204,21 +266,23 @@ NXG_DEV TileOut process_tile(const Src& s, uint64_t t0, uint64_t entry, uint32_t
     if (lane < a) has = false;
     to.anchor = __shfl(e, (int)a, 64);
     LaneRes r{e, 0, 0, 0, 0, S_NONE, 0};
-    if (has) {
-        if (lane == a && entry != NONE) walk<M_EXACT>(s, e, cend, r);
-        else walk<M_BOUNDED>(s, e, cend, r);
-    }
-    // Exact repair, one lane per round in lane order. Lane j > a is consistent when, with x the
-    // exit of the nearest lane below it that has a start: x < stop_j and j starts exactly at x,
-    // or x >= stop_j and j has no start. Events: the first inconsistent lane (re-walked from x,
-    // or cleared), a consistent lane whose bounded walk ran out of budget (re-walked exactly),
-    // a consistent lane whose walk failed (the tile's error: everything after it is moot).
+    // Round 1 walks every lane with a start (the anchor exactly when its entry is known, the
+    // guesses with a budget). Each later round repairs one lane, in lane order: lane j > a is
+    // consistent when, with x the exit of the nearest lane below it that has a start, x < stop_j
+    // and j starts exactly at x, or x >= stop_j and j has no start. Events: the first
+    // inconsistent lane (re-walked from x, or cleared), a consistent lane whose bounded walk ran
+    // out of budget (re-walked exactly), a consistent lane whose walk failed (the tile's error:
+    // everything after it is moot).
     const uint64_t lt = (1ull << lane) - 1;
     const uint64_t from_a = ~0ull << a;
     int errlane = -1;
     uint32_t rounds = 0;
+    bool need = has;
+    uint32_t budget = (lane == a && entry != NONE) ? kExact.budget : kBounded.budget;
 #pragma unroll 1
     for (;;) {
+        if (need) walk(s, e, cend, r, budget);
+        need = false;
         if (++rounds > 2 * 64 + 4) {
             errlane = -2;  // logic error guard: reported as a timeout, never a hang
             break;
@@ -239,13 +303,16 @@ NXG_DEV TileOut process_tile(const Src& s, uint64_t t0, uint64_t entry, uint32_t
             errlane = bl;
             break;
         }
+        const uint32_t cause = ev_exh ? 0u : (px < stop ? (has ? 1u : 2u) : 3u);
+        to.why += 1ull << (16 * __shfl(cause, bl, 64));
         if ((int)lane == bl) {
+            budget = kExact.budget;
             if (ev_exh) {
-                walk<M_EXACT>(s, e, cend, r);
+                need = true;
             } else if (px < stop) {
                 has = true;
                 e = px;
-                walk<M_EXACT>(s, e, cend, r);
+                need = true;
             } else {
                 has = false;
                 e = NONE;
@@ -260,9 +327,12 @@ NXG_DEV TileOut process_tile(const Src& s, uint64_t t0, uint64_t entry, uint32_t
         lwo = NOSTART;
         return to;
     }
+    // With a broken length prefix in lane errlane, that lane stays live: the emit pass decodes
+    // its messages up to and including the broken one, so a content error earlier in the lane
+    // still wins.
     bool live = has;
     if (errlane >= 0) {
-        live = has && (int)lane < errlane;
+        live = has && (int)lane <= errlane;
         to.ek = __shfl(r.ek, errlane, 64);
         to.exit = __shfl(r.x, errlane, 64);
     } else {
@@ -310,23 +380,33 @@ NXG_DEV void g_stage(uint8_t* buf, const GRegs& g, uint32_t lane) {
 }
 NXG_DEV Src g_src(const uint8_t* buf, const uint8_t* wire, uint64_t t0, uint64_t W) {
     const uint64_t n = W - t0;
-    return Src{buf, t0, (uint32_t)(n < IMG ? n : IMG), wire, W};
+    return Src{(lds_bytes)buf, t0, (uint32_t)(n < IMG ? n : IMG), (gbl_bytes)wire, W};
 }
 
 NXG_DEV uint64_t run_begin(uint64_t nt, uint32_t R, uint32_t r) { return nt * r / R; }
 
-// Re-walk / first walk of the tiles [b, e) of a run from `entry` (NONE: guessed). Lane words go
-// to lws + 64*tile. Fills the run summary (in registers; lane 0 stores it).
+// First walk (or re-walk) of the tiles [b, e) of a run from `entry` (NONE: guessed). Lane words
+// go to lws + 64*tile. Fills the run summary (in registers; lane 0 stores it).
+//
+// Re-walk (old_last != NONE): the run was walked before from a wrong entry and its lane words
+// are valid for tiles up to old_last. As soon as some lane starts at the same position in both
+// walks, the two message chains are the same from there on, so the re-walk stops (`merged`)
+// and d[] holds the changes to the run's rows / children / control messages.
 struct RunSum {
-    uint64_t spec, exit, rows, ch, ctl, hb, err;
+    uint64_t spec, exit, rows, ch, ctl, err;
     uint32_t rounds, tries;
+    uint64_t why;
 };
 NXG_DEV RunSum run_tiles(const uint8_t* __restrict__ wire, uint64_t W, uint64_t b, uint64_t e,
-                         uint64_t entry, uint32_t* __restrict__ lws, uint8_t* buf) {
+                         uint64_t entry, uint32_t* __restrict__ lws, uint8_t* buf,
+                         uint64_t old_last, bool& merged, int64_t* d) {
     const uint32_t lane = __lane_id();
-    RunSum rs{NONE, entry, 0, 0, 0, 0, 0, 0, 0};
+    RunSum rs{NONE, entry, 0, 0, 0, 0, 0, 0};
     bool have_spec = entry != NONE;
     if (have_spec) rs.spec = entry;
+    merged = false;
+    bool cmp = old_last != NONE;
+    int64_t dr = 0, dc = 0, dk = 0;
     GRegs g;
     if (b < e) g_load(g, wire, b * TILE, W, lane);
     uint64_t cur = entry;
@@ -338,10 +418,40 @@ NXG_DEV RunSum run_tiles(const uint8_t* __restrict__ wire, uint64_t W, uint64_t 
         const Src s = g_src(buf, wire, t0, W);
         uint32_t tries = 0;
         uint32_t lwv;
+        const bool cmp_t = cmp && t <= old_last;
+        const uint32_t ow = cmp_t ? lws[t * 64 + lane] : NOSTART;
         const TileOut to = process_tile(s, t0, cur, lwv, tries);
         lws[t * 64 + lane] = lwv;
+        if (cmp_t && !to.ek) {
+            const bool hn = lw_off(lwv) != NOSTART, ho = lw_off(ow) != NOSTART;
+            const uint64_t same = __ballot(hn && ho && lw_off(lwv) == lw_off(ow));
+            const uint32_t j0 = same ? (uint32_t)__builtin_ctzll(same) : 64u;
+            const bool in = lane < j0;  // lanes before the chains meet
+            const bool esc = in && ((hn && lw_ch(lwv) == CH_ESC) || (ho && lw_ch(ow) == CH_ESC));
+            if (__any(esc)) {
+                cmp = false;  // counts not in the words: finish with a full re-walk
+            } else {
+                dr += wave_sum<int64_t>(in ? (int64_t)(hn ? lw_rows(lwv) : 0u) -
+                                                 (int64_t)(ho ? lw_rows(ow) : 0u)
+                                           : 0);
+                dk += wave_sum<int64_t>(in ? (int64_t)(hn ? lw_ctl(lwv) : 0u) -
+                                                 (int64_t)(ho ? lw_ctl(ow) : 0u)
+                                           : 0);
+                dc += wave_sum<int64_t>(in ? (int64_t)(hn ? lw_ch(lwv) : 0u) -
+                                                 (int64_t)(ho ? lw_ch(ow) : 0u)
+                                           : 0);
+                if (same) {
+                    merged = true;
+                    d[0] = dr;
+                    d[1] = dc;
+                    d[2] = dk;
+                    return rs;
+                }
+            }
+        }
         rs.tries += wave_sum<uint32_t>(tries);
         rs.rounds += to.rounds;
+        rs.why += to.why;
         if (!have_spec && to.anchor != NONE) {
             rs.spec = to.anchor;
             have_spec = true;
@@ -349,7 +459,6 @@ NXG_DEV RunSum run_tiles(const uint8_t* __restrict__ wire, uint64_t W, uint64_t 
         rs.rows += to.rows;
         rs.ch += to.ch;
         rs.ctl += to.ctl;
-        rs.hb += to.hb;
         if (to.ek) {
             rs.err = ((uint64_t)to.ek << 56) | (to.exit & POSM);
             rs.exit = to.exit;
@@ -368,13 +477,16 @@ __global__ __launch_bounds__(TPB) void nxg_gen_count_kernel(
     const uint8_t* __restrict__ wire, uint64_t W, uint64_t nt, uint32_t* __restrict__ lws,
     uint64_t* __restrict__ runs, DevStatus* __restrict__ st, DevStatus* zst) {
     zero_status(zst);
-    __shared__ __attribute__((aligned(16))) uint8_t bufs[WAVES][IMG];
+    __shared__ __attribute__((aligned(16))) uint8_t bufs[WAVES][IMG + 16];  // +16: word reads past the image
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const uint32_t R = gridDim.x * WAVES, r = blockIdx.x * WAVES + w;
     const uint64_t b = run_begin(nt, R, r), e = run_begin(nt, R, r + 1);
-    const RunSum rs = run_tiles(wire, W, b, e, b == 0 ? 0ull : NONE, lws, bufs[w]);
+    bool merged;
+    int64_t d[3];
+    const RunSum rs =
+        run_tiles(wire, W, b, e, b == 0 ? 0ull : NONE, lws, bufs[w], NONE, merged, d);
     if (lane < R_WORDS) {
-        const uint64_t v[R_WORDS] = {rs.spec, rs.exit, rs.rows, rs.ch, rs.ctl, rs.hb, rs.err, 0};
+        const uint64_t v[R_WORDS] = {rs.spec, rs.exit, rs.rows, rs.ch, rs.ctl, rs.err, 0, 0};
         uint64_t x = v[0];
 #pragma unroll
         for (int i = 1; i < R_WORDS; i++)
@@ -384,6 +496,9 @@ __global__ __launch_bounds__(TPB) void nxg_gen_count_kernel(
     if (lane == 0) {
         atomicAdd(&st->diag[2], (unsigned long long)rs.rounds);
         atomicAdd(&st->diag[4], (unsigned long long)rs.tries);
+        for (int i = 0; i < 4; i++)
+            atomicAdd(&st->diag[i == 0 ? 1 : i == 1 ? 3 : i == 2 ? 5 : 6],
+                      (unsigned long long)((rs.why >> (16 * i)) & 0xffffu));
     }
 }
 
@@ -437,14 +552,13 @@ __global__ __launch_bounds__(RES_TPB) void nxg_gen_resolve_kernel(
     const uint8_t* __restrict__ wire, uint64_t W, uint64_t nt, uint32_t R,
     uint32_t* __restrict__ lws, uint64_t* __restrict__ runs, uint64_t* __restrict__ base,
     DevStatus* __restrict__ st) {
-    __shared__ __attribute__((aligned(16))) uint8_t buf[IMG];
+    __shared__ __attribute__((aligned(16))) uint8_t buf[IMG + 16];
     __shared__ uint64_t tmp[RES_TPB / 64];
     __shared__ uint32_t sh_first;
     __shared__ uint64_t sh_x;
     const uint32_t tid = threadIdx.x;
     const uint32_t r0 = tid * RES_K;
     uint32_t from = 0, fixes = 0;
-    bool failed = false;
 #pragma unroll 1
     for (;;) {
         // latest run (index + 1) with a start among this thread's runs, then across threads
@@ -484,22 +598,36 @@ __global__ __launch_bounds__(RES_TPB) void nxg_gen_resolve_kernel(
         const uint64_t spec = q[R_SPEC];
         const uint64_t rend = run_begin(nt, R, F + 1) * TILE;
         const bool ok = F == 0 || (spec == NONE ? (XF >= rend || XF >= W) : spec == XF);
-        if (ok) {  // the first error on the true chain: the frame fails here
+        if (ok) {
+            // The first broken length prefix on the true chain: the chain ends in run F. The
+            // emit pass decodes the runs up to F (an earlier content error still wins).
             if (tid == 0) {
                 const uint64_t er = q[R_ERR];
-                st->err_kind = (uint32_t)(er >> 56);
-                st->err_offset = er & POSM;
+                st->err_key = err_key(er & POSM, (uint32_t)(er >> 56));
+                st->runs_valid = F + 1;
             }
-            failed = true;
             break;
         }
         __syncthreads();
         if (tid < 64) {  // wave 0 re-walks run F from its true entry
             const uint64_t b = run_begin(nt, R, F), e = run_begin(nt, R, F + 1);
-            const RunSum rs = run_tiles(wire, W, b, e, XF, lws, buf);
+            // pass 1 wrote lane words up to its last tile (its error tile, if it stopped early)
+            const uint64_t oerr = q[R_ERR];
+            const uint64_t old_last = oerr ? (oerr & POSM) / TILE : e - 1;
+            bool merged;
+            int64_t d[3];
+            const RunSum rs = run_tiles(wire, W, b, e, XF, lws, buf, old_last, merged, d);
             if (tid < R_WORDS) {
-                const uint64_t v[R_WORDS] = {rs.spec, rs.exit, rs.rows, rs.ch,
-                                             rs.ctl,  rs.hb,   rs.err,  1};
+                // merged: the old chain from the meeting point on stands (exit, error)
+                const uint64_t v[R_WORDS] = {
+                    XF,
+                    merged ? q[R_EXIT] : rs.exit,
+                    merged ? q[R_ROWS] + (uint64_t)d[0] : rs.rows,
+                    merged ? q[R_CH] + (uint64_t)d[1] : rs.ch,
+                    merged ? q[R_CTL] + (uint64_t)d[2] : rs.ctl,
+                    merged ? q[R_ERR] : rs.err,
+                    1,
+                    0};
                 uint64_t x = v[0];
 #pragma unroll
                 for (int i = 1; i < R_WORDS; i++)
@@ -516,9 +644,8 @@ __global__ __launch_bounds__(RES_TPB) void nxg_gen_resolve_kernel(
         st->path = 2;
         st->diag[0] = fixes;
     }
-    if (failed) return;
     // prefix sums of the run totals -> bases
-    uint64_t lr = 0, lc = 0, lk = 0, lh = 0;
+    uint64_t lr = 0, lc = 0, lk = 0;
     for (int k = 0; k < RES_K; k++) {
         const uint32_t r = r0 + k;
         if (r >= R) break;
@@ -526,13 +653,11 @@ __global__ __launch_bounds__(RES_TPB) void nxg_gen_resolve_kernel(
         lr += q[R_ROWS];
         lc += q[R_CH];
         lk += q[R_CTL];
-        lh += q[R_HB];
     }
-    uint64_t tr, tc, tk, th;
+    uint64_t tr, tc, tk;
     uint64_t br = res_scan<uint64_t>(lr, tmp, tr);
     uint64_t bc = res_scan<uint64_t>(lc, tmp, tc);
     uint64_t bk = res_scan<uint64_t>(lk, tmp, tk);
-    res_scan<uint64_t>(lh, tmp, th);
     for (int k = 0; k < RES_K; k++) {
         const uint32_t r = r0 + k;
         if (r >= R) break;
@@ -548,7 +673,6 @@ __global__ __launch_bounds__(RES_TPB) void nxg_gen_resolve_kernel(
         st->n_rows = tr;
         st->n_children = tc;
         st->n_ctl = tk;
-        st->n_heartbeat = th;
     }
 }
 
@@ -556,23 +680,28 @@ __global__ __launch_bounds__(RES_TPB) void nxg_gen_resolve_kernel(
 __global__ __launch_bounds__(TPB) void nxg_gen_emit_kernel(
     const uint8_t* __restrict__ wire, uint64_t W, uint64_t nt, const uint32_t* __restrict__ lws,
     const uint64_t* __restrict__ base, ColsDesc cols, DevStatus* __restrict__ st) {
-    if (ld_agent32(&st->err_kind)) return;  // the frame failed: no columns
-    __shared__ __attribute__((aligned(16))) uint8_t bufs[WAVES][IMG];
+    __shared__ __attribute__((aligned(16))) uint8_t bufs[WAVES][IMG + 16];  // +16: word reads past the image
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const uint32_t R = gridDim.x * WAVES, r = blockIdx.x * WAVES + w;
     const uint64_t b = run_begin(nt, R, r), e = run_begin(nt, R, r + 1);
-    if (b >= e) return;
+    // a broken length prefix (resolve) ends the chain: later runs and tiles hold no messages
+    const uint32_t rv = st->runs_valid;
+    const uint64_t ck = st->err_key;
+    const uint64_t chain_end = ck ? (~ck) >> 8 : ~0ull;
+    if (b >= e || (rv && r >= rv)) return;
     uint8_t* buf = bufs[w];
     const Sink sink{cols, &st->capacity, &st->nonf64};
     uint64_t row = base[(uint64_t)r * 4 + 0];
     uint64_t child = base[(uint64_t)r * 4 + 1];
     uint64_t ctl = base[(uint64_t)r * 4 + 2];
+    uint32_t hb = 0;  // heartbeats (counted here: the lane words have no room for them)
     GRegs g;
     g_load(g, wire, b * TILE, W, lane);
     uint32_t lwn = lws[b * 64 + lane];
 #pragma unroll 1
     for (uint64_t t = b; t < e; t++) {
         const uint64_t t0 = t * TILE;
+        if (t0 > chain_end) break;
         const uint32_t lw = lwn;
         g_stage(buf, g, lane);
         if (t + 1 < e) {
@@ -585,49 +714,65 @@ __global__ __launch_bounds__(TPB) void nxg_gen_emit_kernel(
         const bool has = lw_off(lw) != NOSTART;
         uint32_t nr = has ? lw_rows(lw) : 0u, nk = has ? lw_ctl(lw) : 0u;
         uint64_t nch = has ? lw_ch(lw) : 0u;
-        if (has && nch == CH_ESC) {  // children count did not fit the lane word: recount
-            LaneRes rr;
-            walk<M_EXACT>(s, c + lw_off(lw), c + CH, rr);
-            nch = rr.children;
-        }
-        const uint32_t rin = wave_incl_scan(nr);
-        const uint32_t kin = wave_incl_scan(nk);
-        const uint64_t cin = wave_incl_scan<uint64_t>(nch);
-        uint64_t myrow = row + rin - nr, myctl = ctl + kin - nk, mych = child + cin - nch;
-        row += __shfl(rin, 63, 64);
-        ctl += __shfl(kin, 63, 64);
-        child += __shfl(cin, 63, 64);
-        uint64_t pos = has ? c + lw_off(lw) : stop;
-        uint32_t work = 0;
+        // A lane whose children count did not fit its word counts them first (phase 0, no
+        // writes); then the wave scans the counts and every lane decodes + writes (phase 1).
+        const bool recount = has && nch == CH_ESC;
+        uint64_t myrow = 0, myctl = 0, mych = 0;
 #pragma unroll 1
-        while (pos < stop) {
-            MsgInfo mi;
-            const uint32_t err = decode_msg<true, M_EXACT>(s, pos, mi, &sink, myrow, mych, work);
-            if (err) {  // unreachable: the count pass validated this chain
-                atomicOr(&st->timeout, 2u);
-                break;
+        for (int ph = __any(recount) ? 0 : 1; ph < 2; ph++) {
+            if (ph == 1) {
+                const uint32_t rin = wave_incl_scan(nr);
+                const uint32_t kin = wave_incl_scan(nk);
+                const uint64_t cin = wave_incl_scan<uint64_t>(nch);
+                myrow = row + rin - nr;
+                myctl = ctl + kin - nk;
+                mych = child + cin - nch;
+                row += __shfl(rin, 63, 64);
+                ctl += __shfl(kin, 63, 64);
+                child += __shfl(cin, 63, 64);
             }
-            if (mi.variant == 4) {
-                if (myrow < cols.cap_rows) cols.id[myrow] = mi.id;
-                else atomicOr(&st->capacity, 1u);
-                myrow++;
-            } else if (!cols.ctl_row) {
-                atomicOr(&st->nonf64, 1u);
-                myctl++;
-            } else {
-                if (myctl < cols.cap_ctl) {
-                    cols.ctl_row[myctl] = myrow;
-                    cols.ctl_off[myctl] = pos;
-                    cols.ctl_len[myctl] = (uint32_t)(mi.next - pos);
-                    cols.ctl_variant[myctl] = (uint8_t)mi.variant;
-                } else {
-                    atomicOr(&st->capacity, 1u);
+            const bool act = ph == 1 ? has : recount;
+            uint64_t pos = act ? c + lw_off(lw) : stop;
+            uint64_t cn = ph == 1 ? mych : 0;
+            uint32_t work = 0;
+            const DMode md{0xffffffffu, 0, (uint32_t)ph};
+#pragma unroll 1
+            while (pos < stop) {
+                MsgInfo mi;
+                const uint32_t err = decode_msg<true>(s, pos, mi, &sink, myrow, cn, work, md);
+                if (err) {  // the frame's first error is the earliest of these (and resolve's)
+                    atomicMax((unsigned long long*)&st->err_key,
+                              (unsigned long long)err_key(pos, err));
+                    break;
                 }
-                myctl++;
+                if (ph == 1) {
+                    hb += mi.variant == 5;
+                    if (mi.variant == 4) {
+                        if (myrow < cols.cap_rows) cols.id[myrow] = mi.id;
+                        else atomicOr(&st->capacity, 1u);
+                        myrow++;
+                    } else if (!cols.ctl_row) {
+                        atomicOr(&st->nonf64, 1u);
+                        myctl++;
+                    } else {
+                        if (myctl < cols.cap_ctl) {
+                            cols.ctl_row[myctl] = myrow;
+                            cols.ctl_off[myctl] = pos;
+                            cols.ctl_len[myctl] = (uint32_t)(mi.next - pos);
+                            cols.ctl_variant[myctl] = (uint8_t)mi.variant;
+                        } else {
+                            atomicOr(&st->capacity, 1u);
+                        }
+                        myctl++;
+                    }
+                }
+                pos = mi.next;
             }
-            pos = mi.next;
+            if (ph == 0 && recount) nch = cn;
         }
     }
+    hb = wave_sum<uint32_t>(hb);
+    if (lane == 0 && hb) atomicAdd((unsigned long long*)&st->n_heartbeat, (unsigned long long)hb);
 }
 
 uint64_t nxg_dec_gen_tiles(uint64_t W) { return (W + TILE - 1) / TILE; }

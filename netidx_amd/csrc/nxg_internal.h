@@ -14,11 +14,13 @@ struct DevStatus {
     uint32_t fast_fail;  // homogeneous-f64 kernel rejected the frame (=> general path)
     uint32_t timeout;    // a bounded spin expired (protocol bug); reported as NXG_TIMEOUT
     uint32_t capacity;   // a column overflowed its capacity
-    uint32_t done;       // number of tiles completed (diagnostics)
+    uint32_t runs_valid;   // general decode: runs on the true chain, 0 = all (resolve -> emit)
     uint64_t total_bytes;  // encode: bytes written
     uint32_t nonf64;       // general path ran into content that F64-only columns cannot hold
     uint32_t pad0;
-    uint64_t pad[2];
+    // general decode: first error as ~(offset << 8 | kind), combined with atomicMax (0 = none)
+    uint64_t err_key;
+    uint64_t pad1;
     // diagnostics (general decode): 0 redo tiles, 1 look-back fallbacks, 2 repair rounds,
     // 3 lane walks, 4 speculation attempts, 5 tiles without a speculated entry,
     // 6 exhausted (budgeted) walks, 7 unused
@@ -59,16 +61,7 @@ constexpr int MAX_WGS = 2048;            // workgroups per pass (one run per wav
 constexpr int SCRATCH_WORDS = MAX_WGS * WAVES / 2 + MAX_WGS / 2;  // wcnt + gcnt (u32)
 }  // namespace f64dec
 
-// ---- general decode geometry (nxg_decode_general.hip) ----
-namespace gdec {
-constexpr int TPB = 256;
-constexpr int CHUNK = 32;
-constexpr int TILE = TPB * CHUNK;  // 8 KiB per tile
-constexpr int HALO = 256;
-constexpr int SLOT_WORDS = 16;     // per-tile look-back descriptor (agg 8 words + inc 8 words)
-}  // namespace gdec
-
-// ---- general decode v2 geometry (nxg_decode_gen.hip) ----
+// ---- general decode geometry (nxg_decode_gen.hip) ----
 namespace gdec2 {
 constexpr int TPB = 256;            // 4 independent waves per workgroup, one run each
 constexpr int CH = 64;              // bytes per lane
@@ -103,23 +96,19 @@ hipError_t nxg_launch_dec_f64(const uint8_t* wire, uint64_t W, uint64_t* oid, ui
                               uint64_t cap, uint64_t* scratch, uint8_t* moff, int wgs,
                               DevStatus* st, hipStream_t s);
 int nxg_dec_f64_wgs(int ncu);
-hipError_t nxg_launch_dec_general(const uint8_t* wire, uint64_t W, const ColsDesc& cols,
-                                  uint64_t* tslots, uint32_t epoch, DevStatus* st, int emit,
-                                  int grid, hipStream_t s);
 hipError_t nxg_launch_enc_f64(const uint64_t* id, const uint64_t* val, uint64_t n, uint8_t* out,
                               uint64_t cap, uint64_t* tstat, uint32_t epoch, DevStatus* st,
                               int grid, hipStream_t s);
 hipError_t nxg_launch_enc_general(const ColsDesc& cols, const uint8_t* heap, uint8_t* out,
                                   uint64_t cap, uint64_t* scratch, uint64_t* tstat,
                                   uint32_t epoch, DevStatus* st, int grid, hipStream_t s);
-// general decode v2: count + resolve + emit. `lws` holds 64 u32 per tile (nxg_dec_gen_tiles),
+// general decode: count + resolve + emit. `lws` holds 64 u32 per tile (nxg_dec_gen_tiles),
 // `runs` gdec2::MAX_RUNS * RUN_WORDS u64, `base` gdec2::MAX_RUNS * 4 u64; none needs zeroing.
 uint64_t nxg_dec_gen_tiles(uint64_t W);
 hipError_t nxg_launch_dec_gen(const uint8_t* wire, uint64_t W, const ColsDesc& cols, uint32_t* lws,
                               uint64_t* runs, uint64_t* base, int wgs, DevStatus* st,
                               hipStream_t s);
 int nxg_dec_gen_wgs(int ncu);
-int nxg_occupancy_dec_general();
 int nxg_occupancy_enc_f64();
 int nxg_occupancy_enc_general();
 

@@ -9,16 +9,21 @@
 //                              array.rs:595-612, pack.rs:1225-1239, pbuf.rs:139-147,
 //                              pack.rs:457-469, 1567-1575, 1591-1595, 614-622,
 //                              abstract_type.rs:280-298
-// A value is decoded without a stack when it is nested at most one level deep (dvalue_flat, the
-// common case); deeper values are walked iteratively with an explicit stack (dvalue_deep).
-// Children are allocated depth-first, the same order as the recursive reference decoder, which
-// produces them as it goes.
+// Values are walked iteratively; the top level and the first container level live in registers
+// and only deeper nesting uses an explicit stack. Children are allocated depth-first, the same
+// order as the recursive reference decoder, which produces them as it goes.
 //
-// Modes:
-//   M_SPEC    plausibility only (no UTF-8 scan), small work budget: used to GUESS a start
-//   M_BOUNDED full validation with a work budget (E_BUDGET when exceeded): speculative walks,
+// Byte sources. A message whose bytes all lie in the wave's LDS image is decoded from LDS with
+// unchecked reads, multi-byte fields read a word at a time (LdsSrc); any other message is
+// decoded from global memory (GlbSrc). The choice is made once per message, after its length
+// prefix, so the common path never waits on global memory and never branches per byte.
+//
+// Modes (DMode, a runtime value so that each kernel inlines ONE copy of the decoder per source):
+//   kSpec     plausibility only (no UTF-8 scan), small work budget, minimal length varint and a
+//             value that fills the message exactly: used to GUESS a start
+//   kBounded  full validation with a work budget (E_BUDGET when exceeded): speculative walks,
 //             which may start from a wrong position and must not wander through megabytes
-//   M_EXACT   full validation, unbounded: walks from positions known to be message starts
+//   kExact    full validation, unbounded: walks from positions known to be message starts
 #pragma once
 #include "nxg_device.h"
 
@@ -27,38 +32,122 @@ namespace nxgmsg {
 constexpr uint32_t E_OK = 0, E_UNKNOWN_TAG = 1, E_TOO_BIG = 2, E_INVALID = 3, E_SHORT = 4,
                    E_DEPTH = 6, E_BUDGET = 100;  // E_BUDGET: gave up, not a decode error
 constexpr uint64_t kMaxVec = 2ull * 1024 * 1024 * 1024;  // pack.rs:917
-enum Mode { M_SPEC = 0, M_BOUNDED = 1, M_EXACT = 2 };
 constexpr uint32_t kSpecBudget = 256;     // value headers per speculative decode
 constexpr uint32_t kWalkBudget = 2048;    // work units per bounded walk (headers + 16 B of text)
+struct DMode {
+    uint32_t budget;  // work units before E_BUDGET (~0u: unbounded)
+    uint32_t spec;    // plausibility mode (see above)
+    uint32_t write;   // with EMIT: write the decoded values to the sink
+};
+constexpr DMode kSpec{kSpecBudget, 1, 0}, kBounded{kWalkBudget, 0, 0}, kExact{0xffffffffu, 0, 0};
 
-// Bytes of the frame: [t0, t0+nlds) come from LDS, everything else from global memory.
+typedef const __attribute__((address_space(3))) uint8_t* lds_bytes;
+typedef const __attribute__((address_space(3))) uint32_t* lds_words;
+typedef const __attribute__((address_space(1))) uint8_t* gbl_bytes;
+
+// The frame as a wave sees it: bytes [t0, t0+nlds) are in the LDS image `lds` (which has at
+// least 16 readable bytes past nlds), the whole frame [0, W) is at `g` in global memory.
 struct Src {
-    const uint8_t* lds;
+    lds_bytes lds;
     uint64_t t0;
     uint32_t nlds;
-    const uint8_t* __restrict__ g;
+    gbl_bytes g;
     uint64_t W;
-    NXG_DEV uint32_t byte(uint64_t p) const {
+    // a byte known to be inside the image
+    NXG_DEV uint32_t img_byte(uint64_t p) const { return lds[(uint32_t)(p - t0)]; }
+    // any byte of the frame (p < W)
+    NXG_DEV uint32_t any_byte(uint64_t p) const {
         const uint64_t r = p - t0;
-        return r < nlds ? (uint32_t)lds[r] : (uint32_t)g[p];
+        if (r < nlds) return lds[(uint32_t)r];
+        return g[p];
     }
 };
 
-// std::str::from_utf8 (pack.rs:462) over a Src: four ASCII bytes per step while the text lies
-// in the LDS image, the byte-wise state machine (nxg_device.h utf8_valid) otherwise.
-NXG_DEV bool utf8_valid_src(const Src& s, uint64_t p, uint64_t n) {
+// unchecked reads from the LDS image; word() reads up to 7 bytes past p
+struct LdsSrc {
+    lds_bytes lds;
+    uint64_t t0;
+    NXG_DEV uint32_t byte(uint64_t p) const { return lds[(uint32_t)(p - t0)]; }
+    // bytes p..p+3, little-endian, any alignment
+    NXG_DEV uint32_t word(uint64_t p) const {
+        const uint32_t r = (uint32_t)(p - t0);
+        lds_words w = (lds_words)(lds + (r & ~3u));
+        return alignbyte(w[1], w[0], r & 3u);
+    }
+};
+// reads from global memory (callers stay inside the frame)
+struct GlbSrc {
+    gbl_bytes g;
+    NXG_DEV uint32_t byte(uint64_t p) const { return g[p]; }
+    NXG_DEV uint32_t word(uint64_t p) const {
+        return g[p] | ((uint32_t)g[p + 1] << 8) | ((uint32_t)g[p + 2] << 16) |
+               ((uint32_t)g[p + 3] << 24);
+    }
+};
+
+// Where a decoded value goes.
+struct Sink {
+    ColsDesc c;
+    uint32_t* cap_flag;
+    uint32_t* nonf64;  // F64-only columns (tag == nullptr) met a value they cannot hold
+};
+
+// LEB128 (pack.rs:504-520): at most 10 bytes, bits past 64 dropped, no minimality check.
+// With 8 bytes available, one pair of word reads finds the terminator (ends in 1..8 bytes).
+template <class S>
+NXG_DEV uint32_t dvar(const S& s, uint64_t& p, uint64_t lim, uint64_t& v) {
+    if (lim - p >= 8 && lim > p) {
+        const uint64_t x = (uint64_t)s.word(p) | ((uint64_t)s.word(p + 4) << 32);
+        const uint64_t stop = ~x & 0x8080808080808080ull;
+        if (stop) {
+            const uint32_t nb = ((uint32_t)__builtin_ctzll(stop) >> 3) + 1;  // 1..8
+            const uint64_t y = nb == 8 ? x : (x & ((1ull << (8 * nb)) - 1));
+            uint64_t val = 0;
+#pragma unroll
+            for (int i = 0; i < 8; i++) val |= ((y >> (8 * i)) & 0x7full) << (7 * i);
+            p += nb;
+            v = val;
+            return E_OK;
+        }
+    }
+    uint64_t val = 0;
+#pragma unroll 1
+    for (uint32_t i = 0; i < 10; i++) {
+        if (p + i >= lim) return E_SHORT;
+        const uint32_t b = s.byte(p + i);
+        val |= (uint64_t)(b & 0x7fu) << (7 * i);
+        if (b < 0x80u) {
+            p += i + 1;
+            v = val;
+            return E_OK;
+        }
+    }
+    return E_INVALID;
+}
+
+// big-endian fixed-width field of n = 1, 2, 4 or 8 bytes (bytes::Buf::get_*)
+template <class S>
+NXG_DEV uint32_t dfix(const S& s, uint64_t& p, uint64_t lim, uint32_t n, uint64_t& v) {
+    if (lim - p < n) return E_SHORT;
+    uint64_t x;
+    if (n == 8) x = ((uint64_t)bswap32(s.word(p)) << 32) | bswap32(s.word(p + 4));
+    else if (n == 4) x = bswap32(s.word(p));
+    else if (n == 2) x = (s.byte(p) << 8) | s.byte(p + 1);
+    else x = s.byte(p);
+    p += n;
+    v = x;
+    return E_OK;
+}
+
+// std::str::from_utf8 (pack.rs:462): four ASCII bytes per step, the state machine otherwise
+template <class S>
+NXG_DEV bool utf8_ok(const S& s, uint64_t p, uint64_t n) {
     uint64_t i = 0;
-    const uint64_t r0 = p - s.t0;
 #pragma unroll 1
     while (i < n) {
-        const uint64_t r = r0 + i;
-        if (i + 4 <= n && r + 8 <= s.nlds) {
-            const uint32_t* w = reinterpret_cast<const uint32_t*>(s.lds + (r & ~3ull));
-            const uint32_t x = alignbyte(w[1], w[0], (uint32_t)(r & 3));
-            if (!(x & 0x80808080u)) {
-                i += 4;
-                continue;
-            }
+        if (i + 4 <= n && !(s.word(p + i) & 0x80808080u)) {
+            i += 4;
+            continue;
         }
         const uint32_t c = s.byte(p + i);
         if (c < 0x80) {
@@ -84,41 +173,11 @@ NXG_DEV bool utf8_valid_src(const Src& s, uint64_t p, uint64_t n) {
     return true;
 }
 
-// Where a decoded value goes. EMIT=false only counts children.
-struct Sink {
-    ColsDesc c;
-    uint32_t* cap_flag;
-    uint32_t* nonf64;  // F64-only columns (tag == nullptr) met a value they cannot hold
-};
-
-NXG_DEV uint32_t dvar(const Src& s, uint64_t& p, uint64_t lim, uint64_t& v) {
-    uint64_t val = 0;
-#pragma unroll 1
-    for (uint32_t i = 0; i < 10; i++) {
-        if (p + i >= lim) return E_SHORT;
-        const uint32_t b = s.byte(p + i);
-        val |= (uint64_t)(b & 0x7fu) << (7 * i);
-        if (b < 0x80u) {
-            p += i + 1;
-            v = val;
-            return E_OK;
-        }
-    }
-    return E_INVALID;
-}
-
-NXG_DEV uint32_t dfix(const Src& s, uint64_t& p, uint64_t lim, uint32_t n, uint64_t& v) {
-    if (lim - p < n) return E_SHORT;
-    uint64_t x = 0;
-    for (uint32_t i = 0; i < n; i++) x = (x << 8) | s.byte(p + i);
-    p += n;
-    v = x;
-    return E_OK;
-}
-
+// wr == false: nothing is written (counting, or the values of control messages)
 template <bool EMIT>
-NXG_DEV void put(const Sink* k, bool row, uint64_t slot, uint32_t tag, uint64_t fixed, uint32_t aux) {
-    if (!EMIT) return;
+NXG_DEV void put(const Sink* k, bool wr, bool row, uint64_t slot, uint32_t tag, uint64_t fixed,
+                 uint32_t aux) {
+    if (!EMIT || !wr) return;
     if (row) {
         if (!k->c.tag) {  // F64-only columns
             if (tag != 9) atomicOr(k->nonf64, 1u);
@@ -142,20 +201,20 @@ NXG_DEV void put(const Sink* k, bool row, uint64_t slot, uint32_t tag, uint64_t 
 }
 
 // string/bytes payload: varint len; TooBig if len > remaining; UTF-8 for strings (not in
-// M_SPEC). In M_BOUNDED a long text spends work, one unit per 16 bytes.
-template <int MODE>
-NXG_DEV uint32_t dstr(const Src& s, uint64_t& p, uint64_t lim, bool utf8, uint64_t& off,
-                      uint64_t& len, uint32_t& work) {
+// kSpec). A bounded walk spends one work unit per 16 bytes of text.
+template <class S>
+NXG_DEV uint32_t dstr(const S& s, uint64_t& p, uint64_t lim, bool utf8, uint64_t& off,
+                      uint64_t& len, uint32_t& work, const DMode& md) {
     uint64_t n;
     uint32_t e = dvar(s, p, lim, n);
     if (e) return e;
     if (n > lim - p) return E_TOO_BIG;
-    if (utf8 && MODE != M_SPEC) {
-        if (MODE == M_BOUNDED) {
+    if (utf8 && !md.spec) {
+        if (md.budget != 0xffffffffu) {
             work += (uint32_t)min<uint64_t>(n >> 4, kWalkBudget);
-            if (work > kWalkBudget) return E_BUDGET;
+            if (work > md.budget) return E_BUDGET;
         }
-        if (!utf8_valid_src(s, p, n)) return E_INVALID;
+        if (!utf8_ok(s, p, n)) return E_INVALID;
     }
     off = p;
     len = n;
@@ -165,44 +224,44 @@ NXG_DEV uint32_t dstr(const Src& s, uint64_t& p, uint64_t lim, bool utf8, uint64
 
 // Payload of one non-container value with wire tag t (the tag byte already consumed) into
 // (row?, slot). Containers (19 Array, 21 Map, 22 Error(Value) whose inner is not a String) are
-// handled by the callers. Tag 22 reaches here only as Error(String).
-template <bool EMIT, int MODE>
-NXG_DEV uint32_t dleaf(const Src& s, uint32_t t, uint64_t& p, uint64_t lim, const Sink* k,
-                       bool is_row, uint64_t cur, uint32_t& work) {
+// handled by the caller. Tag 22 reaches here only as Error(String).
+template <bool EMIT, class S>
+NXG_DEV uint32_t dleaf(const S& s, uint32_t t, uint64_t& p, uint64_t lim, const Sink* k,
+                       bool is_row, uint64_t cur, uint32_t& work, const DMode& md) {
     uint64_t v, v2, off, len;
     uint32_t e = E_OK;
     switch (t) {
     case 0:
-        if (!(e = dfix(s, p, lim, 4, v))) put<EMIT>(k, is_row, cur, 0, v, 0);
+        if (!(e = dfix(s, p, lim, 4, v))) put<EMIT>(k, md.write, is_row, cur, 0, v, 0);
         break;
     case 1:
-        if (!(e = dvar(s, p, lim, v))) put<EMIT>(k, is_row, cur, 1, (uint32_t)v, 0);
+        if (!(e = dvar(s, p, lim, v))) put<EMIT>(k, md.write, is_row, cur, 1, (uint32_t)v, 0);
         break;
     case 2:
         if (!(e = dfix(s, p, lim, 4, v)))
-            put<EMIT>(k, is_row, cur, 2, (uint64_t)(int64_t)(int32_t)(uint32_t)v, 0);
+            put<EMIT>(k, md.write, is_row, cur, 2, (uint64_t)(int64_t)(int32_t)(uint32_t)v, 0);
         break;
     case 3:
         if (!(e = dvar(s, p, lim, v))) {
             const uint32_t n = (uint32_t)v;
             const int32_t r = (int32_t)(n >> 1) ^ (int32_t)(0u - (n & 1u));
-            put<EMIT>(k, is_row, cur, 3, (uint64_t)(int64_t)r, 0);
+            put<EMIT>(k, md.write, is_row, cur, 3, (uint64_t)(int64_t)r, 0);
         }
         break;
     case 4:
     case 6:
     case 9:
-        if (!(e = dfix(s, p, lim, 8, v))) put<EMIT>(k, is_row, cur, t, v, 0);
+        if (!(e = dfix(s, p, lim, 8, v))) put<EMIT>(k, md.write, is_row, cur, t, v, 0);
         break;
     case 5:
-        if (!(e = dvar(s, p, lim, v))) put<EMIT>(k, is_row, cur, 5, v, 0);
+        if (!(e = dvar(s, p, lim, v))) put<EMIT>(k, md.write, is_row, cur, 5, v, 0);
         break;
     case 7:
         if (!(e = dvar(s, p, lim, v)))
-            put<EMIT>(k, is_row, cur, 7, (v >> 1) ^ (0ull - (v & 1ull)), 0);
+            put<EMIT>(k, md.write, is_row, cur, 7, (v >> 1) ^ (0ull - (v & 1ull)), 0);
         break;
     case 8:
-        if (!(e = dfix(s, p, lim, 4, v))) put<EMIT>(k, is_row, cur, 8, v, 0);
+        if (!(e = dfix(s, p, lim, 4, v))) put<EMIT>(k, md.write, is_row, cur, 8, v, 0);
         break;
     case 10:
         if ((e = dfix(s, p, lim, 8, v))) break;
@@ -211,7 +270,7 @@ NXG_DEV uint32_t dleaf(const Src& s, uint32_t t, uint64_t& p, uint64_t lim, cons
             e = E_INVALID;
             break;
         }
-        put<EMIT>(k, is_row, cur, 10, v, (uint32_t)v2);
+        put<EMIT>(k, md.write, is_row, cur, 10, v, (uint32_t)v2);
         break;
     case 11: {
         if ((e = dfix(s, p, lim, 8, v))) break;
@@ -227,54 +286,54 @@ NXG_DEV uint32_t dleaf(const Src& s, uint32_t t, uint64_t& p, uint64_t lim, cons
             secs += add;
             ns %= 1000000000u;
         }
-        put<EMIT>(k, is_row, cur, 11, secs, ns);
+        put<EMIT>(k, md.write, is_row, cur, 11, secs, ns);
         break;
     }
     case 12:
     case 18:
-        if (!(e = dstr<MODE>(s, p, lim, true, off, len, work)))
-            put<EMIT>(k, is_row, cur, t, off, (uint32_t)len);
+        if (!(e = dstr(s, p, lim, true, off, len, work, md)))
+            put<EMIT>(k, md.write, is_row, cur, t, off, (uint32_t)len);
         break;
     case 13:
-        if (!(e = dstr<MODE>(s, p, lim, false, off, len, work)))
-            put<EMIT>(k, is_row, cur, 13, off, (uint32_t)len);
+        if (!(e = dstr(s, p, lim, false, off, len, work, md)))
+            put<EMIT>(k, md.write, is_row, cur, 13, off, (uint32_t)len);
         break;
     case 14:
-        put<EMIT>(k, is_row, cur, 14, 1, 0);
+        put<EMIT>(k, md.write, is_row, cur, 14, 1, 0);
         break;
     case 15:
-        put<EMIT>(k, is_row, cur, 15, 0, 0);
+        put<EMIT>(k, md.write, is_row, cur, 15, 0, 0);
         break;
     case 16:
     case 17:
-        put<EMIT>(k, is_row, cur, 16, 0, 0);
+        put<EMIT>(k, md.write, is_row, cur, 16, 0, 0);
         break;
     case 20:
         if (lim - p < 16) {
             e = E_SHORT;
             break;
         }
-        put<EMIT>(k, is_row, cur, 20, p, 16);
+        put<EMIT>(k, md.write, is_row, cur, 20, p, 16);
         p += 16;
         break;
     case 22:  // Error(Value) whose inner value is a String: wire tag 18 in the columns
         p++;  // the inner String tag (12), checked by the caller
-        if (!(e = dstr<MODE>(s, p, lim, true, off, len, work)))
-            put<EMIT>(k, is_row, cur, 18, off, (uint32_t)len);
+        if (!(e = dstr(s, p, lim, true, off, len, work, md)))
+            put<EMIT>(k, md.write, is_row, cur, 18, off, (uint32_t)len);
         break;
     case 23:
-        if (!(e = dfix(s, p, lim, 1, v))) put<EMIT>(k, is_row, cur, 23, v, 0);
+        if (!(e = dfix(s, p, lim, 1, v))) put<EMIT>(k, md.write, is_row, cur, 23, v, 0);
         break;
     case 24:
         if (!(e = dfix(s, p, lim, 1, v)))
-            put<EMIT>(k, is_row, cur, 24, (uint64_t)(int64_t)(int8_t)(uint8_t)v, 0);
+            put<EMIT>(k, md.write, is_row, cur, 24, (uint64_t)(int64_t)(int8_t)(uint8_t)v, 0);
         break;
     case 25:
-        if (!(e = dfix(s, p, lim, 2, v))) put<EMIT>(k, is_row, cur, 25, v, 0);
+        if (!(e = dfix(s, p, lim, 2, v))) put<EMIT>(k, md.write, is_row, cur, 25, v, 0);
         break;
     case 26:
         if (!(e = dfix(s, p, lim, 2, v)))
-            put<EMIT>(k, is_row, cur, 26, (uint64_t)(int64_t)(int16_t)(uint16_t)v, 0);
+            put<EMIT>(k, md.write, is_row, cur, 26, (uint64_t)(int64_t)(int16_t)(uint16_t)v, 0);
         break;
     case 27: {
         if ((e = dvar(s, p, lim, v))) break;
@@ -288,7 +347,7 @@ NXG_DEV uint32_t dleaf(const Src& s, uint32_t t, uint64_t& p, uint64_t lim, cons
             e = E_SHORT;
             break;
         }
-        put<EMIT>(k, is_row, cur, 27, p, (uint32_t)(l2 - p));
+        put<EMIT>(k, md.write, is_row, cur, 27, p, (uint32_t)(l2 - p));
         p = l2;
         break;
     }
@@ -299,17 +358,19 @@ NXG_DEV uint32_t dleaf(const Src& s, uint32_t t, uint64_t& p, uint64_t lim, cons
 }
 
 // Does the value whose tag t was just consumed (next byte at p) contain other values?
-NXG_DEV bool is_container(const Src& s, uint32_t t, uint64_t p, uint64_t lim) {
+template <class S>
+NXG_DEV bool is_container(const S& s, uint32_t t, uint64_t p, uint64_t lim) {
     return t == 19 || t == 21 || (t == 22 && !(p < lim && s.byte(p) == 12u));
 }
 
 // Container header at p (tag t consumed): element count -> kids, and the container's own row.
-template <bool EMIT>
-NXG_DEV uint32_t dcontainer(const Src& s, uint32_t t, uint64_t& p, uint64_t lim, const Sink* k,
-                            bool is_row, uint64_t cur, uint64_t child_next, uint64_t& kids) {
+template <bool EMIT, class S>
+NXG_DEV uint32_t dcontainer(const S& s, uint32_t t, uint64_t& p, uint64_t lim, const Sink* k,
+                            const DMode& md, bool is_row, uint64_t cur, uint64_t child_next,
+                            uint64_t& kids) {
     if (t == 22) {
         kids = 1;
-        put<EMIT>(k, is_row, cur, 22, child_next, 1);
+        put<EMIT>(k, md.write, is_row, cur, 22, child_next, 1);
         return E_OK;
     }
     uint64_t v;
@@ -320,93 +381,71 @@ NXG_DEV uint32_t dcontainer(const Src& s, uint32_t t, uint64_t& p, uint64_t lim,
     const uint64_t unit = t == 19 ? 16 : 32;
     if (v > maxe || v * unit > ((lim - p) << 8)) return E_TOO_BIG;
     kids = t == 19 ? v : 2 * v;
-    put<EMIT>(k, is_row, cur, t, child_next, (uint32_t)v);
+    put<EMIT>(k, md.write, is_row, cur, t, child_next, (uint32_t)v);
     return E_OK;
 }
 
-constexpr uint32_t E_NESTED = 101;  // internal: flat decoder met a nested container
-
-// One Value at p, for values nested at most one level deep (a container of leaves): no stack,
-// so nothing spills to scratch. A deeper value returns E_NESTED (after the same checks the
-// general decoder would have made up to that point), and the caller re-decodes it with dvalue.
-template <bool EMIT, int MODE>
-NXG_DEV uint32_t dvalue_flat(const Src& s, uint64_t& p, uint64_t lim, const Sink* k, bool row,
-                             uint64_t slot, uint64_t& child_next, uint32_t& work) {
-    if (MODE == M_SPEC && ++work > kSpecBudget) return E_BUDGET;
-    if (MODE == M_BOUNDED && ++work > kWalkBudget) return E_BUDGET;
-    if (p >= lim) return E_SHORT;
-    const uint32_t t = s.byte(p++);
-    if (!is_container(s, t, p, lim)) return dleaf<EMIT, MODE>(s, t, p, lim, k, row, slot, work);
-    uint64_t kids;
-    uint32_t e = dcontainer<EMIT>(s, t, p, lim, k, row, slot, child_next, kids);
-    if (e) return e;
-    const uint64_t base = child_next;
-    child_next += kids;
-#pragma unroll 1
-    for (uint64_t i = 0; i < kids; i++) {
-        if (MODE == M_SPEC && ++work > kSpecBudget) return E_BUDGET;
-        if (MODE == M_BOUNDED && ++work > kWalkBudget) return E_BUDGET;
-        if (p >= lim) return E_SHORT;
-        const uint32_t t2 = s.byte(p++);
-        if (is_container(s, t2, p, lim)) return E_NESTED;
-        if ((e = dleaf<EMIT, MODE>(s, t2, p, lim, k, false, base + i, work))) return e;
-    }
-    return E_OK;
-}
-
-// Any Value at p: iterative depth-first walk with an explicit stack (scratch memory), used only
-// for values nested deeper than dvalue_flat handles. Children are allocated depth-first, the
-// order in which the recursive reference decoder produces them.
-template <bool EMIT, int MODE>
-__device__ __attribute__((noinline)) uint32_t dvalue_deep(const Src& s, uint64_t& p, uint64_t lim,
-                                                          const Sink* k, bool row, uint64_t slot,
-                                                          uint64_t& child_next, uint32_t& work) {
-    uint64_t frem[NXG_MAX_DEPTH + 2];
+// Decode one Value at p (limit lim) into (row?, slot); children are allocated from child_next,
+// depth-first, the order in which the recursive reference decoder produces them. One leaf
+// decoder serves every level. The top level and the first container level live in registers;
+// only values nested two or more levels deep touch the stack arrays (scratch memory).
+template <bool EMIT, class S>
+NXG_DEV uint32_t dvalue(const S& s, uint64_t& p, uint64_t lim, const Sink* k, bool row,
+                        uint64_t slot, uint64_t& child_next, uint32_t& work, const DMode& md) {
+    uint64_t frem[NXG_MAX_DEPTH + 2];  // levels >= 2: values left, next slot
     uint64_t fslot[NXG_MAX_DEPTH + 2];
     int top = -1;
+    uint64_t left = 1, cur = slot;     // current level
+    uint64_t sv_left = 0, sv_cur = 0;  // level 0 while level 1 is decoded
     int depth = 0;
     bool is_row = row;
-    uint64_t cur = slot;
 #pragma unroll 1
     for (;;) {
+        while (left == 0) {  // level finished: pop
+            if (depth == 0) return E_OK;
+            if (depth == 1) {
+                left = sv_left;
+                cur = sv_cur;
+            } else {
+                left = frem[top];
+                cur = fslot[top];
+                top--;
+            }
+            depth--;
+        }
         if (depth > NXG_MAX_DEPTH) return E_DEPTH;
-        if (MODE == M_SPEC && ++work > kSpecBudget) return E_BUDGET;
-        if (MODE == M_BOUNDED && ++work > kWalkBudget) return E_BUDGET;
+        if (++work > md.budget) return E_BUDGET;
         if (p >= lim) return E_SHORT;
         const uint32_t t = s.byte(p++);
         uint32_t e;
-        uint64_t kids = 0;
-        if (is_container(s, t, p, lim)) e = dcontainer<EMIT>(s, t, p, lim, k, is_row, cur, child_next, kids);
-        else e = dleaf<EMIT, MODE>(s, t, p, lim, k, is_row, cur, work);
-        if (e) return e;
-        if (kids) {
-            const uint64_t base = child_next;
-            child_next += kids;
-            ++top;
-            frem[top] = kids;
-            fslot[top] = base;
+        if (is_container(s, t, p, lim)) {
+            uint64_t kids;
+            e = dcontainer<EMIT>(s, t, p, lim, k, md, is_row, cur, child_next, kids);
+            if (e) return e;
+            left--;
+            cur++;
+            is_row = false;
+            if (kids) {
+                if (depth == 0) {
+                    sv_left = left;
+                    sv_cur = cur;
+                } else {
+                    ++top;
+                    frem[top] = left;
+                    fslot[top] = cur;
+                }
+                depth++;
+                left = kids;
+                cur = child_next;
+                child_next += kids;
+            }
+            continue;
         }
-        while (top >= 0 && frem[top] == 0) top--;
-        if (top < 0) return E_OK;
-        frem[top]--;
-        cur = fslot[top]++;
+        if ((e = dleaf<EMIT>(s, t, p, lim, k, is_row, cur, work, md))) return e;
+        left--;
+        cur++;
         is_row = false;
-        depth = top + 1;
     }
-}
-
-// Decode one Value at p (limit lim) into (row?, slot), children from `child_next`.
-template <bool EMIT, int MODE>
-NXG_DEV uint32_t dvalue(const Src& s, uint64_t& p, uint64_t lim, const Sink* k, bool row,
-                        uint64_t slot, uint64_t& child_next, uint32_t& work) {
-    const uint64_t p0 = p, c0 = child_next;
-    const uint32_t w0 = work;
-    const uint32_t e = dvalue_flat<EMIT, MODE>(s, p, lim, k, row, slot, child_next, work);
-    if (e != E_NESTED) return e;
-    p = p0;
-    child_next = c0;
-    work = w0;
-    return dvalue_deep<EMIT, MODE>(s, p, lim, k, row, slot, child_next, work);
 }
 
 struct MsgInfo {
@@ -415,53 +454,125 @@ struct MsgInfo {
     uint64_t id;
 };
 
+// The message body after its length prefix: variant byte and fields, from source s.
+template <bool EMIT, class S>
+NXG_DEV uint32_t decode_body(const S& s, uint64_t p, uint64_t lim, MsgInfo& info, const Sink* k,
+                             uint64_t row, uint64_t& child_next, uint32_t& work,
+                             const DMode& md) {
+    if (p >= lim) return E_SHORT;
+    const uint32_t variant = s.byte(p++);
+    info.variant = variant;
+    uint64_t v, off, len;
+    uint32_t e;
+    bool upd = false, tail = false;
+    switch (variant) {
+    case 0:  // NoSuchValue(Path)
+    case 1:  // Denied(Path)
+        return dstr(s, p, lim, true, off, len, work, md);
+    case 2:  // Unsubscribed(Id)
+        return dvar(s, p, lim, v);
+    case 3:  // Subscribed(Path, Id, Value)
+        if ((e = dstr(s, p, lim, true, off, len, work, md))) return e;
+        if ((e = dvar(s, p, lim, v))) return e;
+        break;
+    case 4:  // Update(Id, Value)
+        if ((e = dvar(s, p, lim, v))) return e;
+        info.id = v;
+        upd = true;
+        break;
+    case 5:  // Heartbeat
+        return E_OK;
+    case 6:  // WriteResult(Id, Value, #[pack(default)] WriteId)
+        if ((e = dvar(s, p, lim, v))) return e;
+        tail = true;
+        break;
+    default:
+        return E_UNKNOWN_TAG;
+    }
+    uint64_t cn = upd ? child_next : 0;
+    const DMode mv{md.budget, md.spec, md.write && upd};
+    e = dvalue<EMIT>(s, p, lim, k, upd, row, cn, work, mv);
+    if (upd) child_next = cn;
+    if (e) return e;
+    if (upd && md.spec && p != lim) return E_INVALID;  // exact fit (see decode_msg)
+    if (tail) {
+        e = dvar(s, p, lim, v);
+        return e == E_SHORT ? E_OK : e;  // #[pack(default)] WriteId (derive lib.rs:392-401)
+    }
+    return E_OK;
+}
+
 // Decode the message starting at `pos`. On success, info.next is the position after the
 // length-wrapped region (trailing bytes skipped, pack.rs:551-553). Update values are written
-// to row `row` (EMIT); children are allocated from child_next.
-template <bool EMIT, int MODE>
+// to row `row` (EMIT with md.write); their children are allocated from child_next. The values
+// inside control messages (Subscribed, WriteResult) are validated, not written.
+template <bool EMIT>
 NXG_DEV uint32_t decode_msg(const Src& s, uint64_t pos, MsgInfo& info, const Sink* k,
-                            uint64_t row, uint64_t& child_next, uint32_t& work) {
+                            uint64_t row, uint64_t& child_next, uint32_t& work, const DMode& md) {
+    const LdsSrc ls{s.lds, s.t0};
+    const GlbSrc gs{s.g};
     uint64_t p = pos, L;
-    uint32_t e = dvar(s, p, s.W, L);
+    // the length prefix (<= 10 bytes) from the image when it lies there
+    const bool img = pos >= s.t0 && pos - s.t0 + 10 <= s.nlds;
+    uint32_t e = img ? dvar(ls, p, s.W, L) : dvar(gs, p, s.W, L);
     if (e) return e;
     if (L < 1) return E_SHORT;
     // a guess must look like encoder output: minimal length varint (and, below, content that
     // fills the length-wrapped region exactly). Otherwise a payload byte >= 0x80 just before a
     // true start makes a "shadow" message with a huge length and skipped trailing bytes.
-    if (MODE == M_SPEC && p - pos != vl64(L)) return E_INVALID;
+    if (md.spec && p - pos != vl64(L)) return E_INVALID;
     const uint64_t take = L - vl64(L);
     const uint64_t lim = take < s.W - p ? p + take : s.W;
     info.next = lim;
-    if (p >= lim) return E_SHORT;
+    if (img && lim - s.t0 <= s.nlds)
+        return decode_body<EMIT>(ls, p, lim, info, k, row, child_next, work, md);
+    return decode_body<EMIT>(gs, p, lim, info, k, row, child_next, work, md);
+}
+
+// ---- structure only (the general decoder's count pass) ---------------------------------------
+// Message boundaries depend only on the length prefixes (len_wrapped_decode, pack.rs:537-555),
+// so the count pass reads just the prefix, the variant and, for an Update whose value is a
+// container, the container structure (to count the child slots the emit pass will allocate).
+// Content is not validated here: the emit pass decodes every message on the chain and reports
+// the first content error. Only errors in the length prefix, which break the chain, are
+// returned (and E_BUDGET from a bounded container walk).
+template <class S>
+NXG_DEV uint32_t skim_body(const S& s, uint64_t p, uint64_t lim, MsgInfo& info,
+                           uint64_t& children, uint32_t& work, uint32_t budget) {
     const uint32_t variant = s.byte(p++);
     info.variant = variant;
-    uint64_t v, off, len, dummy = 0;
-    switch (variant) {
-    case 0:
-    case 1:
-        return dstr<MODE>(s, p, lim, true, off, len, work);
-    case 2:
-        return dvar(s, p, lim, v);
-    case 3:
-        if ((e = dstr<MODE>(s, p, lim, true, off, len, work))) return e;
-        if ((e = dvar(s, p, lim, v))) return e;
-        return dvalue<false, MODE>(s, p, lim, k, false, 0, dummy, work);
-    case 4:
-        if ((e = dvar(s, p, lim, v))) return e;
-        info.id = v;
-        e = dvalue<EMIT, MODE>(s, p, lim, k, true, row, child_next, work);
-        if (MODE == M_SPEC && !e && p != lim) return E_INVALID;  // exact fit (see above)
-        return e;
-    case 5:
-        return E_OK;
-    case 6:
-        if ((e = dvar(s, p, lim, v))) return e;
-        if ((e = dvalue<false, MODE>(s, p, lim, k, false, 0, dummy, work))) return e;
-        e = dvar(s, p, lim, v);
-        return e == E_SHORT ? E_OK : e;  // #[pack(default)] WriteId
-    default:
-        return E_UNKNOWN_TAG;
-    }
+    if (variant != 4) return E_OK;
+    uint64_t v;
+    if (dvar(s, p, lim, v) || p >= lim) return E_OK;  // content error: reported by emit
+    const uint32_t t = s.byte(p);
+    if (!is_container(s, t, p + 1, lim)) return E_OK;
+    uint64_t cn = 0;
+    const DMode md{budget, 1, 0};  // structure: no UTF-8 scan, no writes
+    const uint32_t e = dvalue<false>(s, p, lim, nullptr, true, 0, cn, work, md);
+    children = cn;
+    return e == E_BUDGET ? E_BUDGET : E_OK;
 }
+
+NXG_DEV uint32_t skim_msg(const Src& s, uint64_t pos, MsgInfo& info, uint64_t& children,
+                          uint32_t& work, uint32_t budget) {
+    const LdsSrc ls{s.lds, s.t0};
+    const GlbSrc gs{s.g};
+    uint64_t p = pos, L;
+    const bool img = pos >= s.t0 && pos - s.t0 + 10 <= s.nlds;
+    const uint32_t e = img ? dvar(ls, p, s.W, L) : dvar(gs, p, s.W, L);
+    if (e) return e;
+    if (L < 1) return E_SHORT;
+    const uint64_t take = L - vl64(L);
+    const uint64_t lim = take < s.W - p ? p + take : s.W;
+    info.next = lim;
+    info.variant = 0xff;  // no variant byte: a content error (BufferShort), reported by emit
+    children = 0;
+    if (p >= lim) return E_OK;
+    if (img && lim - s.t0 <= s.nlds) return skim_body(ls, p, lim, info, children, work, budget);
+    return skim_body(gs, p, lim, info, children, work, budget);
+}
+
+// the first-error key: the larger key is the earlier (offset, kind); 0 = no error
+NXG_DEV uint64_t err_key(uint64_t off, uint32_t kind) { return ~((off << 8) | (kind & 0xffu)); }
 
 }  // namespace nxgmsg
