@@ -66,6 +66,8 @@ struct NxgCtx {
     size_t glws_cap = 0;
     uint64_t* gruns = nullptr;     // general decode: run summaries + bases
     int wgs_dec_gen = 0;
+    int wgs_dec_f64_1p = 0;
+    bool f64_2pass = false;  // NXG_F64_2PASS=1: the two-pass count/emit f64 decoder
     uint8_t* dframe = nullptr;
     size_t dframe_cap = 0;
     uint64_t* escratch = nullptr;
@@ -265,6 +267,12 @@ NxgColumns staged_view(NxgCtx* c, const NxgColumns* like) {
 
 bool enqueue_dec_fast(NxgCtx* c, const uint8_t* f, uint64_t len, NxgColumns* out, DevStatus* st,
                       NetidxError* err) {
+    if (!c->f64_2pass && c->wgs_dec_f64_1p >= 2) {
+        if (!ensure_tstat(c, 2 * nxg_dec_f64_1p_tiles(len), err)) return false;
+        HIPCHK(nxg_launch_dec_f64_1p(f, len, out->id, out->fixed, out->cap_rows, c->tstat,
+                                     c->epoch, c->wgs_dec_f64_1p, st, c->stream));
+        return true;
+    }
     if (!ensure_fmoff(c, 64 * nxg_dec_f64_tiles(len), err)) return false;
     HIPCHK(nxg_launch_dec_f64(f, len, out->id, out->fixed, out->cap_rows, c->fscratch, c->fmoff,
                               c->wgs_dec_f64, st, c->stream));
@@ -514,6 +522,9 @@ NxgCtx* nxg_ctx_new(int device, NetidxError* err) {
     const size_t gw = (size_t)gdec2::MAX_RUNS * (gdec2::RUN_WORDS + 4);
     if ((e = hipMalloc(&c->gruns, gw * 8)) != hipSuccess) return fail("hipMalloc(gruns)", e);
     c->wgs_dec_gen = nxg_dec_gen_wgs(c->ncu);
+    c->wgs_dec_f64_1p = nxg_dec_f64_1p_wgs(c->ncu);
+    const char* f2 = getenv("NXG_F64_2PASS");
+    c->f64_2pass = f2 && f2[0] == '1';
     return c;
 }
 

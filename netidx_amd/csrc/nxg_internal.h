@@ -96,6 +96,13 @@ hipError_t nxg_launch_dec_f64(const uint8_t* wire, uint64_t W, uint64_t* oid, ui
                               uint64_t cap, uint64_t* scratch, uint8_t* moff, int wgs,
                               DevStatus* st, hipStream_t s);
 int nxg_dec_f64_wgs(int ncu);
+// f64 decode, single pass (nxg_decode_f64_1p.hip): `tstat` holds 2 epoch-tagged words per tile
+// (nxg_dec_f64_1p_tiles(W) tiles); `wgs` from nxg_dec_f64_1p_wgs (all co-resident).
+uint64_t nxg_dec_f64_1p_tiles(uint64_t W);
+hipError_t nxg_launch_dec_f64_1p(const uint8_t* wire, uint64_t W, uint64_t* oid, uint64_t* oval,
+                                 uint64_t cap, uint64_t* tstat, uint32_t epoch, int wgs,
+                                 DevStatus* st, hipStream_t s);
+int nxg_dec_f64_1p_wgs(int ncu);
 hipError_t nxg_launch_enc_f64(const uint64_t* id, const uint64_t* val, uint64_t n, uint8_t* out,
                               uint64_t cap, uint64_t* tstat, uint32_t epoch, DevStatus* st,
                               int grid, hipStream_t s);

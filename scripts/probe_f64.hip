@@ -1,7 +1,8 @@
 // probe_f64.hip -- standalone timing probe for the f64 decode (diagnostics, not product).
 // Builds an all-f64 frame on the host, then times with HIP events:
-//   dec       the product decode (count + emit per segment); outputs are checked on the host
-//   dec_sc    the experimental single-pass scanner variant (nxg_decode_f64_sc.hip)
+//   dec2p     the two-pass decode (count + emit); outputs are checked on the host
+//   dec1p*    the single-pass decode (nxg_decode_f64_1p.hip) and its ablations (no wait for the
+//             scanner's prefixes, no column stores), with per-phase cycle counters
 //   stream    a plain kernel reading W bytes and writing 16N bytes (practical HBM ceiling)
 //   d2d       hipMemcpyDeviceToDevice of the frame
 // Usage: probe_f64 [records] [reps]
@@ -14,14 +15,15 @@
 namespace prod {
 #include "../netidx_amd/csrc/nxg_decode_f64.hip"
 }
-namespace sc {
-#include "../netidx_amd/csrc/nxg_decode_f64_sc.hip"
+namespace p1 {
+#define NXG_1P_PROBE
+#include "../netidx_amd/csrc/nxg_decode_f64_1p.hip"
+#undef NXG_1P_PROBE
 }
-#undef PROBE_MARK
-namespace sct {
-#define NXG_PROBE_TRACE
-#include "../netidx_amd/csrc/nxg_decode_f64_sc.hip"
-#undef NXG_PROBE_TRACE
+#undef P1_FLAGS
+#undef P1_STAMP
+namespace p1n {  // the product build (no stamps)
+#include "../netidx_amd/csrc/nxg_decode_f64_1p.hip"
 }
 thread_local DevStatus* nxg_zero_slot = nullptr;
 
@@ -116,7 +118,7 @@ int main(int argc, char** argv) {
     CK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0));
     CK(hipMalloc(&st, sizeof(DevStatus)));
     CK(hipMemcpy(dw, w.data(), W, hipMemcpyHostToDevice));
-    const uint64_t ntiles = (W + 4095) / 4096;
+    const uint64_t ntiles = (W + 3967) / 3968 + 1;  // >= the 1p kernel's tiles
     uint64_t* tstat;
     CK(hipMalloc(&tstat, 2 * ntiles * 8 + 64));
     CK(hipMemset(tstat, 0, 2 * ntiles * 8 + 64));
@@ -159,37 +161,35 @@ int main(int argc, char** argv) {
             CK(hipMemsetAsync(st, 0, sizeof(DevStatus), 0));
             CK(hipMemsetAsync(oid, 0, 8, 0));
             if (v == 0) LAUNCH(prod);
-            if (v == 5) {
+            if (v == 2) {
                 epoch++;
-                CK(sc::nxg_launch_dec_f64_sc(dw, W, oid, oval, N, tstat, epoch,
-                                             sc::nxg_dec_f64_sc_wgs(ncu), st, 0));
+                CK(p1n::nxg_launch_dec_f64_1p(dw, W, oid, oval, N, tstat, epoch,
+                                              p1n::nxg_dec_f64_1p_wgs(ncu), st, 0));
+            }
+            if (v == 1) {
+                epoch++;
+                CK(p1::nxg_launch_dec_f64_1p(dw, W, oid, oval, N, tstat, epoch,
+                                             p1::nxg_dec_f64_1p_wgs(ncu), st, 0));
             }
         };
     };
-    printf("wgs=%d\n", prod::nxg_dec_f64_wgs(ncu));
-    printf("records=%llu wire=%llu bytes tiles=%llu\n", (unsigned long long)N,
-           (unsigned long long)W, (unsigned long long)((W + 4095) / 4096));
-    timeit("dec", dec(0), true);
-    printf("sc wgs=%d\n", sc::nxg_dec_f64_sc_wgs(ncu));
-    timeit("dec_sc", dec(5), true);
-    {
-        uint64_t* dtr;
-        CK(hipMalloc(&dtr, ntiles * 4 * 8));
-        CK(hipMemset(dtr, 0, ntiles * 4 * 8));
-        CK(hipMemcpyToSymbol(HIP_SYMBOL(sct::g_probe_trace), &dtr, sizeof dtr));
-        timeit("dec_sct", [&]() {
-            CK(hipMemsetAsync(st, 0, sizeof(DevStatus), 0));
-            epoch++;
-            CK(sct::nxg_launch_dec_f64_sc(dw, W, oid, oval, N, tstat, epoch,
-                                          sct::nxg_dec_f64_sc_wgs(ncu), st, 0));
-        }, true);
-        std::vector<uint64_t> h(ntiles * 4);
-        CK(hipMemcpy(h.data(), dtr, ntiles * 4 * 8, hipMemcpyDeviceToHost));
-        FILE* f = fopen("gpurun_out/probe_trace.bin", "wb");
-        if (f) {
-            fwrite(h.data(), 8, h.size(), f);
-            fclose(f);
-        }
+    printf("wgs=%d 1p_wgs=%d\n", prod::nxg_dec_f64_wgs(ncu), p1::nxg_dec_f64_1p_wgs(ncu));
+    printf("records=%llu wire=%llu bytes\n", (unsigned long long)N, (unsigned long long)W);
+    timeit("dec2p", dec(0), true);
+    timeit("dec1p_prod", dec(2), true);
+    const char* names[4] = {"dec1p", "1p_nowait", "1p_nostore", "1p_nowait_nostore"};
+    for (uint32_t f = 0; f < 4; f++) {
+        CK(hipMemcpyToSymbol(HIP_SYMBOL(p1::g_1p_dbg), &f, sizeof f));
+        unsigned long long z[8] = {0};
+        CK(hipMemcpyToSymbol(HIP_SYMBOL(p1::g_1p_cyc), z, sizeof z));
+        timeit(names[f], dec(1), f == 0);
+        unsigned long long c[8];
+        CK(hipMemcpyFromSymbol(c, HIP_SYMBOL(p1::g_1p_cyc), sizeof c));
+        double tot = 0;
+        for (int i = 0; i < 5; i++) tot += (double)c[i];
+        printf("   cycles/wave-step share: stage %.1f%% starts %.1f%% decode %.1f%% wait %.1f%% "
+               "store %.1f%% (total %.3g)\n", 100 * c[0] / tot, 100 * c[1] / tot,
+               100 * c[2] / tot, 100 * c[3] / tot, 100 * c[4] / tot, tot);
     }
     uint32_t* sink;
     CK(hipMalloc(&sink, 64));
