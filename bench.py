@@ -27,7 +27,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-KERNEL_DEC_F64 = "nxg_f64_count_kernel+nxg_f64_emit_kernel"
+KERNEL_DEC_F64 = "nxg_f64_1p_kernel"  # single launch (nxg_decode_f64_1p.hip)
 
 
 def log(*a):

@@ -46,19 +46,23 @@ namespace {
 
 constexpr int TPB1 = 256;
 constexpr int WAVES1 = TPB1 / 64;
-constexpr int LAG = 2;
+#ifndef NXG_1P_LAG
+#define NXG_1P_LAG 2
+#endif
+constexpr int LAG = NXG_1P_LAG;
 constexpr int NSLOT = LAG + 1;
 constexpr int MAXR = f64dec::STRIDE / 12 + 1;  // records per tile (>= 12 bytes each): 337
 constexpr int SCAN_K = 8;                      // scanner: tiles per thread per step
 constexpr int MAXL = 6;  // records a lane owns: its span is < 64 + 15 bytes, >= 12 B each
 constexpr uint32_t SLOTB = f64dec::IMG + f64dec::HALO;  // image, then its decoded records
 constexpr uint32_t VALOFF = (MAXR * 4 + 7) & ~7u;       // decoded: u32 ids, then u64 values
-static_assert(VALOFF + MAXR * 8 <= SLOTB, "decoded records fit the image they replace");
+constexpr uint32_t CNTOFF = SLOTB - 4;                  // decoded: the tile's record count
+static_assert(VALOFF + MAXR * 8 <= CNTOFF, "decoded records fit the image they replace");
 
 struct WaveLds {
     uint8_t slot[NSLOT][SLOTB] __attribute__((aligned(16)));
 };
-static_assert(sizeof(WaveLds) * WAVES1 * 3 <= 160 * 1024, "three workgroups per CU");
+static_assert(sizeof(WaveLds) * WAVES1 <= 80 * 1024, "two workgroups per CU at least");
 
 }  // namespace
 
@@ -156,7 +160,6 @@ NXG_DEV void f64_work(const uint8_t* __restrict__ wire, uint64_t W, uint64_t nt,
     const uint64_t nfull = W >= f64dec::IMG + f64dec::HALO
                                ? (W - f64dec::IMG - f64dec::HALO) / f64dec::STRIDE + 1
                                : 0;
-    uint32_t nslot0 = 0, nslot1 = 0, nslot2 = 0;
 #ifdef NXG_1P_PROBE
     uint64_t tprev = __builtin_amdgcn_s_memtime(), cyc0 = 0, cyc1 = 0, cyc2 = 0, cyc3 = 0,
              cyc4 = 0;
@@ -231,9 +234,7 @@ NXG_DEV void f64_work(const uint8_t* __restrict__ wire, uint64_t W, uint64_t nt,
             }
             if (lane == 0) st_agent(&agg[t], lb_word(kFlagAgg, epoch, ntile));
             const int sl = (int)(k % NSLOT);
-            if (sl == 0) nslot0 = ntile;
-            else if (sl == 1) nslot1 = ntile;
-            else nslot2 = ntile;
+            if (lane == 0) *reinterpret_cast<uint32_t*>(img + CNTOFF) = ntile;
             P1_STAMP(2);
         }
         if (k >= LAG) {
@@ -241,7 +242,7 @@ NXG_DEV void f64_work(const uint8_t* __restrict__ wire, uint64_t W, uint64_t nt,
             const uint64_t ke = k - LAG;
             const uint64_t te = ke * V + v;
             const int se = (int)(ke % NSLOT);
-            const uint32_t ne = se == 0 ? nslot0 : se == 1 ? nslot1 : nslot2;
+            const uint32_t ne = *reinterpret_cast<const uint32_t*>(L.slot[se] + CNTOFF);
             const uint32_t* sid = reinterpret_cast<const uint32_t*>(L.slot[se]);
             const uint64_t* sval = reinterpret_cast<const uint64_t*>(L.slot[se] + VALOFF);
             P1_STAMP(4);

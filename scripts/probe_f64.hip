@@ -25,6 +25,11 @@ namespace p1 {
 namespace p1n {  // the product build (no stamps)
 #include "../netidx_amd/csrc/nxg_decode_f64_1p.hip"
 }
+#undef NXG_1P_LAG
+#define NXG_1P_LAG 1
+namespace p1l3 {  // lag 1 (two slots per wave, four workgroups per CU)
+#include "../netidx_amd/csrc/nxg_decode_f64_1p.hip"
+}
 thread_local DevStatus* nxg_zero_slot = nullptr;
 
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
@@ -166,6 +171,11 @@ int main(int argc, char** argv) {
                 CK(p1n::nxg_launch_dec_f64_1p(dw, W, oid, oval, N, tstat, epoch,
                                               p1n::nxg_dec_f64_1p_wgs(ncu), st, 0));
             }
+            if (v == 3) {
+                epoch++;
+                CK(p1l3::nxg_launch_dec_f64_1p(dw, W, oid, oval, N, tstat, epoch,
+                                               p1l3::nxg_dec_f64_1p_wgs(ncu), st, 0));
+            }
             if (v == 1) {
                 epoch++;
                 CK(p1::nxg_launch_dec_f64_1p(dw, W, oid, oval, N, tstat, epoch,
@@ -177,6 +187,7 @@ int main(int argc, char** argv) {
     printf("records=%llu wire=%llu bytes\n", (unsigned long long)N, (unsigned long long)W);
     timeit("dec2p", dec(0), true);
     timeit("dec1p_prod", dec(2), true);
+    timeit("dec1p_lag1", dec(3), true);
     const char* names[4] = {"dec1p", "1p_nowait", "1p_nostore", "1p_nowait_nostore"};
     for (uint32_t f = 0; f < 4; f++) {
         CK(hipMemcpyToSymbol(HIP_SYMBOL(p1::g_1p_dbg), &f, sizeof f));

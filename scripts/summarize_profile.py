@@ -21,7 +21,7 @@ import sys
 from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-DEC = ("nxg_f64_count_kernel", "nxg_f64_emit_kernel")
+DEC = ("nxg_f64_1p_kernel",)
 
 
 def rows(pattern):
