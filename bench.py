@@ -14,8 +14,9 @@ Also reported on the same JSON line:
   roofline       the decode's algorithmic bytes (W + 16 N) / mean time of one decode (HIP
                  events on the codec stream) vs the 8 TB/s HBM3E peak;
   cpu_baseline   the C restatement of the reference decoder (oracle/, 1 core) on this host;
-  extras         10^8-record decode (north-star size), mixed-tag decode (config 3), f64 encode
-                 (config 4); with N>1, the config-5 sharded encode + RCCL all-gather.
+  extras         10^8-record decode (north-star size), mixed-tag decode (config 3), the
+                 host-memory (PCIe-inclusive) decode path, f64 encode (config 4), the oracle on
+                 16 host threads; with N>1, the config-5 sharded encode + RCCL all-gather.
 """
 import argparse
 import json
@@ -106,6 +107,36 @@ def cpu_baseline(wire_host, n, seconds):
     return n * reps / t_total, reps, t_total
 
 
+def cpu_baseline_threads(wire_host, ids, seconds, threads=16):
+    """Upper bound the reference does not reach: the oracle on `threads` host
+    threads, the frame pre-cut at record boundaries (known from the ids: an f64 record is
+    11 + varint_len(id) bytes). ctypes releases the GIL around each oracle call."""
+    import numpy as np
+    from concurrent.futures import ThreadPoolExecutor
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import nxo
+    vl = 1 + (ids >= 2**7) + (ids >= 2**14) + (ids >= 2**21) + (ids >= 2**28)
+    ends = np.cumsum(11 + vl.astype(np.int64))
+    n = len(ids)
+    cuts = [0] + [int(ends[n * k // threads - 1]) for k in range(1, threads)] + [len(wire_host)]
+    parts = [wire_host[cuts[k]:cuts[k + 1]] for k in range(threads)]
+    counts = [int(np.searchsorted(ends, cuts[k + 1], "right") - np.searchsorted(ends, cuts[k], "right"))
+              for k in range(threads)]
+
+    def one(k):
+        d = nxo.decode(parts[k], cap_rows=counts[k] + 1, cap_children=1, cap_ctl=1)
+        assert d.s.err_kind == 0 and d.s.n_rows == counts[k]
+
+    reps, t_total = 0, 0.0
+    with ThreadPoolExecutor(threads) as ex:
+        while t_total < seconds or reps == 0:
+            t0 = time.perf_counter()
+            list(ex.map(one, range(threads)))
+            t_total += time.perf_counter() - t0
+            reps += 1
+    return n * reps / t_total, reps, t_total
+
+
 def read_traffic(records):
     """HBM bytes per launch from the committed rocprofv3 PMC summary, if it matches."""
     p = os.path.join(ROOT, "profiles", "pmc_dec_f64.json")
@@ -168,6 +199,30 @@ def extras_single_gpu(codec, stream, steps, warmup):
         torch.cuda.empty_cache()
     except Exception as e:
         ex["decode_mixed_1e7"] = {"error": repr(e)}
+    # (b2) the socket-buffer path: host (pinned) frame -> device decode -> host (pinned) columns,
+    # through the same synchronous call (nxg_decode_updates stages H2D and D2H itself); wall
+    # clock, so PCIe Gen5 transfers are included. Never the bench `value`.
+    try:
+        n = 10_000_000
+        cols, wire = make_f64_wire(codec, n, 0)
+        hframe = wire.cpu().pin_memory()
+        hout = Columns(n, 0, 0, netidx_amd.LAYOUT_F64, "cpu")
+        for _ in range(2):
+            codec.decode_into(hframe, hframe.numel(), hout)
+        k = max(3, steps // 4)
+        t0 = time.perf_counter()
+        for _ in range(k):
+            st = codec.decode_into(hframe, hframe.numel(), hout)
+        dt = (time.perf_counter() - t0) / k
+        assert st.path == 1 and st.n_rows == n
+        assert torch.equal(hout.fixed[:n], cols.fixed[:n].cpu())
+        ex["decode_f64_1e7_host_pcie"] = {
+            "records": n, "M_updates_s": round(n / dt / 1e6, 1), "ms": round(dt * 1e3, 3),
+            "host_bytes_moved": wire.numel() + 16 * n,
+            "GB_s_host_to_host": round((wire.numel() + 16 * n) / dt / 1e9, 2)}
+        del cols, wire, hframe, hout
+    except Exception as e:
+        ex["decode_f64_1e7_host_pcie"] = {"error": repr(e)}
     # (c) config 4: f64 encode from device columns, byte-identical round trip
     try:
         n = 10_000_000
@@ -292,6 +347,13 @@ def main():
                                           f"({secs:.1f} s) by oracle/nx_oracle.c"}
         if not args.no_extras:
             line["extras"] = extras_single_gpu(codec, stream, args.steps, args.warmup)
+            ups, reps, secs = cpu_baseline_threads(host, cols.id.cpu().numpy().view("uint64"),
+                                                   min(args.cpu_seconds, 5.0))
+            line["extras"]["cpu_baseline_16_threads"] = {
+                "value": round(ups / 1e6, 3), "unit": "M updates/s", "cores": 16,
+                "kind": "port",
+                "sample": f"full {n}-record frame cut at record boundaries into 16 sub-frames, "
+                          f"decoded {reps}x ({secs:.1f} s) by oracle/nx_oracle.c on 16 threads"}
     elif world > 1 and not args.no_extras:
         ex = extras_multi_gpu(codec, world, rank, stream)
         if rank == 0:
