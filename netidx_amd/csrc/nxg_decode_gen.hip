@@ -677,10 +677,279 @@ __global__ __launch_bounds__(RES_TPB) void nxg_gen_resolve_kernel(
 }
 
 // ---- pass 3: emit ----------------------------------------------------------------------------
+// Type-bucketed, message-parallel. Per tile:
+//   1. each lane walks only the length chain of the messages that start in its chunk (from the
+//      start its lane word records) and lists their positions in LDS, in wire order;
+//   2. message-parallel: every message's header is parsed and the message classified (fixed-size
+//      scalar, text, DateTime/Duration, varint scalar, flat array of fixed-size scalars, or
+//      other); row / control / child indices are scanned in wire order;
+//   3. a counting sort buckets the messages by class, and each bucket is decoded by all lanes
+//      running the same code, 64 messages at a time.
+// "Other" (control messages, nested or unusual values, messages that leave the LDS image) and any
+// message a fast path does not accept go through decode_msg, which also reports the exact error.
+// Tiles with more than MAXM messages (tiny messages) or a children count that overflowed a lane
+// word use the per-lane path (emit_tile_lanes).
+namespace {
+
+constexpr int MAXM = 512;  // messages per tile on the bucketed path
+enum { K_FIX = 0, K_TEXT, K_TIME, K_VAR, K_ARR, K_OTHER, K_N };
+
+struct EmitLds {
+    uint16_t mpos[MAXM];  // message start, tile-relative
+    uint8_t cls[MAXM];    // class | 0x80 for an Update
+    uint32_t ridx[MAXM];  // row (Update) or control-message index within the tile
+    uint32_t cb[MAXM];    // first child slot (Update) or the row it precedes (control)
+    uint16_t bucket[MAXM];
+};
+
+// the fixed-size scalar tags: payload bytes, or -1
+NXG_DEV int fix_bytes(uint32_t t) {
+    switch (t) {
+    case 0: case 2: case 8: return 4;
+    case 4: case 6: case 9: return 8;
+    case 14: case 15: case 16: case 17: return 0;
+    case 23: case 24: return 1;
+    case 25: case 26: return 2;
+    default: return -1;
+    }
+}
+// column value of a fixed-size scalar whose n payload bytes start at p (Value::decode,
+// lib.rs:470-506: signed types sign-extended, bool as 1/0, Null for 16/17)
+NXG_DEV uint64_t fix_value(const LdsSrc& s, uint32_t t, uint64_t p, int n) {
+    const uint64_t raw = ((uint64_t)bswap32(s.word(p)) << 32) | bswap32(s.word(p + 4));
+    uint64_t v = n ? raw >> (64 - 8 * n) : 0ull;
+    if (t == 2 || t == 24 || t == 26) {  // i32 / i8 / i16
+        const int sh = 64 - 8 * n;
+        v = (uint64_t)((int64_t)(v << sh) >> sh);
+    }
+    if (t == 14) v = 1;
+    return v;
+}
+
+// Header of the message at p: returns the class in bits 0..3, bit 4 for an Update, and the
+// number of child slots (K_ARR) from bit 8. The Update bit is exact for every well-formed
+// message (it sets the row / control numbering); anything unusual, or a message not wholly in
+// the image, is K_OTHER (decoded by decode_msg, which also reports errors).
+constexpr uint32_t C_UPD = 16;
+NXG_DEV uint32_t classify(const Src& s, uint64_t p) {
+    const LdsSrc ls{s.lds, s.t0};
+    uint64_t q = p, L;
+    const uint32_t e = p - s.t0 + 10 <= s.nlds ? dvar(ls, q, s.W, L) : dvar(GlbSrc{s.g}, q, s.W, L);
+    if (e || L < 1 || q >= s.W) return K_OTHER;  // an error: decode_msg reports it
+    const uint64_t take = L - vl64(L);
+    const uint64_t lim = take < s.W - q ? q + take : s.W;
+    const uint32_t variant = s.any_byte(q++);
+    if (variant != 4) return K_OTHER;  // control messages: validated and written by decode_msg
+    if (lim - s.t0 + 8 > s.nlds || q >= lim) return K_OTHER | C_UPD;  // not wholly in the image
+    uint64_t id;
+    if (dvar(ls, q, lim, id) || q >= lim) return K_OTHER | C_UPD;
+    const uint32_t t = ls.byte(q++);
+    const int n = fix_bytes(t);
+    uint32_t k = K_OTHER;
+    if (n >= 0) k = q + n <= lim ? K_FIX : K_OTHER;
+    else if (t == 12 || t == 13 || t == 18) k = K_TEXT;
+    else if (t == 10 || t == 11) k = q + 12 <= lim ? K_TIME : K_OTHER;
+    else if (t == 1 || t == 3 || t == 5 || t == 7) k = K_VAR;
+    else if (t == 19) {  // an array of fixed-size scalars that fits: its children are its elements
+        uint64_t cnt;
+        bool ok = !dvar(ls, q, lim, cnt) && cnt <= (kMaxVec / 16) && cnt * 16 <= ((lim - q) << 8);
+#pragma unroll 1
+        for (uint64_t i = 0; ok && i < cnt; i++) {
+            const int m = q < lim ? fix_bytes(ls.byte(q)) : -1;
+            ok = m >= 0 && q + 1 + m <= lim;
+            q += 1 + m;
+        }
+        if (ok) return K_ARR | C_UPD | ((uint32_t)cnt << 8);
+    }
+    return k | C_UPD;
+}
+
+// the general path for one message: decode_msg writes the row / children; the control columns
+// and the id are written here (as the per-lane path does)
+NXG_DEV uint32_t emit_other(const Src& s, const Sink& sink, const ColsDesc& cols, DevStatus* st,
+                            uint64_t pos, uint64_t row, uint64_t ctl, uint64_t child) {
+    MsgInfo mi;
+    uint32_t work = 0;
+    uint64_t cn = child;
+    const DMode md{0xffffffffu, 0, 1};
+    const uint32_t err = decode_msg<true>(s, pos, mi, &sink, row, cn, work, md);
+    if (err) {
+        atomicMax((unsigned long long*)&st->err_key, (unsigned long long)err_key(pos, err));
+        return 0;
+    }
+    if (mi.variant == 4) {
+        if (row < cols.cap_rows) cols.id[row] = mi.id;
+        else atomicOr(&st->capacity, 1u);
+    } else if (!cols.ctl_row) {
+        atomicOr(&st->nonf64, 1u);
+    } else if (ctl < cols.cap_ctl) {
+        cols.ctl_row[ctl] = row;
+        cols.ctl_off[ctl] = pos;
+        cols.ctl_len[ctl] = (uint32_t)(mi.next - pos);
+        cols.ctl_variant[ctl] = (uint8_t)mi.variant;
+    } else {
+        atomicOr(&st->capacity, 1u);
+    }
+    return mi.variant;
+}
+
+NXG_DEV void put_row(const ColsDesc& cols, DevStatus* st, uint64_t row, uint64_t id, uint32_t tag,
+                     uint64_t fixed, uint32_t aux) {
+    if (row < cols.cap_rows) {
+        cols.id[row] = id;
+        cols.tag[row] = (uint8_t)tag;
+        cols.fixed[row] = fixed;
+        cols.aux[row] = aux;
+    } else {
+        atomicOr(&st->capacity, 1u);
+    }
+}
+
+// Fast decode of one Update of class k at pos; false = not accepted (the caller falls back to
+// emit_other, which reports any error exactly).
+NXG_DEV bool emit_fast(uint32_t k, const Src& s, const ColsDesc& cols, DevStatus* st,
+                       uint64_t pos, uint64_t row, uint64_t child) {
+    const LdsSrc ls{s.lds, s.t0};
+    uint64_t q = pos, L, id;
+    dvar(ls, q, s.W, L);
+    const uint64_t take = L - vl64(L);
+    const uint64_t lim = take < s.W - q ? q + take : s.W;
+    q++;  // variant 4
+    dvar(ls, q, lim, id);
+    const uint32_t t = ls.byte(q++);
+    if (k == K_FIX) {
+        const int n = fix_bytes(t);
+        put_row(cols, st, row, id, t == 17 ? 16u : t, fix_value(ls, t, q, n), 0);
+        return true;
+    }
+    if (k == K_TEXT) {
+        uint64_t n;
+        if (dvar(ls, q, lim, n) || n > lim - q) return false;
+        if (t != 13 && !utf8_ok(ls, q, n)) return false;
+        put_row(cols, st, row, id, t, q, (uint32_t)n);
+        return true;
+    }
+    if (k == K_TIME) {
+        uint64_t secs, v2;
+        dfix(ls, q, lim, 8, secs);
+        dfix(ls, q, lim, 4, v2);
+        uint32_t ns = (uint32_t)v2;
+        if (t == 10) {
+            if (!datetime_valid((int64_t)secs, ns)) return false;
+        } else if (ns >= 1000000000u) {  // Duration::new normalisation (overflow: error path)
+            const uint64_t add = ns / 1000000000u;
+            if (secs + add < secs) return false;
+            secs += add;
+            ns %= 1000000000u;
+        }
+        put_row(cols, st, row, id, t, secs, ns);
+        return true;
+    }
+    if (k == K_VAR) {
+        uint64_t v;
+        if (dvar(ls, q, lim, v)) return false;
+        uint64_t x = v;
+        if (t == 1) x = (uint32_t)v;
+        else if (t == 3) {
+            const uint32_t u = (uint32_t)v;
+            x = (uint64_t)(int64_t)((int32_t)(u >> 1) ^ (int32_t)(0u - (u & 1u)));
+        } else if (t == 7) x = (v >> 1) ^ (0ull - (v & 1ull));
+        put_row(cols, st, row, id, t, x, 0);
+        return true;
+    }
+    // K_ARR: the elements were checked by classify
+    uint64_t cnt;
+    dvar(ls, q, lim, cnt);
+    put_row(cols, st, row, id, 19, child, (uint32_t)cnt);
+    for (uint64_t i = 0; i < cnt; i++) {
+        const uint32_t et = ls.byte(q++);
+        const int n = fix_bytes(et);
+        const uint64_t slot = child + i;
+        if (slot < cols.cap_children) {
+            cols.ctag[slot] = (uint8_t)(et == 17 ? 16u : et);
+            cols.cfixed[slot] = fix_value(ls, et, q, n);
+            cols.caux[slot] = 0;
+        } else {
+            atomicOr(&st->capacity, 1u);
+        }
+        q += n;
+    }
+    return true;
+}
+
+// The per-lane path (tiles the bucketed path does not take): each lane decodes its messages in
+// order with decode_msg.
+NXG_DEV void emit_tile_lanes(const Src& s, const Sink& sink, const ColsDesc& cols, DevStatus* st,
+                             uint32_t lw, uint64_t c, uint64_t& row, uint64_t& ctl,
+                             uint64_t& child, uint32_t& hb) {
+    const uint64_t stop = c + CH < s.W ? c + CH : s.W;
+    const bool has = lw_off(lw) != NOSTART;
+    uint32_t nr = has ? lw_rows(lw) : 0u, nk = has ? lw_ctl(lw) : 0u;
+    uint64_t nch = has ? lw_ch(lw) : 0u;
+    // A lane whose children count did not fit its word counts them first (phase 0, no
+    // writes); then the wave scans the counts and every lane decodes + writes (phase 1).
+    const bool recount = has && nch == CH_ESC;
+    uint64_t myrow = 0, myctl = 0, mych = 0;
+#pragma unroll 1
+    for (int ph = __any(recount) ? 0 : 1; ph < 2; ph++) {
+        if (ph == 1) {
+            const uint32_t rin = wave_incl_scan(nr);
+            const uint32_t kin = wave_incl_scan(nk);
+            const uint64_t cin = wave_incl_scan<uint64_t>(nch);
+            myrow = row + rin - nr;
+            myctl = ctl + kin - nk;
+            mych = child + cin - nch;
+            row += __shfl(rin, 63, 64);
+            ctl += __shfl(kin, 63, 64);
+            child += __shfl(cin, 63, 64);
+        }
+        const bool act = ph == 1 ? has : recount;
+        uint64_t pos = act ? c + lw_off(lw) : stop;
+        uint64_t cn = ph == 1 ? mych : 0;
+        uint32_t work = 0;
+        const DMode md{0xffffffffu, 0, (uint32_t)ph};
+#pragma unroll 1
+        while (pos < stop) {
+            MsgInfo mi;
+            const uint32_t err = decode_msg<true>(s, pos, mi, &sink, myrow, cn, work, md);
+            if (err) {  // the frame's first error is the earliest of these (and resolve's)
+                atomicMax((unsigned long long*)&st->err_key, (unsigned long long)err_key(pos, err));
+                break;
+            }
+            if (ph == 1) {
+                hb += mi.variant == 5;
+                if (mi.variant == 4) {
+                    if (myrow < cols.cap_rows) cols.id[myrow] = mi.id;
+                    else atomicOr(&st->capacity, 1u);
+                    myrow++;
+                } else if (!cols.ctl_row) {
+                    atomicOr(&st->nonf64, 1u);
+                    myctl++;
+                } else {
+                    if (myctl < cols.cap_ctl) {
+                        cols.ctl_row[myctl] = myrow;
+                        cols.ctl_off[myctl] = pos;
+                        cols.ctl_len[myctl] = (uint32_t)(mi.next - pos);
+                        cols.ctl_variant[myctl] = (uint8_t)mi.variant;
+                    } else {
+                        atomicOr(&st->capacity, 1u);
+                    }
+                    myctl++;
+                }
+            }
+            pos = mi.next;
+        }
+        if (ph == 0 && recount) nch = cn;
+    }
+}
+
+}  // namespace
+
 __global__ __launch_bounds__(TPB) void nxg_gen_emit_kernel(
     const uint8_t* __restrict__ wire, uint64_t W, uint64_t nt, const uint32_t* __restrict__ lws,
     const uint64_t* __restrict__ base, ColsDesc cols, DevStatus* __restrict__ st) {
     __shared__ __attribute__((aligned(16))) uint8_t bufs[WAVES][IMG + 16];  // +16: word reads past the image
+    __shared__ EmitLds tabs[WAVES];
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const uint32_t R = gridDim.x * WAVES, r = blockIdx.x * WAVES + w;
     const uint64_t b = run_begin(nt, R, r), e = run_begin(nt, R, r + 1);
@@ -690,11 +959,13 @@ __global__ __launch_bounds__(TPB) void nxg_gen_emit_kernel(
     const uint64_t chain_end = ck ? (~ck) >> 8 : ~0ull;
     if (b >= e || (rv && r >= rv)) return;
     uint8_t* buf = bufs[w];
+    EmitLds& T = tabs[w];
     const Sink sink{cols, &st->capacity, &st->nonf64};
     uint64_t row = base[(uint64_t)r * 4 + 0];
     uint64_t child = base[(uint64_t)r * 4 + 1];
     uint64_t ctl = base[(uint64_t)r * 4 + 2];
     uint32_t hb = 0;  // heartbeats (counted here: the lane words have no room for them)
+    const bool bucketed = cols.tag != nullptr && cols.ctl_row != nullptr;
     GRegs g;
     g_load(g, wire, b * TILE, W, lane);
     uint32_t lwn = lws[b * 64 + lane];
@@ -710,66 +981,106 @@ __global__ __launch_bounds__(TPB) void nxg_gen_emit_kernel(
         }
         const Src s = g_src(buf, wire, t0, W);
         const uint64_t c = t0 + (uint64_t)lane * CH;
-        const uint64_t stop = c + CH < W ? c + CH : W;
         const bool has = lw_off(lw) != NOSTART;
-        uint32_t nr = has ? lw_rows(lw) : 0u, nk = has ? lw_ctl(lw) : 0u;
-        uint64_t nch = has ? lw_ch(lw) : 0u;
-        // A lane whose children count did not fit its word counts them first (phase 0, no
-        // writes); then the wave scans the counts and every lane decodes + writes (phase 1).
-        const bool recount = has && nch == CH_ESC;
-        uint64_t myrow = 0, myctl = 0, mych = 0;
-#pragma unroll 1
-        for (int ph = __any(recount) ? 0 : 1; ph < 2; ph++) {
-            if (ph == 1) {
-                const uint32_t rin = wave_incl_scan(nr);
-                const uint32_t kin = wave_incl_scan(nk);
-                const uint64_t cin = wave_incl_scan<uint64_t>(nch);
-                myrow = row + rin - nr;
-                myctl = ctl + kin - nk;
-                mych = child + cin - nch;
-                row += __shfl(rin, 63, 64);
-                ctl += __shfl(kin, 63, 64);
-                child += __shfl(cin, 63, 64);
-            }
-            const bool act = ph == 1 ? has : recount;
-            uint64_t pos = act ? c + lw_off(lw) : stop;
-            uint64_t cn = ph == 1 ? mych : 0;
-            uint32_t work = 0;
-            const DMode md{0xffffffffu, 0, (uint32_t)ph};
-#pragma unroll 1
-            while (pos < stop) {
-                MsgInfo mi;
-                const uint32_t err = decode_msg<true>(s, pos, mi, &sink, myrow, cn, work, md);
-                if (err) {  // the frame's first error is the earliest of these (and resolve's)
-                    atomicMax((unsigned long long*)&st->err_key,
-                              (unsigned long long)err_key(pos, err));
-                    break;
-                }
-                if (ph == 1) {
-                    hb += mi.variant == 5;
-                    if (mi.variant == 4) {
-                        if (myrow < cols.cap_rows) cols.id[myrow] = mi.id;
-                        else atomicOr(&st->capacity, 1u);
-                        myrow++;
-                    } else if (!cols.ctl_row) {
-                        atomicOr(&st->nonf64, 1u);
-                        myctl++;
-                    } else {
-                        if (myctl < cols.cap_ctl) {
-                            cols.ctl_row[myctl] = myrow;
-                            cols.ctl_off[myctl] = pos;
-                            cols.ctl_len[myctl] = (uint32_t)(mi.next - pos);
-                            cols.ctl_variant[myctl] = (uint8_t)mi.variant;
-                        } else {
-                            atomicOr(&st->capacity, 1u);
-                        }
-                        myctl++;
-                    }
-                }
-                pos = mi.next;
-            }
-            if (ph == 0 && recount) nch = cn;
+        const uint32_t nr = has ? lw_rows(lw) : 0u, nk = has ? lw_ctl(lw) : 0u;
+        const uint32_t nch = has ? lw_ch(lw) : 0u;
+        const uint32_t nm = nr + nk;
+        const uint32_t minc = wave_incl_scan(nm);
+        const uint32_t nmsg = __shfl(minc, 63, 64);
+        if (!bucketed || nmsg > (uint32_t)MAXM || __any(nch == CH_ESC)) {
+            emit_tile_lanes(s, sink, cols, st, lw, c, row, ctl, child, hb);
+            continue;
         }
+        // 1. message starts (length chain only), in wire order
+        {
+            uint64_t pos = c + lw_off(lw);
+            uint32_t m = minc - nm;
+            const LdsSrc ls{s.lds, s.t0};
+            for (uint32_t i = 0; i < nm; i++) {
+                T.mpos[m++] = (uint16_t)(pos - t0);
+                uint64_t q = pos, L = 1;
+                if (pos - t0 + 10 <= s.nlds) dvar(ls, q, W, L);
+                else dvar(GlbSrc{s.g}, q, W, L);
+                const uint64_t take = L - vl64(L);
+                pos = take < W - q ? q + take : W;
+            }
+        }
+        wave_lds_order();
+        // 2. classify, scan the row / control / child indices in wire order
+        uint32_t rcar = 0, kcar = 0, ccar = 0;
+        uint32_t kcnt[K_N] = {0, 0, 0, 0, 0, 0};
+        for (uint32_t m0 = 0; m0 < nmsg; m0 += 64) {
+            const uint32_t m = m0 + lane;
+            const bool in = m < nmsg;
+            const uint32_t cw = in ? classify(s, t0 + T.mpos[m]) : (uint32_t)K_OTHER;
+            const uint32_t k = cw & 15u;
+            const bool upd = cw & C_UPD;
+            uint32_t kids = cw >> 8;
+            const uint32_t ctlm = in && !upd;
+            if (k == K_OTHER && in && upd) {  // child slots of a value only decode_msg handles
+                MsgInfo mi;
+                uint64_t ch = 0;
+                uint32_t work = 0;
+                if (!skim_msg(s, t0 + T.mpos[m], mi, ch, work, 0xffffffffu)) kids = (uint32_t)ch;
+            }
+            const uint32_t ri = wave_incl_scan((uint32_t)(in && upd));
+            const uint32_t ki = wave_incl_scan(ctlm);
+            const uint32_t ci = wave_incl_scan(in ? kids : 0u);
+            if (in) {  // control messages keep the row they precede in cb
+                T.cls[m] = (uint8_t)(k | (upd ? 0x80u : 0u));
+                T.ridx[m] = upd ? rcar + ri - 1 : kcar + ki - 1;
+                T.cb[m] = upd ? ccar + ci - kids : rcar + ri;
+            }
+            rcar += __shfl(ri, 63, 64);
+            kcar += __shfl(ki, 63, 64);
+            ccar += __shfl(ci, 63, 64);
+#pragma unroll
+            for (int kk = 0; kk < K_N; kk++) kcnt[kk] += __popcll(__ballot(in && k == (uint32_t)kk));
+        }
+        wave_lds_order();
+        // 3. counting sort by class, then one uniform pass per class
+        uint32_t koff[K_N];
+        uint32_t acc = 0;
+#pragma unroll
+        for (int kk = 0; kk < K_N; kk++) {
+            koff[kk] = acc;
+            acc += kcnt[kk];
+        }
+        {
+            uint32_t fill[K_N];
+#pragma unroll
+            for (int kk = 0; kk < K_N; kk++) fill[kk] = koff[kk];
+            for (uint32_t m0 = 0; m0 < nmsg; m0 += 64) {
+                const uint32_t m = m0 + lane;
+                const uint32_t k = m < nmsg ? (T.cls[m] & 0x7fu) : (uint32_t)K_N;
+#pragma unroll
+                for (int kk = 0; kk < K_N; kk++) {
+                    const uint64_t bm = __ballot(k == (uint32_t)kk);
+                    if (k == (uint32_t)kk)
+                        T.bucket[fill[kk] + __popcll(bm & ((1ull << lane) - 1))] = (uint16_t)m;
+                    fill[kk] += __popcll(bm);
+                }
+            }
+        }
+        wave_lds_order();
+#pragma unroll 1
+        for (int kk = 0; kk < K_N; kk++) {
+            for (uint32_t i = koff[kk] + lane; i < koff[kk] + kcnt[kk]; i += 64) {
+                const uint32_t m = T.bucket[i];
+                const uint64_t pos = t0 + T.mpos[m];
+                if (T.cls[m] & 0x80u) {  // Update
+                    const uint64_t r1 = row + T.ridx[m], c1 = child + T.cb[m];
+                    if (kk == K_OTHER || !emit_fast((uint32_t)kk, s, cols, st, pos, r1, c1))
+                        emit_other(s, sink, cols, st, pos, r1, 0, c1);
+                } else {
+                    hb += emit_other(s, sink, cols, st, pos, row + T.cb[m], ctl + T.ridx[m], 0) == 5;
+                }
+            }
+        }
+        row += rcar;
+        ctl += kcar;
+        child += wave_sum<uint32_t>(nch);
+        wave_lds_order();
     }
     hb = wave_sum<uint32_t>(hb);
     if (lane == 0 && hb) atomicAdd((unsigned long long*)&st->n_heartbeat, (unsigned long long)hb);

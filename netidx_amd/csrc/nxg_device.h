@@ -53,6 +53,14 @@ NXG_DEV uint32_t zero_bytes(uint32_t x) {
 // gather the 0x80 flags of a zero_bytes() result into 4 bits
 NXG_DEV uint32_t nib(uint32_t zb) { return (((zb >> 7) & 0x01010101u) * 0x01020408u) >> 24; }
 
+// A wave's LDS image is private to it and LDS operations of one wave complete in order, so only
+// the compiler has to be kept from moving accesses across this point.
+NXG_DEV void wave_lds_order() {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+}
+
 // ---- wave/block scans (wave64) -----------------------------------------------------------
 NXG_DEV uint32_t lane_id() { return __lane_id(); }
 

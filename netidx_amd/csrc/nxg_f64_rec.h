@@ -166,13 +166,6 @@ NXG_DEV void tile_store(uint8_t* buf, const TileRegs& r, uint32_t lane) {
     // branch, so the compiler can keep later tiles' loads in flight across this store)
     *reinterpret_cast<u32x4*>(buf + IMG + (lane & (HALO / 16 - 1)) * 16) = r.h;
 }
-// A wave's LDS image is private to it and LDS operations of one wave complete in order, so only
-// the compiler has to be kept from moving accesses across this point.
-NXG_DEV void wave_lds_order() {
-    asm volatile("" ::: "memory");
-    __builtin_amdgcn_wave_barrier();
-    asm volatile("" ::: "memory");
-}
 
 // Merge point X_lane of this lane's chunk [64*lane, 64*lane+64) of `tile` (buf = the tile's
 // LDS image): FAIL if the walks starting there do not merge. Lane 63's chunk starts at STRIDE,
