@@ -47,7 +47,7 @@ namespace {
 constexpr int TPB1 = 256;
 constexpr int WAVES1 = TPB1 / 64;
 #ifndef NXG_1P_LAG
-#define NXG_1P_LAG 2
+#define NXG_1P_LAG 1
 #endif
 constexpr int LAG = NXG_1P_LAG;
 constexpr int NSLOT = LAG + 1;
@@ -191,27 +191,36 @@ NXG_DEV void f64_work(const uint8_t* __restrict__ wire, uint64_t W, uint64_t nt,
             const bool owner = lane != 63;  // lane 63's merge point is the next tile's first
             bool bad = (xa == FAIL) | (owner & ((xb == FAIL) | (xa > xb)));
             const uint64_t t0 = t * f64dec::STRIDE;
-            uint32_t rid[MAXL];
-            uint64_t rval[MAXL];
+            // the chain of record starts reads one length byte per step; the records are then
+            // loaded together (independent reads) and each is fully checked (rec_check: its
+            // length must be the byte the chain stepped by)
+            uint32_t ps[MAXL];
             uint32_t pos = xa, n = 0;
+            const bool walk = owner && !bad;
 #pragma unroll
             for (int q = 0; q < MAXL; q++) {
-                rid[q] = 0;
-                rval[q] = 0;
-                if (owner && !bad && pos < xb) {
-                    uint32_t e0, e1, e2, e3;
-                    load16(img, pos, e0, e1, e2, e3);
-                    const uint32_t Lr = rec_check(e0, e1, W - (t0 + pos));
-                    bad |= Lr == 0;
-                    uint64_t id, val;
-                    rec_decode(e0, e1, e2, e3, Lr ? Lr : 12u, id, val);
-                    rid[q] = (uint32_t)id;
-                    rval[q] = val;
-                    pos += Lr ? Lr : 12u;
+                ps[q] = walk && pos < xb ? pos : 0u;
+                if (walk && pos < xb) {
+                    const uint32_t Lb = img[pos];
+                    bad |= Lb - 12u > 3u;
+                    pos += Lb - 12u > 3u ? 12u : Lb;
                     n++;
                 }
             }
             bad |= owner && pos != xb;
+            uint32_t rid[MAXL];
+            uint64_t rval[MAXL];
+#pragma unroll
+            for (int q = 0; q < MAXL; q++) {
+                uint32_t e0, e1, e2, e3;
+                load16(img, ps[q], e0, e1, e2, e3);
+                const uint32_t Lr = rec_check(e0, e1, W - (t0 + ps[q]));
+                bad |= (uint32_t)q < n && Lr == 0;
+                uint64_t id, val;
+                rec_decode(e0, e1, e2, e3, Lr ? Lr : 12u, id, val);
+                rid[q] = (uint32_t)id;
+                rval[q] = val;
+            }
             if (__any(bad)) {
                 if (lane == 0) atomicOr(&st->fast_fail, 1u);
                 return;

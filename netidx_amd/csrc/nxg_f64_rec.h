@@ -72,14 +72,14 @@ NXG_DEV void rec_decode(uint32_t e0, uint32_t e1, uint32_t e2, uint32_t e3, uint
 }
 
 
-// Merge point of all record walks starting in [r, r+15) (tile-relative). r is 4-aligned.
-NXG_DEV uint32_t merge_point(const uint8_t* buf, uint32_t r, uint64_t t0, uint64_t W) {
+// Merge point of all record walks starting in [r, r+15) (tile-relative). r is 4-aligned;
+// d0..d4 are the 20 bytes at r (the candidate mask comes from them; the candidates' records and
+// the walks are read from the LDS image `buf`).
+NXG_DEV uint32_t merge_point_d(const uint8_t* buf, uint32_t r, uint64_t t0, uint64_t W,
+                               uint32_t d0, uint32_t d1, uint32_t d2, uint32_t d3, uint32_t d4) {
     const uint64_t abs_r = t0 + r;
     if (abs_r >= W) return (uint32_t)(W - t0);  // chunk past the end: the END position
     const uint64_t remr = W - abs_r;
-    const u32x4 q = *reinterpret_cast<const u32x4*>(buf + r);  // r is 64-byte aligned
-    const uint32_t d0 = q.x, d1 = q.y, d2 = q.z, d3 = q.w;
-    const uint32_t d4 = *reinterpret_cast<const uint32_t*>(buf + r + 16);
     // candidate starts: byte in 12..15 followed by 0x04
     const uint32_t a = nib(zero_bytes((d0 & 0xfcfcfcfcu) ^ 0x0c0c0c0cu)) |
                        (nib(zero_bytes((d1 & 0xfcfcfcfcu) ^ 0x0c0c0c0cu)) << 4) |
@@ -117,6 +117,12 @@ NXG_DEV uint32_t merge_point(const uint8_t* buf, uint32_t r, uint64_t t0, uint64
     }
     if (__popcll(S) != 1) return FAIL;
     return r + (uint32_t)__builtin_ctzll(S);
+}
+NXG_DEV uint32_t merge_point(const uint8_t* buf, uint32_t r, uint64_t t0, uint64_t W) {
+    if (t0 + r >= W) return (uint32_t)(W - t0);
+    const u32x4 q = *reinterpret_cast<const u32x4*>(buf + r);  // r is 64-byte aligned
+    const uint32_t d4 = *reinterpret_cast<const uint32_t*>(buf + r + 16);
+    return merge_point_d(buf, r, t0, W, q.x, q.y, q.z, q.w, d4);
 }
 
 NXG_DEV uint4 ld16_guard(const uint8_t* __restrict__ wire, uint64_t off, uint64_t W) {
