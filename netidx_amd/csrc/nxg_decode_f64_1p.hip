@@ -210,11 +210,12 @@ NXG_DEV void f64_work(const uint8_t* __restrict__ wire, uint64_t W, uint64_t nt,
             bad |= owner && pos != xb;
             uint32_t rid[MAXL];
             uint64_t rval[MAXL];
+            const uint32_t remt = W - t0 < 0xffffffffull ? (uint32_t)(W - t0) : 0xffffffffu;
 #pragma unroll
             for (int q = 0; q < MAXL; q++) {
                 uint32_t e0, e1, e2, e3;
                 load16(img, ps[q], e0, e1, e2, e3);
-                const uint32_t Lr = rec_check(e0, e1, W - (t0 + ps[q]));
+                const uint32_t Lr = rec_check32(e0, e1, remt - ps[q]);
                 bad |= (uint32_t)q < n && Lr == 0;
                 uint64_t id, val;
                 rec_decode(e0, e1, e2, e3, Lr ? Lr : 12u, id, val);

@@ -59,6 +59,19 @@ NXG_DEV uint32_t rec_check(uint32_t e0, uint32_t e1, uint64_t rem) {
     return L;
 }
 
+// rec_check without branches (the same checks): `rem` = bytes from the record start to the end
+// of the frame, saturated to 32 bits.
+NXG_DEV uint32_t rec_check32(uint32_t e0, uint32_t e1, uint32_t rem) {
+    const uint32_t L = e0 & 0xffu;
+    const bool head = (e0 & 0xfffcu) == 0x040cu;        // L in 12..15, then From::Update
+    const uint32_t sh = 8u * ((L & 3u) + 1u);           // 8 * nb (nb = L - 11 when head)
+    const uint32_t m = 0xffffffffu >> (32u - sh);       // the nb id bytes
+    const uint32_t x = alignbyte(e1, e0, 2);            // bytes 2..5
+    const bool var = (x & 0x80808080u & m) == (0x80808080u & (m >> 8));  // exactly nb bytes
+    const uint32_t tag = __builtin_amdgcn_ubfe(alignbyte(e1, e0, 3), sh - 8u, 8u);  // byte 2+nb
+    return (head && var && tag == 9u && rem >= L) ? L : 0u;
+}
+
 NXG_DEV void rec_decode(uint32_t e0, uint32_t e1, uint32_t e2, uint32_t e3, uint32_t L,
                         uint64_t& id, uint64_t& val) {
     const uint32_t nb = L - 11u;
