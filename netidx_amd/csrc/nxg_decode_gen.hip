@@ -101,14 +101,6 @@ NXG_DEV void walk(const Src& s, uint64_t e, uint64_t end, LaneRes& r, uint32_t b
     r.x = pos;
 }
 
-// 1 + payload size of the fixed-size value tags (pack.rs / value lib.rs:361-468), 4 bits per
-// tag; 0 = variable size (varints, text, containers) or not checked (Decimal)
-constexpr uint64_t kFixLo = 0x1100DD9509090505ull;  // tags 0..15
-constexpr uint64_t kFixHi = 0x0000033220000011ull;  // tags 16..27
-NXG_DEV uint32_t fixed_size1(uint32_t t) {
-    return (uint32_t)(((t < 16 ? kFixLo >> (4 * t) : kFixHi >> (4 * (t - 16)))) & 0xfu);
-}
-
 // Structural plausibility of an Update at p with an nb-byte length prefix L (minimal): the
 // Update variant is already matched by the caller. Checks that the id varint and the value tag
 // fit in the message, that a fixed-size value fills it exactly, and that the next position

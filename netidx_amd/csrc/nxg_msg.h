@@ -85,6 +85,15 @@ struct GlbSrc {
     }
 };
 
+// 1 + payload size of the fixed-size value tags (pack.rs / value lib.rs:361-468), 4 bits per
+// tag; 0 = variable size (varints, text, containers), not checked (Decimal) or unknown (>= 28)
+constexpr uint64_t kFixLo = 0x1100DD9509090505ull;  // tags 0..15
+constexpr uint64_t kFixHi = 0x0000033220000011ull;  // tags 16..27
+NXG_DEV uint32_t fixed_size1(uint32_t t) {
+    if (t >= 28u) return 0u;
+    return (uint32_t)(((t < 16 ? kFixLo >> (4 * t) : kFixHi >> (4 * (t - 16)))) & 0xfu);
+}
+
 // Where a decoded value goes.
 struct Sink {
     ColsDesc c;
@@ -546,6 +555,22 @@ NXG_DEV uint32_t skim_body(const S& s, uint64_t p, uint64_t lim, MsgInfo& info,
     if (dvar(s, p, lim, v) || p >= lim) return E_OK;  // content error: reported by emit
     const uint32_t t = s.byte(p);
     if (!is_container(s, t, p + 1, lim)) return E_OK;
+    if (t == 19) {  // an array of fixed-size scalars: one child slot per element (as dvalue)
+        uint64_t q = p + 1, cnt;
+        if (!dvar(s, q, lim, cnt) && cnt <= kMaxVec / 16 && cnt * 16 <= ((lim - q) << 8)) {
+            bool flat = true;
+#pragma unroll 1
+            for (uint64_t i = 0; flat && i < cnt; i++) {
+                const uint32_t f1 = q < lim ? fixed_size1(s.byte(q)) : 0u;  // 1 + payload bytes
+                flat = f1 != 0 && q + f1 <= lim;
+                q += f1;
+            }
+            if (flat) {
+                children = cnt;
+                return E_OK;
+            }
+        }
+    }
     uint64_t cn = 0;
     const DMode md{budget, 1, 0};  // structure: no UTF-8 scan, no writes
     const uint32_t e = dvalue<false>(s, p, lim, nullptr, true, 0, cn, work, md);
