@@ -202,6 +202,18 @@ NXG_DEV bool utf8_valid(const Src& s, uint64_t p, uint64_t n) {
 constexpr int64_t kMinDaysCE = -95746129;  // days_from_civil(-262143,1,1) + 719163
 constexpr int64_t kMaxDaysCE = 95745399;   // days_from_civil(262142,12,31) + 719163
 NXG_DEV bool datetime_valid(int64_t secs, uint32_t ns) {
+    if (ns >= 2000000000u) return false;
+    // |secs| < 2^42 (about 139,000 years) lies inside the range below: no day arithmetic, and
+    // the leap-second test needs only secs mod 60 (86400 is a multiple of 60)
+    if (secs > -(1ll << 42) && secs < (1ll << 42)) {
+        if (ns < 1000000000u) return true;
+        const int32_t hi = (int32_t)(secs >> 21);  // secs = hi * 2^21 + lo, exactly
+        const int32_t lo = (int32_t)(secs & ((1 << 21) - 1));
+        // 2^21 mod 60 = 32; floored mod of hi * 32 + lo, all within 32 bits
+        int32_t m = ((hi % 60) * 32 + lo % 60) % 60;
+        if (m < 0) m += 60;
+        return m == 59;
+    }
     int64_t days = secs / 86400;
     int64_t sod = secs % 86400;
     if (sod < 0) {

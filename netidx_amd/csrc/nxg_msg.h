@@ -103,20 +103,32 @@ struct Sink {
 
 // LEB128 (pack.rs:504-520): at most 10 bytes, bits past 64 dropped, no minimality check.
 // With 8 bytes available, one pair of word reads finds the terminator (ends in 1..8 bytes).
+// A terminator in the first 4 bytes (almost every varint on this path) is decoded with 32-bit
+// operations; 5..8 bytes with a 3-step 64-bit compress of the 7-bit groups.
 template <class S>
 NXG_DEV uint32_t dvar(const S& s, uint64_t& p, uint64_t lim, uint64_t& v) {
-    if (lim - p >= 8 && lim > p) {
-        const uint64_t x = (uint64_t)s.word(p) | ((uint64_t)s.word(p + 4) << 32);
-        const uint64_t stop = ~x & 0x8080808080808080ull;
-        if (stop) {
-            const uint32_t nb = ((uint32_t)__builtin_ctzll(stop) >> 3) + 1;  // 1..8
-            const uint64_t y = nb == 8 ? x : (x & ((1ull << (8 * nb)) - 1));
-            uint64_t val = 0;
-#pragma unroll
-            for (int i = 0; i < 8; i++) val |= ((y >> (8 * i)) & 0x7full) << (7 * i);
+    if (lim > p && lim - p >= 4) {
+        const uint32_t lo = s.word(p);
+        const uint32_t st4 = ~lo & 0x80808080u;
+        if (st4) {
+            const uint32_t nb = ((uint32_t)__builtin_ctz(st4) >> 3) + 1;  // 1..4
+            const uint32_t y = lo & (0xffffffffu >> (32u - 8u * nb));
+            v = (y & 0x7fu) | ((y >> 1) & 0x3f80u) | ((y >> 2) & 0x1fc000u) | ((y >> 3) & 0xfe00000u);
             p += nb;
-            v = val;
             return E_OK;
+        }
+        if (lim - p >= 8) {
+            const uint64_t x = (uint64_t)lo | ((uint64_t)s.word(p + 4) << 32);
+            const uint64_t stop = ~x & 0x8080808080808080ull;
+            if (stop) {
+                const uint32_t nb = ((uint32_t)__builtin_ctzll(stop) >> 3) + 1;  // 5..8
+                const uint64_t y = nb == 8 ? x : (x & ((1ull << (8 * nb)) - 1));
+                const uint64_t z1 = (y & 0x007f007f007f007full) | ((y >> 1) & 0x3f803f803f803f80ull);
+                const uint64_t z2 = (z1 & 0x00003fff00003fffull) | ((z1 >> 2) & 0x0fffc0000fffc000ull);
+                v = (z2 & 0x0fffffffull) | ((z2 >> 4) & 0x00fffffff0000000ull);
+                p += nb;
+                return E_OK;
+            }
         }
     }
     uint64_t val = 0;
