@@ -293,7 +293,7 @@ bool ensure_glws(NxgCtx* c, size_t bytes, NetidxError* err) {
 
 bool enqueue_dec_general(NxgCtx* c, const uint8_t* f, uint64_t len, NxgColumns* out,
                          DevStatus* st, NetidxError* err) {
-    if (!ensure_glws(c, 256 * nxg_dec_gen_tiles(len), err)) return false;
+    if (!ensure_glws(c, nxg_dec_gen_scratch_bytes(len), err)) return false;
     const ColsDesc d = desc_of(out);
     HIPCHK(nxg_launch_dec_gen(f, len, d, c->glws, c->gruns,
                               c->gruns + (size_t)gdec2::MAX_RUNS * gdec2::RUN_WORDS,

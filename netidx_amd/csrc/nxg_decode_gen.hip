@@ -467,8 +467,9 @@ NXG_DEV RunSum run_tiles(const uint8_t* __restrict__ wire, uint64_t W, uint64_t 
 // ---- pass 1: count ---------------------------------------------------------------------------
 __global__ __launch_bounds__(TPB) void nxg_gen_count_kernel(
     const uint8_t* __restrict__ wire, uint64_t W, uint64_t nt, uint32_t* __restrict__ lws,
-    uint64_t* __restrict__ runs, DevStatus* __restrict__ st, DevStatus* zst) {
+    uint64_t* __restrict__ runs, DevStatus* __restrict__ st, DevStatus* zst, uint64_t* __restrict__ fix) {
     zero_status(zst);
+    if (blockIdx.x == 0 && threadIdx.x == 0) fix[0] = 0;  // emit's work list (read by fix)
     __shared__ __attribute__((aligned(16))) uint8_t bufs[WAVES][IMG + 16];  // +16: word reads past the image
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const uint32_t R = gridDim.x * WAVES, r = blockIdx.x * WAVES + w;
@@ -669,22 +670,26 @@ __global__ __launch_bounds__(RES_TPB) void nxg_gen_resolve_kernel(
 }
 
 // ---- pass 3: emit ----------------------------------------------------------------------------
-// Type-bucketed, message-parallel. Per tile:
+// Two kernels. The emit kernel is type-bucketed and message-parallel; per tile:
 //   1. each lane walks only the length chain of the messages that start in its chunk (from the
 //      start its lane word records) and lists their positions in LDS, in wire order;
 //   2. message-parallel: every message's header is parsed and the message classified (fixed-size
-//      scalar, text, DateTime/Duration, varint scalar, flat array of fixed-size scalars, or
-//      other); row / control / child indices are scanned in wire order;
+//      scalar, text, DateTime/Duration, varint scalar, flat array of fixed-size scalars,
+//      Heartbeat, or other); row / control / child indices are scanned in wire order;
 //   3. a counting sort buckets the messages by class, and each bucket is decoded by all lanes
 //      running the same code, 64 messages at a time.
-// "Other" (control messages, nested or unusual values, messages that leave the LDS image) and any
-// message a fast path does not accept go through decode_msg, which also reports the exact error.
-// Tiles with more than MAXM messages (tiny messages) or a children count that overflowed a lane
-// word use the per-lane path (emit_tile_lanes).
+// A tile holding an "other" message (other control messages, nested or unusual values, messages
+// that leave the LDS image), a message a fast path does not accept (it may be an error), more
+// than MAXM messages, or columns without the mixed layout goes on a work list with its row /
+// control / child bases; a tile whose lane words lost a children count (CH_ESC) puts the rest of
+// its run there (the bases after it are not known). The fix kernel then re-emits the listed tiles
+// with the per-lane path (decode_msg for every message, exact errors). The emit kernel itself
+// never runs the general decoder, which keeps it small (registers, instruction cache).
 namespace {
 
 constexpr int MAXM = 512;  // messages per tile on the bucketed path
-enum { K_FIX = 0, K_TEXT, K_TIME, K_VAR, K_ARR, K_OTHER, K_N };
+enum { K_FIX = 0, K_TEXT, K_TIME, K_VAR, K_ARR, K_HB, K_OTHER, K_N };
+constexpr int FIX_WORDS = 5;  // work list entry: first tile, end tile, row, control, child bases
 
 struct EmitLds {
     uint16_t mpos[MAXM];  // message start, tile-relative
@@ -721,18 +726,21 @@ NXG_DEV uint64_t fix_value(const LdsSrc& s, uint32_t t, uint64_t p, int n) {
 // Header of the message at p: returns the class in bits 0..3, bit 4 for an Update, and the
 // number of child slots (K_ARR) from bit 8. The Update bit is exact for every well-formed
 // message (it sets the row / control numbering); anything unusual, or a message not wholly in
-// the image, is K_OTHER (decoded by decode_msg, which also reports errors).
+// the image, is K_OTHER.
 constexpr uint32_t C_UPD = 16;
 NXG_DEV uint32_t classify(const Src& s, uint64_t p) {
     const LdsSrc ls{s.lds, s.t0};
     uint64_t q = p, L;
     const uint32_t e = p - s.t0 + 10 <= s.nlds ? dvar(ls, q, s.W, L) : dvar(GlbSrc{s.g}, q, s.W, L);
-    if (e || L < 1 || q >= s.W) return K_OTHER;  // an error: decode_msg reports it
+    if (e || L < 1 || q >= s.W) return K_OTHER;  // an error: the fix kernel reports it
     const uint64_t take = L - vl64(L);
     const uint64_t lim = take < s.W - q ? q + take : s.W;
     const uint32_t variant = s.any_byte(q++);
-    if (variant != 4) return K_OTHER;  // control messages: validated and written by decode_msg
-    if (lim - s.t0 + 8 > s.nlds || q >= lim) return K_OTHER | C_UPD;  // not wholly in the image
+    if (variant == 5) return K_HB;  // Heartbeat: no fields (trailing bytes skipped, pack.rs:551)
+    if (variant != 4) return K_OTHER;
+    // wholly in the image (word reads reach at most 7 bytes past the message: the 16 spare
+    // bytes after the image cover them)
+    if (lim - s.t0 > s.nlds || q >= lim) return K_OTHER | C_UPD;
     uint64_t id;
     if (dvar(ls, q, lim, id) || q >= lim) return K_OTHER | C_UPD;
     const uint32_t t = ls.byte(q++);
@@ -754,35 +762,6 @@ NXG_DEV uint32_t classify(const Src& s, uint64_t p) {
         if (ok) return K_ARR | C_UPD | ((uint32_t)cnt << 8);
     }
     return k | C_UPD;
-}
-
-// the general path for one message: decode_msg writes the row / children; the control columns
-// and the id are written here (as the per-lane path does)
-NXG_DEV uint32_t emit_other(const Src& s, const Sink& sink, const ColsDesc& cols, DevStatus* st,
-                            uint64_t pos, uint64_t row, uint64_t ctl, uint64_t child) {
-    MsgInfo mi;
-    uint32_t work = 0;
-    uint64_t cn = child;
-    const DMode md{0xffffffffu, 0, 1};
-    const uint32_t err = decode_msg<true>(s, pos, mi, &sink, row, cn, work, md);
-    if (err) {
-        atomicMax((unsigned long long*)&st->err_key, (unsigned long long)err_key(pos, err));
-        return 0;
-    }
-    if (mi.variant == 4) {
-        if (row < cols.cap_rows) cols.id[row] = mi.id;
-        else atomicOr(&st->capacity, 1u);
-    } else if (!cols.ctl_row) {
-        atomicOr(&st->nonf64, 1u);
-    } else if (ctl < cols.cap_ctl) {
-        cols.ctl_row[ctl] = row;
-        cols.ctl_off[ctl] = pos;
-        cols.ctl_len[ctl] = (uint32_t)(mi.next - pos);
-        cols.ctl_variant[ctl] = (uint8_t)mi.variant;
-    } else {
-        atomicOr(&st->capacity, 1u);
-    }
-    return mi.variant;
 }
 
 NXG_DEV void put_row(const ColsDesc& cols, DevStatus* st, uint64_t row, uint64_t id, uint32_t tag,
@@ -869,6 +848,67 @@ NXG_DEV bool emit_fast(uint32_t k, const Src& s, const ColsDesc& cols, DevStatus
     return true;
 }
 
+// A Heartbeat at pos (validated by classify): its control-message columns.
+NXG_DEV void emit_hb(const Src& s, const ColsDesc& cols, DevStatus* st, uint64_t pos, uint64_t row,
+                     uint64_t ctl) {
+    uint64_t q = pos, L;
+    if (pos - s.t0 + 10 <= s.nlds) dvar(LdsSrc{s.lds, s.t0}, q, s.W, L);
+    else dvar(GlbSrc{s.g}, q, s.W, L);
+    const uint64_t take = L - vl64(L);
+    const uint64_t lim = take < s.W - q ? q + take : s.W;
+    if (ctl < cols.cap_ctl) {
+        cols.ctl_row[ctl] = row;
+        cols.ctl_off[ctl] = pos;
+        cols.ctl_len[ctl] = (uint32_t)(lim - pos);
+        cols.ctl_variant[ctl] = 5;
+    } else {
+        atomicOr(&st->capacity, 1u);
+    }
+}
+
+// work list: fix[0] = entries, then FIX_WORDS words per entry (at most one per tile)
+NXG_DEV void fix_push(uint64_t* fix, uint64_t tb, uint64_t te, uint64_t row, uint64_t ctl,
+                      uint64_t child) {
+    if (__lane_id() == 0) {
+        const uint64_t i = atomicAdd((unsigned long long*)fix, 1ull);
+        uint64_t* e = fix + 1 + i * FIX_WORDS;
+        e[0] = tb;
+        e[1] = te;
+        e[2] = row;
+        e[3] = ctl;
+        e[4] = child;
+    }
+}
+
+// the general path for one message: decode_msg writes the row / children; the control columns
+// and the id are written here (as the per-lane path does)
+NXG_DEV uint32_t emit_other(const Src& s, const Sink& sink, const ColsDesc& cols, DevStatus* st,
+                            uint64_t pos, uint64_t row, uint64_t ctl, uint64_t child) {
+    MsgInfo mi;
+    uint32_t work = 0;
+    uint64_t cn = child;
+    const DMode md{0xffffffffu, 0, 1};
+    const uint32_t err = decode_msg<true>(s, pos, mi, &sink, row, cn, work, md);
+    if (err) {
+        atomicMax((unsigned long long*)&st->err_key, (unsigned long long)err_key(pos, err));
+        return 0;
+    }
+    if (mi.variant == 4) {
+        if (row < cols.cap_rows) cols.id[row] = mi.id;
+        else atomicOr(&st->capacity, 1u);
+    } else if (!cols.ctl_row) {
+        atomicOr(&st->nonf64, 1u);
+    } else if (ctl < cols.cap_ctl) {
+        cols.ctl_row[ctl] = row;
+        cols.ctl_off[ctl] = pos;
+        cols.ctl_len[ctl] = (uint32_t)(mi.next - pos);
+        cols.ctl_variant[ctl] = (uint8_t)mi.variant;
+    } else {
+        atomicOr(&st->capacity, 1u);
+    }
+    return mi.variant;
+}
+
 // The per-lane path (tiles the bucketed path does not take): each lane decodes its messages in
 // order with decode_msg.
 NXG_DEV void emit_tile_lanes(const Src& s, const Sink& sink, const ColsDesc& cols, DevStatus* st,
@@ -939,7 +979,8 @@ NXG_DEV void emit_tile_lanes(const Src& s, const Sink& sink, const ColsDesc& col
 
 __global__ __launch_bounds__(TPB) void nxg_gen_emit_kernel(
     const uint8_t* __restrict__ wire, uint64_t W, uint64_t nt, const uint32_t* __restrict__ lws,
-    const uint64_t* __restrict__ base, ColsDesc cols, DevStatus* __restrict__ st) {
+    const uint64_t* __restrict__ base, ColsDesc cols, DevStatus* __restrict__ st,
+    uint64_t* __restrict__ fix) {
     __shared__ __attribute__((aligned(16))) uint8_t bufs[WAVES][IMG + 16];  // +16: word reads past the image
     __shared__ EmitLds tabs[WAVES];
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -952,12 +993,14 @@ __global__ __launch_bounds__(TPB) void nxg_gen_emit_kernel(
     if (b >= e || (rv && r >= rv)) return;
     uint8_t* buf = bufs[w];
     EmitLds& T = tabs[w];
-    const Sink sink{cols, &st->capacity, &st->nonf64};
     uint64_t row = base[(uint64_t)r * 4 + 0];
     uint64_t child = base[(uint64_t)r * 4 + 1];
     uint64_t ctl = base[(uint64_t)r * 4 + 2];
-    uint32_t hb = 0;  // heartbeats (counted here: the lane words have no room for them)
-    const bool bucketed = cols.tag != nullptr && cols.ctl_row != nullptr;
+    if (cols.tag == nullptr || cols.ctl_row == nullptr) {  // not the mixed layout: all per lane
+        fix_push(fix, b, e, row, ctl, child);
+        return;
+    }
+    uint32_t hb = 0;  // heartbeats in tiles this kernel completes
     GRegs g;
     g_load(g, wire, b * TILE, W, lane);
     uint32_t lwn = lws[b * 64 + lane];
@@ -976,11 +1019,19 @@ __global__ __launch_bounds__(TPB) void nxg_gen_emit_kernel(
         const bool has = lw_off(lw) != NOSTART;
         const uint32_t nr = has ? lw_rows(lw) : 0u, nk = has ? lw_ctl(lw) : 0u;
         const uint32_t nch = has ? lw_ch(lw) : 0u;
+        if (__any(nch == CH_ESC)) {  // this tile's children are not in the words: the rest per lane
+            fix_push(fix, t, e, row, ctl, child);
+            break;
+        }
         const uint32_t nm = nr + nk;
         const uint32_t minc = wave_incl_scan(nm);
         const uint32_t nmsg = __shfl(minc, 63, 64);
-        if (!bucketed || nmsg > (uint32_t)MAXM || __any(nch == CH_ESC)) {
-            emit_tile_lanes(s, sink, cols, st, lw, c, row, ctl, child, hb);
+        const uint64_t row_t = row, ctl_t = ctl, child_t = child;
+        row += wave_sum<uint32_t>(nr);
+        ctl += wave_sum<uint32_t>(nk);
+        child += wave_sum<uint32_t>(nch);
+        if (nmsg > (uint32_t)MAXM) {
+            fix_push(fix, t, t + 1, row_t, ctl_t, child_t);
             continue;
         }
         // 1. message starts (length chain only), in wire order
@@ -1000,23 +1051,16 @@ __global__ __launch_bounds__(TPB) void nxg_gen_emit_kernel(
         wave_lds_order();
         // 2. classify, scan the row / control / child indices in wire order
         uint32_t rcar = 0, kcar = 0, ccar = 0;
-        uint32_t kcnt[K_N] = {0, 0, 0, 0, 0, 0};
+        uint32_t kcnt[K_N] = {0, 0, 0, 0, 0, 0, 0};
         for (uint32_t m0 = 0; m0 < nmsg; m0 += 64) {
             const uint32_t m = m0 + lane;
             const bool in = m < nmsg;
             const uint32_t cw = in ? classify(s, t0 + T.mpos[m]) : (uint32_t)K_OTHER;
             const uint32_t k = cw & 15u;
             const bool upd = cw & C_UPD;
-            uint32_t kids = cw >> 8;
-            const uint32_t ctlm = in && !upd;
-            if (k == K_OTHER && in && upd) {  // child slots of a value only decode_msg handles
-                MsgInfo mi;
-                uint64_t ch = 0;
-                uint32_t work = 0;
-                if (!skim_msg(s, t0 + T.mpos[m], mi, ch, work, 0xffffffffu)) kids = (uint32_t)ch;
-            }
+            const uint32_t kids = cw >> 8;
             const uint32_t ri = wave_incl_scan((uint32_t)(in && upd));
-            const uint32_t ki = wave_incl_scan(ctlm);
+            const uint32_t ki = wave_incl_scan((uint32_t)(in && !upd));
             const uint32_t ci = wave_incl_scan(in ? kids : 0u);
             if (in) {  // control messages keep the row they precede in cb
                 T.cls[m] = (uint8_t)(k | (upd ? 0x80u : 0u));
@@ -1028,6 +1072,11 @@ __global__ __launch_bounds__(TPB) void nxg_gen_emit_kernel(
             ccar += __shfl(ci, 63, 64);
 #pragma unroll
             for (int kk = 0; kk < K_N; kk++) kcnt[kk] += __popcll(__ballot(in && k == (uint32_t)kk));
+        }
+        if (kcnt[K_OTHER]) {  // a message only decode_msg handles
+            fix_push(fix, t, t + 1, row_t, ctl_t, child_t);
+            wave_lds_order();
+            continue;
         }
         wave_lds_order();
         // 3. counting sort by class, then one uniform pass per class
@@ -1055,30 +1104,62 @@ __global__ __launch_bounds__(TPB) void nxg_gen_emit_kernel(
             }
         }
         wave_lds_order();
+        bool fail = false;
 #pragma unroll 1
-        for (int kk = 0; kk < K_N; kk++) {
+        for (int kk = 0; kk < K_OTHER; kk++) {
             for (uint32_t i = koff[kk] + lane; i < koff[kk] + kcnt[kk]; i += 64) {
                 const uint32_t m = T.bucket[i];
                 const uint64_t pos = t0 + T.mpos[m];
-                if (T.cls[m] & 0x80u) {  // Update
-                    const uint64_t r1 = row + T.ridx[m], c1 = child + T.cb[m];
-                    if (kk == K_OTHER || !emit_fast((uint32_t)kk, s, cols, st, pos, r1, c1))
-                        emit_other(s, sink, cols, st, pos, r1, 0, c1);
-                } else {
-                    hb += emit_other(s, sink, cols, st, pos, row + T.cb[m], ctl + T.ridx[m], 0) == 5;
-                }
+                if (kk == K_HB) emit_hb(s, cols, st, pos, row_t + T.cb[m], ctl_t + T.ridx[m]);
+                else fail |= !emit_fast((uint32_t)kk, s, cols, st, pos, row_t + T.ridx[m],
+                                        child_t + T.cb[m]);
             }
         }
-        row += rcar;
-        ctl += kcar;
-        child += wave_sum<uint32_t>(nch);
+        if (__any(fail)) fix_push(fix, t, t + 1, row_t, ctl_t, child_t);  // exact errors there
+        else hb += kcnt[K_HB];
         wave_lds_order();
+    }
+    if (lane == 0 && hb) atomicAdd((unsigned long long*)&st->n_heartbeat, (unsigned long long)hb);
+}
+
+// Re-emits the work list's tiles with the per-lane path (every message through decode_msg).
+__global__ __launch_bounds__(TPB) void nxg_gen_fix_kernel(
+    const uint8_t* __restrict__ wire, uint64_t W, const uint32_t* __restrict__ lws, ColsDesc cols,
+    DevStatus* __restrict__ st, const uint64_t* __restrict__ fix) {
+    __shared__ __attribute__((aligned(16))) uint8_t bufs[WAVES][IMG + 16];
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint64_t n = fix[0];
+    if (blockIdx.x == 0 && threadIdx.x == 0) st->diag[7] = n;  // tiles re-emitted per lane
+    const uint64_t ck = st->err_key;
+    const uint64_t chain_end = ck ? (~ck) >> 8 : ~0ull;
+    uint8_t* buf = bufs[w];
+    const Sink sink{cols, &st->capacity, &st->nonf64};
+    uint32_t hb = 0;
+#pragma unroll 1
+    for (uint64_t i = (uint64_t)blockIdx.x * WAVES + w; i < n; i += (uint64_t)gridDim.x * WAVES) {
+        const uint64_t* en = fix + 1 + i * FIX_WORDS;
+        uint64_t row = en[2], ctl = en[3], child = en[4];
+#pragma unroll 1
+        for (uint64_t t = en[0]; t < en[1]; t++) {
+            const uint64_t t0 = t * TILE;
+            if (t0 > chain_end) break;
+            GRegs g;
+            g_load(g, wire, t0, W, lane);
+            g_stage(buf, g, lane);
+            const Src s = g_src(buf, wire, t0, W);
+            emit_tile_lanes(s, sink, cols, st, lws[t * 64 + lane], t0 + (uint64_t)lane * CH, row,
+                            ctl, child, hb);
+        }
     }
     hb = wave_sum<uint32_t>(hb);
     if (lane == 0 && hb) atomicAdd((unsigned long long*)&st->n_heartbeat, (unsigned long long)hb);
 }
 
 uint64_t nxg_dec_gen_tiles(uint64_t W) { return (W + TILE - 1) / TILE; }
+uint64_t nxg_dec_gen_scratch_bytes(uint64_t W) {
+    const uint64_t nt = nxg_dec_gen_tiles(W);
+    return 256 * nt + 8 * (1 + FIX_WORDS * nt);  // lane words, then emit's work list
+}
 
 hipError_t nxg_launch_dec_gen(const uint8_t* wire, uint64_t W, const ColsDesc& cd, uint32_t* lws,
                               uint64_t* runs, uint64_t* base, int wgs, DevStatus* st,
@@ -1090,12 +1171,14 @@ hipError_t nxg_launch_dec_gen(const uint8_t* wire, uint64_t W, const ColsDesc& c
     uint64_t g = (nt + WAVES - 1) / WAVES;
     if (g > (uint64_t)wgs) g = wgs;
     const uint32_t R = (uint32_t)g * WAVES;
+    uint64_t* fix = reinterpret_cast<uint64_t*>(lws + 64 * nt);  // nxg_dec_gen_scratch_bytes
     hipLaunchKernelGGL(nxg_gen_count_kernel, dim3(g), dim3(TPB), 0, s, wire, W, nt, lws, runs, st,
-                       nxg_zero_slot);
+                       nxg_zero_slot, fix);
     hipLaunchKernelGGL(nxg_gen_resolve_kernel, dim3(1), dim3(RES_TPB), 0, s, wire, W, nt, R, lws,
                        runs, base, st);
     hipLaunchKernelGGL(nxg_gen_emit_kernel, dim3(g), dim3(TPB), 0, s, wire, W, nt, lws, base, cd,
-                       st);
+                       st, fix);
+    hipLaunchKernelGGL(nxg_gen_fix_kernel, dim3(g), dim3(TPB), 0, s, wire, W, lws, cd, st, fix);
     return hipGetLastError();
 }
 

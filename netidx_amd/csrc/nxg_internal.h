@@ -23,7 +23,7 @@ struct DevStatus {
     uint64_t pad1;
     // diagnostics (general decode): 0 redo tiles, 1 look-back fallbacks, 2 repair rounds,
     // 3 lane walks, 4 speculation attempts, 5 tiles without a speculated entry,
-    // 6 exhausted (budgeted) walks, 7 unused
+    // 6 exhausted (budgeted) walks, 7 work-list entries of the emit pass
     unsigned long long diag[8];
 };
 static_assert(sizeof(DevStatus) == 160, "DevStatus layout");
@@ -109,9 +109,11 @@ hipError_t nxg_launch_enc_f64(const uint64_t* id, const uint64_t* val, uint64_t 
 hipError_t nxg_launch_enc_general(const ColsDesc& cols, const uint8_t* heap, uint8_t* out,
                                   uint64_t cap, uint64_t* scratch, uint64_t* tstat,
                                   uint32_t epoch, DevStatus* st, int grid, hipStream_t s);
-// general decode: count + resolve + emit. `lws` holds 64 u32 per tile (nxg_dec_gen_tiles),
-// `runs` gdec2::MAX_RUNS * RUN_WORDS u64, `base` gdec2::MAX_RUNS * 4 u64; none needs zeroing.
+// general decode: count + resolve + emit + fix. `lws` holds nxg_dec_gen_scratch_bytes(W) bytes
+// (64 u32 lane words per tile, then the emit pass's work list), `runs` gdec2::MAX_RUNS *
+// RUN_WORDS u64, `base` gdec2::MAX_RUNS * 4 u64; none needs zeroing.
 uint64_t nxg_dec_gen_tiles(uint64_t W);
+uint64_t nxg_dec_gen_scratch_bytes(uint64_t W);
 hipError_t nxg_launch_dec_gen(const uint8_t* wire, uint64_t W, const ColsDesc& cols, uint32_t* lws,
                               uint64_t* runs, uint64_t* base, int wgs, DevStatus* st,
                               hipStream_t s);

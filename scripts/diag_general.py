@@ -13,7 +13,7 @@ import netidx_amd
 from netidx_amd import synth
 from netidx_amd.codec import Columns, lib
 
-NAMES = ["run_fixes", "rep_exhausted", "repair_rounds", "rep_wrong_guess", "spec_tries", "rep_missed", "rep_spurious", "-"]
+NAMES = ["run_fixes", "rep_exhausted", "repair_rounds", "rep_wrong_guess", "spec_tries", "rep_missed", "rep_spurious", "fix_entries"]
 
 
 def diag(codec):
