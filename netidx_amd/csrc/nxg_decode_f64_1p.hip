@@ -10,19 +10,22 @@
 // Pipeline (one launch)
 // ---------------------
 // Block 0 is a scanner; every other wave is a worker. Worker v of V handles tiles v, v+V, ...
-// (tiles start 4032 bytes apart; lane 63's merge point is the next tile's first). Step k:
-//   1. stage tile t_k in LDS slot k mod 3 (its bytes were loaded during step k-1) and issue
-//      the loads of t_{k+1};
-//   2. merge points, a counting walk, a wave scan, then a decoding walk into registers (at most
-//      6 records per lane); the decoded records (32-bit id: ids of f64 records are < 2^28;
-//      64-bit value) then replace the tile's image in its LDS slot, in record order; publish
+// (tiles start 4032 bytes apart; lane 63's merge point is the next tile's first). Step k, with
+// LAG = 1 (NXG_1P_LAG) and LAG + 1 LDS slots per wave:
+//   1. stage tile t_k in LDS slot k mod (LAG+1) (its bytes were loaded during step k-1) and
+//      issue the loads of t_{k+1};
+//   2. merge points; each lane's chain of record starts, one length byte per step; then the
+//      lane's records (at most 6) are loaded together and checked and decoded without branches
+//      (32-bit id: ids of f64 records are < 2^28; 64-bit value); a wave scan numbers them; the
+//      decoded records then replace the tile's image in its LDS slot, in record order; publish
 //      the tile's count (agg[t_k]);
-//   3. wait for t_{k-2}'s first record index (pre[t_{k-2}], published by the scanner meanwhile)
-//      and copy its slot to the id / value columns with coalesced stores.
+//   3. wait for t_{k-LAG}'s first record index (pre[t_{k-LAG}], published by the scanner
+//      meanwhile) and copy its slot to the id / value columns with coalesced stores.
 // The scanner turns agg[] into pre[] in tile order. Each step waits on the prefix of the tile
-// from two steps before, so a slow wave elsewhere does not stall the others at once; every spin
-// is bounded (watchdog) and gives up once fast_fail is raised. Three 4.2 KiB slots per wave
-// (image and decoded records share a slot): three 4-wave workgroups per CU.
+// from LAG steps before, so a slow wave elsewhere does not stall the others at once (and the
+// waves stay on a compact address window, which HBM rewards); every spin is bounded (watchdog)
+// and gives up once fast_fail is raised. Two 4.2 KiB slots per wave (image and decoded records
+// share a slot): four 4-wave workgroups per CU.
 #include "nxg_f64_rec.h"
 
 #ifdef NXG_1P_PROBE  // scripts/probe_f64.hip only: phase cycle counters and ablation flags
