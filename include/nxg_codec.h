@@ -158,6 +158,47 @@ bool nxg_encode_updates(NxgCtx* ctx, const NxgColumns* in, const uint8_t* heap, 
 bool nxg_encode_updates_async(NxgCtx* ctx, const NxgColumns* din, const uint8_t* dheap,
                               uint8_t* dout, uint64_t cap, uint64_t* len_out, NetidxError* err);
 
+/* ---- dispatch: replaces ConnectionCtx::process_updates_batch (connection.rs:546-567) ------
+ * The decoded Update rows fanned out to the subscriber's channels. For each row, in batch
+ * order: the subscription of its Id, found by a dense table (publisher Ids come from a counter
+ * starting at 0, netidx-core/src/utils.rs:130-134); an Id with no subscription, or >= n_ids, is
+ * dropped, as `self.subscriptions.get(&i)` returning None. For each stream of the
+ * subscription, in stream order, the entry (SubId, row) is appended to that stream's channel
+ * batch (by_chan, connection.rs:551-557), so every channel sees its updates in batch order. A
+ * subscription that keeps `last` records its last row in the batch (connection.rs:559-561).
+ *
+ * The table is a CSR built by the host from its subscriptions map; every array is device
+ * memory: */
+#define NXG_NO_SLOT 0xffffffffu
+typedef struct NxgSubTable {
+    uint64_t n_ids;                   /* slot_of_id covers Ids [0, n_ids) */
+    const uint32_t* slot_of_id;       /* [n_ids]: subscription slot, or NXG_NO_SLOT */
+    uint64_t n_slots;                 /* subscriptions */
+    const uint64_t* slot_sub_id;      /* [n_slots]: SubId (subscriber/mod.rs:85) */
+    const uint32_t* slot_stream_off;  /* [n_slots + 1]: the slot's streams, CSR */
+    const uint32_t* stream_chan;      /* [n_streams]: channel of each stream, < n_chans */
+    const uint8_t* slot_has_last;     /* [n_slots]: 1 if the subscription keeps `last` */
+    uint32_t n_chans;                 /* channels (ChanId) */
+} NxgSubTable;
+/* Output (device memory, capacities from the caller):
+ *   chan_off[n_chans + 1]  channel c's batch is entries [chan_off[c], chan_off[c+1])
+ *   ent_sub[cap], ent_row[cap]  (SubId, index of the update's row in the decoded columns)
+ *   last_row[n_slots]      1 + the last row of the slot's subscription in this batch, 0 if none
+ *                          (or if the slot keeps no `last`) */
+typedef struct NxgDispatch {
+    uint64_t cap_entries;
+    uint64_t* chan_off;
+    uint64_t* ent_sub;
+    uint64_t* ent_row;
+    uint64_t* last_row;
+    uint64_t n_entries;   /* written by the call */
+    uint64_t n_unmatched; /* rows whose Id has no subscription */
+} NxgDispatch;
+/* `id` = the decoded id column (device), n_rows rows. Synchronous. Returns false on API misuse,
+ * a HIP failure, or entries > cap_entries (n_entries then holds the required capacity). */
+bool nxg_dispatch_updates(NxgCtx* ctx, const NxgSubTable* tab, const uint64_t* id,
+                          uint64_t n_rows, NxgDispatch* out, NetidxError* err);
+
 /* ---- host framing (netidx/src/channel.rs) ------------------------------------------------
  * Frame boundaries exactly as WriteChannel::queue_send/try_flush split the buffer. The split
  * happens at MAX_BATCH = 0x3FFFFFFF (channel.rs:34, 187-191) and is recorded between messages.

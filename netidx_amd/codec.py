@@ -63,6 +63,19 @@ class NxgColumns(C.Structure):
     ]
 
 
+class NxgSubTable(C.Structure):
+    _fields_ = [("n_ids", C.c_uint64), ("slot_of_id", C.c_void_p), ("n_slots", C.c_uint64),
+                ("slot_sub_id", C.c_void_p), ("slot_stream_off", C.c_void_p),
+                ("stream_chan", C.c_void_p), ("slot_has_last", C.c_void_p),
+                ("n_chans", C.c_uint32)]
+
+
+class NxgDispatch(C.Structure):
+    _fields_ = [("cap_entries", C.c_uint64), ("chan_off", C.c_void_p), ("ent_sub", C.c_void_p),
+                ("ent_row", C.c_void_p), ("last_row", C.c_void_p), ("n_entries", C.c_uint64),
+                ("n_unmatched", C.c_uint64)]
+
+
 class NxgStatus(C.Structure):
     _fields_ = [
         ("n_rows", C.c_uint64), ("n_children", C.c_uint64), ("n_ctl", C.c_uint64),
@@ -95,6 +108,8 @@ SIGNATURES = {
     "nxg_encode_updates_async": (C.c_bool, [C.c_void_p, C.POINTER(NxgColumns), C.c_void_p,
                                             C.c_void_p, C.c_uint64, C.POINTER(C.c_uint64),
                                             C.POINTER(NetidxError)]),
+    "nxg_dispatch_updates": (C.c_bool, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64,
+                                        C.c_void_p, C.POINTER(NetidxError)]),
     "nxg_frame_split": (C.c_int64, [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64]),
     "nxg_frame_header": (None, [C.c_uint32, C.c_bool, C.c_void_p]),
     "nxg_frame_parse_header": (C.c_uint32, [C.c_void_p, C.c_uint64, C.POINTER(C.c_uint32),
@@ -265,6 +280,29 @@ class Codec:
             raise PackError(st.err_kind, st.err_offset)
         return st
 
+    def dispatch_updates(self, table, ids, n_rows=None, cap=None):
+        """process_updates_batch (connection.rs:546-567) for decoded rows: `ids` is the device id
+        column (int64/uint64 tensor). Returns a Dispatch."""
+        import torch
+        n = ids.numel() if n_rows is None else int(n_rows)
+        dev = ids.device
+        streams = table.stream_chan.numel()
+        if cap is None:  # each row reaches at most the largest fan-out of any subscription
+            offs = table.slot_stream_off.cpu().numpy().view(np.uint32).astype(np.int64)
+            cap = n * int((offs[1:] - offs[:-1]).max()) if streams else 0
+        chan_off = torch.zeros(table.n_chans + 1, dtype=torch.int64, device=dev)
+        ent_sub = torch.empty(max(cap, 1), dtype=torch.int64, device=dev)
+        ent_row = torch.empty(max(cap, 1), dtype=torch.int64, device=dev)
+        last_row = torch.empty(max(table.slot_sub_id.numel(), 1), dtype=torch.int64, device=dev)
+        tb = table.c_struct()
+        out = NxgDispatch(cap, chan_off.data_ptr(), ent_sub.data_ptr(), ent_row.data_ptr(),
+                          last_row.data_ptr(), 0, 0)
+        err = NetidxError()
+        _check(lib().nxg_dispatch_updates(self.ctx, C.byref(tb), C.c_void_p(ids.data_ptr()), n,
+                                          C.byref(out), C.byref(err)), err)
+        return Dispatch(chan_off, ent_sub, ent_row, last_row[: table.slot_sub_id.numel()],
+                        out.n_entries, out.n_unmatched)
+
     def encoded_len(self, cols, heap=None):
         n, err = C.c_uint64(0), NetidxError()
         _check(lib().nxg_encoded_len(self.ctx, C.byref(cols.s), _heap_ptr(heap), C.byref(n),
@@ -294,6 +332,73 @@ class Codec:
                                               C.c_void_p(out_ptr), cap, C.byref(n),
                                               C.byref(err)), err)
         return n
+
+
+NO_SLOT = 0xFFFFFFFF
+
+
+class SubTable:
+    """Device-resident Id -> subscription table: ConnectionCtx.subscriptions and each Sub's
+    sub_id / streams / last (netidx/src/subscriber/connection.rs:54-60), as the CSR arrays of
+    include/nxg_codec.h's NxgSubTable. Publisher Ids are dense (netidx-core/src/utils.rs:130-134),
+    so the map is a table indexed by Id."""
+
+    def __init__(self, slot_of_id, slot_sub_id, slot_stream_off, stream_chan, slot_has_last,
+                 n_chans, device="cuda"):
+        import torch
+
+        def t(a, dt):
+            return torch.as_tensor(np.ascontiguousarray(a, dtype=dt)).to(device)
+
+        self.slot_of_id = t(slot_of_id, np.uint32).view(torch.int32)
+        self.slot_sub_id = t(slot_sub_id, np.uint64).view(torch.int64)
+        self.slot_stream_off = t(slot_stream_off, np.uint32).view(torch.int32)
+        self.stream_chan = t(stream_chan, np.uint32).view(torch.int32)
+        self.slot_has_last = t(slot_has_last, np.uint8)
+        self.n_chans = int(n_chans)
+        assert self.slot_stream_off.numel() == self.slot_sub_id.numel() + 1
+        assert self.slot_has_last.numel() == self.slot_sub_id.numel()
+
+    @classmethod
+    def from_subscriptions(cls, subs, n_chans, n_ids=None, device="cuda"):
+        """subs: {id: (sub_id, [chan, ...], keeps_last)} -- one subscription per Id, its streams
+        in registration order (handle_connect_stream, connection.rs:320-359)."""
+        n_ids = (max(subs) + 1 if subs else 0) if n_ids is None else n_ids
+        slot_of_id = np.full(n_ids, NO_SLOT, np.uint32)
+        sub_ids, offs, chans, last = [], [0], [], []
+        for slot, (i, (sid, streams, keep)) in enumerate(sorted(subs.items())):
+            if i < n_ids:
+                slot_of_id[i] = slot
+            sub_ids.append(sid)
+            chans.extend(streams)
+            offs.append(len(chans))
+            last.append(1 if keep else 0)
+        return cls(slot_of_id, np.array(sub_ids, np.uint64), np.array(offs, np.uint32),
+                   np.array(chans, np.uint32), np.array(last, np.uint8), n_chans, device)
+
+    def c_struct(self):
+        return NxgSubTable(self.slot_of_id.numel(), self.slot_of_id.data_ptr(),
+                           self.slot_sub_id.numel(), self.slot_sub_id.data_ptr(),
+                           self.slot_stream_off.data_ptr(), self.stream_chan.data_ptr(),
+                           self.slot_has_last.data_ptr(), self.n_chans)
+
+
+class Dispatch:
+    """Per-channel update batches (by_chan, connection.rs:62-65): channel c's batch is
+    (ent_sub, ent_row)[chan_off[c]:chan_off[c+1]], in batch order; last_row[slot] = 1 + the last
+    row of the slot's subscription (0: none)."""
+
+    def __init__(self, chan_off, ent_sub, ent_row, last_row, n_entries, n_unmatched):
+        self.chan_off, self.ent_sub, self.ent_row, self.last_row = chan_off, ent_sub, ent_row, last_row
+        self.n_entries, self.n_unmatched = n_entries, n_unmatched
+
+    def batches(self):
+        """{chan: [(sub_id, row), ...]} on the host (non-empty channels only)."""
+        off = self.chan_off.cpu().numpy().view(np.uint64)
+        sub = self.ent_sub[: self.n_entries].cpu().numpy().view(np.uint64)
+        row = self.ent_row[: self.n_entries].cpu().numpy().view(np.uint64)
+        return {c: list(zip(sub[off[c]:off[c + 1]].tolist(), row[off[c]:off[c + 1]].tolist()))
+                for c in range(len(off) - 1) if off[c + 1] > off[c]}
 
 
 def _heap_ptr(heap):

@@ -65,6 +65,8 @@ struct NxgCtx {
     uint32_t* glws = nullptr;      // general decode: lane words, 256 B per tile
     size_t glws_cap = 0;
     uint64_t* gruns = nullptr;     // general decode: run summaries + bases
+    uint8_t* dscratch = nullptr;   // dispatch: counters, offsets, block sums, unmatched count
+    size_t dscratch_cap = 0;
     int wgs_dec_gen = 0;
     int wgs_dec_f64_1p = 0;
     bool f64_2pass = false;  // NXG_F64_2PASS=1: the two-pass count/emit f64 decoder
@@ -538,6 +540,7 @@ void nxg_ctx_destroy(NxgCtx* c) {
     if (c->fmoff) (void)hipFree(c->fmoff);
     if (c->glws) (void)hipFree(c->glws);
     if (c->gruns) (void)hipFree(c->gruns);
+    if (c->dscratch) (void)hipFree(c->dscratch);
     if (c->dframe) (void)hipFree(c->dframe);
     if (c->escratch) (void)hipFree(c->escratch);
     if (c->dheap) (void)hipFree(c->dheap);
@@ -784,6 +787,52 @@ static bool encode_impl(NxgCtx* c, const NxgColumns* in, const uint8_t* heap, ui
         HIPCHK(hipStreamSynchronize(c->stream));
     }
     if (len_out) *len_out = total;
+    return true;
+}
+
+// ---- dispatch (connection.rs:546-567) --------------------------------------------------------
+bool nxg_dispatch_updates(NxgCtx* c, const NxgSubTable* tab, const uint64_t* id, uint64_t n_rows,
+                          NxgDispatch* out, NetidxError* err) {
+    if (!c || !tab || !out || (n_rows && !id) || !out->chan_off) {
+        set_err(err, "null argument");
+        return false;
+    }
+    if ((tab->n_ids && !tab->slot_of_id) ||
+        (tab->n_slots && (!tab->slot_sub_id || !tab->slot_stream_off || !tab->slot_has_last ||
+                          !out->last_row)) ||
+        (out->cap_entries && (!out->ent_sub || !out->ent_row))) {
+        set_err(err, "null table or output array");
+        return false;
+    }
+    if (n_rows && tab->n_slots && !tab->stream_chan && tab->n_chans) {
+        set_err(err, "null stream_chan");
+        return false;
+    }
+    HIPCHK(hipSetDevice(c->device));
+    const size_t need = 64 + nxg_disp_scratch_bytes(n_rows, tab->n_chans);
+    if (need > c->dscratch_cap) {
+        HIPCHK(hipStreamSynchronize(c->stream));
+        if (c->dscratch) HIPCHK(hipFree(c->dscratch));
+        c->dscratch = nullptr;
+        const size_t n = std::max(need, c->dscratch_cap * 2);
+        HIPCHK(hipMalloc(&c->dscratch, n));
+        c->dscratch_cap = n;
+    }
+    uint64_t* um = reinterpret_cast<uint64_t*>(c->dscratch);
+    HIPCHK(nxg_launch_dispatch(*tab, id, n_rows, c->dscratch + 64, out->chan_off, out->ent_sub,
+                               out->ent_row, out->cap_entries, out->last_row, um, c->ncu,
+                               c->stream));
+    uint64_t res[2] = {0, 0};
+    HIPCHK(hipMemcpyAsync(&res[0], out->chan_off + tab->n_chans, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(&res[1], um, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    out->n_entries = res[0];
+    out->n_unmatched = res[1];
+    if (res[0] > out->cap_entries) {
+        set_err(err, "dispatch needs %llu entries, capacity is %llu", (unsigned long long)res[0],
+                (unsigned long long)out->cap_entries);
+        return false;
+    }
     return true;
 }
 

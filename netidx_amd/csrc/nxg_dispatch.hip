@@ -1,0 +1,292 @@
+// nxg_dispatch.hip -- subscriber update dispatch for gfx950: the decoded Update rows fanned out
+// to the subscriber's channels. Replaces ConnectionCtx::process_updates_batch
+// (netidx/src/subscriber/connection.rs:546-567): per update, in batch order, the Id -> Sub lookup
+// (a dense table here: publisher Ids count up from 0, netidx-core/src/utils.rs:130-134), one
+// (SubId, update) entry per stream of the subscription appended to that stream's channel batch
+// (by_chan, connection.rs:551-557), and the subscription's `last` (connection.rs:559-561).
+//
+// Output is grouped by channel, each channel's batch in batch order (CSR, chan_off). Three
+// launches, deterministic (no atomics decide an order):
+//   count    one wave per segment of SEG rows (64 rows per step). Per step the wave visits the
+//            distinct channels its 64 rows reach in increasing channel order ("match" loop:
+//            wave minimum of each lane's next channel); per channel, the rows' entry counts are
+//            added to the segment's counter. Counters end in hist[chan * n_seg + seg]
+//            (channel-major). Also: last_row (atomicMax of row + 1), unmatched rows.
+//   scan     exclusive scan of hist in that order: the first entry of every (channel, segment)
+//            pair; chan_off[c] is the (c, 0) value.
+//   scatter  the count pass again; a lane's position within a step is the wave's running count
+//            for the channel plus an inclusive scan over lanes, so each channel's entries come
+//            out in row order.
+// Counters live in LDS when there are at most LCH channels, in global memory otherwise.
+#include "nxg_device.h"
+#include "nxg_internal.h"
+
+namespace {
+
+constexpr int TPB = 256;
+constexpr int WAVES = TPB / 64;
+constexpr uint32_t LCH = 1024;        // channels with LDS counters (u64 per channel per wave)
+constexpr uint32_t NONE = 0xffffffffu;
+constexpr int SCAN_K = 16;            // scan: elements per thread
+constexpr uint32_t SCAN_B = TPB * SCAN_K;
+
+struct Row {
+    uint32_t k0, k1;  // the row's streams [k0, k1) in stream_chan (empty: no subscription)
+    uint32_t slot;
+};
+
+NXG_DEV Row row_of(const NxgSubTable& tb, const uint64_t* __restrict__ id, uint64_t i, uint64_t n) {
+    Row r{0, 0, NONE};
+    if (i < n) {
+        const uint64_t x = id[i];
+        const uint32_t s = x < tb.n_ids ? tb.slot_of_id[x] : NONE;
+        if (s != NONE) {
+            r.slot = s;
+            r.k0 = tb.slot_stream_off[s];
+            r.k1 = tb.slot_stream_off[s + 1];
+        }
+    }
+    return r;
+}
+
+// the smallest channel above `prev` among the row's streams (NONE: none), and how many of the
+// row's streams name channel `d`
+NXG_DEV uint32_t next_chan(const NxgSubTable& tb, const Row& r, uint32_t prev, bool first) {
+    uint32_t m = NONE;
+    for (uint32_t k = r.k0; k < r.k1; k++) {
+        const uint32_t c = tb.stream_chan[k];
+        if ((first || c > prev) && c < m && c < tb.n_chans) m = c;  // others: ignored
+    }
+    return m;
+}
+NXG_DEV uint32_t count_chan(const NxgSubTable& tb, const Row& r, uint32_t d) {
+    uint32_t n = 0;
+    for (uint32_t k = r.k0; k < r.k1; k++) n += tb.stream_chan[k] == d;
+    return n;
+}
+
+NXG_DEV uint32_t wave_min(uint32_t v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        const uint32_t o = __shfl_xor(v, d, 64);
+        v = o < v ? o : v;
+    }
+    return v;
+}
+
+}  // namespace
+
+// ---- pass 1: per (channel, segment) entry counts ---------------------------------------------
+__global__ __launch_bounds__(TPB) void nxg_disp_count_kernel(
+    NxgSubTable tb, const uint64_t* __restrict__ id, uint64_t n, uint64_t seg_rows, uint64_t n_seg,
+    uint32_t* __restrict__ hist, uint64_t* __restrict__ last_row, uint64_t* __restrict__ unmatched) {
+    __shared__ uint32_t cnt_lds[WAVES][LCH];
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const bool lds = tb.n_chans <= LCH;
+    uint32_t* cnt = cnt_lds[w];
+    uint64_t um = 0;
+#pragma unroll 1
+    for (uint64_t seg = (uint64_t)blockIdx.x * WAVES + w; seg < n_seg;
+         seg += (uint64_t)gridDim.x * WAVES) {
+        if (lds) {
+            for (uint32_t c = lane; c < tb.n_chans; c += 64) cnt[c] = 0;
+            wave_lds_order();
+        }
+        const uint64_t r0 = seg * seg_rows, r1 = r0 + seg_rows < n ? r0 + seg_rows : n;
+#pragma unroll 1
+        for (uint64_t b = r0; b < r1; b += 64) {
+            const uint64_t i = b + lane;
+            const Row r = row_of(tb, id, i, r1);
+            um += (i < r1 && r.slot == NONE);
+            if (r.slot != NONE && tb.slot_has_last[r.slot])
+                atomicMax((unsigned long long*)&last_row[r.slot], (unsigned long long)(i + 1));
+            uint32_t prev = 0;
+            bool first = true;
+#pragma unroll 1
+            for (;;) {
+                const uint32_t d = wave_min(next_chan(tb, r, prev, first));
+                if (d == NONE) break;
+                const uint32_t tot = wave_sum<uint32_t>(count_chan(tb, r, d));
+                if (lane == 0) {
+                    if (lds) cnt[d] += tot;
+                    else atomicAdd(&hist[(uint64_t)d * n_seg + seg], tot);
+                }
+                prev = d;
+                first = false;
+            }
+        }
+        if (lds) {
+            wave_lds_order();
+            for (uint32_t c = lane; c < tb.n_chans; c += 64) hist[(uint64_t)c * n_seg + seg] = cnt[c];
+            wave_lds_order();
+        }
+    }
+    um = wave_sum<uint64_t>(um);
+    if (lane == 0 && um) atomicAdd((unsigned long long*)unmatched, (unsigned long long)um);
+}
+
+// ---- pass 2: exclusive scan of hist (M values) into off (u64), block totals in bsum ----------
+__global__ __launch_bounds__(TPB) void nxg_disp_scan_block_kernel(
+    const uint32_t* __restrict__ hist, uint64_t M, uint64_t* __restrict__ off,
+    uint64_t* __restrict__ bsum) {
+    __shared__ uint64_t tmp[WAVES];
+    const uint64_t base = (uint64_t)blockIdx.x * SCAN_B + (uint64_t)threadIdx.x * SCAN_K;
+    uint64_t v[SCAN_K], local = 0;
+#pragma unroll
+    for (int k = 0; k < SCAN_K; k++) {
+        v[k] = base + k < M ? hist[base + k] : 0u;
+        local += v[k];
+    }
+    uint64_t total;
+    uint64_t p = block_excl_scan<uint64_t, TPB>(local, tmp, &total);
+#pragma unroll
+    for (int k = 0; k < SCAN_K; k++) {
+        if (base + k < M) off[base + k] = p;
+        p += v[k];
+    }
+    if (threadIdx.x == 0) bsum[blockIdx.x] = total;
+}
+
+// one workgroup: exclusive scan of the block totals (nb values), grand total in bsum[nb]
+__global__ __launch_bounds__(1024) void nxg_disp_scan_top_kernel(uint64_t* __restrict__ bsum,
+                                                                 uint64_t nb) {
+    __shared__ uint64_t tmp[16];
+    __shared__ uint64_t carry;
+    if (threadIdx.x == 0) carry = 0;
+    __syncthreads();
+#pragma unroll 1
+    for (uint64_t b0 = 0; b0 < nb; b0 += 1024) {
+        const uint64_t i = b0 + threadIdx.x;
+        const uint64_t v = i < nb ? bsum[i] : 0;
+        uint64_t total;
+        const uint64_t p = block_excl_scan<uint64_t, 1024>(v, tmp, &total);
+        const uint64_t c = carry;
+        if (i < nb) bsum[i] = c + p;
+        __syncthreads();
+        if (threadIdx.x == 0) carry = c + total;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) bsum[nb] = carry;
+}
+
+__global__ __launch_bounds__(TPB) void nxg_disp_scan_add_kernel(
+    uint64_t* __restrict__ off, uint64_t M, const uint64_t* __restrict__ bsum, uint64_t nb,
+    uint64_t n_seg, uint32_t n_chans, uint64_t* __restrict__ chan_off) {
+    const uint64_t i = (uint64_t)blockIdx.x * TPB + threadIdx.x;
+    if (i < M) {
+        const uint64_t x = off[i] + bsum[i / SCAN_B];
+        off[i] = x;
+        if (i % n_seg == 0) chan_off[i / n_seg] = x;
+    }
+    if (i == 0) chan_off[n_chans] = bsum[nb];
+}
+
+// ---- pass 3: entries --------------------------------------------------------------------------
+__global__ __launch_bounds__(TPB) void nxg_disp_scatter_kernel(
+    NxgSubTable tb, const uint64_t* __restrict__ id, uint64_t n, uint64_t seg_rows, uint64_t n_seg,
+    uint64_t* __restrict__ off, uint64_t* __restrict__ ent_sub, uint64_t* __restrict__ ent_row,
+    uint64_t cap) {
+    __shared__ uint64_t cur_lds[WAVES][LCH];
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const bool lds = tb.n_chans <= LCH;
+    uint64_t* cur = cur_lds[w];
+#pragma unroll 1
+    for (uint64_t seg = (uint64_t)blockIdx.x * WAVES + w; seg < n_seg;
+         seg += (uint64_t)gridDim.x * WAVES) {
+        if (lds) {
+            for (uint32_t c = lane; c < tb.n_chans; c += 64) cur[c] = off[(uint64_t)c * n_seg + seg];
+            wave_lds_order();
+        }
+        const uint64_t r0 = seg * seg_rows, r1 = r0 + seg_rows < n ? r0 + seg_rows : n;
+#pragma unroll 1
+        for (uint64_t b = r0; b < r1; b += 64) {
+            const uint64_t i = b + lane;
+            const Row r = row_of(tb, id, i, r1);
+            const uint64_t sub = r.slot != NONE ? tb.slot_sub_id[r.slot] : 0;
+            uint32_t prev = 0;
+            bool first = true;
+#pragma unroll 1
+            for (;;) {
+                const uint32_t d = wave_min(next_chan(tb, r, prev, first));
+                if (d == NONE) break;
+                const uint32_t c = count_chan(tb, r, d);
+                const uint32_t inc = wave_incl_scan(c);
+                // the wave owns this (channel, segment) cursor; in global memory it is read and
+                // written past the L1 (the same wave reads its own store back next)
+                uint64_t* gcur = &off[(uint64_t)d * n_seg + seg];
+                const uint64_t base = lds ? cur[d] : ld_agent(gcur);
+                for (uint32_t j = 0; j < c; j++) {
+                    const uint64_t e = base + inc - c + j;
+                    if (e < cap) {
+                        ent_sub[e] = sub;
+                        ent_row[e] = i;
+                    }
+                }
+                const uint64_t nb = base + __shfl(inc, 63, 64);
+                wave_lds_order();
+                if (lane == 0) {
+                    if (lds) cur[d] = nb;
+                    else {
+                        st_agent(gcur, nb);
+                        drain_stores();
+                    }
+                }
+                wave_lds_order();
+                prev = d;
+                first = false;
+            }
+        }
+    }
+}
+
+// ---- launch -------------------------------------------------------------------------------------
+namespace {
+constexpr uint64_t MAX_M = 1ull << 26;  // (channel, segment) counters
+}
+
+uint64_t nxg_disp_seg_rows(uint64_t n, uint32_t n_chans) {
+    uint64_t seg = 1024;
+    const uint64_t ch = n_chans ? n_chans : 1;
+    while (((n + seg - 1) / seg) * ch > MAX_M) seg *= 2;
+    return seg;
+}
+
+uint64_t nxg_disp_scratch_bytes(uint64_t n, uint32_t n_chans) {
+    const uint64_t seg = nxg_disp_seg_rows(n, n_chans);
+    const uint64_t M = ((n + seg - 1) / seg) * (uint64_t)n_chans;
+    const uint64_t nb = (M + SCAN_B - 1) / SCAN_B;
+    return M * 4 + M * 8 + (nb + 1) * 8 + 64;
+}
+
+hipError_t nxg_launch_dispatch(const NxgSubTable& tb, const uint64_t* id, uint64_t n,
+                               uint8_t* scratch, uint64_t* chan_off, uint64_t* ent_sub,
+                               uint64_t* ent_row, uint64_t cap, uint64_t* last_row,
+                               uint64_t* unmatched, int ncu, hipStream_t s) {
+    const uint64_t seg = nxg_disp_seg_rows(n, tb.n_chans);
+    const uint64_t n_seg = (n + seg - 1) / seg;
+    const uint64_t M = n_seg * (uint64_t)tb.n_chans;
+    const uint64_t nb = (M + SCAN_B - 1) / SCAN_B;
+    uint32_t* hist = reinterpret_cast<uint32_t*>(scratch);
+    uint64_t* off = reinterpret_cast<uint64_t*>(scratch + ((M * 4 + 7) & ~7ull));
+    uint64_t* bsum = off + M;
+    hipError_t e;
+    if ((e = hipMemsetAsync(unmatched, 0, 8, s)) != hipSuccess) return e;
+    if (tb.n_slots && (e = hipMemsetAsync(last_row, 0, tb.n_slots * 8, s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(chan_off, 0, ((uint64_t)tb.n_chans + 1) * 8, s)) != hipSuccess) return e;
+    if (n == 0) return hipSuccess;
+    if (tb.n_chans > LCH && (e = hipMemsetAsync(hist, 0, M * 4, s)) != hipSuccess) return e;
+    const uint64_t want = (n_seg + WAVES - 1) / WAVES;
+    const uint32_t g = (uint32_t)(want < (uint64_t)ncu * 8 ? want : (uint64_t)ncu * 8);
+    hipLaunchKernelGGL(nxg_disp_count_kernel, dim3(g), dim3(TPB), 0, s, tb, id, n, seg, n_seg, hist,
+                       last_row, unmatched);
+    if (M) {
+        hipLaunchKernelGGL(nxg_disp_scan_block_kernel, dim3((uint32_t)nb), dim3(TPB), 0, s, hist, M,
+                           off, bsum);
+        hipLaunchKernelGGL(nxg_disp_scan_top_kernel, dim3(1), dim3(1024), 0, s, bsum, nb);
+        hipLaunchKernelGGL(nxg_disp_scan_add_kernel, dim3((uint32_t)((M + TPB - 1) / TPB)),
+                           dim3(TPB), 0, s, off, M, bsum, nb, n_seg, tb.n_chans, chan_off);
+        hipLaunchKernelGGL(nxg_disp_scatter_kernel, dim3(g), dim3(TPB), 0, s, tb, id, n, seg, n_seg,
+                           off, ent_sub, ent_row, cap);
+    }
+    return hipGetLastError();
+}

@@ -118,6 +118,13 @@ hipError_t nxg_launch_dec_gen(const uint8_t* wire, uint64_t W, const ColsDesc& c
                               uint64_t* runs, uint64_t* base, int wgs, DevStatus* st,
                               hipStream_t s);
 int nxg_dec_gen_wgs(int ncu);
+// subscriber dispatch (nxg_dispatch.hip): `scratch` holds nxg_disp_scratch_bytes(n, n_chans)
+// bytes (no initialisation needed); `unmatched` one u64.
+uint64_t nxg_disp_scratch_bytes(uint64_t n, uint32_t n_chans);
+hipError_t nxg_launch_dispatch(const NxgSubTable& tb, const uint64_t* id, uint64_t n,
+                               uint8_t* scratch, uint64_t* chan_off, uint64_t* ent_sub,
+                               uint64_t* ent_row, uint64_t cap, uint64_t* last_row,
+                               uint64_t* unmatched, int ncu, hipStream_t s);
 int nxg_occupancy_enc_f64();
 int nxg_occupancy_enc_general();
 

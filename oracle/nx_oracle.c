@@ -11,6 +11,7 @@
  */
 #include "nx_oracle.h"
 #include <string.h>
+#include <stdlib.h>
 
 #define MAX_VEC ((uint64_t)2 * 1024 * 1024 * 1024) /* pack.rs:917 */
 
@@ -592,5 +593,47 @@ int64_t nxo_encode_f64(const uint64_t* id, const uint64_t* val, uint64_t n, uint
         putbe(&o, val[i], 8);
         total += L;
     }
+    return (int64_t)total;
+}
+
+/* ---- subscriber update dispatch (connection.rs:546-567) ------------------------------------ */
+int64_t nxo_dispatch(const uint64_t* id, uint64_t n_rows, uint64_t n_ids,
+                     const uint32_t* slot_of_id, uint64_t n_slots, const uint64_t* slot_sub_id,
+                     const uint32_t* slot_stream_off, const uint32_t* stream_chan,
+                     const uint8_t* slot_has_last, uint32_t n_chans, uint64_t* chan_off,
+                     uint64_t* ent_sub, uint64_t* ent_row, uint64_t cap, uint64_t* last_row,
+                     uint64_t* n_unmatched) {
+    /* pass 1: per-channel batch lengths (the by_chan vectors' final sizes) */
+    for (uint32_t c = 0; c <= n_chans; c++) chan_off[c] = 0;
+    for (uint64_t s = 0; s < n_slots; s++) last_row[s] = 0;
+    uint64_t unmatched = 0;
+    for (uint64_t i = 0; i < n_rows; i++) {
+        const uint32_t s = id[i] < n_ids ? slot_of_id[id[i]] : NXO_NO_SLOT;
+        if (s == NXO_NO_SLOT) { /* self.subscriptions.get(&i) == None */
+            unmatched++;
+            continue;
+        }
+        for (uint32_t k = slot_stream_off[s]; k < slot_stream_off[s + 1]; k++)
+            chan_off[stream_chan[k] + 1]++;
+    }
+    for (uint32_t c = 0; c < n_chans; c++) chan_off[c + 1] += chan_off[c];
+    const uint64_t total = chan_off[n_chans];
+    if (n_unmatched) *n_unmatched = unmatched;
+    if (total > cap) return -NXO_CAPACITY;
+    /* pass 2: the pushes, in batch order, each channel's batch in push order */
+    uint64_t* cur = (uint64_t*)malloc((n_chans ? n_chans : 1) * sizeof(uint64_t));
+    if (!cur) return -NXO_CAPACITY;
+    for (uint32_t c = 0; c < n_chans; c++) cur[c] = chan_off[c];
+    for (uint64_t i = 0; i < n_rows; i++) {
+        const uint32_t s = id[i] < n_ids ? slot_of_id[id[i]] : NXO_NO_SLOT;
+        if (s == NXO_NO_SLOT) continue;
+        for (uint32_t k = slot_stream_off[s]; k < slot_stream_off[s + 1]; k++) {
+            const uint64_t e = cur[stream_chan[k]]++;
+            ent_sub[e] = slot_sub_id[s]; /* (sub.sub_id, Event::Update(m.clone())) */
+            ent_row[e] = i;
+        }
+        if (slot_has_last[s]) last_row[s] = i + 1; /* *last.lock() = Event::Update(m) */
+    }
+    free(cur);
     return (int64_t)total;
 }

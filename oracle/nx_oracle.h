@@ -92,6 +92,27 @@ int nxo_datetime_valid(int64_t secs, uint32_t nsecs);
 /* std str::from_utf8 validity (pack.rs:462) */
 int nxo_utf8_valid(const uint8_t* p, uint64_t n);
 
+/*
+ * Subscriber update dispatch: ConnectionCtx::process_updates_batch
+ * (netidx/src/subscriber/connection.rs:546-567). For each Update row i, in batch order: the
+ * subscription of id[i] (the Id -> Sub map, here a dense table: slot_of_id[id], NXO_NO_SLOT or
+ * an id >= n_ids = not subscribed, the update is dropped); for each of the subscription's
+ * streams (chan_id, channel), in stream order, (sub_id, Event::Update) is pushed onto that
+ * channel's batch; and the subscription's `last` (if kept) becomes this update.
+ *
+ * Output, grouped by channel: chan_off[n_chans + 1] (CSR), ent_sub / ent_row (SubId and the
+ * row of the update) in push order; last_row[slot] = 1 + the last row of the slot's
+ * subscription in the batch, 0 if none (or if the slot keeps no `last`). Returns the number of
+ * entries, or -NXO_CAPACITY if they exceed cap. *n_unmatched: rows without a subscription.
+ */
+#define NXO_NO_SLOT 0xffffffffu
+int64_t nxo_dispatch(const uint64_t* id, uint64_t n_rows, uint64_t n_ids,
+                     const uint32_t* slot_of_id, uint64_t n_slots, const uint64_t* slot_sub_id,
+                     const uint32_t* slot_stream_off, const uint32_t* stream_chan,
+                     const uint8_t* slot_has_last, uint32_t n_chans, uint64_t* chan_off,
+                     uint64_t* ent_sub, uint64_t* ent_row, uint64_t cap, uint64_t* last_row,
+                     uint64_t* n_unmatched);
+
 #ifdef __cplusplus
 }
 #endif

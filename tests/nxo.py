@@ -57,6 +57,11 @@ def lib():
         L.nxo_datetime_valid.argtypes = [C.c_int64, C.c_uint32]
         L.nxo_utf8_valid.restype = C.c_int
         L.nxo_utf8_valid.argtypes = [C.c_void_p, C.c_uint64]
+        L.nxo_dispatch.restype = C.c_int64
+        L.nxo_dispatch.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_void_p, C.c_uint64,
+                                   C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
+                                   C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p,
+                                   C.c_void_p]
         _lib = L
     return _lib
 
@@ -129,3 +134,32 @@ def encode_f64(ids, vals):
     if n < 0:
         raise ValueError(f"encode error {-n}")
     return out[:n]
+
+
+NO_SLOT = 0xFFFFFFFF
+
+
+def dispatch(ids, slot_of_id, slot_sub_id, slot_stream_off, stream_chan, slot_has_last, n_chans):
+    """nxo_dispatch (process_updates_batch, connection.rs:546-567) on numpy arrays.
+    Returns (chan_off, ent_sub, ent_row, last_row, n_unmatched)."""
+    ids = np.ascontiguousarray(ids, np.uint64)
+    slot_of_id = np.ascontiguousarray(slot_of_id, np.uint32)
+    slot_sub_id = np.ascontiguousarray(slot_sub_id, np.uint64)
+    slot_stream_off = np.ascontiguousarray(slot_stream_off, np.uint32)
+    stream_chan = np.ascontiguousarray(stream_chan, np.uint32)
+    slot_has_last = np.ascontiguousarray(slot_has_last, np.uint8)
+    fan = int((slot_stream_off[1:].astype(np.int64) - slot_stream_off[:-1]).max()) if len(slot_sub_id) else 0
+    cap = max(len(ids) * fan, 1)
+    chan_off = np.zeros(n_chans + 1, np.uint64)
+    ent_sub = np.zeros(cap, np.uint64)
+    ent_row = np.zeros(cap, np.uint64)
+    last_row = np.zeros(max(len(slot_sub_id), 1), np.uint64)
+    um = np.zeros(1, np.uint64)
+    n = lib().nxo_dispatch(ids.ctypes.data, len(ids), len(slot_of_id), slot_of_id.ctypes.data,
+                           len(slot_sub_id), slot_sub_id.ctypes.data, slot_stream_off.ctypes.data,
+                           stream_chan.ctypes.data, slot_has_last.ctypes.data, n_chans,
+                           chan_off.ctypes.data, ent_sub.ctypes.data, ent_row.ctypes.data, cap,
+                           last_row.ctypes.data, um.ctypes.data)
+    if n < 0:
+        raise ValueError(f"dispatch error {-n}")
+    return chan_off, ent_sub[:n], ent_row[:n], last_row[: len(slot_sub_id)], int(um[0])
