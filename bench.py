@@ -250,6 +250,56 @@ def extras_single_gpu(codec, stream, steps, warmup):
                                 "roundtrip_identical": True}
     except Exception as e:
         ex["encode_f64_1e7"] = {"error": repr(e)}
+    # (d) SURVEY 8f row 2: subscriber dispatch (process_updates_batch, connection.rs:546-567) of
+    # 10^7 decoded updates: every id subscribed once, its stream on one of 16 channels, half of
+    # the subscriptions keeping `last`. Checked against the oracle, which is also timed (1 core).
+    try:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import nxo
+        n = 10_000_000
+        n_chans = 16
+        cols, wire = make_f64_wire(codec, n, 0)
+        rng = np.random.default_rng(0x5EED0008)
+        slot_of_id = np.arange(n, dtype=np.uint32)
+        sub_id = rng.integers(0, 2**63, n, dtype=np.uint64)
+        off = np.arange(n + 1, dtype=np.uint32)
+        chan = rng.integers(0, n_chans, n, dtype=np.uint32)
+        keep = (rng.random(n) < 0.5).astype(np.uint8)
+        tab = netidx_amd.SubTable(slot_of_id, sub_id, off, chan, keep, n_chans)
+        for _ in range(2):
+            d = codec.dispatch_updates(tab, cols.id, n, cap=n)
+        torch.cuda.synchronize()
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        k = max(3, steps // 4)
+        e0.record(stream)
+        for _ in range(k):
+            d = codec.dispatch_updates(tab, cols.id, n, cap=n)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        kms = e0.elapsed_time(e1) / k
+        ids_h = cols.id[:n].cpu().numpy().view(np.uint64)
+        t0 = time.perf_counter()
+        w = nxo.dispatch(ids_h, slot_of_id, sub_id, off, chan, keep, n_chans)
+        cpu_s = time.perf_counter() - t0
+        assert d.n_entries == n and np.array_equal(
+            d.ent_row[:n].cpu().numpy().view(np.uint64), w[2])
+        assert np.array_equal(d.ent_sub[:n].cpu().numpy().view(np.uint64), w[1])
+        assert np.array_equal(d.last_row.cpu().numpy().view(np.uint64), w[3])
+        n_last = int(keep.sum())
+        # each row once: id, slot, stream offsets, channel, keep flag, SubId; entry written;
+        # last row written for the kept subscriptions
+        b = n * (8 + 4 + 8 + 4 + 1 + 8) + n * 16 + n_last * 8
+        ex["dispatch_1e7"] = {"records": n, "channels": n_chans,
+                              "M_updates_s": round(n / (kms / 1e3) / 1e6, 1),
+                              "call_ms": round(kms, 4),
+                              "hbm_frac": round(b / (kms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                              "algorithmic_bytes": b,
+                              "cpu_oracle_M_updates_s_1core": round(n / cpu_s / 1e6, 1)}
+        del cols, wire, tab, d
+        torch.cuda.empty_cache()
+    except Exception as e:
+        ex["dispatch_1e7"] = {"error": repr(e)}
     return ex
 
 

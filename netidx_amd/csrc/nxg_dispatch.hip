@@ -7,16 +7,17 @@
 //
 // Output is grouped by channel, each channel's batch in batch order (CSR, chan_off). Three
 // launches, deterministic (no atomics decide an order):
-//   count    one wave per segment of SEG rows (64 rows per step). Per step the wave visits the
-//            distinct channels its 64 rows reach in increasing channel order ("match" loop:
-//            wave minimum of each lane's next channel); per channel, the rows' entry counts are
-//            added to the segment's counter. Counters end in hist[chan * n_seg + seg]
-//            (channel-major). Also: last_row (atomicMax of row + 1), unmatched rows.
+//   count    one wave per segment of SEG rows (64 rows per step); one counter increment per
+//            (row, stream), order-free. Counters end in hist[chan * n_seg + seg] (channel-major).
+//            Also: last_row (atomicMax of row + 1), unmatched rows.
 //   scan     exclusive scan of hist in that order: the first entry of every (channel, segment)
 //            pair; chan_off[c] is the (c, 0) value.
-//   scatter  the count pass again; a lane's position within a step is the wave's running count
-//            for the channel plus an inclusive scan over lanes, so each channel's entries come
-//            out in row order.
+//   scatter  the rows again; an entry's position is the wave's running count for its channel
+//            plus its rank within the 64-row step: each (row, stream) sets its lane's bit in its
+//            channel's LDS mask and counts the lower bits (a row names a channel at most once,
+//            connection.rs:328-356); steps with a repeated channel in one row, or rows with more
+//            than RF streams, use a "match" loop instead (wave minimum of each lane's next
+//            channel, an inclusive scan over lanes per channel). Entries come out in row order.
 // Counters live in LDS when there are at most LCH channels, in global memory otherwise.
 #include "nxg_device.h"
 #include "nxg_internal.h"
@@ -30,13 +31,16 @@ constexpr uint32_t NONE = 0xffffffffu;
 constexpr int SCAN_K = 16;            // scan: elements per thread
 constexpr uint32_t SCAN_B = TPB * SCAN_K;
 
+constexpr uint32_t RF = 4;  // streams per row held in registers (more: read from memory)
+
 struct Row {
     uint32_t k0, k1;  // the row's streams [k0, k1) in stream_chan (empty: no subscription)
     uint32_t slot;
+    uint32_t c[RF];   // their channels (NONE past k1 or >= n_chans), when k1 - k0 <= RF
 };
 
 NXG_DEV Row row_of(const NxgSubTable& tb, const uint64_t* __restrict__ id, uint64_t i, uint64_t n) {
-    Row r{0, 0, NONE};
+    Row r{0, 0, NONE, {NONE, NONE, NONE, NONE}};
     if (i < n) {
         const uint64_t x = id[i];
         const uint32_t s = x < tb.n_ids ? tb.slot_of_id[x] : NONE;
@@ -44,6 +48,11 @@ NXG_DEV Row row_of(const NxgSubTable& tb, const uint64_t* __restrict__ id, uint6
             r.slot = s;
             r.k0 = tb.slot_stream_off[s];
             r.k1 = tb.slot_stream_off[s + 1];
+#pragma unroll
+            for (uint32_t j = 0; j < RF; j++) {
+                const uint32_t c = r.k0 + j < r.k1 ? tb.stream_chan[r.k0 + j] : NONE;
+                r.c[j] = c < tb.n_chans ? c : NONE;  // channels past n_chans: ignored
+            }
         }
     }
     return r;
@@ -53,6 +62,12 @@ NXG_DEV Row row_of(const NxgSubTable& tb, const uint64_t* __restrict__ id, uint6
 // row's streams name channel `d`
 NXG_DEV uint32_t next_chan(const NxgSubTable& tb, const Row& r, uint32_t prev, bool first) {
     uint32_t m = NONE;
+    if (r.k1 - r.k0 <= RF) {
+#pragma unroll
+        for (uint32_t j = 0; j < RF; j++)
+            if ((first || r.c[j] > prev) && r.c[j] < m) m = r.c[j];
+        return m;
+    }
     for (uint32_t k = r.k0; k < r.k1; k++) {
         const uint32_t c = tb.stream_chan[k];
         if ((first || c > prev) && c < m && c < tb.n_chans) m = c;  // others: ignored
@@ -61,6 +76,11 @@ NXG_DEV uint32_t next_chan(const NxgSubTable& tb, const Row& r, uint32_t prev, b
 }
 NXG_DEV uint32_t count_chan(const NxgSubTable& tb, const Row& r, uint32_t d) {
     uint32_t n = 0;
+    if (r.k1 - r.k0 <= RF) {
+#pragma unroll
+        for (uint32_t j = 0; j < RF; j++) n += r.c[j] == d;
+        return n;
+    }
     for (uint32_t k = r.k0; k < r.k1; k++) n += tb.stream_chan[k] == d;
     return n;
 }
@@ -100,19 +120,21 @@ __global__ __launch_bounds__(TPB) void nxg_disp_count_kernel(
             um += (i < r1 && r.slot == NONE);
             if (r.slot != NONE && tb.slot_has_last[r.slot])
                 atomicMax((unsigned long long*)&last_row[r.slot], (unsigned long long)(i + 1));
-            uint32_t prev = 0;
-            bool first = true;
-#pragma unroll 1
-            for (;;) {
-                const uint32_t d = wave_min(next_chan(tb, r, prev, first));
-                if (d == NONE) break;
-                const uint32_t tot = wave_sum<uint32_t>(count_chan(tb, r, d));
-                if (lane == 0) {
-                    if (lds) cnt[d] += tot;
-                    else atomicAdd(&hist[(uint64_t)d * n_seg + seg], tot);
+            // order-free: one atomic per (row, stream)
+            if (r.k1 - r.k0 <= RF) {
+#pragma unroll
+                for (uint32_t j = 0; j < RF; j++) {
+                    if (r.c[j] == NONE) continue;
+                    if (lds) atomicAdd(&cnt[r.c[j]], 1u);
+                    else atomicAdd(&hist[(uint64_t)r.c[j] * n_seg + seg], 1u);
                 }
-                prev = d;
-                first = false;
+            } else {
+                for (uint32_t k = r.k0; k < r.k1; k++) {
+                    const uint32_t c = tb.stream_chan[k];
+                    if (c >= tb.n_chans) continue;
+                    if (lds) atomicAdd(&cnt[c], 1u);
+                    else atomicAdd(&hist[(uint64_t)c * n_seg + seg], 1u);
+                }
             }
         }
         if (lds) {
@@ -187,14 +209,20 @@ __global__ __launch_bounds__(TPB) void nxg_disp_scatter_kernel(
     uint64_t* __restrict__ off, uint64_t* __restrict__ ent_sub, uint64_t* __restrict__ ent_row,
     uint64_t cap) {
     __shared__ uint64_t cur_lds[WAVES][LCH];
+    __shared__ uint64_t mask_lds[WAVES][LCH];
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const bool lds = tb.n_chans <= LCH;
     uint64_t* cur = cur_lds[w];
+    uint64_t* mask = mask_lds[w];
+    const uint64_t lt = (1ull << lane) - 1;
 #pragma unroll 1
     for (uint64_t seg = (uint64_t)blockIdx.x * WAVES + w; seg < n_seg;
          seg += (uint64_t)gridDim.x * WAVES) {
         if (lds) {
-            for (uint32_t c = lane; c < tb.n_chans; c += 64) cur[c] = off[(uint64_t)c * n_seg + seg];
+            for (uint32_t c = lane; c < tb.n_chans; c += 64) {
+                cur[c] = off[(uint64_t)c * n_seg + seg];
+                mask[c] = 0;
+            }
             wave_lds_order();
         }
         const uint64_t r0 = seg * seg_rows, r1 = r0 + seg_rows < n ? r0 + seg_rows : n;
@@ -203,6 +231,42 @@ __global__ __launch_bounds__(TPB) void nxg_disp_scatter_kernel(
             const uint64_t i = b + lane;
             const Row r = row_of(tb, id, i, r1);
             const uint64_t sub = r.slot != NONE ? tb.slot_sub_id[r.slot] : 0;
+            const bool dup = (r.c[0] != NONE && (r.c[0] == r.c[1] || r.c[0] == r.c[2] ||
+                                                 r.c[0] == r.c[3])) ||
+                             (r.c[1] != NONE && (r.c[1] == r.c[2] || r.c[1] == r.c[3])) ||
+                             (r.c[2] != NONE && r.c[2] == r.c[3]);
+            if (lds && !__any(r.k1 - r.k0 > RF || dup)) {
+                // each (row, stream) sets its lane's bit in its channel's mask; a row names a
+                // channel at most once here, so the entry's rank among the step's entries for
+                // that channel is the number of lower lanes in the mask (row order)
+#pragma unroll
+                for (uint32_t j = 0; j < RF; j++)
+                    if (r.c[j] != NONE) atomicOr((unsigned long long*)&mask[r.c[j]], 1ull << lane);
+                wave_lds_order();
+                uint64_t m[RF];
+#pragma unroll
+                for (uint32_t j = 0; j < RF; j++) {
+                    m[j] = r.c[j] != NONE ? mask[r.c[j]] : 0ull;
+                    if (r.c[j] != NONE) {
+                        const uint64_t e = cur[r.c[j]] + __popcll(m[j] & lt);
+                        if (e < cap) {
+                            ent_sub[e] = sub;
+                            ent_row[e] = i;
+                        }
+                    }
+                }
+                wave_lds_order();
+                // the channel's highest lane advances its cursor and clears its mask
+#pragma unroll
+                for (uint32_t j = 0; j < RF; j++) {
+                    if (r.c[j] != NONE && 63u - (uint32_t)__builtin_clzll(m[j]) == lane) {
+                        cur[r.c[j]] += __popcll(m[j]);
+                        mask[r.c[j]] = 0;
+                    }
+                }
+                wave_lds_order();
+                continue;
+            }
             uint32_t prev = 0;
             bool first = true;
 #pragma unroll 1
