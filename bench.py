@@ -223,6 +223,67 @@ def extras_single_gpu(codec, stream, steps, warmup):
         del cols, wire, hframe, hout
     except Exception as e:
         ex["decode_f64_1e7_host_pcie"] = {"error": repr(e)}
+    # (b3) the same socket-buffer path for a stream of frames (a connection's read_task hands
+    # over frame after frame, channel.rs:379-443): two contexts, each on its own stream, take
+    # alternate frames; frame j's H2D and decode overlap frame j-1's D2H (PCIe is full duplex).
+    # Wall clock per frame over F frames. Never the bench `value`.
+    try:
+        n = 10_000_000
+        cols, wire = make_f64_wire(codec, n, 0)
+        hframe = wire.cpu().pin_memory()
+        W = wire.numel()
+        ctxs, streams, dins, douts, hid, hval = [], [], [], [], [], []
+        for k in range(2):
+            c = netidx_amd.Codec(0)
+            s = torch.cuda.Stream()
+            c.set_stream(s.cuda_stream)
+            ctxs.append(c)
+            streams.append(s)
+            dins.append(torch.empty(W, dtype=torch.uint8, device="cuda"))
+            douts.append(Columns(n, 0, 0, netidx_amd.LAYOUT_F64, "cuda"))
+            hid.append(torch.empty(n, dtype=torch.int64).pin_memory())
+            hval.append(torch.empty(n, dtype=torch.int64).pin_memory())
+
+        def enqueue_in(j):
+            k = j % 2
+            with torch.cuda.stream(streams[k]):
+                dins[k].copy_(hframe, non_blocking=True)
+            ctxs[k].decode_async(dins[k].data_ptr(), W, douts[k])
+
+        def finish(j):
+            k = j % 2
+            st = ctxs[k].sync()
+            assert st.path == 1 and st.n_rows == n
+            with torch.cuda.stream(streams[k]):
+                hid[k].copy_(douts[k].id[: st.n_rows], non_blocking=True)
+                hval[k].copy_(douts[k].fixed[: st.n_rows], non_blocking=True)
+
+        def run(frames):
+            for j in range(frames):
+                enqueue_in(j)
+                if j > 0:
+                    finish(j - 1)
+            finish(frames - 1)
+            for s in streams:
+                s.synchronize()
+
+        run(2)
+        F = max(6, steps // 2)
+        t0 = time.perf_counter()
+        run(F)
+        dt = (time.perf_counter() - t0) / F
+        for k in range(2):
+            assert torch.equal(hval[k], cols.fixed[:n].cpu()) and torch.equal(hid[k], cols.id[:n].cpu())
+        ex["decode_f64_1e7_host_pipelined"] = {
+            "records": n, "frames": F, "M_updates_s": round(n / dt / 1e6, 1),
+            "ms_per_frame": round(dt * 1e3, 3),
+            "GB_s_host_to_host": round((W + 16 * n) / dt / 1e9, 2)}
+        for c in ctxs:
+            c.close()
+        del cols, wire, hframe, dins, douts, hid, hval
+        torch.cuda.empty_cache()
+    except Exception as e:
+        ex["decode_f64_1e7_host_pipelined"] = {"error": repr(e)}
     # (c) config 4: f64 encode from device columns, byte-identical round trip
     try:
         n = 10_000_000
