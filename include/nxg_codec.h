@@ -78,6 +78,8 @@ enum NxgErrKind {
     NXG_CAPACITY = 7, /* output columns too small */
     NXG_NOT_F64 = 8,  /* valid batch, but F64-only columns were supplied for mixed content */
     NXG_TIMEOUT = 9,  /* device-side progress watchdog fired (should never happen) */
+    NXG_UNSUPPORTED = 10, /* publish: UpdateChanged compares a Decimal/Array/Map/Error(Value)/
+                             Abstract value, whose equality the columns do not carry */
 };
 
 #define NXG_MAX_DEPTH 32
@@ -198,6 +200,38 @@ typedef struct NxgDispatch {
  * a HIP failure, or entries > cap_entries (n_entries then holds the required capacity). */
 bool nxg_dispatch_updates(NxgCtx* ctx, const NxgSubTable* tab, const uint64_t* id,
                           uint64_t n_rows, NxgDispatch* out, NetidxError* err);
+
+/* ---- publisher commit: replaces UpdateBatch::commit (publisher/mod.rs:776-845) ----------
+ * A queued batch (its rows in NxgColumns form: id, tag, fixed, aux, text in `heap`; kind[i] per
+ * row; to_client[i] for NXG_PUB_UPDATE_CLIENT rows) becomes per-client batches of
+ * From::Update(id, v), in batch order:
+ *   NXG_PUB_UPDATE          Update(None, id, v)  (Val::update, mod.rs:517-519): to every client
+ *                           subscribed to id (pb.by_id[id].subscribed), then current = v;
+ *   NXG_PUB_UPDATE_CHANGED  UpdateChanged(id, v) (update_changed): the same, only if
+ *                           current != v (Value::eq, netidx-value/src/op.rs:133-172);
+ *   NXG_PUB_UPDATE_CLIENT   Update(Some(cl), id, v) (update_subscriber): to client cl only.
+ * Ids that are not published are dropped (counted in n_unmatched). The table (device memory):
+ * by_id as a dense slot table, each slot's subscribed clients as a CSR, and each slot's current
+ * value (cur_tag NULL: all F64; text bytes at cur_heap + cur_fixed). Output in NxgDispatch: per
+ * client c, entries [chan_off[c], chan_off[c+1]) of (ent_sub = Id, ent_row = row); last_row[slot]
+ * = 1 + the row that became current (0: unchanged). Synchronous; false on misuse, HIP failure,
+ * capacity, or NXG_UNSUPPORTED (err->msg says which). */
+enum NxgPubKind { NXG_PUB_UPDATE = 0, NXG_PUB_UPDATE_CHANGED = 1, NXG_PUB_UPDATE_CLIENT = 2 };
+typedef struct NxgPubTable {
+    uint64_t n_ids;                   /* slot_of_id covers Ids [0, n_ids) */
+    const uint32_t* slot_of_id;       /* [n_ids]: published-value slot, or NXG_NO_SLOT */
+    uint64_t n_slots;
+    const uint32_t* slot_client_off;  /* [n_slots + 1]: subscribed clients, CSR */
+    const uint32_t* client;           /* [n_subscriptions]: client index, < n_clients */
+    uint32_t n_clients;
+    const uint8_t* cur_tag;           /* [n_slots] current values, columns as NxgColumns */
+    const uint64_t* cur_fixed;
+    const uint32_t* cur_aux;          /* NULL: 0 */
+    const uint8_t* cur_heap;
+} NxgPubTable;
+bool nxg_publish_commit(NxgCtx* ctx, const NxgPubTable* tab, const NxgColumns* batch,
+                        const uint8_t* heap, const uint8_t* kind, const uint32_t* to_client,
+                        NxgDispatch* out, NetidxError* err);
 
 /* ---- host framing (netidx/src/channel.rs) ------------------------------------------------
  * Frame boundaries exactly as WriteChannel::queue_send/try_flush split the buffer. The split

@@ -76,6 +76,13 @@ class NxgDispatch(C.Structure):
                 ("n_unmatched", C.c_uint64)]
 
 
+class NxgPubTable(C.Structure):
+    _fields_ = [("n_ids", C.c_uint64), ("slot_of_id", C.c_void_p), ("n_slots", C.c_uint64),
+                ("slot_client_off", C.c_void_p), ("client", C.c_void_p), ("n_clients", C.c_uint32),
+                ("cur_tag", C.c_void_p), ("cur_fixed", C.c_void_p), ("cur_aux", C.c_void_p),
+                ("cur_heap", C.c_void_p)]
+
+
 class NxgStatus(C.Structure):
     _fields_ = [
         ("n_rows", C.c_uint64), ("n_children", C.c_uint64), ("n_ctl", C.c_uint64),
@@ -110,6 +117,9 @@ SIGNATURES = {
                                             C.POINTER(NetidxError)]),
     "nxg_dispatch_updates": (C.c_bool, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64,
                                         C.c_void_p, C.POINTER(NetidxError)]),
+    "nxg_publish_commit": (C.c_bool, [C.c_void_p, C.c_void_p, C.POINTER(NxgColumns), C.c_void_p,
+                                      C.c_void_p, C.c_void_p, C.c_void_p,
+                                      C.POINTER(NetidxError)]),
     "nxg_frame_split": (C.c_int64, [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64]),
     "nxg_frame_header": (None, [C.c_uint32, C.c_bool, C.c_void_p]),
     "nxg_frame_parse_header": (C.c_uint32, [C.c_void_p, C.c_uint64, C.POINTER(C.c_uint32),
@@ -303,6 +313,36 @@ class Codec:
         return Dispatch(chan_off, ent_sub, ent_row, last_row[: table.slot_sub_id.numel()],
                         out.n_entries, out.n_unmatched)
 
+    def publish_commit(self, table, batch, kind, to_client=None, heap=None, cap=None):
+        """UpdateBatch::commit on device columns: `batch` (Columns: id, tag, fixed, aux), per-row
+        `kind` (PUB_UPDATE / PUB_UPDATE_CHANGED / PUB_UPDATE_CLIENT, uint8 tensor) and
+        `to_client` (int32 tensor, for PUB_UPDATE_CLIENT rows). Returns a Dispatch whose
+        channels are the clients and whose entries are (Id, row); last_row[slot] = 1 + the row
+        that became current."""
+        import torch
+        n = batch.s.n_rows
+        dev = batch.id.device
+        if to_client is None:
+            to_client = torch.zeros(max(n, 1), dtype=torch.int32, device=dev)
+        if cap is None:
+            offs = table.slot_client_off.cpu().numpy().view(np.uint32).astype(np.int64)
+            cap = n * max(1, int((offs[1:] - offs[:-1]).max()) if len(offs) > 1 else 1)
+        chan_off = torch.zeros(table.n_clients + 1, dtype=torch.int64, device=dev)
+        ent_id = torch.empty(max(cap, 1), dtype=torch.int64, device=dev)
+        ent_row = torch.empty(max(cap, 1), dtype=torch.int64, device=dev)
+        n_slots = table.slot_client_off.numel() - 1
+        last_row = torch.empty(max(n_slots, 1), dtype=torch.int64, device=dev)
+        out = NxgDispatch(cap, chan_off.data_ptr(), ent_id.data_ptr(), ent_row.data_ptr(),
+                          last_row.data_ptr(), 0, 0)
+        tb = table.c_struct()
+        err = NetidxError()
+        _check(lib().nxg_publish_commit(self.ctx, C.byref(tb), C.byref(batch.s), _heap_ptr(heap),
+                                        C.c_void_p(kind.data_ptr()),
+                                        C.c_void_p(to_client.data_ptr()), C.byref(out),
+                                        C.byref(err)), err)
+        return Dispatch(chan_off, ent_id, ent_row, last_row[:n_slots], out.n_entries,
+                        out.n_unmatched)
+
     def encoded_len(self, cols, heap=None):
         n, err = C.c_uint64(0), NetidxError()
         _check(lib().nxg_encoded_len(self.ctx, C.byref(cols.s), _heap_ptr(heap), C.byref(n),
@@ -348,7 +388,7 @@ class SubTable:
         import torch
 
         def t(a, dt):
-            return torch.as_tensor(np.ascontiguousarray(a, dtype=dt)).to(device)
+            return torch.as_tensor(np.array(a, dtype=dt, copy=True)).to(device)
 
         self.slot_of_id = t(slot_of_id, np.uint32).view(torch.int32)
         self.slot_sub_id = t(slot_sub_id, np.uint64).view(torch.int64)
@@ -399,6 +439,39 @@ class Dispatch:
         row = self.ent_row[: self.n_entries].cpu().numpy().view(np.uint64)
         return {c: list(zip(sub[off[c]:off[c + 1]].tolist(), row[off[c]:off[c + 1]].tolist()))
                 for c in range(len(off) - 1) if off[c + 1] > off[c]}
+
+
+PUB_UPDATE, PUB_UPDATE_CHANGED, PUB_UPDATE_CLIENT = 0, 1, 2
+
+
+class PubTable:
+    """Device-resident publisher state for UpdateBatch::commit (netidx/src/publisher/mod.rs:
+    776-845): pb.by_id as a dense slot table (Id -> slot), each slot's subscribed clients (CSR)
+    and current value (tag/fixed/aux columns; text bytes in cur_heap)."""
+
+    def __init__(self, slot_of_id, slot_client_off, client, n_clients, cur_tag, cur_fixed,
+                 cur_aux=None, cur_heap=None, device="cuda"):
+        import torch
+
+        def t(a, dt):
+            return torch.as_tensor(np.array(a, dtype=dt, copy=True)).to(device)
+
+        self.slot_of_id = t(slot_of_id, np.uint32).view(torch.int32)
+        self.slot_client_off = t(slot_client_off, np.uint32).view(torch.int32)
+        self.client = t(client, np.uint32).view(torch.int32)
+        self.n_clients = int(n_clients)
+        self.cur_tag = None if cur_tag is None else t(cur_tag, np.uint8)
+        self.cur_fixed = t(cur_fixed, np.uint64).view(torch.int64)
+        self.cur_aux = None if cur_aux is None else t(cur_aux, np.uint32).view(torch.int32)
+        self.cur_heap = None if cur_heap is None else t(cur_heap, np.uint8)
+
+    def c_struct(self):
+        def p(x):
+            return x.data_ptr() if x is not None and x.numel() else None
+        return NxgPubTable(self.slot_of_id.numel(), p(self.slot_of_id),
+                           self.slot_client_off.numel() - 1, p(self.slot_client_off),
+                           p(self.client), self.n_clients, p(self.cur_tag), p(self.cur_fixed),
+                           p(self.cur_aux), p(self.cur_heap))
 
 
 def _heap_ptr(heap):

@@ -836,6 +836,84 @@ bool nxg_dispatch_updates(NxgCtx* c, const NxgSubTable* tab, const uint64_t* id,
     return true;
 }
 
+// ---- publisher commit (publisher/mod.rs:776-845) -----------------------------------------------
+bool nxg_publish_commit(NxgCtx* c, const NxgPubTable* tab, const NxgColumns* batch,
+                        const uint8_t* heap, const uint8_t* kind, const uint32_t* to_client,
+                        NxgDispatch* out, NetidxError* err) {
+    if (!c || !tab || !batch || !out || !out->chan_off) {
+        set_err(err, "null argument");
+        return false;
+    }
+    const uint64_t n = batch->n_rows;
+    if (n && (!batch->id || !batch->fixed || !kind || !to_client)) {
+        set_err(err, "null batch column, kind or to_client");
+        return false;
+    }
+    if ((tab->n_ids && !tab->slot_of_id) ||
+        (tab->n_slots && (!tab->slot_client_off || !tab->cur_fixed || !out->last_row)) ||
+        (out->cap_entries && (!out->ent_sub || !out->ent_row))) {
+        set_err(err, "null table or output array");
+        return false;
+    }
+    if (n >= 0xffffffffull) {
+        set_err(err, "publish batches are limited to 2^32 - 1 rows");
+        return false;
+    }
+    HIPCHK(hipSetDevice(c->device));
+    const size_t pub = (nxg_pub_scratch_bytes(n, tab->n_slots) + 255) & ~size_t(255);
+    const size_t need = pub + 64 + nxg_disp_scratch_bytes(n, tab->n_clients);
+    if (need > c->dscratch_cap) {
+        HIPCHK(hipStreamSynchronize(c->stream));
+        if (c->dscratch) HIPCHK(hipFree(c->dscratch));
+        c->dscratch = nullptr;
+        const size_t sz = std::max(need, c->dscratch_cap * 2);
+        HIPCHK(hipMalloc(&c->dscratch, sz));
+        c->dscratch_cap = sz;
+    }
+    const NxgPubBatch b{batch->id, batch->tag, batch->fixed, batch->aux, heap, kind, n};
+    HIPCHK(nxg_launch_pub_stage1(*tab, b, c->dscratch, c->stream));
+    uint32_t flags[3] = {0, 0, 0};
+    HIPCHK(hipMemcpyAsync(flags, nxg_pub_flags(c->dscratch), 12, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    const uint8_t* mode = nullptr;
+    HIPCHK(nxg_launch_pub_stage2(*tab, b, c->dscratch, flags[0] != 0, flags[1] != 0, c->ncu,
+                                 c->stream, &mode));
+    if (flags[1]) {
+        HIPCHK(hipMemcpyAsync(&flags[2], nxg_pub_flags(c->dscratch) + 2, 4, hipMemcpyDeviceToHost,
+                              c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        if (flags[2]) {
+            set_err(err, "NXG_UNSUPPORTED: an UpdateChanged compares a Decimal, Array, Map, "
+                         "Error(Value) or Abstract value");
+            return false;
+        }
+    } else {
+        mode = kind;  // Update(None) = 0 and Update(Some(cl)) = 2 route as they are
+    }
+    // the client fan-out is the subscriber dispatch with per-row routing: clients as channels,
+    // entries tagged with the row's Id, every slot tracking `current`
+    const NxgSubTable st{tab->n_ids, tab->slot_of_id, tab->n_slots, nullptr, tab->slot_client_off,
+                         tab->client, nullptr, tab->n_clients};
+    uint8_t* ds = c->dscratch + pub;
+    uint64_t* um = reinterpret_cast<uint64_t*>(ds);
+    HIPCHK(nxg_launch_dispatch(st, batch->id, n, ds + 64, out->chan_off, out->ent_sub, out->ent_row,
+                               out->cap_entries, out->last_row, um, c->ncu, c->stream, mode,
+                               to_client));
+    uint64_t res[2] = {0, 0};
+    HIPCHK(hipMemcpyAsync(&res[0], out->chan_off + tab->n_clients, 8, hipMemcpyDeviceToHost,
+                          c->stream));
+    HIPCHK(hipMemcpyAsync(&res[1], um, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    out->n_entries = res[0];
+    out->n_unmatched = res[1];
+    if (res[0] > out->cap_entries) {
+        set_err(err, "publish needs %llu entries, capacity is %llu", (unsigned long long)res[0],
+                (unsigned long long)out->cap_entries);
+        return false;
+    }
+    return true;
+}
+
 bool nxg_encoded_len(NxgCtx* c, const NxgColumns* in, const uint8_t* heap, uint64_t* len_out,
                      NetidxError* err) {
     return encode_impl(c, in, heap, nullptr, 0, len_out, err);

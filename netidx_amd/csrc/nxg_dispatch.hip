@@ -39,11 +39,29 @@ struct Row {
     uint32_t c[RF];   // their channels (NONE past k1 or >= n_chans), when k1 - k0 <= RF
 };
 
-NXG_DEV Row row_of(const NxgSubTable& tb, const uint64_t* __restrict__ id, uint64_t i, uint64_t n) {
+// Per-row routing (publisher commit, nxg_publish.hip): mode 0 = through the Id's slot, 1 = not
+// pushed (an unchanged UpdateChanged), 2 = to client to_client[i] only. `mode` null: all 0.
+struct Route {
+    const uint8_t* mode;
+    const uint32_t* to_client;
+};
+
+NXG_DEV Row row_of(const NxgSubTable& tb, const Route& rt, const uint64_t* __restrict__ id,
+                   uint64_t i, uint64_t n, bool& unmatched) {
     Row r{0, 0, NONE, {NONE, NONE, NONE, NONE}};
+    unmatched = false;
     if (i < n) {
+        const uint32_t m = rt.mode ? rt.mode[i] : 0u;
+        if (m == 2) {  // one stream: the named client
+            const uint32_t c = rt.to_client[i];
+            r.k1 = 1;
+            r.c[0] = c < tb.n_chans ? c : NONE;
+            return r;
+        }
+        if (m == 1) return r;
         const uint64_t x = id[i];
         const uint32_t s = x < tb.n_ids ? tb.slot_of_id[x] : NONE;
+        unmatched = s == NONE;
         if (s != NONE) {
             r.slot = s;
             r.k0 = tb.slot_stream_off[s];
@@ -98,7 +116,8 @@ NXG_DEV uint32_t wave_min(uint32_t v) {
 
 // ---- pass 1: per (channel, segment) entry counts ---------------------------------------------
 __global__ __launch_bounds__(TPB) void nxg_disp_count_kernel(
-    NxgSubTable tb, const uint64_t* __restrict__ id, uint64_t n, uint64_t seg_rows, uint64_t n_seg,
+    NxgSubTable tb, Route rt, const uint64_t* __restrict__ id, uint64_t n, uint64_t seg_rows,
+    uint64_t n_seg,
     uint32_t* __restrict__ hist, uint64_t* __restrict__ last_row, uint64_t* __restrict__ unmatched) {
     __shared__ uint32_t cnt_lds[WAVES][LCH];
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -116,9 +135,10 @@ __global__ __launch_bounds__(TPB) void nxg_disp_count_kernel(
 #pragma unroll 1
         for (uint64_t b = r0; b < r1; b += 64) {
             const uint64_t i = b + lane;
-            const Row r = row_of(tb, id, i, r1);
-            um += (i < r1 && r.slot == NONE);
-            if (r.slot != NONE && tb.slot_has_last[r.slot])
+            bool unm;
+            const Row r = row_of(tb, rt, id, i, r1, unm);
+            um += unm;
+            if (r.slot != NONE && (!tb.slot_has_last || tb.slot_has_last[r.slot]))
                 atomicMax((unsigned long long*)&last_row[r.slot], (unsigned long long)(i + 1));
             // order-free: one atomic per (row, stream)
             if (r.k1 - r.k0 <= RF) {
@@ -205,7 +225,8 @@ __global__ __launch_bounds__(TPB) void nxg_disp_scan_add_kernel(
 
 // ---- pass 3: entries --------------------------------------------------------------------------
 __global__ __launch_bounds__(TPB) void nxg_disp_scatter_kernel(
-    NxgSubTable tb, const uint64_t* __restrict__ id, uint64_t n, uint64_t seg_rows, uint64_t n_seg,
+    NxgSubTable tb, Route rt, const uint64_t* __restrict__ id, uint64_t n, uint64_t seg_rows,
+    uint64_t n_seg,
     uint64_t* __restrict__ off, uint64_t* __restrict__ ent_sub, uint64_t* __restrict__ ent_row,
     uint64_t cap) {
     __shared__ uint64_t cur_lds[WAVES][LCH];
@@ -229,8 +250,11 @@ __global__ __launch_bounds__(TPB) void nxg_disp_scatter_kernel(
 #pragma unroll 1
         for (uint64_t b = r0; b < r1; b += 64) {
             const uint64_t i = b + lane;
-            const Row r = row_of(tb, id, i, r1);
-            const uint64_t sub = r.slot != NONE ? tb.slot_sub_id[r.slot] : 0;
+            bool unm;
+            const Row r = row_of(tb, rt, id, i, r1, unm);
+            // the entry's tag: the subscription's SubId, or (no SubId table) the row's own Id
+            const uint64_t sub = !tb.slot_sub_id ? (i < r1 ? id[i] : 0)
+                                 : (r.slot != NONE ? tb.slot_sub_id[r.slot] : 0);
             const bool dup = (r.c[0] != NONE && (r.c[0] == r.c[1] || r.c[0] == r.c[2] ||
                                                  r.c[0] == r.c[3])) ||
                              (r.c[1] != NONE && (r.c[1] == r.c[2] || r.c[1] == r.c[3])) ||
@@ -325,7 +349,9 @@ uint64_t nxg_disp_scratch_bytes(uint64_t n, uint32_t n_chans) {
 hipError_t nxg_launch_dispatch(const NxgSubTable& tb, const uint64_t* id, uint64_t n,
                                uint8_t* scratch, uint64_t* chan_off, uint64_t* ent_sub,
                                uint64_t* ent_row, uint64_t cap, uint64_t* last_row,
-                               uint64_t* unmatched, int ncu, hipStream_t s) {
+                               uint64_t* unmatched, int ncu, hipStream_t s,
+                               const uint8_t* row_mode, const uint32_t* to_client) {
+    const Route rt{row_mode, to_client};
     const uint64_t seg = nxg_disp_seg_rows(n, tb.n_chans);
     const uint64_t n_seg = (n + seg - 1) / seg;
     const uint64_t M = n_seg * (uint64_t)tb.n_chans;
@@ -341,16 +367,16 @@ hipError_t nxg_launch_dispatch(const NxgSubTable& tb, const uint64_t* id, uint64
     if (tb.n_chans > LCH && (e = hipMemsetAsync(hist, 0, M * 4, s)) != hipSuccess) return e;
     const uint64_t want = (n_seg + WAVES - 1) / WAVES;
     const uint32_t g = (uint32_t)(want < (uint64_t)ncu * 8 ? want : (uint64_t)ncu * 8);
-    hipLaunchKernelGGL(nxg_disp_count_kernel, dim3(g), dim3(TPB), 0, s, tb, id, n, seg, n_seg, hist,
-                       last_row, unmatched);
+    hipLaunchKernelGGL(nxg_disp_count_kernel, dim3(g), dim3(TPB), 0, s, tb, rt, id, n, seg, n_seg,
+                       hist, last_row, unmatched);
     if (M) {
         hipLaunchKernelGGL(nxg_disp_scan_block_kernel, dim3((uint32_t)nb), dim3(TPB), 0, s, hist, M,
                            off, bsum);
         hipLaunchKernelGGL(nxg_disp_scan_top_kernel, dim3(1), dim3(1024), 0, s, bsum, nb);
         hipLaunchKernelGGL(nxg_disp_scan_add_kernel, dim3((uint32_t)((M + TPB - 1) / TPB)),
                            dim3(TPB), 0, s, off, M, bsum, nb, n_seg, tb.n_chans, chan_off);
-        hipLaunchKernelGGL(nxg_disp_scatter_kernel, dim3(g), dim3(TPB), 0, s, tb, id, n, seg, n_seg,
-                           off, ent_sub, ent_row, cap);
+        hipLaunchKernelGGL(nxg_disp_scatter_kernel, dim3(g), dim3(TPB), 0, s, tb, rt, id, n, seg,
+                           n_seg, off, ent_sub, ent_row, cap);
     }
     return hipGetLastError();
 }

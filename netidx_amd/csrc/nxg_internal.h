@@ -124,7 +124,28 @@ uint64_t nxg_disp_scratch_bytes(uint64_t n, uint32_t n_chans);
 hipError_t nxg_launch_dispatch(const NxgSubTable& tb, const uint64_t* id, uint64_t n,
                                uint8_t* scratch, uint64_t* chan_off, uint64_t* ent_sub,
                                uint64_t* ent_row, uint64_t cap, uint64_t* last_row,
-                               uint64_t* unmatched, int ncu, hipStream_t s);
+                               uint64_t* unmatched, int ncu, hipStream_t s,
+                               const uint8_t* row_mode = nullptr,
+                               const uint32_t* to_client = nullptr);
+// publisher commit (nxg_publish.hip): stage 1 counts slots and sets flags (dup, changed,
+// unsupported: three u32 at nxg_pub_flags(scratch)); stage 2 routes the UpdateChanged rows
+// (mode array for nxg_launch_dispatch, or null when the kinds route as they are).
+struct NxgPubBatch {
+    const uint64_t* id;
+    const uint8_t* tag;
+    const uint64_t* fixed;
+    const uint32_t* aux;
+    const uint8_t* heap;
+    const uint8_t* kind;
+    uint64_t n_rows;
+};
+uint64_t nxg_pub_scratch_bytes(uint64_t n, uint64_t n_slots);
+hipError_t nxg_launch_pub_stage1(const NxgPubTable& tb, const NxgPubBatch& b, uint8_t* scratch,
+                                 hipStream_t s);
+const uint32_t* nxg_pub_flags(uint8_t* scratch);
+hipError_t nxg_launch_pub_stage2(const NxgPubTable& tb, const NxgPubBatch& b, uint8_t* scratch,
+                                 bool dup, bool changed, int ncu, hipStream_t s,
+                                 const uint8_t** mode_out);
 int nxg_occupancy_enc_f64();
 int nxg_occupancy_enc_general();
 

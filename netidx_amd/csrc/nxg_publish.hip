@@ -1,0 +1,338 @@
+// nxg_publish.hip -- the publisher's commit for gfx950: UpdateBatch::commit
+// (netidx/src/publisher/mod.rs:776-845). Queued messages, in batch order:
+//   Update(None, id, v)   if id is published (pb.by_id), From::Update(id, v) goes to every
+//                         subscribed client's batch and becomes the value's `current`;
+//   UpdateChanged(id, v)  the same, only if current != v (Value::eq, netidx-value/src/op.rs:133-172);
+//   Update(Some(cl), ..)  From::Update(id, v) to client cl only.
+// The per-client batches are built by the dispatch kernels (nxg_dispatch.hip) with per-row
+// routing; this file decides the routing of the UpdateChanged rows.
+//
+// UpdateChanged without a sequential loop. Value::eq is an equivalence relation (NaN == NaN,
+// +0 == -0, otherwise exact), and `current` only ever takes values of the rows that are pushed,
+// each of which differs from the value before it. So `current != v` at row i equals
+// `prev(i) != v`, where prev(i) is the previous row of the same Id in the batch (any Update(None)
+// or UpdateChanged row, pushed or not: an unpushed one equals current), or the table's current
+// value when there is none. prev() is found by a stable LSD radix sort of (slot, row) -- only
+// when some slot occurs twice in a batch that has UpdateChanged rows.
+//
+// Equality on the columns covers the scalar tags and text (String, Bytes, Error(String)). A
+// comparison involving Decimal (numeric equality), Array, Map, Error(Value) or Abstract raises
+// `unsupported` (the call fails with NXG_UNSUPPORTED) instead of guessing.
+#include "nxg_device.h"
+#include "nxg_internal.h"
+
+namespace {
+
+constexpr int TPB = 256;
+constexpr int WAVES = TPB / 64;
+constexpr uint32_t NONE = 0xffffffffu;
+constexpr uint32_t SEG = 1024;  // radix pass: items per wave segment (64 per step)
+constexpr uint32_t BINS = 256;
+
+// Value::eq on (tag, fixed, aux, text at heap + fixed): 1 equal, 0 different, -1 unsupported
+NXG_DEV int val_eq(uint32_t ta, uint64_t fa, uint32_t aa, const uint8_t* ha, uint32_t tb,
+                   uint64_t fb, uint32_t ab, const uint8_t* hb) {
+    auto opaque = [](uint32_t t) { return t == 19 || t == 20 || t == 21 || t == 22 || t == 27; };
+    if (opaque(ta) || opaque(tb)) return -1;
+    if (ta != tb) return 0;  // different Typ, or Bool(true) vs Bool(false)
+    switch (ta) {
+    case 8: {  // F32: NaN == NaN, otherwise IEEE ==
+        const float l = __uint_as_float((uint32_t)fa), r = __uint_as_float((uint32_t)fb);
+        return (l != l && r != r) || l == r;
+    }
+    case 9: {
+        const double l = __longlong_as_double((long long)fa), r = __longlong_as_double((long long)fb);
+        return (l != l && r != r) || l == r;
+    }
+    case 10: case 11: return fa == fb && aa == ab;  // DateTime / Duration
+    case 12: case 13: case 18: {                    // String / Bytes / Error(String): contents
+        if (aa != ab) return 0;
+        const uint8_t* p = ha + fa;
+        const uint8_t* q = hb + fb;
+        for (uint32_t k = 0; k < aa; k++)
+            if (p[k] != q[k]) return 0;
+        return 1;
+    }
+    case 14: case 15: case 16: return 1;
+    default: return fa == fb;  // integers (signed sign-extended), V32/Z32 as stored
+    }
+}
+
+struct PubIn {
+    const uint64_t* id;
+    const uint8_t* tag;  // null: all F64 (tag 9)
+    const uint64_t* fixed;
+    const uint32_t* aux;  // null: 0
+    const uint8_t* heap;
+    const uint8_t* kind;
+    uint64_t n;
+};
+
+NXG_DEV uint32_t slot_of(const NxgPubTable& tb, uint64_t x) {
+    return x < tb.n_ids ? tb.slot_of_id[x] : NONE;
+}
+
+}  // namespace
+
+// flags[0]: some slot occurs twice among the non-directed rows; flags[1]: UpdateChanged rows
+// exist; flags[2]: unsupported comparison
+__global__ __launch_bounds__(TPB) void nxg_pub_count_kernel(NxgPubTable tb, PubIn in,
+                                                            uint32_t* __restrict__ cnt,
+                                                            uint32_t* __restrict__ flags) {
+    const uint64_t i = (uint64_t)blockIdx.x * TPB + threadIdx.x;
+    bool dup = false, chg = false;
+    if (i < in.n && in.kind[i] != NXG_PUB_UPDATE_CLIENT) {
+        chg = in.kind[i] == NXG_PUB_UPDATE_CHANGED;
+        const uint32_t s = slot_of(tb, in.id[i]);
+        if (s != NONE) dup = atomicAdd(&cnt[s], 1u) != 0;
+    }
+    if (__any(dup) && (threadIdx.x & 63) == 0) atomicOr(&flags[0], 1u);
+    if (__any(chg) && (threadIdx.x & 63) == 0) atomicOr(&flags[1], 1u);
+}
+
+// radix keys: the slot of every non-directed row with one, else NONE (sorted last, ignored)
+__global__ __launch_bounds__(TPB) void nxg_pub_keys_kernel(NxgPubTable tb, PubIn in,
+                                                           uint32_t* __restrict__ key,
+                                                           uint32_t* __restrict__ val) {
+    const uint64_t i = (uint64_t)blockIdx.x * TPB + threadIdx.x;
+    if (i >= in.n) return;
+    key[i] = in.kind[i] != NXG_PUB_UPDATE_CLIENT ? slot_of(tb, in.id[i]) : NONE;
+    val[i] = (uint32_t)i;
+}
+
+// one stable counting-sort pass on bits [shift, shift+8) of key: per 1024-item segment (one
+// wave) the digit counts, hist[bin * n_seg + seg]
+__global__ __launch_bounds__(TPB) void nxg_radix_count_kernel(const uint32_t* __restrict__ key,
+                                                              uint64_t n, uint32_t shift,
+                                                              uint64_t n_seg,
+                                                              uint32_t* __restrict__ hist) {
+    __shared__ uint32_t cnt_lds[WAVES][BINS];
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t* cnt = cnt_lds[w];
+    for (uint64_t seg = (uint64_t)blockIdx.x * WAVES + w; seg < n_seg;
+         seg += (uint64_t)gridDim.x * WAVES) {
+        for (uint32_t c = lane; c < BINS; c += 64) cnt[c] = 0;
+        wave_lds_order();
+        const uint64_t r0 = seg * SEG, r1 = r0 + SEG < n ? r0 + SEG : n;
+        for (uint64_t i = r0 + lane; i < r1; i += 64) atomicAdd(&cnt[(key[i] >> shift) & 255u], 1u);
+        wave_lds_order();
+        for (uint32_t c = lane; c < BINS; c += 64) hist[(uint64_t)c * n_seg + seg] = cnt[c];
+        wave_lds_order();
+    }
+}
+
+// the pass's scatter: an item's rank within its 64-item step is the number of lower lanes with
+// the same digit (an LDS lane mask per digit), so equal digits keep their order (stable)
+__global__ __launch_bounds__(TPB) void nxg_radix_scatter_kernel(
+    const uint32_t* __restrict__ key, const uint32_t* __restrict__ val, uint64_t n, uint32_t shift,
+    uint64_t n_seg, const uint64_t* __restrict__ off, uint32_t* __restrict__ key_out,
+    uint32_t* __restrict__ val_out) {
+    __shared__ uint64_t cur_lds[WAVES][BINS];
+    __shared__ uint64_t mask_lds[WAVES][BINS];
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint64_t* cur = cur_lds[w];
+    uint64_t* mask = mask_lds[w];
+    const uint64_t lt = (1ull << lane) - 1;
+    for (uint64_t seg = (uint64_t)blockIdx.x * WAVES + w; seg < n_seg;
+         seg += (uint64_t)gridDim.x * WAVES) {
+        for (uint32_t c = lane; c < BINS; c += 64) {
+            cur[c] = off[(uint64_t)c * n_seg + seg];
+            mask[c] = 0;
+        }
+        wave_lds_order();
+        const uint64_t r0 = seg * SEG, r1 = r0 + SEG < n ? r0 + SEG : n;
+        for (uint64_t b = r0; b < r1; b += 64) {
+            const uint64_t i = b + lane;
+            const bool in = i < r1;
+            const uint32_t k = in ? key[i] : 0u, v = in ? val[i] : 0u;
+            const uint32_t d = (k >> shift) & 255u;
+            if (in) atomicOr((unsigned long long*)&mask[d], 1ull << lane);
+            wave_lds_order();
+            const uint64_t m = in ? mask[d] : 0ull;
+            if (in) {
+                const uint64_t e = cur[d] + __popcll(m & lt);
+                key_out[e] = k;
+                val_out[e] = v;
+            }
+            wave_lds_order();
+            if (in && 63u - (uint32_t)__builtin_clzll(m) == lane) {
+                cur[d] += __popcll(m);
+                mask[d] = 0;
+            }
+            wave_lds_order();
+        }
+    }
+}
+
+// prev(row) from the sorted (slot, row) pairs: the preceding pair of the same slot
+__global__ __launch_bounds__(TPB) void nxg_pub_prev_kernel(const uint32_t* __restrict__ key,
+                                                           const uint32_t* __restrict__ val,
+                                                           uint64_t n, uint32_t* __restrict__ prev) {
+    const uint64_t k = (uint64_t)blockIdx.x * TPB + threadIdx.x;
+    if (k >= n || key[k] == NONE) return;
+    prev[val[k]] = (k > 0 && key[k - 1] == key[k]) ? val[k - 1] : NONE;
+}
+
+// routing of every row (nxg_dispatch.hip Route): 0 through the slot, 1 not pushed, 2 one client
+__global__ __launch_bounds__(TPB) void nxg_pub_mode_kernel(NxgPubTable tb, PubIn in,
+                                                           const uint32_t* __restrict__ prev,
+                                                           uint8_t* __restrict__ mode,
+                                                           uint32_t* __restrict__ flags) {
+    const uint64_t i = (uint64_t)blockIdx.x * TPB + threadIdx.x;
+    if (i >= in.n) return;
+    const uint32_t kd = in.kind[i];
+    uint32_t m = kd == NXG_PUB_UPDATE_CLIENT ? 2u : 0u;
+    if (kd == NXG_PUB_UPDATE_CHANGED) {
+        const uint32_t s = slot_of(tb, in.id[i]);
+        if (s != NONE) {  // unpublished Ids stay 0: no slot, counted as unmatched
+            const uint32_t ti = in.tag ? in.tag[i] : 9u;
+            const uint32_t ai = in.aux ? in.aux[i] : 0u;
+            const uint32_t j = prev ? prev[i] : NONE;
+            int eq;
+            if (j != NONE)
+                eq = val_eq(in.tag ? in.tag[j] : 9u, in.fixed[j], in.aux ? in.aux[j] : 0u, in.heap,
+                            ti, in.fixed[i], ai, in.heap);
+            else
+                eq = val_eq(tb.cur_tag ? tb.cur_tag[s] : 9u, tb.cur_fixed[s],
+                            tb.cur_aux ? tb.cur_aux[s] : 0u, tb.cur_heap, ti, in.fixed[i], ai,
+                            in.heap);
+            if (eq < 0) atomicOr(&flags[2], 1u);
+            m = eq > 0 ? 1u : 0u;
+        }
+    }
+    mode[i] = (uint8_t)m;
+}
+
+// ---- launch (host) ------------------------------------------------------------------------------
+// kernels shared with the dispatch's scan (nxg_dispatch.hip)
+__global__ void nxg_disp_scan_block_kernel(const uint32_t* __restrict__ hist, uint64_t M,
+                                           uint64_t* __restrict__ off, uint64_t* __restrict__ bsum);
+__global__ void nxg_disp_scan_top_kernel(uint64_t* __restrict__ bsum, uint64_t nb);
+
+namespace {
+constexpr uint32_t SCAN_B = 256 * 16;  // = nxg_dispatch.hip's scan block
+
+hipError_t exclusive_scan(const uint32_t* hist, uint64_t M, uint64_t* off, uint64_t* bsum,
+                          hipStream_t s);
+__global__ __launch_bounds__(TPB) void add_block_kernel(uint64_t* __restrict__ off, uint64_t M,
+                                                        const uint64_t* __restrict__ bsum) {
+    const uint64_t i = (uint64_t)blockIdx.x * TPB + threadIdx.x;
+    if (i < M) off[i] += bsum[i / SCAN_B];
+}
+hipError_t exclusive_scan(const uint32_t* hist, uint64_t M, uint64_t* off, uint64_t* bsum,
+                          hipStream_t s) {
+    const uint64_t nb = (M + SCAN_B - 1) / SCAN_B;
+    hipLaunchKernelGGL(nxg_disp_scan_block_kernel, dim3((uint32_t)nb), dim3(256), 0, s, hist, M, off,
+                       bsum);
+    hipLaunchKernelGGL(nxg_disp_scan_top_kernel, dim3(1), dim3(1024), 0, s, bsum, nb);
+    hipLaunchKernelGGL(add_block_kernel, dim3((uint32_t)((M + TPB - 1) / TPB)), dim3(TPB), 0, s, off,
+                       M, bsum);
+    return hipGetLastError();
+}
+}  // namespace
+
+uint64_t nxg_pub_scratch_bytes(uint64_t n, uint64_t n_slots) {
+    const uint64_t n_seg = (n + SEG - 1) / SEG;
+    const uint64_t M = n_seg * BINS;
+    const uint64_t nb = (M + SCAN_B - 1) / SCAN_B;
+    // flags, cnt[n_slots], keys/vals x2, prev, mode, hist, off, bsum
+    return 64 + 4 * n_slots + 16 * n + 4 * n + n + 4 * M + 8 * M + 8 * (nb + 1) + 64;
+}
+
+// Stage 1 (flags); the host then decides which of stage 2 runs. Returns the scratch layout.
+struct PubScratch {
+    uint32_t* flags;
+    uint32_t* cnt;
+    uint32_t *k0, *v0, *k1, *v1;
+    uint32_t* prev;
+    uint8_t* mode;
+    uint32_t* hist;
+    uint64_t* off;
+    uint64_t* bsum;
+};
+static PubScratch pub_layout(uint8_t* p, uint64_t n, uint64_t n_slots) {
+    PubScratch sc;
+    const uint64_t n_seg = (n + SEG - 1) / SEG;
+    const uint64_t M = n_seg * BINS;
+    sc.flags = reinterpret_cast<uint32_t*>(p);
+    p += 64;
+    sc.cnt = reinterpret_cast<uint32_t*>(p);
+    p += 4 * n_slots;
+    sc.k0 = reinterpret_cast<uint32_t*>(p);
+    p += 4 * n;
+    sc.v0 = reinterpret_cast<uint32_t*>(p);
+    p += 4 * n;
+    sc.k1 = reinterpret_cast<uint32_t*>(p);
+    p += 4 * n;
+    sc.v1 = reinterpret_cast<uint32_t*>(p);
+    p += 4 * n;
+    sc.prev = reinterpret_cast<uint32_t*>(p);
+    p += 4 * n;
+    sc.hist = reinterpret_cast<uint32_t*>(p);
+    p += 4 * M;
+    p = reinterpret_cast<uint8_t*>((reinterpret_cast<uintptr_t>(p) + 7) & ~uintptr_t(7));
+    sc.off = reinterpret_cast<uint64_t*>(p);
+    p += 8 * M;
+    sc.bsum = reinterpret_cast<uint64_t*>(p);
+    p += 8 * ((M + SCAN_B - 1) / SCAN_B + 1);
+    sc.mode = p;
+    return sc;
+}
+
+hipError_t nxg_launch_pub_stage1(const NxgPubTable& tb, const NxgPubBatch& b, uint8_t* scratch,
+                                 hipStream_t s) {
+    PubScratch sc = pub_layout(scratch, b.n_rows, tb.n_slots);
+    const PubIn in{b.id, b.tag, b.fixed, b.aux, b.heap, b.kind, b.n_rows};
+    hipError_t e;
+    if ((e = hipMemsetAsync(sc.flags, 0, 64, s)) != hipSuccess) return e;
+    if (tb.n_slots && (e = hipMemsetAsync(sc.cnt, 0, 4 * tb.n_slots, s)) != hipSuccess) return e;
+    if (b.n_rows)
+        hipLaunchKernelGGL(nxg_pub_count_kernel, dim3((uint32_t)((b.n_rows + TPB - 1) / TPB)),
+                           dim3(TPB), 0, s, tb, in, sc.cnt, sc.flags);
+    return hipGetLastError();
+}
+
+const uint32_t* nxg_pub_flags(uint8_t* scratch) { return reinterpret_cast<uint32_t*>(scratch); }
+
+// Stage 2: the UpdateChanged routing (prev() by radix sort when `dup`), then returns the mode
+// array (null: no UpdateChanged rows, the kinds route as they are).
+hipError_t nxg_launch_pub_stage2(const NxgPubTable& tb, const NxgPubBatch& b, uint8_t* scratch,
+                                 bool dup, bool changed, int ncu, hipStream_t s,
+                                 const uint8_t** mode_out) {
+    PubScratch sc = pub_layout(scratch, b.n_rows, tb.n_slots);
+    const PubIn in{b.id, b.tag, b.fixed, b.aux, b.heap, b.kind, b.n_rows};
+    const uint64_t n = b.n_rows;
+    const uint32_t gi = (uint32_t)((n + TPB - 1) / TPB);
+    *mode_out = nullptr;
+    if (!changed || n == 0) return hipSuccess;
+    const uint32_t* prev = nullptr;
+    if (dup) {
+        hipLaunchKernelGGL(nxg_pub_keys_kernel, dim3(gi), dim3(TPB), 0, s, tb, in, sc.k0, sc.v0);
+        hipError_t e = hipMemsetAsync(sc.prev, 0xff, 4 * n, s);
+        if (e != hipSuccess) return e;
+        const uint64_t n_seg = (n + SEG - 1) / SEG;
+        const uint64_t M = n_seg * BINS;
+        const uint64_t want = (n_seg + WAVES - 1) / WAVES;
+        const uint32_t g = (uint32_t)(want < (uint64_t)ncu * 8 ? want : (uint64_t)ncu * 8);
+        // keys are < n_slots or NONE: sorting the low `bits` bits (2^bits > n_slots) groups the
+        // slots and puts NONE (all ones) after every slot
+        uint32_t bits = 1;
+        while (bits < 32 && (1ull << bits) <= tb.n_slots) bits++;
+        uint32_t *ka = sc.k0, *va = sc.v0, *kb = sc.k1, *vb = sc.v1;
+        for (uint32_t shift = 0; shift < bits; shift += 8) {
+            hipLaunchKernelGGL(nxg_radix_count_kernel, dim3(g), dim3(TPB), 0, s, ka, n, shift,
+                               n_seg, sc.hist);
+            if ((e = exclusive_scan(sc.hist, M, sc.off, sc.bsum, s)) != hipSuccess) return e;
+            hipLaunchKernelGGL(nxg_radix_scatter_kernel, dim3(g), dim3(TPB), 0, s, ka, va, n, shift,
+                               n_seg, sc.off, kb, vb);
+            uint32_t* t = ka; ka = kb; kb = t;
+            t = va; va = vb; vb = t;
+        }
+        hipLaunchKernelGGL(nxg_pub_prev_kernel, dim3(gi), dim3(TPB), 0, s, ka, va, n, sc.prev);
+        prev = sc.prev;
+    }
+    hipLaunchKernelGGL(nxg_pub_mode_kernel, dim3(gi), dim3(TPB), 0, s, tb, in, prev, sc.mode,
+                       sc.flags);
+    *mode_out = sc.mode;
+    return hipGetLastError();
+}

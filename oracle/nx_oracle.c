@@ -637,3 +637,116 @@ int64_t nxo_dispatch(const uint64_t* id, uint64_t n_rows, uint64_t n_ids,
     free(cur);
     return (int64_t)total;
 }
+
+/* ---- publisher commit (publisher/mod.rs:776-845) ------------------------------------------- */
+/* Value::eq (netidx-value/src/op.rs:133-172) on (tag, fixed, aux, text bytes); -1: unsupported */
+static int val_eq(uint8_t ta, uint64_t fa, uint32_t aa, const uint8_t* ha, uint8_t tb, uint64_t fb,
+                  uint32_t ab, const uint8_t* hb) {
+    if (ta == 20 || ta == 19 || ta == 21 || ta == 22 || ta == 27) return -1;
+    if (tb == 20 || tb == 19 || tb == 21 || tb == 22 || tb == 27) return -1;
+    if (ta != tb) return 0; /* different Typ, or Bool(true) vs Bool(false) */
+    switch (ta) {
+    case 8: { /* F32: NaN == NaN, otherwise IEEE == */
+        float l, r;
+        uint32_t lb = (uint32_t)fa, rb = (uint32_t)fb;
+        memcpy(&l, &lb, 4);
+        memcpy(&r, &rb, 4);
+        return (l != l && r != r) || l == r;
+    }
+    case 9: {
+        double l, r;
+        memcpy(&l, &fa, 8);
+        memcpy(&r, &fb, 8);
+        return (l != l && r != r) || l == r;
+    }
+    case 10: case 11: return fa == fb && aa == ab; /* DateTime / Duration */
+    case 12: case 13: case 18: /* String / Bytes / Error(String): contents */
+        return aa == ab && memcmp(ha + fa, hb + fb, aa) == 0;
+    case 14: case 15: case 16: return 1;
+    default: return fa == fb; /* integers (sign-extended), V32/Z32 as u32 */
+    }
+}
+
+int64_t nxo_publish_commit(const uint64_t* id, const uint8_t* tag, const uint64_t* fixed,
+                           const uint32_t* aux, const uint8_t* heap, const uint8_t* kind,
+                           const uint32_t* to_client, uint64_t n_rows, uint64_t n_ids,
+                           const uint32_t* slot_of_id, uint64_t n_slots,
+                           const uint32_t* slot_client_off, const uint32_t* client,
+                           uint32_t n_clients, const uint8_t* cur_tag, const uint64_t* cur_fixed,
+                           const uint32_t* cur_aux, const uint8_t* cur_heap, uint64_t* client_off,
+                           uint64_t* ent_id, uint64_t* ent_row, uint64_t cap, uint64_t* cur_row,
+                           uint64_t* n_unmatched) {
+    /* current value of each slot: the table's, or the batch row that replaced it */
+    uint64_t* cur = (uint64_t*)malloc((n_slots ? n_slots : 1) * sizeof(uint64_t));
+    uint8_t* emit = (uint8_t*)malloc(n_rows ? n_rows : 1);
+    if (!cur || !emit) return -NXO_CAPACITY;
+    for (uint64_t s = 0; s < n_slots; s++) cur[s] = 0; /* 0: the table's value */
+    for (uint32_t c = 0; c <= n_clients; c++) client_off[c] = 0;
+    uint64_t unmatched = 0;
+    int64_t rc = 0;
+    /* pass 1: which messages are pushed, and the per-client batch lengths */
+    for (uint64_t i = 0; i < n_rows && rc == 0; i++) {
+        emit[i] = 0;
+        if (kind[i] == NXO_PUB_UPDATE_CLIENT) { /* batch.entry(cl).push(Update(id, v)) */
+            if (to_client[i] < n_clients) {
+                emit[i] = 1;
+                client_off[to_client[i] + 1]++;
+            }
+            continue;
+        }
+        const uint32_t s = id[i] < n_ids ? slot_of_id[id[i]] : NXO_NO_SLOT;
+        if (s == NXO_NO_SLOT) { /* pb.by_id.get_mut(&id) == None */
+            unmatched++;
+            continue;
+        }
+        if (kind[i] == NXO_PUB_UPDATE_CHANGED) { /* if pbl.current != v */
+            int eq;
+            if (cur[s]) {
+                const uint64_t j = cur[s] - 1;
+                eq = val_eq(tag[j], fixed[j], aux[j], heap, tag[i], fixed[i], aux[i], heap);
+            } else {
+                eq = val_eq(cur_tag[s], cur_fixed[s], cur_aux[s], cur_heap, tag[i], fixed[i],
+                            aux[i], heap);
+            }
+            if (eq < 0) {
+                rc = -NXO_UNSUPPORTED;
+                break;
+            }
+            if (eq) continue;
+        }
+        emit[i] = 2;
+        for (uint32_t k = slot_client_off[s]; k < slot_client_off[s + 1]; k++)
+            if (client[k] < n_clients) client_off[client[k] + 1]++;
+        cur[s] = i + 1; /* pbl.current = v */
+    }
+    if (rc == 0) {
+        for (uint32_t c = 0; c < n_clients; c++) client_off[c + 1] += client_off[c];
+        if (client_off[n_clients] > cap) rc = -NXO_CAPACITY;
+    }
+    if (rc == 0) {
+        uint64_t* pos = (uint64_t*)malloc((n_clients ? n_clients : 1) * sizeof(uint64_t));
+        for (uint32_t c = 0; c < n_clients; c++) pos[c] = client_off[c];
+        for (uint64_t i = 0; i < n_rows; i++) {
+            if (emit[i] == 1) {
+                const uint64_t e = pos[to_client[i]]++;
+                ent_id[e] = id[i];
+                ent_row[e] = i;
+            } else if (emit[i] == 2) {
+                const uint32_t s = slot_of_id[id[i]];
+                for (uint32_t k = slot_client_off[s]; k < slot_client_off[s + 1]; k++) {
+                    if (client[k] >= n_clients) continue;
+                    const uint64_t e = pos[client[k]]++;
+                    ent_id[e] = id[i];
+                    ent_row[e] = i;
+                }
+            }
+        }
+        free(pos);
+        for (uint64_t s = 0; s < n_slots; s++) cur_row[s] = cur[s];
+        rc = (int64_t)client_off[n_clients];
+    }
+    if (n_unmatched) *n_unmatched = unmatched;
+    free(cur);
+    free(emit);
+    return rc;
+}

@@ -113,6 +113,32 @@ int64_t nxo_dispatch(const uint64_t* id, uint64_t n_rows, uint64_t n_ids,
                      uint64_t* ent_sub, uint64_t* ent_row, uint64_t cap, uint64_t* last_row,
                      uint64_t* n_unmatched);
 
+/*
+ * Publisher commit: UpdateBatch::commit (netidx/src/publisher/mod.rs:776-845). For each queued
+ * message, in batch order (kind[i]):
+ *   NXO_PUB_UPDATE          Update(None, id, v): if id is published (by_id), push Update(id, v)
+ *                           onto every subscribed client's batch, then current = v;
+ *   NXO_PUB_UPDATE_CHANGED  UpdateChanged(id, v): the same, only if current != v (Value::eq,
+ *                           netidx-value/src/op.rs:133-172);
+ *   NXO_PUB_UPDATE_CLIENT   Update(Some(cl), id, v): push Update(id, v) onto client cl's batch.
+ * Values are rows of (tag, fixed, aux) columns with text bytes at heap + fixed (cur_heap for the
+ * current values). Output as nxo_dispatch: per-client CSR (client_off, ent_id, ent_row) in push
+ * order, cur_row[slot] = 1 + the row that became current (0: unchanged). Returns the number of
+ * entries, -NXO_CAPACITY, or -NXO_UNSUPPORTED when an UpdateChanged compares a value whose
+ * equality the columns do not carry (Decimal, Array, Map, Error(Value), Abstract).
+ */
+enum { NXO_PUB_UPDATE = 0, NXO_PUB_UPDATE_CHANGED = 1, NXO_PUB_UPDATE_CLIENT = 2 };
+#define NXO_UNSUPPORTED 10
+int64_t nxo_publish_commit(const uint64_t* id, const uint8_t* tag, const uint64_t* fixed,
+                           const uint32_t* aux, const uint8_t* heap, const uint8_t* kind,
+                           const uint32_t* to_client, uint64_t n_rows, uint64_t n_ids,
+                           const uint32_t* slot_of_id, uint64_t n_slots,
+                           const uint32_t* slot_client_off, const uint32_t* client,
+                           uint32_t n_clients, const uint8_t* cur_tag, const uint64_t* cur_fixed,
+                           const uint32_t* cur_aux, const uint8_t* cur_heap, uint64_t* client_off,
+                           uint64_t* ent_id, uint64_t* ent_row, uint64_t cap, uint64_t* cur_row,
+                           uint64_t* n_unmatched);
+
 #ifdef __cplusplus
 }
 #endif

@@ -57,6 +57,11 @@ def lib():
         L.nxo_datetime_valid.argtypes = [C.c_int64, C.c_uint32]
         L.nxo_utf8_valid.restype = C.c_int
         L.nxo_utf8_valid.argtypes = [C.c_void_p, C.c_uint64]
+        L.nxo_publish_commit.restype = C.c_int64
+        L.nxo_publish_commit.argtypes = [C.c_void_p] * 7 + [C.c_uint64, C.c_uint64, C.c_void_p,
+                                                            C.c_uint64, C.c_void_p, C.c_void_p,
+                                                            C.c_uint32] + [C.c_void_p] * 7 + \
+            [C.c_uint64, C.c_void_p, C.c_void_p]
         L.nxo_dispatch.restype = C.c_int64
         L.nxo_dispatch.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_void_p, C.c_uint64,
                                    C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
@@ -163,3 +168,39 @@ def dispatch(ids, slot_of_id, slot_sub_id, slot_stream_off, stream_chan, slot_ha
     if n < 0:
         raise ValueError(f"dispatch error {-n}")
     return chan_off, ent_sub[:n], ent_row[:n], last_row[: len(slot_sub_id)], int(um[0])
+
+
+PUB_UPDATE, PUB_UPDATE_CHANGED, PUB_UPDATE_CLIENT = 0, 1, 2
+UNSUPPORTED = 10
+
+
+def publish_commit(id, tag, fixed, aux, heap, kind, to_client, slot_of_id, slot_client_off,
+                   client, n_clients, cur_tag, cur_fixed, cur_aux, cur_heap):
+    """nxo_publish_commit (UpdateBatch::commit, publisher/mod.rs:776-845) on numpy arrays.
+    Returns (client_off, ent_id, ent_row, cur_row, n_unmatched), or raises ValueError(code)."""
+    a = {}
+    for k, v, dt in [("id", id, np.uint64), ("tag", tag, np.uint8), ("fixed", fixed, np.uint64),
+                     ("aux", aux, np.uint32), ("heap", heap, np.uint8), ("kind", kind, np.uint8),
+                     ("to", to_client, np.uint32), ("soi", slot_of_id, np.uint32),
+                     ("off", slot_client_off, np.uint32), ("cl", client, np.uint32),
+                     ("ctag", cur_tag, np.uint8), ("cfix", cur_fixed, np.uint64),
+                     ("caux", cur_aux, np.uint32), ("cheap", cur_heap, np.uint8)]:
+        a[k] = np.ascontiguousarray(v if len(v) else np.zeros(1), dt)
+    n = len(id)
+    n_slots = len(slot_client_off) - 1
+    fan = int((a["off"][1:].astype(np.int64) - a["off"][:-1]).max()) if n_slots > 0 else 0
+    cap = max(n * max(fan, 1), 1)
+    client_off = np.zeros(n_clients + 1, np.uint64)
+    ent_id = np.zeros(cap, np.uint64)
+    ent_row = np.zeros(cap, np.uint64)
+    cur_row = np.zeros(max(n_slots, 1), np.uint64)
+    um = np.zeros(1, np.uint64)
+    d = lambda k: a[k].ctypes.data
+    r = lib().nxo_publish_commit(d("id"), d("tag"), d("fixed"), d("aux"), d("heap"), d("kind"),
+                                 d("to"), n, len(slot_of_id), d("soi"), n_slots, d("off"), d("cl"),
+                                 n_clients, d("ctag"), d("cfix"), d("caux"), d("cheap"),
+                                 client_off.ctypes.data, ent_id.ctypes.data, ent_row.ctypes.data,
+                                 cap, cur_row.ctypes.data, um.ctypes.data)
+    if r < 0:
+        raise ValueError(-r)
+    return client_off, ent_id[:r], ent_row[:r], cur_row[:n_slots], int(um[0])
