@@ -361,6 +361,65 @@ def extras_single_gpu(codec, stream, steps, warmup):
         torch.cuda.empty_cache()
     except Exception as e:
         ex["dispatch_1e7"] = {"error": repr(e)}
+    # (e) SURVEY 8a row a23: the publisher's commit (UpdateBatch::commit, publisher/mod.rs:
+    # 776-845) of 10^7 queued f64 updates, each Id published once and subscribed by 1 or 2 of 16
+    # clients; half the rows are UpdateChanged, half of those equal to the current value.
+    try:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import nxo
+        n = 10_000_000
+        n_cl = 16
+        rng = np.random.default_rng(0x5EED0009)
+        ids, vals = synth.f64_columns(n, synth.SEED_F64)
+        fan = 1 + (rng.random(n) < 0.5).astype(np.int64)
+        off = np.concatenate([[0], np.cumsum(fan)]).astype(np.uint32)
+        first = rng.integers(0, n_cl, n)
+        second = (first + 1 + rng.integers(0, n_cl - 1, n)) % n_cl
+        client = np.empty(int(off[-1]), np.uint32)
+        client[off[:-1]] = first
+        two = fan == 2
+        client[off[:-1][two] + 1] = second[two]
+        kind = np.where(np.arange(n) % 2 == 0, 1, 0).astype(np.uint8)
+        same = rng.random(n) < 0.5
+        cur = np.where(same, vals, vals ^ np.uint64(1)).astype(np.uint64)
+        slot_of_id = np.zeros(int(ids.max()) + 1, np.uint32)
+        slot_of_id[ids] = np.arange(n, dtype=np.uint32)
+        tab = netidx_amd.PubTable(slot_of_id, off, client, n_cl, None, cur)  # slot s = row s
+        batch = netidx_amd.columns_from_arrays(ids, vals)
+        dkind = torch.from_numpy(kind).cuda()
+        cap = int(off[-1])
+        for _ in range(2):
+            d = codec.publish_commit(tab, batch, dkind, cap=cap)
+        torch.cuda.synchronize()
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        k = max(3, steps // 4)
+        e0.record(stream)
+        for _ in range(k):
+            d = codec.publish_commit(tab, batch, dkind, cap=cap)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        kms = e0.elapsed_time(e1) / k
+        t0 = time.perf_counter()
+        w = nxo.publish_commit(ids, np.full(n, 9, np.uint8), vals, np.zeros(n, np.uint32),
+                               np.zeros(1, np.uint8), kind, np.zeros(n, np.uint32), slot_of_id,
+                               off, client, n_cl, np.full(n, 9, np.uint8), cur,
+                               np.zeros(n, np.uint32), np.zeros(1, np.uint8))
+        cpu_s = time.perf_counter() - t0
+        assert d.n_entries == len(w[1])
+        assert np.array_equal(d.ent_row[: d.n_entries].cpu().numpy().view(np.uint64), w[2])
+        assert np.array_equal(d.last_row.cpu().numpy().view(np.uint64), w[3])
+        # each row once: Id, value, kind, slot, client offsets, current value; entries written
+        b = n * (8 + 8 + 1 + 4 + 8 + 8) + d.n_entries * (16 + 4) + n * 8
+        ex["publish_commit_1e7"] = {"records": n, "clients": n_cl, "entries": int(d.n_entries),
+                                    "M_updates_s": round(n / (kms / 1e3) / 1e6, 1),
+                                    "call_ms": round(kms, 4),
+                                    "hbm_frac": round(b / (kms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                                    "cpu_oracle_M_updates_s_1core": round(n / cpu_s / 1e6, 1)}
+        del tab, batch, d
+        torch.cuda.empty_cache()
+    except Exception as e:
+        ex["publish_commit_1e7"] = {"error": repr(e)}
     return ex
 
 

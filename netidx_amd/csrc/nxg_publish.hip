@@ -86,8 +86,9 @@ __global__ __launch_bounds__(TPB) void nxg_pub_count_kernel(NxgPubTable tb, PubI
         const uint32_t s = slot_of(tb, in.id[i]);
         if (s != NONE) dup = atomicAdd(&cnt[s], 1u) != 0;
     }
-    if (__any(dup) && (threadIdx.x & 63) == 0) atomicOr(&flags[0], 1u);
-    if (__any(chg) && (threadIdx.x & 63) == 0) atomicOr(&flags[1], 1u);
+    // one flag word for the whole grid: read it first, so only the first few waves contend
+    if (__any(dup) && (threadIdx.x & 63) == 0 && !ld_agent32(&flags[0])) atomicOr(&flags[0], 1u);
+    if (__any(chg) && (threadIdx.x & 63) == 0 && !ld_agent32(&flags[1])) atomicOr(&flags[1], 1u);
 }
 
 // radix keys: the slot of every non-directed row with one, else NONE (sorted last, ignored)
@@ -196,7 +197,7 @@ __global__ __launch_bounds__(TPB) void nxg_pub_mode_kernel(NxgPubTable tb, PubIn
                 eq = val_eq(tb.cur_tag ? tb.cur_tag[s] : 9u, tb.cur_fixed[s],
                             tb.cur_aux ? tb.cur_aux[s] : 0u, tb.cur_heap, ti, in.fixed[i], ai,
                             in.heap);
-            if (eq < 0) atomicOr(&flags[2], 1u);
+            if (eq < 0 && !ld_agent32(&flags[2])) atomicOr(&flags[2], 1u);
             m = eq > 0 ? 1u : 0u;
         }
     }
