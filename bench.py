@@ -15,8 +15,10 @@ Also reported on the same JSON line:
                  events on the codec stream) vs the 8 TB/s HBM3E peak;
   cpu_baseline   the C restatement of the reference decoder (oracle/, 1 core) on this host;
   extras         10^8-record decode (north-star size), mixed-tag decode (config 3), the
-                 host-memory (PCIe-inclusive) decode path, f64 encode (config 4), the oracle on
-                 16 host threads; with N>1, the config-5 sharded encode + RCCL all-gather.
+                 host-memory (PCIe-inclusive) decode path, f64 encode (config 4), subscriber
+                 dispatch and publisher commit, the oracle on 16 host threads; with N>1, the
+                 config-5 sharded encode + RCCL all-gather, the 10^8 batch decoded sharded by
+                 record, and mixed decode at 10^7 records per GPU.
 """
 import argparse
 import json
@@ -35,16 +37,31 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+# Rehearsal of the N > 1 path on a one-GPU box: BENCH_DIST_BACKEND=gloo BENCH_FORCE_DEVICE0=1
+# runs every rank on cuda:0 with gloo collectives over host tensors (the driver's multi-GPU runs
+# use RCCL, one GPU per rank).
+BACKEND = os.environ.get("BENCH_DIST_BACKEND", "nccl")
+
+
+def coll_device():
+    return "cpu" if BACKEND == "gloo" else "cuda"
+
+
 def dist_setup():
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("BENCH_FORCE_DEVICE0") == "1":
+        local = 0
     torch.cuda.set_device(local)
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if BACKEND == "gloo":
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     return world, rank, local
 
 
@@ -56,7 +73,7 @@ def barrier(world):
 
 def max_over_ranks(x, world):
     from netidx_amd import shard
-    return shard.max_over_ranks(x, world, device="cuda")
+    return shard.max_over_ranks(x, world, device=coll_device())
 
 
 def make_f64_wire(codec, n, rank):
@@ -424,9 +441,11 @@ def extras_single_gpu(codec, stream, steps, warmup):
 
 
 def extras_multi_gpu(codec, world, rank, stream):
-    """Config 5: 10^8 records sharded by record; each rank encodes its shard, then an RCCL
-    all-gather (padded to the longest shard, netidx_amd/shard.py) assembles the full frame on
-    every GPU. This is the path's only collective."""
+    """N > 1. Config 5: 10^8 records sharded by record; each rank encodes its shard, then an
+    RCCL all-gather (padded to the longest shard, netidx_amd/shard.py) assembles the full frame
+    on every GPU -- the path's only collective. Then the same 10^8 records decoded sharded by
+    record (strong scaling), and config 3 (mixed) at 10^7 records per GPU (weak scaling); times
+    are the slowest rank's kernel time (HIP events)."""
     import netidx_amd
     import torch
     from netidx_amd import shard, synth
@@ -443,13 +462,45 @@ def extras_multi_gpu(codec, world, rank, stream):
         t0 = time.perf_counter()
         ln = codec.encode_async(cols, None, dout.data_ptr(), dout.numel())
         codec.sync()
-        full, lengths = shard.gather_frames(dout, ln.value, world)
+        src = dout if coll_device() == "cuda" else dout.cpu()
+        full, lengths = shard.gather_frames(src, ln.value, world)
         torch.cuda.synchronize()
         times.append(time.perf_counter() - t0)
     t = max_over_ranks(min(times), world)
-    return {"records": total, "wire_bytes": int(full.numel()), "world": world,
-            "encode_allgather_ms": round(t * 1e3, 3),
-            "M_updates_s": round(total / t / 1e6, 1)}
+    ex = {"encode_allgather_1e8": {"records": total, "wire_bytes": int(full.numel()),
+                                   "world": world, "encode_allgather_ms": round(t * 1e3, 3),
+                                   "M_updates_s": round(total / t / 1e6, 1)}}
+    del cols, dout, full
+    # the same 10^8-record f64 batch decoded sharded by record (strong scaling): each rank
+    # decodes the frame of its own records; the job's time is the slowest rank's
+    from netidx_amd.codec import Columns
+    wire = codec.encode_batch(netidx_amd.columns_from_arrays(ids, vals))
+    out = Columns(n, 0, 0, netidx_amd.LAYOUT_F64, "cuda")
+    wall, kms, st = time_decode(codec, wire, out, n, 10, 2, world, stream)
+    assert st.path == 1 and st.n_rows == n and st.err_kind == 0, st
+    got = out.fixed[:n].cpu().numpy().view("uint64")
+    assert (got == vals).all(), "sharded decode is not bit-exact"
+    kmax = max_over_ranks(kms, world)
+    ex["decode_f64_1e8_sharded"] = {
+        "records": total, "world": world, "records_per_gpu_max": total - total * (world - 1) // world,
+        "kernel_ms_slowest_rank": round(kmax, 4), "M_updates_s": round(total / (kmax / 1e3) / 1e6, 1)}
+    del wire, out
+    # config 3 per GPU (weak scaling): each rank decodes its own 10^7-record mixed batch
+    nm = 10_000_000
+    m = synth.mixed_columns(nm)
+    mc = netidx_amd.columns_from_arrays(m.id, m.fixed, m.tag, m.aux, m.ctag, m.cfixed, m.caux)
+    heap = torch.from_numpy(m.heap.copy()).cuda()
+    wire = codec.encode_batch(mc, heap)
+    out = Columns(nm + 1, len(m.ctag) + 1, 1, netidx_amd.LAYOUT_MIXED, "cuda")
+    wall, kms, st = time_decode(codec, wire, out, nm, 5, 1, world, stream,
+                                flags=netidx_amd.HINT_MIXED)
+    assert st.path == 2 and st.n_rows == nm and st.err_kind == 0, st
+    assert torch.equal(out.id[:nm], mc.id[:nm]) and torch.equal(out.tag[:nm], mc.tag[:nm])
+    kmax = max_over_ranks(kms, world)
+    ex["decode_mixed_1e7_per_gpu"] = {
+        "records_per_gpu": nm, "world": world, "kernel_ms_slowest_rank": round(kmax, 4),
+        "M_updates_s": round(world * nm / (kmax / 1e3) / 1e6, 1)}
+    return ex
 
 
 def main():
@@ -527,7 +578,7 @@ def main():
     elif world > 1 and not args.no_extras:
         ex = extras_multi_gpu(codec, world, rank, stream)
         if rank == 0:
-            line["extras"] = {"encode_allgather_1e8": ex}
+            line["extras"] = ex
     if rank == 0:
         print(json.dumps(line), flush=True)
     codec.close()
