@@ -301,6 +301,72 @@ def extras_single_gpu(codec, stream, steps, warmup):
         torch.cuda.empty_cache()
     except Exception as e:
         ex["decode_f64_1e7_host_pipelined"] = {"error": repr(e)}
+    # (b4) end to end through a loopback TCP socket: the publisher thread encodes on the GPU,
+    # copies the frame to host memory and sends it (flush_buf framing); the subscriber receives
+    # into a socket buffer, reassembles the frame (read_task logic, nxg_frame_reader_*) and
+    # decodes it from host memory (H2D + decode + D2H of the columns). Wall clock per frame.
+    try:
+        import socket
+        import threading
+        n = 10_000_000
+        cols, wire = make_f64_wire(codec, n, 0)
+        W = wire.numel()
+        F = 3
+        pub = netidx_amd.Codec(0)
+        dwire = torch.empty(W + 64, dtype=torch.uint8, device="cuda")
+        hwire = torch.empty(W, dtype=torch.uint8).pin_memory()
+        hout = Columns(n, 0, 0, netidx_amd.LAYOUT_F64, "cpu")
+        srv = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+        srv.bind(("127.0.0.1", 0))
+        srv.listen(1)
+        port = srv.getsockname()[1]
+
+        def publisher():
+            c = socket.create_connection(("127.0.0.1", port))
+            c.setsockopt(socket.SOL_SOCKET, socket.SO_SNDBUF, 8 << 20)
+            for _ in range(F):
+                ln = pub.encode_async(cols, None, dwire.data_ptr(), dwire.numel())
+                pub.sync()
+                hwire[: ln.value].copy_(dwire[: ln.value])
+                c.sendall(netidx_amd.frame_header(ln.value))
+                c.sendall(memoryview(hwire.numpy())[: ln.value])
+            c.close()
+
+        th = threading.Thread(target=publisher)
+        t0 = time.perf_counter()
+        th.start()
+        conn, _ = srv.accept()
+        conn.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 8 << 20)
+        r = netidx_amd.FrameReader()
+        rbuf = bytearray(8 << 20)
+        frames = 0
+        while True:
+            k = conn.recv_into(rbuf)
+            if not k:
+                break
+            r.feed(rbuf, k)
+            while True:
+                v = r.next_view()
+                if v is None:
+                    break
+                st = codec.decode_into(v[0], v[1], hout)
+                assert st.path == 1 and st.n_rows == n
+                frames += 1
+        th.join()
+        dt = (time.perf_counter() - t0) / F
+        conn.close()
+        srv.close()
+        pub.close()
+        assert frames == F and torch.equal(hout.fixed[:n], cols.fixed[:n].cpu())
+        ex["socket_e2e_f64_1e7"] = {
+            "records": n, "frames": F, "ms_per_frame": round(dt * 1e3, 2),
+            "M_updates_s": round(n / dt / 1e6, 1),
+            "path": "GPU encode -> D2H -> TCP loopback -> frame reassembly -> H2D -> GPU decode "
+                    "-> D2H columns"}
+        del cols, wire, dwire, hwire, hout
+        torch.cuda.empty_cache()
+    except Exception as e:
+        ex["socket_e2e_f64_1e7"] = {"error": repr(e)}
     # (c) config 4: f64 encode from device columns, byte-identical round trip
     try:
         n = 10_000_000

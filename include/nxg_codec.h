@@ -248,6 +248,18 @@ void nxg_frame_header(uint32_t payload_len, bool encrypted, uint8_t out[4]);
  * 0 if fewer than 4 bytes are present. */
 uint32_t nxg_frame_parse_header(const uint8_t* buf, uint64_t avail, uint32_t* payload_len,
                                 bool* encrypted);
+/* read_task's frame assembly (channel.rs:379-443), incremental: push the bytes read from the
+ * socket in any pieces; _next hands out each complete frame payload, in order (the pointer stays
+ * valid until the next _push or _free). _next returns 1 with a frame, 0 when the next frame is not
+ * complete yet ("reading more"), -1 on an encrypted frame: this layer has no security context
+ * ("encryption is not supported", channel.rs:420-422; krb5 is out of scope). */
+typedef struct NxgFrameReader NxgFrameReader;
+NxgFrameReader* nxg_frame_reader_new(NetidxError* err);
+void nxg_frame_reader_free(NxgFrameReader* r);
+bool nxg_frame_reader_push(NxgFrameReader* r, const uint8_t* data, uint64_t len, NetidxError* err);
+int nxg_frame_reader_next(NxgFrameReader* r, const uint8_t** payload, uint64_t* len,
+                          NetidxError* err);
+uint64_t nxg_frame_reader_buffered(const NxgFrameReader* r);
 
 #ifdef __cplusplus
 }

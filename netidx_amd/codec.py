@@ -120,6 +120,13 @@ SIGNATURES = {
     "nxg_publish_commit": (C.c_bool, [C.c_void_p, C.c_void_p, C.POINTER(NxgColumns), C.c_void_p,
                                       C.c_void_p, C.c_void_p, C.c_void_p,
                                       C.POINTER(NetidxError)]),
+    "nxg_frame_reader_new": (C.c_void_p, [C.POINTER(NetidxError)]),
+    "nxg_frame_reader_free": (None, [C.c_void_p]),
+    "nxg_frame_reader_push": (C.c_bool, [C.c_void_p, C.c_void_p, C.c_uint64,
+                                         C.POINTER(NetidxError)]),
+    "nxg_frame_reader_next": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p),
+                                        C.POINTER(C.c_uint64), C.POINTER(NetidxError)]),
+    "nxg_frame_reader_buffered": (C.c_uint64, [C.c_void_p]),
     "nxg_frame_split": (C.c_int64, [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64]),
     "nxg_frame_header": (None, [C.c_uint32, C.c_bool, C.c_void_p]),
     "nxg_frame_parse_header": (C.c_uint32, [C.c_void_p, C.c_uint64, C.POINTER(C.c_uint32),
@@ -485,6 +492,60 @@ def _heap_ptr(heap):
 
 
 # ---- host framing (netidx/src/channel.rs) ----------------------------------------------------
+class FrameReader:
+    """read_task's frame assembly (channel.rs:379-443): feed() the bytes read from a socket in
+    any pieces; frames() yields each complete frame payload in order (a copy, as bytes, or
+    written into `into`). An encrypted frame raises CodecError("encryption is not supported")."""
+
+    def __init__(self):
+        err = NetidxError()
+        r = lib().nxg_frame_reader_new(C.byref(err))
+        if not r:
+            _check(False, err)
+        self.r = r
+
+    def close(self):
+        if getattr(self, "r", None):
+            lib().nxg_frame_reader_free(self.r)
+            self.r = None
+
+    def __del__(self):
+        self.close()
+
+    def feed(self, data, n=None):
+        """Append bytes (bytes, bytearray, memoryview or numpy uint8); `n`: only the first n."""
+        if isinstance(data, np.ndarray):
+            ptr, size = data.ctypes.data, data.nbytes
+        elif isinstance(data, bytes):
+            ptr, size = C.cast(C.c_char_p(data), C.c_void_p).value, len(data)
+        else:
+            mv = memoryview(data).cast("B")
+            size = mv.nbytes
+            ptr = C.addressof((C.c_uint8 * size).from_buffer(mv)) if size else 0
+        size = size if n is None else min(size, int(n))
+        err = NetidxError()
+        _check(lib().nxg_frame_reader_push(self.r, C.c_void_p(ptr), size, C.byref(err)), err)
+
+    def next_view(self):
+        """(address, length) of the next complete payload, valid until the next feed(); None
+        if it is not complete yet."""
+        p, n, err = C.c_void_p(), C.c_uint64(), NetidxError()
+        rc = lib().nxg_frame_reader_next(self.r, C.byref(p), C.byref(n), C.byref(err))
+        if rc < 0:
+            _check(False, err)
+        return (p.value or 0, n.value) if rc == 1 else None
+
+    def frames(self):
+        while True:
+            v = self.next_view()
+            if v is None:
+                return
+            yield C.string_at(v[0], v[1]) if v[1] else b""
+
+    def buffered(self):
+        return lib().nxg_frame_reader_buffered(self.r)
+
+
 def frame_split(msg_lens):
     """Frame payload lengths for a queue of encoded messages (WriteChannel::queue_send)."""
     a = np.ascontiguousarray(msg_lens, np.uint64)

@@ -1000,4 +1000,66 @@ uint32_t nxg_frame_parse_header(const uint8_t* buf, uint64_t avail, uint32_t* pa
     return 4;
 }
 
+// ---- read_task's frame assembly (channel.rs:379-443) -------------------------------------------
+struct NxgFrameReader {
+    std::vector<uint8_t> buf;  // bytes read from the socket, not yet handed out
+    size_t head = 0;           // start of the unconsumed bytes
+};
+
+NxgFrameReader* nxg_frame_reader_new(NetidxError* err) {
+    try {
+        return new NxgFrameReader();
+    } catch (...) {
+        set_err(err, "out of memory");
+        return nullptr;
+    }
+}
+
+void nxg_frame_reader_free(NxgFrameReader* r) { delete r; }
+
+bool nxg_frame_reader_push(NxgFrameReader* r, const uint8_t* data, uint64_t len,
+                           NetidxError* err) {
+    if (!r || (len && !data)) {
+        set_err(err, "null argument");
+        return false;
+    }
+    // drop what was handed out before growing (payload pointers from _next end here)
+    if (r->head) {
+        r->buf.erase(r->buf.begin(), r->buf.begin() + (ptrdiff_t)r->head);
+        r->head = 0;
+    }
+    try {
+        r->buf.insert(r->buf.end(), data, data + len);
+    } catch (...) {
+        set_err(err, "out of memory");
+        return false;
+    }
+    return true;
+}
+
+int nxg_frame_reader_next(NxgFrameReader* r, const uint8_t** payload, uint64_t* len,
+                          NetidxError* err) {
+    if (!r || !payload || !len) {
+        set_err(err, "null argument");
+        return -1;
+    }
+    const uint64_t avail = r->buf.size() - r->head;
+    uint32_t plen = 0;
+    bool enc = false;
+    if (!nxg_frame_parse_header(r->buf.data() + r->head, avail, &plen, &enc)) return 0;
+    if (avail - 4 < plen) return 0;  // "less than batch len, reading more"
+    if (enc) {  // no security context here (krb5 is out of scope): channel.rs:420-422
+        set_err(err, "encryption is not supported");
+        return -1;
+    }
+    *payload = r->buf.data() + r->head + 4;
+    *len = plen;
+    r->head += 4 + (size_t)plen;
+    return 1;
+}
+
+uint64_t nxg_frame_reader_buffered(const NxgFrameReader* r) {
+    return r ? r->buf.size() - r->head : 0;
+}
+
 }  // extern "C"
