@@ -134,7 +134,7 @@ __global__ __launch_bounds__(TPB) void nxg_f64_emit_kernel(
             const uint32_t n = chunk_walk<true>(buf, xa, lane, pslot, bad);
             const uint32_t inc = wave_incl_scan(n);
             const uint32_t off = inc - n;
-            const uint32_t ntile = __shfl(inc, 63, 64);
+            const uint32_t ntile = wave_last(inc);
             for (uint32_t q = 0; q < n; q++) rpos[off + q] = pslot[lane * SLOTS + q];
             wave_lds_order();
             uint32_t lim = ntile;

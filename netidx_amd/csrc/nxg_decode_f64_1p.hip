@@ -190,7 +190,7 @@ NXG_DEV void f64_work(const uint8_t* __restrict__ wire, uint64_t W, uint64_t nt,
             // decoding into registers as it goes (at most MAXL records; each fully checked:
             // variant, id varint, value tag); it must land exactly on the next merge point
             const uint32_t xa = chunk_merge(img, t, W, lane);
-            const uint32_t xb = __shfl_down(xa, 1, 64);
+            const uint32_t xb = wave_next(xa);
             const bool owner = lane != 63;  // lane 63's merge point is the next tile's first
             bool bad = (xa == FAIL) | (owner & ((xb == FAIL) | (xa > xb)));
             const uint64_t t0 = t * f64dec::STRIDE;
@@ -231,7 +231,7 @@ NXG_DEV void f64_work(const uint8_t* __restrict__ wire, uint64_t W, uint64_t nt,
             }
             P1_STAMP(1);
             const uint32_t inc = wave_incl_scan(n);
-            const uint32_t ntile = __shfl(inc, 63, 64);
+            const uint32_t ntile = wave_last(inc);
             // the decoded records replace the image (u32 ids at 0, u64 values at VALOFF, in
             // record order) once every lane has read its records
             wave_lds_order();

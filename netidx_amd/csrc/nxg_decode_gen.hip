@@ -931,9 +931,9 @@ NXG_DEV void emit_tile_lanes(const Src& s, const Sink& sink, const ColsDesc& col
             myrow = row + rin - nr;
             myctl = ctl + kin - nk;
             mych = child + cin - nch;
-            row += __shfl(rin, 63, 64);
-            ctl += __shfl(kin, 63, 64);
-            child += __shfl(cin, 63, 64);
+            row += wave_last(rin);
+            ctl += wave_last(kin);
+            child += wave_last(cin);
         }
         const bool act = ph == 1 ? has : recount;
         uint64_t pos = act ? c + lw_off(lw) : stop;
@@ -1025,7 +1025,7 @@ __global__ __launch_bounds__(TPB) void nxg_gen_emit_kernel(
         }
         const uint32_t nm = nr + nk;
         const uint32_t minc = wave_incl_scan(nm);
-        const uint32_t nmsg = __shfl(minc, 63, 64);
+        const uint32_t nmsg = wave_last(minc);
         const uint64_t row_t = row, ctl_t = ctl, child_t = child;
         row += wave_sum<uint32_t>(nr);
         ctl += wave_sum<uint32_t>(nk);
@@ -1067,9 +1067,9 @@ __global__ __launch_bounds__(TPB) void nxg_gen_emit_kernel(
                 T.ridx[m] = upd ? rcar + ri - 1 : kcar + ki - 1;
                 T.cb[m] = upd ? ccar + ci - kids : rcar + ri;
             }
-            rcar += __shfl(ri, 63, 64);
-            kcar += __shfl(ki, 63, 64);
-            ccar += __shfl(ci, 63, 64);
+            rcar += wave_last(ri);
+            kcar += wave_last(ki);
+            ccar += wave_last(ci);
 #pragma unroll
             for (int kk = 0; kk < K_N; kk++) kcnt[kk] += __popcll(__ballot(in && k == (uint32_t)kk));
         }

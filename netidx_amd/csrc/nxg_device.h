@@ -64,22 +64,61 @@ NXG_DEV void wave_lds_order() {
 // ---- wave/block scans (wave64) -----------------------------------------------------------
 NXG_DEV uint32_t lane_id() { return __lane_id(); }
 
+// Wave scans with DPP (no LDS round trips; __shfl_up/__shfl_xor would compile to
+// ds_bpermute_b32, one dependent LDS trip per step). The GFX9 inclusive scan: row_shr 1, 2, 4, 8
+// within each 16-lane row, then row_bcast:15 into rows 1 and 3, row_bcast:31 into rows 2 and 3.
+// A lane whose source is outside its row reads 0 (old = 0, bound_ctrl off). All 64 lanes must be
+// active.
+template <int CTRL, int ROWS>
+NXG_DEV uint32_t dpp0(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROWS, 0xf, false);
+}
+template <int CTRL, int ROWS>
+NXG_DEV uint64_t dpp0_64(uint64_t v) {
+    return (uint64_t)dpp0<CTRL, ROWS>((uint32_t)v) | ((uint64_t)dpp0<CTRL, ROWS>((uint32_t)(v >> 32)) << 32);
+}
 template <typename T>
 NXG_DEV T wave_incl_scan(T v) {
-    const uint32_t l = lane_id();
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        T o = __shfl_up(v, d, 64);
-        if (l >= (uint32_t)d) v += o;
+    static_assert(sizeof(T) == 4 || sizeof(T) == 8, "32- or 64-bit");
+    if constexpr (sizeof(T) == 4) {
+        uint32_t x = (uint32_t)v;
+        x += dpp0<0x111, 0xf>(x);
+        x += dpp0<0x112, 0xf>(x);
+        x += dpp0<0x114, 0xf>(x);
+        x += dpp0<0x118, 0xf>(x);
+        x += dpp0<0x142, 0xa>(x);
+        x += dpp0<0x143, 0xc>(x);
+        return (T)x;
+    } else {
+        uint64_t x = (uint64_t)v;
+        x += dpp0_64<0x111, 0xf>(x);
+        x += dpp0_64<0x112, 0xf>(x);
+        x += dpp0_64<0x114, 0xf>(x);
+        x += dpp0_64<0x118, 0xf>(x);
+        x += dpp0_64<0x142, 0xa>(x);
+        x += dpp0_64<0x143, 0xc>(x);
+        return (T)x;
     }
-    return v;
+}
+
+// the next lane's value (lane 63: 0) -- DPP wave_shl:1
+NXG_DEV uint32_t wave_next(uint32_t v) { return dpp0<0x130, 0xf>(v); }
+
+// lane 63's value, wave-uniform (a scalar read, no LDS)
+template <typename T>
+NXG_DEV T wave_last(T v) {
+    if constexpr (sizeof(T) == 4) {
+        return (T)__builtin_amdgcn_readlane((int)v, 63);
+    } else {
+        const uint64_t x = (uint64_t)v;
+        return (T)((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, 63) |
+                   ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), 63) << 32));
+    }
 }
 
 template <typename T>
 NXG_DEV T wave_sum(T v) {
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
-    return v;
+    return wave_last<T>(wave_incl_scan<T>(v));
 }
 
 // ---- decoupled look-back with a wide window ---------------------------------------------------

@@ -310,7 +310,7 @@ __global__ __launch_bounds__(TPB) void nxg_disp_scatter_kernel(
                         ent_row[e] = i;
                     }
                 }
-                const uint64_t nb = base + __shfl(inc, 63, 64);
+                const uint64_t nb = base + wave_last(inc);
                 wave_lds_order();
                 if (lane == 0) {
                     if (lds) cur[d] = nb;
