@@ -93,11 +93,8 @@ NXG_DEV void f64_scan(uint64_t nt, const uint64_t* agg, uint64_t* pre, uint32_t 
             const uint64_t i = c + (uint64_t)k * TPB1 + tid;
             if (i < nt && lb_flag(v[k], epoch) == 0) fu = i < fu ? i : fu;
         }
-#pragma unroll
-        for (int d = 32; d >= 1; d >>= 1) {
-            const uint64_t o = __shfl_xor(fu, d, 64);
-            fu = o < fu ? o : fu;
-        }
+        // tile indices fit 32 bits (nt < 2^32: frames are < 2^44 bytes)
+        fu = wave_min_u32(fu < 0xffffffffull ? (uint32_t)fu : 0xffffffffu);
         if (lane == 0) wmin[w] = fu;
 #pragma unroll
         for (int k = 0; k < SCAN_K; k++) stg[k * TPB1 + tid] = v[k] & kValMask;

@@ -101,6 +101,21 @@ NXG_DEV T wave_incl_scan(T v) {
     }
 }
 
+// wave minimum (uniform), by the same DPP pattern with all-ones as the identity
+template <int CTRL, int ROWS>
+NXG_DEV uint32_t dppmax(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)v, CTRL, ROWS, 0xf, false);
+}
+NXG_DEV uint32_t wave_min_u32(uint32_t x) {
+    x = min(x, dppmax<0x111, 0xf>(x));
+    x = min(x, dppmax<0x112, 0xf>(x));
+    x = min(x, dppmax<0x114, 0xf>(x));
+    x = min(x, dppmax<0x118, 0xf>(x));
+    x = min(x, dppmax<0x142, 0xa>(x));
+    x = min(x, dppmax<0x143, 0xc>(x));
+    return (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+}
+
 // the next lane's value (lane 63: 0) -- DPP wave_shl:1
 NXG_DEV uint32_t wave_next(uint32_t v) { return dpp0<0x130, 0xf>(v); }
 

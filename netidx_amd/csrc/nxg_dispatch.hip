@@ -103,14 +103,7 @@ NXG_DEV uint32_t count_chan(const NxgSubTable& tb, const Row& r, uint32_t d) {
     return n;
 }
 
-NXG_DEV uint32_t wave_min(uint32_t v) {
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) {
-        const uint32_t o = __shfl_xor(v, d, 64);
-        v = o < v ? o : v;
-    }
-    return v;
-}
+NXG_DEV uint32_t wave_min(uint32_t v) { return wave_min_u32(v); }
 
 }  // namespace
 
