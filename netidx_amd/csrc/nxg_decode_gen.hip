@@ -465,7 +465,7 @@ NXG_DEV RunSum run_tiles(const uint8_t* __restrict__ wire, uint64_t W, uint64_t 
 }  // namespace
 
 // ---- pass 1: count ---------------------------------------------------------------------------
-__global__ __launch_bounds__(TPB) void nxg_gen_count_kernel(
+__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4))) void nxg_gen_count_kernel(
     const uint8_t* __restrict__ wire, uint64_t W, uint64_t nt, uint32_t* __restrict__ lws,
     uint64_t* __restrict__ runs, DevStatus* __restrict__ st, DevStatus* zst, uint64_t* __restrict__ fix) {
     zero_status(zst);
@@ -694,8 +694,9 @@ constexpr int FIX_WORDS = 5;  // work list entry: first tile, end tile, row, con
 struct EmitLds {
     uint16_t mpos[MAXM];  // message start, tile-relative
     uint8_t cls[MAXM];    // class | 0x80 for an Update
-    uint32_t ridx[MAXM];  // row (Update) or control-message index within the tile
-    uint32_t cb[MAXM];    // first child slot (Update) or the row it precedes (control)
+    uint16_t ridx[MAXM];  // row (Update) or control-message index within the tile
+    uint16_t cb[MAXM];    // first child slot (Update; < 2^16: a message's elements are >= 1
+                          // byte and lie in the 5 KiB image) or the row it precedes (control)
     uint16_t bucket[MAXM];
 };
 
@@ -977,7 +978,7 @@ NXG_DEV void emit_tile_lanes(const Src& s, const Sink& sink, const ColsDesc& col
 
 }  // namespace
 
-__global__ __launch_bounds__(TPB) void nxg_gen_emit_kernel(
+__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4))) void nxg_gen_emit_kernel(
     const uint8_t* __restrict__ wire, uint64_t W, uint64_t nt, const uint32_t* __restrict__ lws,
     const uint64_t* __restrict__ base, ColsDesc cols, DevStatus* __restrict__ st,
     uint64_t* __restrict__ fix) {
@@ -1064,8 +1065,8 @@ __global__ __launch_bounds__(TPB) void nxg_gen_emit_kernel(
             const uint32_t ci = wave_incl_scan(in ? kids : 0u);
             if (in) {  // control messages keep the row they precede in cb
                 T.cls[m] = (uint8_t)(k | (upd ? 0x80u : 0u));
-                T.ridx[m] = upd ? rcar + ri - 1 : kcar + ki - 1;
-                T.cb[m] = upd ? ccar + ci - kids : rcar + ri;
+                T.ridx[m] = (uint16_t)(upd ? rcar + ri - 1 : kcar + ki - 1);
+                T.cb[m] = (uint16_t)(upd ? ccar + ci - kids : rcar + ri);
             }
             rcar += wave_last(ri);
             kcar += wave_last(ki);
@@ -1189,7 +1190,9 @@ int nxg_dec_gen_wgs(int ncu) {
         hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, nxg_gen_emit_kernel, TPB, 0) !=
             hipSuccess)
         return ncu;
-    const int occ = a < b ? a : b;
+    // the passes share the run partition, so one grid for both; neither waits on another
+    // workgroup, so the grid follows the larger occupancy (extra count workgroups just queue)
+    const int occ = a > b ? a : b;
     int g = ncu * (occ > 0 ? occ : 1);
     return g < gdec2::MAX_RUNS / WAVES ? g : gdec2::MAX_RUNS / WAVES;
 }
