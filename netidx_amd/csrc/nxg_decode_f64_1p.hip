@@ -47,7 +47,10 @@ __device__ unsigned long long g_1p_cyc[8];     // per-phase s_memtime cycles, al
 
 namespace {
 
-constexpr int TPB1 = 256;
+#ifndef NXG_1P_TPB
+#define NXG_1P_TPB 256
+#endif
+constexpr int TPB1 = NXG_1P_TPB;
 constexpr int WAVES1 = TPB1 / 64;
 #ifndef NXG_1P_LAG
 #define NXG_1P_LAG 1

@@ -25,9 +25,9 @@ namespace p1 {
 namespace p1n {  // the product build (no stamps)
 #include "../netidx_amd/csrc/nxg_decode_f64_1p.hip"
 }
-#undef NXG_1P_LAG
-#define NXG_1P_LAG 2
-namespace p1l3 {  // lag 2 (three slots per wave, three workgroups per CU)
+#undef NXG_1P_TPB
+#define NXG_1P_TPB 192
+namespace p1l3 {  // 3-wave workgroups (six per CU by LDS)
 #include "../netidx_amd/csrc/nxg_decode_f64_1p.hip"
 }
 thread_local DevStatus* nxg_zero_slot = nullptr;
@@ -187,7 +187,7 @@ int main(int argc, char** argv) {
     printf("records=%llu wire=%llu bytes\n", (unsigned long long)N, (unsigned long long)W);
     timeit("dec2p", dec(0), true);
     timeit("dec1p_prod", dec(2), true);
-    timeit("dec1p_lag2", dec(3), true);
+    timeit("dec1p_tpb192", dec(3), true);
     const char* names[4] = {"dec1p", "1p_nowait", "1p_nostore", "1p_nowait_nostore"};
     for (uint32_t f = 0; f < 4; f++) {
         CK(hipMemcpyToSymbol(HIP_SYMBOL(p1::g_1p_dbg), &f, sizeof f));
