@@ -25,11 +25,11 @@ namespace p1 {
 namespace p1n {  // the product build (no stamps)
 #include "../netidx_amd/csrc/nxg_decode_f64_1p.hip"
 }
-#undef NXG_1P_TPB
-#define NXG_1P_TPB 192
-namespace p1l3 {  // 3-wave workgroups (six per CU by LDS)
+#define NXG_1P_LAG 2
+namespace p1l3 {  // LAG 2: three LDS slots per wave (three 4-wave workgroups per CU by LDS)
 #include "../netidx_amd/csrc/nxg_decode_f64_1p.hip"
 }
+#undef NXG_1P_LAG
 thread_local DevStatus* nxg_zero_slot = nullptr;
 
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
@@ -125,8 +125,9 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(dw, w.data(), W, hipMemcpyHostToDevice));
     const uint64_t ntiles = (W + 3967) / 3968 + 1;  // >= the 1p kernel's tiles
     uint64_t* tstat;
-    CK(hipMalloc(&tstat, 2 * ntiles * 8 + 64));
-    CK(hipMemset(tstat, 0, 2 * ntiles * 8 + 64));
+    const size_t tstat_bytes = (2 * ntiles + 512 * 16) * 8 + 64;  // agg, pre, dummy lines
+    CK(hipMalloc(&tstat, tstat_bytes));
+    CK(hipMemset(tstat, 0, tstat_bytes));
     uint32_t epoch = 0;
     uint8_t* moff;
     CK(hipMalloc(&moff, 64 * (W / 4032 + 2)));
@@ -183,11 +184,12 @@ int main(int argc, char** argv) {
             }
         };
     };
-    printf("wgs=%d 1p_wgs=%d\n", prod::nxg_dec_f64_wgs(ncu), p1::nxg_dec_f64_1p_wgs(ncu));
+    printf("wgs=%d 1p_wgs=%d (probe build) %d (product) %d (lag2)\n", prod::nxg_dec_f64_wgs(ncu),
+           p1::nxg_dec_f64_1p_wgs(ncu), p1n::nxg_dec_f64_1p_wgs(ncu), p1l3::nxg_dec_f64_1p_wgs(ncu));
     printf("records=%llu wire=%llu bytes\n", (unsigned long long)N, (unsigned long long)W);
     timeit("dec2p", dec(0), true);
     timeit("dec1p_prod", dec(2), true);
-    timeit("dec1p_tpb192", dec(3), true);
+    timeit("dec1p_lag2", dec(3), true);
     const char* names[4] = {"dec1p", "1p_nowait", "1p_nostore", "1p_nowait_nostore"};
     for (uint32_t f = 0; f < 4; f++) {
         CK(hipMemcpyToSymbol(HIP_SYMBOL(p1::g_1p_dbg), &f, sizeof f));
