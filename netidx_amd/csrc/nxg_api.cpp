@@ -417,7 +417,7 @@ bool frame_to_device(NxgCtx* c, const uint8_t* frame, uint64_t len, const uint8_
 bool enqueue_encode(NxgCtx* c, const NxgColumns* in, const uint8_t* heap, uint8_t* out,
                     uint64_t cap, DevStatus* st, NetidxError* err) {
     if (in->layout == NXG_LAYOUT_F64) {
-        const uint64_t nt = (in->n_rows + f64enc::TILE - 1) / f64enc::TILE;
+        const uint64_t nt = nxg_enc_f64_tiles(in->n_rows);
         if (!ensure_tstat(c, nt, err)) return false;
         HIPCHK(nxg_launch_enc_f64(in->id, in->fixed, in->n_rows, out, cap, c->tstat, c->epoch, st,
                                   c->grid_enc_f64, c->stream));

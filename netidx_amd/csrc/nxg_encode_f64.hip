@@ -6,19 +6,36 @@
 // (netidx-derive/src/lib.rs:289-381) + Value::encode (netidx-value/src/lib.rs:404-407) write:
 //     varint(L) 04 varint(id) 09 f64be,   L = lw(1 + vl(id) + 9)
 //
-// One tile = 1024 records: 256 threads x 4 records.
+// One tile = TPB threads x RPT records.
 // 1. Each thread loads its records (16-byte vector loads) and computes their lengths.
 // 2. A block scan gives each record's offset inside the tile.
 // 3. A decoupled look-back over tile byte counts gives the tile's output offset.
-// 4. Records are serialised into LDS at their final 16-byte phase. The tile then leaves LDS as
-//    aligned 16-byte stores, plus byte stores for the two partial 16-byte blocks it shares with
-//    its neighbours.
+// 4. Records are serialised into LDS at their final 16-byte phase. The tile then leaves LDS as aligned 16-byte stores, plus byte stores for the two partial
+//    16-byte blocks it shares with its neighbours. The staging holds STGB bytes per record; a
+//    tile that needs more (ids >= 2^28 throughout) writes its records to global memory byte by
+//    byte instead.
 #include "nxg_device.h"
 
 using namespace f64enc;
 
 namespace {
-constexpr int MAXB_ALL = TILE * 21 + 32;  // worst case: 10-byte ids -> 21-byte records
+// Tuning (scripts/probe_enc.hip, profiles/r01f_probe_enc_1e7.log; 10^7 records on one box):
+// 4 -> 8 records per thread 0.098 -> 0.081 ms (6, 12, 16: 0.087, 0.086, 0.098), staging 21 -> 15
+// bytes per record (5 workgroups per CU by LDS instead of 3), nontemporal frame stores
+// 0.081 -> 0.070 ms; nontemporal column loads were slower (0.094), and so were dword LDS writes.
+#ifndef NXG_ENC_RPT
+#define NXG_ENC_RPT 8
+#endif
+#ifndef NXG_ENC_STGB
+#define NXG_ENC_STGB 15
+#endif
+#ifndef NXG_ENC_NT
+#define NXG_ENC_NT 2  // bit 0: nontemporal column loads, bit 1: nontemporal frame stores
+#endif
+constexpr int ERPT = NXG_ENC_RPT;
+constexpr int ETILE = TPB * ERPT;
+constexpr int MAXB_ALL = ETILE * NXG_ENC_STGB + 32;
+static_assert(NXG_ENC_STGB >= 12 && NXG_ENC_STGB <= 21, "staging bytes per record");
 
 NXG_DEV uint32_t rec_len(uint64_t id) { return (uint32_t)lwlen(1 + vl64(id) + 9); }
 
@@ -37,6 +54,22 @@ NXG_DEV uint32_t put_rec(uint8_t* stg, uint32_t o, uint64_t id, uint64_t val) {
     for (int i = 7; i >= 0; i--) stg[o++] = (uint8_t)(val >> (8 * i));
     return o;
 }
+
+// The slow path for a tile whose records exceed the staging: bytes straight to the frame.
+NXG_DEV void put_rec_global(uint8_t* out, uint64_t o, uint64_t id, uint64_t val) {
+    const uint32_t L = rec_len(id);
+    out[o++] = (uint8_t)L;
+    out[o++] = 4;
+    uint64_t v = id;
+    while (v >= 0x80) {
+        out[o++] = (uint8_t)((v & 0x7f) | 0x80);
+        v >>= 7;
+    }
+    out[o++] = (uint8_t)v;
+    out[o++] = 9;
+#pragma unroll
+    for (int i = 7; i >= 0; i--) out[o++] = (uint8_t)(val >> (8 * i));
+}
 }  // namespace
 
 __global__ __launch_bounds__(TPB) void nxg_enc_f64_kernel(
@@ -50,25 +83,36 @@ __global__ __launch_bounds__(TPB) void nxg_enc_f64_kernel(
 
     const uint32_t tid = threadIdx.x, lane = tid & 63;
     for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        const uint64_t r0 = (uint64_t)tile * TILE + (uint64_t)tid * RPT;
-        uint64_t ids[RPT], vals[RPT];
-        if (r0 + RPT <= n) {
-            const ulonglong2 a = *reinterpret_cast<const ulonglong2*>(id + r0);
-            const ulonglong2 b = *reinterpret_cast<const ulonglong2*>(id + r0 + 2);
-            const ulonglong2 c = *reinterpret_cast<const ulonglong2*>(val + r0);
-            const ulonglong2 d = *reinterpret_cast<const ulonglong2*>(val + r0 + 2);
-            ids[0] = a.x; ids[1] = a.y; ids[2] = b.x; ids[3] = b.y;
-            vals[0] = c.x; vals[1] = c.y; vals[2] = d.x; vals[3] = d.y;
+        const uint64_t r0 = (uint64_t)tile * ETILE + (uint64_t)tid * ERPT;
+        uint64_t ids[ERPT], vals[ERPT];
+        if (r0 + ERPT <= n) {
+#pragma unroll
+            for (int k = 0; k < ERPT; k += 2) {
+                if (NXG_ENC_NT & 1) {
+                    typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+                    const u64x2 a = __builtin_nontemporal_load(
+                        reinterpret_cast<const u64x2*>(id + r0 + k));
+                    const u64x2 c = __builtin_nontemporal_load(
+                        reinterpret_cast<const u64x2*>(val + r0 + k));
+                    ids[k] = a.x; ids[k + 1] = a.y;
+                    vals[k] = c.x; vals[k + 1] = c.y;
+                } else {
+                    const ulonglong2 a = *reinterpret_cast<const ulonglong2*>(id + r0 + k);
+                    const ulonglong2 c = *reinterpret_cast<const ulonglong2*>(val + r0 + k);
+                    ids[k] = a.x; ids[k + 1] = a.y;
+                    vals[k] = c.x; vals[k + 1] = c.y;
+                }
+            }
         } else {
 #pragma unroll
-            for (int k = 0; k < RPT; k++) {
+            for (int k = 0; k < ERPT; k++) {
                 ids[k] = r0 + k < n ? id[r0 + k] : 0;
                 vals[k] = r0 + k < n ? val[r0 + k] : 0;
             }
         }
         uint32_t mylen = 0;
 #pragma unroll
-        for (int k = 0; k < RPT; k++) mylen += (r0 + k < n) ? rec_len(ids[k]) : 0u;
+        for (int k = 0; k < ERPT; k++) mylen += (r0 + k < n) ? rec_len(ids[k]) : 0u;
         uint32_t tbytes;
         const uint32_t off = block_excl_scan<uint32_t, TPB>(mylen, scan_tmp, &tbytes);
         if (tid == 0) st_agent(&tstat[tile], lb_word(tile == 0 ? kFlagInc : kFlagAgg, epoch, tbytes));
@@ -88,23 +132,37 @@ __global__ __launch_bounds__(TPB) void nxg_enc_f64_kernel(
         const uint64_t base = sh_base;
         const uint32_t phase = (uint32_t)(base & 15u);
 
-        if (out) {
+        const uint64_t end = base + tbytes;
+        if (out && end > cap) {
+            if (tid == 0) atomicOr(&st->capacity, 1u);
+        } else if (out && phase + tbytes > (uint32_t)(MAXB_ALL - 16)) {
+            // more bytes than the staging holds: straight to the frame, byte by byte
+            uint64_t o = base + off;
+#pragma unroll
+            for (int k = 0; k < ERPT; k++)
+                if (r0 + k < n) {
+                    put_rec_global(out, o, ids[k], vals[k]);
+                    o += rec_len(ids[k]);
+                }
+        } else if (out) {
             uint32_t o = phase + off;
 #pragma unroll
-            for (int k = 0; k < RPT; k++)
+            for (int k = 0; k < ERPT; k++)
                 if (r0 + k < n) o = put_rec(stg, o, ids[k], vals[k]);
             __syncthreads();
-            const uint64_t end = base + tbytes;
-            if (end > cap) {
-                if (tid == 0) atomicOr(&st->capacity, 1u);
-            } else if (tbytes) {
+            if (tbytes) {
                 const uint64_t gb0 = base & ~15ull;
                 const uint32_t nblk = (uint32_t)((end - gb0 + 15) >> 4);
                 for (uint32_t b = tid; b < nblk; b += TPB) {
                     const uint64_t g = gb0 + 16ull * b;
                     const uint8_t* src = stg + 16 * b;
                     if (g >= base && g + 16 <= end) {
-                        *reinterpret_cast<uint4*>(out + g) = *reinterpret_cast<const uint4*>(src);
+                        typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+                        const u32x4v x = *reinterpret_cast<const u32x4v*>(src);
+                        if (NXG_ENC_NT & 2)
+                            __builtin_nontemporal_store(x, reinterpret_cast<u32x4v*>(out + g));
+                        else
+                            *reinterpret_cast<u32x4v*>(out + g) = x;
                     } else {
                         for (int k = 0; k < 16; k++)
                             if (g + k >= base && g + k < end) out[g + k] = src[k];
@@ -120,10 +178,12 @@ __global__ __launch_bounds__(TPB) void nxg_enc_f64_kernel(
     }
 }
 
+uint64_t nxg_enc_f64_tiles(uint64_t n) { return (n + ETILE - 1) / ETILE; }
+
 hipError_t nxg_launch_enc_f64(const uint64_t* id, const uint64_t* val, uint64_t n, uint8_t* out,
                               uint64_t cap, uint64_t* tstat, uint32_t epoch, DevStatus* st,
                               int grid, hipStream_t s) {
-    const uint64_t nt = (n + TILE - 1) / TILE;
+    const uint64_t nt = nxg_enc_f64_tiles(n);
     if (nt == 0) return hipSuccess;
     const uint64_t g = grid <= 0 ? nt : (nt < (uint64_t)grid ? nt : (uint64_t)grid);
     hipLaunchKernelGGL(nxg_enc_f64_kernel, dim3(g), dim3(TPB), 0, s, id, val, n, out, cap, tstat,

@@ -103,6 +103,7 @@ hipError_t nxg_launch_dec_f64_1p(const uint8_t* wire, uint64_t W, uint64_t* oid,
                                  uint64_t cap, uint64_t* tstat, uint32_t epoch, int wgs,
                                  DevStatus* st, hipStream_t s);
 int nxg_dec_f64_1p_wgs(int ncu);
+uint64_t nxg_enc_f64_tiles(uint64_t n);  // tiles (and tstat words) of an f64 encode
 hipError_t nxg_launch_enc_f64(const uint64_t* id, const uint64_t* val, uint64_t n, uint8_t* out,
                               uint64_t cap, uint64_t* tstat, uint32_t epoch, DevStatus* st,
                               int grid, hipStream_t s);

@@ -4,4 +4,4 @@ timeout -k 10 600 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout
 rc=$?; tail -3 gpurun_out/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 600 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err
 rc=$?; cat gpurun_out/bench.json; [ $rc -eq 0 ] || { tail -5 gpurun_out/bench.err; exit $rc; }
-bash scripts/profile_f64.sh r01c > gpurun_out/profile.log 2>&1; rc=$?; tail -3 gpurun_out/profile.log; exit $rc
+bash scripts/profile_f64.sh ${TAG:-r01f} > gpurun_out/profile.log 2>&1; rc=$?; tail -3 gpurun_out/profile.log; exit $rc
