@@ -30,6 +30,14 @@ namespace p1l3 {  // LAG 2: three LDS slots per wave (three 4-wave workgroups pe
 #include "../netidx_amd/csrc/nxg_decode_f64_1p.hip"
 }
 #undef NXG_1P_LAG
+namespace pos {  // one-shot decoder
+#include "exp_f64_oneshot.hip"
+}
+#define NXG_OS_NT 1
+namespace posnt {  // one-shot decoder, nontemporal column stores
+#include "exp_f64_oneshot.hip"
+}
+#undef NXG_OS_NT
 thread_local DevStatus* nxg_zero_slot = nullptr;
 
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
@@ -172,6 +180,14 @@ int main(int argc, char** argv) {
                 CK(p1n::nxg_launch_dec_f64_1p(dw, W, oid, oval, N, tstat, epoch,
                                               p1n::nxg_dec_f64_1p_wgs(ncu), st, 0));
             }
+            if (v == 7) {
+                epoch++;
+                CK(pos::nxg_launch_dec_f64_os(dw, W, oid, oval, N, tstat, epoch, st, 0));
+            }
+            if (v == 8) {
+                epoch++;
+                CK(posnt::nxg_launch_dec_f64_os(dw, W, oid, oval, N, tstat, epoch, st, 0));
+            }
             if (v == 3) {
                 epoch++;
                 CK(p1l3::nxg_launch_dec_f64_1p(dw, W, oid, oval, N, tstat, epoch,
@@ -189,6 +205,11 @@ int main(int argc, char** argv) {
     printf("records=%llu wire=%llu bytes\n", (unsigned long long)N, (unsigned long long)W);
     timeit("dec2p", dec(0), true);
     timeit("dec1p_prod", dec(2), true);
+    timeit("dec_oneshot", dec(7), true);
+    timeit("dec_oneshot_nt", dec(8), true);
+    timeit("dec1p_prod", dec(2), true);
+    timeit("dec_oneshot", dec(7), true);
+    timeit("dec_oneshot_nt", dec(8), true);
     timeit("dec1p_lag2", dec(3), true);
     const char* names[4] = {"dec1p", "1p_nowait", "1p_nostore", "1p_nowait_nostore"};
     for (uint32_t f = 0; f < 4; f++) {
