@@ -423,7 +423,7 @@ bool enqueue_encode(NxgCtx* c, const NxgColumns* in, const uint8_t* heap, uint8_
                                   c->grid_enc_f64, c->stream));
         return true;
     }
-    const uint64_t nt = (in->n_rows + 255) / 256;
+    const uint64_t nt = nxg_enc_general_tiles(in->n_rows);
     if (!ensure_tstat(c, nt, err)) return false;
     if (!ensure_escratch(c, in->n_ctl ? in->n_ctl + 1 + in->n_rows : 1, err)) return false;
     const ColsDesc d = desc_of(in);

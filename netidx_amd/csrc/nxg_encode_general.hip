@@ -10,16 +10,24 @@
 // Three launches:
 // 1. ctl_scan: prefix of the control spans' lengths. One workgroup; skipped when there are no
 //    control messages.
-// 2. rows: each lane encodes one row. The launch does a block scan plus a decoupled look-back
-//    over byte counts. Each row's position is its rows-prefix plus the ctl bytes that precede
-//    it; the latter is found by binary search over ctl_row. The row is then written straight
-//    to the output.
+// 2. rows: each thread encodes GRPT consecutive rows. The launch does a block scan plus a
+//    decoupled look-back over byte counts. Without control messages the tile's rows are
+//    serialised into LDS at the output's 16-byte phase and leave as aligned nontemporal 16-byte
+//    stores (plus byte stores for the two edge blocks), as nxg_encode_f64.hip. With control
+//    messages, or when a tile's bytes exceed the staging, each row's position is its
+//    rows-prefix plus the ctl bytes that precede it (binary search over ctl_row) and the row is
+//    written straight to the output. Scalars, text and arrays of non-container elements are
+//    sized and written without the explicit stack; Map, Error and nested containers take the
+//    general walk.
 // 3. ctl_write: copies each control span to its position.
 #include "nxg_device.h"
 
 namespace {
 
 constexpr int TPB = 256;
+constexpr int GRPT = 4;                  // rows per thread
+constexpr int GTILE = TPB * GRPT;        // rows per tile
+constexpr int GSTG = GTILE * 28 + 32;    // staging: 28 bytes per row (config 3 averages 21.5)
 constexpr uint64_t kMaxVec = 2ull * 1024 * 1024 * 1024;
 
 struct Slot {
@@ -31,6 +39,28 @@ struct Slot {
 NXG_DEV Slot get_slot(const ColsDesc& c, bool row, uint64_t i) {
     if (row) return Slot{c.tag[i], c.fixed[i], c.aux[i]};
     return Slot{c.ctag[i], c.cfixed[i], c.caux[i]};
+}
+
+NXG_DEV bool is_container(uint32_t tag) { return tag == 19 || tag == 21 || tag == 22; }
+
+// |Value| of a non-container value (tags other than 19, 21, 22); 0 => unknown tag
+NXG_DEV uint64_t scalar_len(const Slot& s) {
+    switch (s.tag) {
+    case 0: case 2: case 8: return 5;
+    case 1: return 1 + vl64((uint32_t)s.fixed);
+    case 3: return 1 + vl64(zz32((int32_t)(uint32_t)s.fixed));
+    case 4: case 6: case 9: return 9;
+    case 5: return 1 + vl64(s.fixed);
+    case 7: return 1 + vl64(zz64((int64_t)s.fixed));
+    case 10: case 11: return 13;
+    case 12: case 13: case 18: return 1 + vl64(s.aux) + s.aux;
+    case 14: case 15: case 16: return 1;
+    case 20: return 17;
+    case 23: case 24: return 2;
+    case 25: case 26: return 3;
+    case 27: return 1 + lwlen(s.aux);
+    default: return 0;
+    }
 }
 
 // |Value| for the value in (row?, slot), children included; 0 => error (*err set)
@@ -149,6 +179,63 @@ NXG_DEV void value_write(const ColsDesc& c, const uint8_t* heap, bool row, uint6
     }
 }
 
+// Writes a non-container value (tag byte included).
+NXG_DEV void scalar_write(const Slot& s, const uint8_t* heap, Out& w) {
+    w.b(s.tag);
+    switch (s.tag) {
+    case 0: case 2: case 8: w.be(s.fixed, 4); break;
+    case 1: w.var((uint32_t)s.fixed); break;
+    case 3: w.var(zz32((int32_t)(uint32_t)s.fixed)); break;
+    case 4: case 6: case 9: w.be(s.fixed, 8); break;
+    case 5: w.var(s.fixed); break;
+    case 7: w.var(zz64((int64_t)s.fixed)); break;
+    case 10: case 11: w.be(s.fixed, 8); w.be(s.aux, 4); break;
+    case 12: case 13: case 18: w.var(s.aux); w.copy(heap + s.fixed, s.aux); break;
+    case 20: w.copy(heap + s.fixed, 16); break;
+    case 23: case 24: w.be(s.fixed, 1); break;
+    case 25: case 26: w.be(s.fixed, 2); break;
+    case 27: w.var(lwlen(s.aux)); w.copy(heap + s.fixed, s.aux); break;
+    default: break;
+    }
+}
+
+// Row r's |Value| without the stack when the value is a scalar, text, or an array whose
+// elements are not containers; `flat` false (and 0) otherwise, or on an unknown tag.
+NXG_DEV uint64_t row_len_flat(const ColsDesc& c, uint64_t r, bool& flat) {
+    const Slot s = get_slot(c, true, r);
+    flat = true;
+    if (!is_container(s.tag)) {
+        const uint64_t l = scalar_len(s);
+        flat = l != 0;
+        return l;
+    }
+    if (s.tag != 19 || (uint64_t)s.aux * 16 > kMaxVec) {
+        flat = false;
+        return 0;
+    }
+    uint64_t total = 1 + vl64(s.aux);
+    for (uint64_t k = 0; k < s.aux; k++) {
+        const Slot e = get_slot(c, false, s.fixed + k);
+        const uint64_t l = is_container(e.tag) ? 0 : scalar_len(e);
+        if (!l) {
+            flat = false;
+            return 0;
+        }
+        total += l;
+    }
+    return total;
+}
+NXG_DEV void row_write_flat(const ColsDesc& c, const uint8_t* heap, uint64_t r, Out& w) {
+    const Slot s = get_slot(c, true, r);
+    if (s.tag != 19) {
+        scalar_write(s, heap, w);
+        return;
+    }
+    w.b(19);
+    w.var(s.aux);
+    for (uint64_t k = 0; k < s.aux; k++) scalar_write(get_slot(c, false, s.fixed + k), heap, w);
+}
+
 // number of ctl entries with ctl_row <= r (ctl_row is non-decreasing)
 NXG_DEV uint64_t ctl_upto(const uint64_t* ctl_row, uint64_t n_ctl, uint64_t r) {
     uint64_t lo = 0, hi = n_ctl;
@@ -185,68 +272,105 @@ __global__ __launch_bounds__(TPB) void nxg_enc_rows_kernel(
     zero_status(zst);
     __shared__ uint64_t tmp[4];
     __shared__ uint64_t sh_base;
+    __shared__ __attribute__((aligned(16))) uint8_t stg[GSTG];
     const uint32_t tid = threadIdx.x, lane = tid & 63;
     const uint64_t n = c.n_rows;
     for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        const uint64_t r = (uint64_t)tile * TPB + tid;
-        uint64_t L = 0;
+        const uint64_t r0 = (uint64_t)tile * GTILE + (uint64_t)tid * GRPT;
+        uint64_t L[GRPT];
+        uint32_t fl = 0;  // bit k: row r0 + k is flat
         uint32_t err = 0;
-        if (r < n) {
-            const uint64_t vlen = value_len(c, true, r, &err);
-            L = err ? 0 : lwlen(1 + vl64(c.id[r]) + vlen);
+        uint64_t mine = 0;
+#pragma unroll
+        for (int k = 0; k < GRPT; k++) {
+            const uint64_t r = r0 + k;
+            L[k] = 0;
+            if (r < n) {
+                bool flat;
+                uint64_t vlen = row_len_flat(c, r, flat);
+                uint32_t e = 0;
+                if (!flat) vlen = value_len(c, true, r, &e);
+                fl |= flat ? 1u << k : 0u;
+                if (e) err = err > e ? err : e;
+                L[k] = e ? 0 : lwlen(1 + vl64(c.id[r]) + vlen);
+            }
+            mine += L[k];
         }
         if (err) atomicMax(&st->err_kind, err);
         uint64_t tot;
-        const uint64_t off = block_excl_scan<uint64_t, TPB>(L, tmp, &tot);
+        const uint64_t off = block_excl_scan<uint64_t, TPB>(mine, tmp, &tot);
         if (tid == 0) st_agent(&tstat[tile], lb_word(tile == 0 ? kFlagInc : kFlagAgg, epoch, tot));
         if (tid < 64) {
             uint64_t base = 0;
             if (tile != 0) {
-                int64_t pred = (int64_t)tile - 1;
-                const uint64_t t_start = rt_now();
-                bool give_up = false;
-                for (;;) {
-                    const int64_t idx = pred - (int64_t)lane;
-                    uint64_t s = idx >= 0 ? ld_agent(&tstat[idx]) : lb_word(kFlagInc, epoch, 0);
-                    while (!__all(lb_flag(s, epoch) != 0)) {
-                        __builtin_amdgcn_s_sleep(1);
-                        if (lb_flag(s, epoch) == 0) s = ld_agent(&tstat[idx]);
-                        if (rt_now() - t_start > kSpinTicks) {
-                            give_up = true;
-                            break;
-                        }
-                    }
-                    if (give_up) break;
-                    const uint64_t inc = __ballot(lb_flag(s, epoch) == kFlagInc);
-                    if (inc) {
-                        const uint32_t first = (uint32_t)__builtin_ctzll(inc);
-                        base += wave_sum<uint64_t>(lane <= first ? (s & kValMask) : 0ull);
-                        break;
-                    }
-                    base += wave_sum<uint64_t>(s & kValMask);
-                    pred -= 64;
-                }
+                bool give_up;
+                base = lookback_prefix<1>(tstat, tile, epoch, nullptr, give_up);
                 if (give_up && lane == 0) atomicOr(&st->timeout, 1u);
                 if (lane == 0) st_agent(&tstat[tile], lb_word(kFlagInc, epoch, base + tot));
             }
             if (lane == 0) sh_base = base;
         }
         __syncthreads();
-        const uint64_t rpos = sh_base + off;  // rows-only prefix
-        if (r < n && !err) {
-            if (row_off) row_off[r] = rpos;
-            uint64_t pos = rpos;
-            if (c.n_ctl) pos += ctl_pre[ctl_upto(c.ctl_row, c.n_ctl, r)];
-            if (out) {
-                if (pos + L > cap) {
-                    atomicOr(&st->capacity, 1u);
-                } else {
-                    Out w{out, pos};
-                    w.var(L);
+        const uint64_t tbase = sh_base;
+        const uint32_t phase = (uint32_t)(tbase & 15u);
+        const bool staged = out && c.n_ctl == 0 && phase + tot <= (uint64_t)(GSTG - 16) &&
+                            tbase + tot <= cap;
+        if (staged) {
+            Out w{stg, phase + off};
+#pragma unroll
+            for (int k = 0; k < GRPT; k++) {
+                const uint64_t r = r0 + k;
+                if (r < n && L[k]) {
+                    w.var(L[k]);
                     w.b(4);
                     w.var(c.id[r]);
-                    value_write(c, heap, true, r, w);
+                    if (fl & (1u << k)) row_write_flat(c, heap, r, w);
+                    else value_write(c, heap, true, r, w);
                 }
+            }
+            __syncthreads();
+            const uint64_t end = tbase + tot;
+            if (tot) {
+                const uint64_t gb0 = tbase & ~15ull;
+                const uint32_t nblk = (uint32_t)((end - gb0 + 15) >> 4);
+                for (uint32_t b = tid; b < nblk; b += TPB) {
+                    const uint64_t g = gb0 + 16ull * b;
+                    const uint8_t* src = stg + 16 * b;
+                    if (g >= tbase && g + 16 <= end) {
+                        typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+                        __builtin_nontemporal_store(*reinterpret_cast<const u32x4v*>(src),
+                                                    reinterpret_cast<u32x4v*>(out + g));
+                    } else {
+                        for (int k = 0; k < 16; k++)
+                            if (g + k >= tbase && g + k < end) out[g + k] = src[k];
+                    }
+                }
+            }
+        } else {
+            uint64_t rpos = tbase + off;  // rows-only prefix
+#pragma unroll
+            for (int k = 0; k < GRPT; k++) {
+                const uint64_t r = r0 + k;
+                if (r < n && L[k]) {
+                    if (row_off) row_off[r] = rpos;
+                    uint64_t pos = rpos;
+                    if (c.n_ctl) pos += ctl_pre[ctl_upto(c.ctl_row, c.n_ctl, r)];
+                    if (out) {
+                        if (pos + L[k] > cap) {
+                            atomicOr(&st->capacity, 1u);
+                        } else {
+                            Out w{out, pos};
+                            w.var(L[k]);
+                            w.b(4);
+                            w.var(c.id[r]);
+                            if (fl & (1u << k)) row_write_flat(c, heap, r, w);
+                            else value_write(c, heap, true, r, w);
+                        }
+                    }
+                } else if (r < n && row_off) {
+                    row_off[r] = rpos;  // an erroring row: its ctl placement still needs a base
+                }
+                rpos += L[k];
             }
         }
         if (tile == ntiles - 1 && tid == 0) {
@@ -277,6 +401,8 @@ __global__ __launch_bounds__(TPB) void nxg_enc_ctl_write_kernel(
     }
 }
 
+uint64_t nxg_enc_general_tiles(uint64_t n) { return (n + GTILE - 1) / GTILE; }
+
 hipError_t nxg_launch_enc_general(const ColsDesc& cd, const uint8_t* heap, uint8_t* out,
                                   uint64_t cap, uint64_t* scratch, uint64_t* tstat,
                                   uint32_t epoch, DevStatus* st, int grid, hipStream_t s) {
@@ -284,7 +410,7 @@ hipError_t nxg_launch_enc_general(const ColsDesc& cd, const uint8_t* heap, uint8
     uint64_t* ctl_pre = scratch;
     uint64_t* row_off = cd.n_ctl ? scratch + cd.n_ctl + 1 : nullptr;
     if (cd.n_ctl) hipLaunchKernelGGL(nxg_enc_ctl_scan_kernel, dim3(1), dim3(TPB), 0, s, cd, ctl_pre);
-    const uint64_t nt = (cd.n_rows + TPB - 1) / TPB;
+    const uint64_t nt = nxg_enc_general_tiles(cd.n_rows);
     if (nt) {
         const uint64_t g = grid <= 0 ? nt : (nt < (uint64_t)grid ? nt : (uint64_t)grid);
         hipLaunchKernelGGL(nxg_enc_rows_kernel, dim3(g), dim3(TPB), 0, s, cd, heap, out, cap,

@@ -107,6 +107,7 @@ uint64_t nxg_enc_f64_tiles(uint64_t n);  // tiles (and tstat words) of an f64 en
 hipError_t nxg_launch_enc_f64(const uint64_t* id, const uint64_t* val, uint64_t n, uint8_t* out,
                               uint64_t cap, uint64_t* tstat, uint32_t epoch, DevStatus* st,
                               int grid, hipStream_t s);
+uint64_t nxg_enc_general_tiles(uint64_t n);  // tiles (and tstat words) of a general encode
 hipError_t nxg_launch_enc_general(const ColsDesc& cols, const uint8_t* heap, uint8_t* out,
                                   uint64_t cap, uint64_t* scratch, uint64_t* tstat,
                                   uint32_t epoch, DevStatus* st, int grid, hipStream_t s);
