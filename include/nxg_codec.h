@@ -143,7 +143,8 @@ bool nxg_decode_updates(NxgCtx* ctx, const uint8_t* frame, uint64_t len, NxgColu
                         uint32_t flags, NxgStatus* st, NetidxError* err);
 /* Asynchronous device-resident variant: enqueue on the ctx stream; no host sync. Only the
  * path selected up front runs (flags). nxg_ctx_sync completes it, runs the general fallback if
- * the homogeneous path rejected the frame, and fills the status. */
+ * the homogeneous path rejected the frame, and fills the status. At most 512 async calls
+ * (decode and encode together) may be in flight between syncs; the next one fails. */
 bool nxg_decode_updates_async(NxgCtx* ctx, const uint8_t* dframe, uint64_t len, NxgColumns* dout,
                               uint32_t flags, NetidxError* err);
 bool nxg_ctx_sync(NxgCtx* ctx, NxgStatus* st, NetidxError* err);

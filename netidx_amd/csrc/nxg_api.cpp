@@ -39,7 +39,7 @@ void set_err(NetidxError* err, const char* fmt, ...) {
         }                                                                                  \
     } while (0)
 
-constexpr int kStatusRing = 256;
+constexpr int kStatusRing = 1024;  // at most kStatusRing/2 async calls in flight
 
 }  // namespace
 
@@ -101,7 +101,7 @@ bool set_device(NxgCtx* c, NetidxError* err) {
 }
 
 // Next status slot + epoch for one call. Slot k is zeroed by block 0 of the call that used
-// slot k-128 (nxg_zero_slot), so at most kStatusRing/2 calls may be in flight.
+// slot k - kStatusRing/2 (nxg_zero_slot), so at most kStatusRing/2 calls may be in flight.
 bool begin_call(NxgCtx* c, DevStatus** st, uint32_t* slot, NetidxError* err) {
     *slot = c->calls % kStatusRing;
     *st = c->dst + *slot;
@@ -305,10 +305,15 @@ bool enqueue_dec_general(NxgCtx* c, const uint8_t* f, uint64_t len, NxgColumns* 
 
 // finish a device decode: read status, fall back to the general kernel if the f64 kernel
 // rejected the frame, fill the user-visible status
+// `fetched`: the caller has already copied the status ring to c->hst after the stream drained.
 bool finish_decode(NxgCtx* c, const uint8_t* f, uint64_t len, NxgColumns* out, int tried_fast,
-                   DevStatus* st, uint32_t slot, NxgStatus* ust, NetidxError* err) {
-    HIPCHK(hipMemcpyAsync(c->hst + slot, st, sizeof(DevStatus), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
+                   DevStatus* st, uint32_t slot, NxgStatus* ust, NetidxError* err,
+                   bool fetched = false) {
+    if (!fetched) {
+        HIPCHK(hipMemcpyAsync(c->hst + slot, st, sizeof(DevStatus), hipMemcpyDeviceToHost,
+                              c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+    }
     DevStatus h = c->hst[slot];
     if (tried_fast && len > 0 && h.fast_fail) {
         DevStatus* st2;
@@ -433,13 +438,17 @@ bool enqueue_encode(NxgCtx* c, const NxgColumns* in, const uint8_t* heap, uint8_
 }
 
 bool finish_encode(NxgCtx* c, const NxgColumns* in, DevStatus* st, uint32_t slot,
-                   uint64_t* len_out, uint64_t cap, bool wrote, NetidxError* err) {
-    HIPCHK(hipMemcpyAsync(c->hst + slot, st, sizeof(DevStatus), hipMemcpyDeviceToHost, c->stream));
+                   uint64_t* len_out, uint64_t cap, bool wrote, NetidxError* err,
+                   bool fetched = false) {
+    if (!fetched)
+        HIPCHK(hipMemcpyAsync(c->hst + slot, st, sizeof(DevStatus), hipMemcpyDeviceToHost,
+                              c->stream));
     uint64_t ctl_total = 0;
     if (in->layout == NXG_LAYOUT_MIXED && in->n_ctl)
         HIPCHK(hipMemcpyAsync(&ctl_total, c->escratch + in->n_ctl, 8, hipMemcpyDeviceToHost,
                               c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
+    if (!fetched || (in->layout == NXG_LAYOUT_MIXED && in->n_ctl))
+        HIPCHK(hipStreamSynchronize(c->stream));
     const DevStatus& h = c->hst[slot];
     if (h.timeout) {
         set_err(err, "device look-back watchdog expired");
@@ -683,12 +692,18 @@ bool nxg_ctx_sync(NxgCtx* c, NxgStatus* ust, NetidxError* err) {
     std::vector<NxgCtx::Pending> ps;
     ps.swap(c->pending);
     HIPCHK(hipStreamSynchronize(c->stream));
+    // every in-flight call's status in one copy (the ring is small), not one round trip each
+    if (!ps.empty()) {
+        HIPCHK(hipMemcpyAsync(c->hst, c->dst, sizeof(DevStatus) * kStatusRing,
+                              hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+    }
     if (ust) memset(ust, 0, sizeof *ust);
     bool reported = false;
     for (auto& p : ps) {
         if (p.kind == 1) {
             NxgStatus s;
-            if (!finish_decode(c, p.frame, p.len, p.cols, p.fast, p.st, p.slot, &s, err))
+            if (!finish_decode(c, p.frame, p.len, p.cols, p.fast, p.st, p.slot, &s, err, true))
                 return false;
             p.cols->layout =
                 (!mixed_capable(p.cols) || s.path == 1) ? NXG_LAYOUT_F64 : NXG_LAYOUT_MIXED;
@@ -698,7 +713,7 @@ bool nxg_ctx_sync(NxgCtx* c, NxgStatus* ust, NetidxError* err) {
             NxgColumns dummy{};
             dummy.layout = NXG_LAYOUT_F64;
             if (!finish_encode(c, p.cols ? p.cols : &dummy, p.st, p.slot, p.len_out, ~0ull, false,
-                               err))
+                               err, true))
                 return false;
         }
     }

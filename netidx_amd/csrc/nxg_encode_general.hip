@@ -258,6 +258,19 @@ NXG_DEV void row_write_flat(const ColsDesc& c, const uint8_t* heap, uint64_t r, 
     for (uint64_t k = 0; k < s.aux; k++) scalar_write(get_slot(c, false, s.fixed + k), heap, w);
 }
 
+// Value classes of the staged path (rows whose value row_len_flat handled, by tag; CLS_GEN for
+// the rest), each written by its own code so that a wave runs one class at a time.
+enum : uint32_t { CLS_FIX8, CLS_TEXT, CLS_TIME, CLS_ARR, CLS_SCAL, CLS_GEN, NCLS };
+NXG_DEV uint32_t value_class(uint32_t tag) {
+    switch (tag) {
+    case 4: case 6: case 9: return CLS_FIX8;
+    case 12: case 13: case 18: return CLS_TEXT;
+    case 10: case 11: return CLS_TIME;
+    case 19: return CLS_ARR;
+    default: return CLS_SCAL;
+    }
+}
+
 // number of ctl entries with ctl_row <= r (ctl_row is non-decreasing)
 NXG_DEV uint64_t ctl_upto(const uint64_t* ctl_row, uint64_t n_ctl, uint64_t r) {
     uint64_t lo = 0, hi = n_ctl;
@@ -295,6 +308,10 @@ __global__ __launch_bounds__(TPB) void nxg_enc_rows_kernel(
     __shared__ uint64_t tmp[4];
     __shared__ uint64_t sh_base;
     __shared__ __attribute__((aligned(16))) uint8_t stg[GSTG];
+    __shared__ uint32_t cls_n[NCLS], cls_b[NCLS + 1];
+    __shared__ uint16_t lst_row[GTILE], lst_off[GTILE], lst_len[GTILE];
+    __shared__ uint8_t lst_cls[GTILE];
+    static_assert(GSTG < 65536, "staging offsets and lengths fit 16 bits");
     const uint32_t tid = threadIdx.x, lane = tid & 63;
     const uint64_t n = c.n_rows;
     for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
@@ -338,16 +355,87 @@ __global__ __launch_bounds__(TPB) void nxg_enc_rows_kernel(
         const bool staged = out && c.n_ctl == 0 && phase + tot <= (uint64_t)(GSTG - 16) &&
                             tbase + tot <= cap;
         if (staged) {
-            Out w{stg, phase + off};
+            // rows bucketed by value class (counting sort in LDS), then written class by class
+            // so that a wave runs one class's code at a time; each row knows its staging offset
+            if (tid < NCLS) cls_n[tid] = 0;
+            __syncthreads();
+            uint32_t cls[GRPT], pos[GRPT];
+            const uint32_t wv = tid >> 6;
+            (void)wv;
 #pragma unroll
             for (int k = 0; k < GRPT; k++) {
                 const uint64_t r = r0 + k;
-                if (r < n && L[k]) {
-                    w.var(L[k]);
-                    w.b(4);
-                    w.var(c.id[r]);
-                    if (fl & (1u << k)) row_write_flat(c, heap, r, w);
-                    else value_write(c, heap, true, r, w);
+                cls[k] = NCLS;  // none
+                if (r < n && L[k]) cls[k] = (fl & (1u << k)) ? value_class(c.tag[r]) : CLS_GEN;
+                pos[k] = 0;
+#pragma unroll
+                for (uint32_t q = 0; q < NCLS; q++) {
+                    const uint64_t m = __ballot(cls[k] == q);
+                    if (!m) continue;
+                    const uint32_t lead = (uint32_t)__builtin_ctzll(m);
+                    uint32_t b0 = 0;
+                    if (lane == lead) b0 = atomicAdd(&cls_n[q], (uint32_t)__popcll(m));
+                    b0 = __shfl(b0, (int)lead);
+                    if (cls[k] == q) pos[k] = b0 + (uint32_t)__popcll(m & ((1ull << lane) - 1));
+                }
+            }
+            __syncthreads();
+            if (tid == 0) {
+                uint32_t acc = 0;
+                for (int q = 0; q < NCLS; q++) {
+                    cls_b[q] = acc;
+                    acc += cls_n[q];
+                }
+                cls_b[NCLS] = acc;
+            }
+            __syncthreads();
+            {
+                uint32_t o = phase + (uint32_t)off;
+#pragma unroll
+                for (int k = 0; k < GRPT; k++) {
+                    if (cls[k] < NCLS) {
+                        const uint32_t e = cls_b[cls[k]] + pos[k];
+                        lst_row[e] = (uint16_t)(tid * GRPT + k);
+                        lst_off[e] = (uint16_t)o;
+                        lst_len[e] = (uint16_t)L[k];
+                        lst_cls[e] = (uint8_t)cls[k];
+                    }
+                    o += (uint32_t)L[k];
+                }
+            }
+            __syncthreads();
+            const uint32_t ne = cls_b[NCLS];
+            const uint64_t rt = (uint64_t)tile * GTILE;
+            for (uint32_t e = tid; e < ne; e += TPB) {
+                const uint64_t r = rt + lst_row[e];
+                Out w{stg, lst_off[e]};
+                w.var(lst_len[e]);
+                w.b(4);
+                w.var(c.id[r]);
+                switch (lst_cls[e]) {
+                case CLS_FIX8: {
+                    const Slot v = get_slot(c, true, r);
+                    w.b(v.tag);
+                    w.be(v.fixed, 8);
+                    break;
+                }
+                case CLS_TEXT: {
+                    const Slot v = get_slot(c, true, r);
+                    w.b(v.tag);
+                    w.var(v.aux);
+                    w.copy(heap + v.fixed, v.aux);
+                    break;
+                }
+                case CLS_TIME: {
+                    const Slot v = get_slot(c, true, r);
+                    w.b(v.tag);
+                    w.be(v.fixed, 8);
+                    w.be(v.aux, 4);
+                    break;
+                }
+                case CLS_ARR: row_write_flat(c, heap, r, w); break;
+                case CLS_SCAL: scalar_write(get_slot(c, true, r), heap, w); break;
+                default: value_write(c, heap, true, r, w); break;
                 }
             }
             __syncthreads();
