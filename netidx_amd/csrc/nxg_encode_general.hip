@@ -258,16 +258,18 @@ NXG_DEV void row_write_flat(const ColsDesc& c, const uint8_t* heap, uint64_t r, 
     for (uint64_t k = 0; k < s.aux; k++) scalar_write(get_slot(c, false, s.fixed + k), heap, w);
 }
 
-// Value classes of the staged path (rows whose value row_len_flat handled, by tag; CLS_GEN for
-// the rest), each written by its own code so that a wave runs one class at a time.
+// Value classes by tag (CLS_GEN: Map, Error, nested containers and unknown tags, which take
+// the stack walk), each sized and written by its own code so that a wave runs one class at a
+// time.
 enum : uint32_t { CLS_FIX8, CLS_TEXT, CLS_TIME, CLS_ARR, CLS_SCAL, CLS_GEN, NCLS };
 NXG_DEV uint32_t value_class(uint32_t tag) {
     switch (tag) {
     case 4: case 6: case 9: return CLS_FIX8;
     case 12: case 13: case 18: return CLS_TEXT;
     case 10: case 11: return CLS_TIME;
-    case 19: return CLS_ARR;
-    default: return CLS_SCAL;
+    case 19: return CLS_ARR;  // CLS_GEN once sizing finds a container element
+    case 21: case 22: return CLS_GEN;
+    default: return tag < 28 ? CLS_SCAL : CLS_GEN;  // unknown tags: the walk reports them
     }
 }
 
@@ -309,33 +311,97 @@ __global__ __launch_bounds__(TPB) void nxg_enc_rows_kernel(
     __shared__ uint64_t sh_base;
     __shared__ __attribute__((aligned(16))) uint8_t stg[GSTG];
     __shared__ uint32_t cls_n[NCLS], cls_b[NCLS + 1];
-    __shared__ uint16_t lst_row[GTILE], lst_off[GTILE], lst_len[GTILE];
-    __shared__ uint8_t lst_cls[GTILE];
-    static_assert(GSTG < 65536, "staging offsets and lengths fit 16 bits");
+    __shared__ uint16_t lst_row[GTILE];  // the tile's rows sorted by value class
+    __shared__ uint16_t off_lds[GTILE];  // staging offset per row (tile-local index)
+    __shared__ uint32_t len_lds[GTILE];  // message length per row (0: absent or erroring)
+    __shared__ uint8_t cls_lds[GTILE];   // value class per row (CLS_GEN: the general walk)
+    static_assert(GSTG < 65536, "staging offsets fit 16 bits");
     const uint32_t tid = threadIdx.x, lane = tid & 63;
     const uint64_t n = c.n_rows;
     for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        const uint64_t r0 = (uint64_t)tile * GTILE + (uint64_t)tid * GRPT;
-        uint64_t L[GRPT];
-        uint32_t fl = 0;  // bit k: row r0 + k is flat
-        uint32_t err = 0;
-        uint64_t mine = 0;
+        const uint64_t rt = (uint64_t)tile * GTILE;
+        const uint64_t r0 = rt + (uint64_t)tid * GRPT;
+        // 1. classify by tag and bucket the rows (wave-ballot counting sort in LDS); a wave then
+        //    sizes and writes one class at a time
+        if (tid < NCLS) cls_n[tid] = 0;
+        __syncthreads();
+        uint32_t cls[GRPT], pos[GRPT];
 #pragma unroll
         for (int k = 0; k < GRPT; k++) {
             const uint64_t r = r0 + k;
-            L[k] = 0;
-            if (r < n) {
-                bool flat;
-                uint64_t vlen = row_len_flat(c, r, flat);
-                uint32_t e = 0;
-                if (!flat) vlen = value_len(c, true, r, &e);
-                fl |= flat ? 1u << k : 0u;
-                if (e) err = err > e ? err : e;
-                L[k] = e ? 0 : lwlen(1 + vl64(c.id[r]) + vlen);
+            cls[k] = r < n ? value_class(c.tag[r]) : NCLS;
+            pos[k] = 0;
+#pragma unroll
+            for (uint32_t q = 0; q < NCLS; q++) {
+                const uint64_t m = __ballot(cls[k] == q);
+                if (!m) continue;
+                const uint32_t lead = (uint32_t)__builtin_ctzll(m);
+                uint32_t b0 = 0;
+                if (lane == lead) b0 = atomicAdd(&cls_n[q], (uint32_t)__popcll(m));
+                b0 = __shfl(b0, (int)lead);
+                if (cls[k] == q) pos[k] = b0 + (uint32_t)__popcll(m & ((1ull << lane) - 1));
             }
+        }
+        __syncthreads();
+        if (tid == 0) {
+            uint32_t acc = 0;
+            for (int q = 0; q < NCLS; q++) {
+                cls_b[q] = acc;
+                acc += cls_n[q];
+            }
+            cls_b[NCLS] = acc;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < GRPT; k++) {
+            const uint32_t rl = tid * GRPT + k;
+            len_lds[rl] = 0;
+            cls_lds[rl] = (uint8_t)cls[k];
+            if (cls[k] < NCLS) lst_row[cls_b[cls[k]] + pos[k]] = (uint16_t)rl;
+        }
+        __syncthreads();
+        const uint32_t ne = cls_b[NCLS];
+        // 2. message lengths, class by class
+        for (uint32_t e = tid; e < ne; e += TPB) {
+            const uint32_t rl = lst_row[e];
+            const uint64_t r = rt + rl;
+            const Slot v = get_slot(c, true, r);
+            uint64_t vlen = 0;
+            uint32_t err = 0;
+            switch (cls_lds[rl]) {
+            case CLS_FIX8: vlen = 9; break;
+            case CLS_TEXT: vlen = 1 + vl64(v.aux) + v.aux; break;
+            case CLS_TIME: vlen = 13; break;
+            case CLS_SCAL:
+                vlen = scalar_len(v);
+                if (!vlen) {  // a tag the encoder does not write (17): the walk reports it
+                    cls_lds[rl] = CLS_GEN;
+                    vlen = value_len(c, true, r, &err);
+                }
+                break;
+            case CLS_ARR: {
+                bool flat;
+                vlen = row_len_flat(c, r, flat);
+                if (!flat) {
+                    cls_lds[rl] = CLS_GEN;
+                    vlen = value_len(c, true, r, &err);
+                }
+                break;
+            }
+            default: vlen = value_len(c, true, r, &err); break;
+            }
+            if (err) atomicMax(&st->err_kind, err);
+            len_lds[rl] = err ? 0u : (uint32_t)lwlen(1 + vl64(c.id[r]) + vlen);
+        }
+        __syncthreads();
+        // 3. the tile's byte offsets: block scan, then look-back over the tiles' byte counts
+        uint64_t L[GRPT];
+        uint64_t mine = 0;
+#pragma unroll
+        for (int k = 0; k < GRPT; k++) {
+            L[k] = len_lds[tid * GRPT + k];
             mine += L[k];
         }
-        if (err) atomicMax(&st->err_kind, err);
         uint64_t tot;
         const uint64_t off = block_excl_scan<uint64_t, TPB>(mine, tmp, &tot);
         if (tid == 0) st_agent(&tstat[tile], lb_word(tile == 0 ? kFlagInc : kFlagAgg, epoch, tot));
@@ -355,64 +421,27 @@ __global__ __launch_bounds__(TPB) void nxg_enc_rows_kernel(
         const bool staged = out && c.n_ctl == 0 && phase + tot <= (uint64_t)(GSTG - 16) &&
                             tbase + tot <= cap;
         if (staged) {
-            // rows bucketed by value class (counting sort in LDS), then written class by class
-            // so that a wave runs one class's code at a time; each row knows its staging offset
-            if (tid < NCLS) cls_n[tid] = 0;
-            __syncthreads();
-            uint32_t cls[GRPT], pos[GRPT];
-            const uint32_t wv = tid >> 6;
-            (void)wv;
-#pragma unroll
-            for (int k = 0; k < GRPT; k++) {
-                const uint64_t r = r0 + k;
-                cls[k] = NCLS;  // none
-                if (r < n && L[k]) cls[k] = (fl & (1u << k)) ? value_class(c.tag[r]) : CLS_GEN;
-                pos[k] = 0;
-#pragma unroll
-                for (uint32_t q = 0; q < NCLS; q++) {
-                    const uint64_t m = __ballot(cls[k] == q);
-                    if (!m) continue;
-                    const uint32_t lead = (uint32_t)__builtin_ctzll(m);
-                    uint32_t b0 = 0;
-                    if (lane == lead) b0 = atomicAdd(&cls_n[q], (uint32_t)__popcll(m));
-                    b0 = __shfl(b0, (int)lead);
-                    if (cls[k] == q) pos[k] = b0 + (uint32_t)__popcll(m & ((1ull << lane) - 1));
-                }
-            }
-            __syncthreads();
-            if (tid == 0) {
-                uint32_t acc = 0;
-                for (int q = 0; q < NCLS; q++) {
-                    cls_b[q] = acc;
-                    acc += cls_n[q];
-                }
-                cls_b[NCLS] = acc;
-            }
-            __syncthreads();
+            // 4. rows into the staging at their offsets, class by class, then aligned
+            //    nontemporal 16-byte stores (edge blocks shared with the neighbours: bytes)
             {
                 uint32_t o = phase + (uint32_t)off;
 #pragma unroll
                 for (int k = 0; k < GRPT; k++) {
-                    if (cls[k] < NCLS) {
-                        const uint32_t e = cls_b[cls[k]] + pos[k];
-                        lst_row[e] = (uint16_t)(tid * GRPT + k);
-                        lst_off[e] = (uint16_t)o;
-                        lst_len[e] = (uint16_t)L[k];
-                        lst_cls[e] = (uint8_t)cls[k];
-                    }
+                    off_lds[tid * GRPT + k] = (uint16_t)o;
                     o += (uint32_t)L[k];
                 }
             }
             __syncthreads();
-            const uint32_t ne = cls_b[NCLS];
-            const uint64_t rt = (uint64_t)tile * GTILE;
             for (uint32_t e = tid; e < ne; e += TPB) {
-                const uint64_t r = rt + lst_row[e];
-                Out w{stg, lst_off[e]};
-                w.var(lst_len[e]);
+                const uint32_t rl = lst_row[e];
+                const uint32_t len = len_lds[rl];
+                if (!len) continue;
+                const uint64_t r = rt + rl;
+                Out w{stg, off_lds[rl]};
+                w.var(len);
                 w.b(4);
                 w.var(c.id[r]);
-                switch (lst_cls[e]) {
+                switch (cls_lds[rl]) {
                 case CLS_FIX8: {
                     const Slot v = get_slot(c, true, r);
                     w.b(v.tag);
@@ -457,28 +486,26 @@ __global__ __launch_bounds__(TPB) void nxg_enc_rows_kernel(
                 }
             }
         } else {
+            // control messages interleaved, or more bytes than the staging: straight to the
+            // frame, each thread its own rows
             uint64_t rpos = tbase + off;  // rows-only prefix
 #pragma unroll
             for (int k = 0; k < GRPT; k++) {
                 const uint64_t r = r0 + k;
-                if (r < n && L[k]) {
-                    if (row_off) row_off[r] = rpos;
+                if (r < n && row_off) row_off[r] = rpos;  // ctl placement needs every row's base
+                if (r < n && L[k] && out) {
                     uint64_t pos = rpos;
                     if (c.n_ctl) pos += ctl_pre[ctl_upto(c.ctl_row, c.n_ctl, r)];
-                    if (out) {
-                        if (pos + L[k] > cap) {
-                            atomicOr(&st->capacity, 1u);
-                        } else {
-                            Out w{out, pos};
-                            w.var(L[k]);
-                            w.b(4);
-                            w.var(c.id[r]);
-                            if (fl & (1u << k)) row_write_flat(c, heap, r, w);
-                            else value_write(c, heap, true, r, w);
-                        }
+                    if (pos + L[k] > cap) {
+                        atomicOr(&st->capacity, 1u);
+                    } else {
+                        Out w{out, pos};
+                        w.var(L[k]);
+                        w.b(4);
+                        w.var(c.id[r]);
+                        if (cls_lds[tid * GRPT + k] != CLS_GEN) row_write_flat(c, heap, r, w);
+                        else value_write(c, heap, true, r, w);
                     }
-                } else if (r < n && row_off) {
-                    row_off[r] = rpos;  // an erroring row: its ctl placement still needs a base
                 }
                 rpos += L[k];
             }

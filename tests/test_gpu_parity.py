@@ -276,6 +276,66 @@ def test_long_values_span_tiles(codec):
     assert_same_as_oracle(cols, st, wire)
 
 
+def _mg():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("mg", os.path.join(GOLD, "make_golden.py"))
+    mg = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mg)
+    return mg
+
+
+def test_encode_staged_every_tag(codec):
+    """Updates only (no control messages): the general encoder's staged, class-bucketed path
+    with every Value tag, Maps, Errors and nesting (the stack walk), byte-identical."""
+    import torch
+    mg = _mg()
+    rng = random.Random(321)
+    msgs = [("u", rng.getrandbits(rng.choice([7, 14, 30, 63])), mg.rand_value(rng))
+            for _ in range(6000)]
+    wire, _ = mg.batch(msgs)
+    cols, st = gpu_decode(codec, wire)
+    assert_same_as_oracle(cols, st, wire)
+    heap = torch.from_numpy(np.frombuffer(wire, np.uint8).copy()).cuda()
+    assert codec.encode_batch(cols, heap).cpu().numpy().tobytes() == wire
+
+
+def test_encode_tiles_past_the_staging(codec):
+    """Values longer than the encoder's LDS staging (28 bytes per row): those tiles write their
+    rows straight to the frame; short tiles around them stay staged."""
+    import torch
+    mg = _mg()
+    rng = random.Random(8)
+    msgs = []
+    for i in range(5000):
+        if i % 1500 == 7:
+            msgs.append(("u", i, (13, bytes(rng.getrandbits(8) for _ in range(40000)))))
+        elif i % 3 == 0:
+            msgs.append(("u", i, (12, b"x" * rng.randrange(0, 33))))
+        else:
+            msgs.append(("u", i, (9, rng.getrandbits(64))))
+    wire, _ = mg.batch(msgs)
+    cols, st = gpu_decode(codec, wire)
+    assert_same_as_oracle(cols, st, wire)
+    heap = torch.from_numpy(np.frombuffer(wire, np.uint8).copy()).cuda()
+    assert codec.encode_batch(cols, heap).cpu().numpy().tobytes() == wire
+
+
+@pytest.mark.parametrize("bad_tag", [17, 28, 200])
+def test_encode_unknown_tag_fails(codec, bad_tag):
+    """A column tag the wire format has no encoding for (Value::encode never writes 17; >= 28
+    are not Value tags) fails the encode instead of writing a frame."""
+    import netidx_amd
+    n = 3000
+    ids = np.arange(n, dtype=np.uint64)
+    fixed = np.arange(n, dtype=np.uint64) * 3
+    tag = np.full(n, 6, np.uint8)
+    tag[n // 2] = bad_tag
+    aux = np.zeros(n, np.uint32)
+    cols = netidx_amd.columns_from_arrays(ids, fixed, tag, aux)
+    with pytest.raises(Exception):
+        codec.encode_batch(cols)
+
+
 # ---- encode f64 + round trip at BASELINE sizes ---------------------------------------------
 def test_f64_encode_matches_oracle(codec):
     import netidx_amd
