@@ -44,6 +44,7 @@ constexpr int kStatusRing = 1024;  // at most kStatusRing/2 async calls in fligh
 }  // namespace
 
 thread_local DevStatus* nxg_zero_slot = nullptr;
+thread_local bool nxg_zero_used = false;
 
 struct NxgCtx {
     int device = 0;
@@ -70,6 +71,14 @@ struct NxgCtx {
     int wgs_dec_gen = 0;
     int wgs_dec_f64_1p = 0;
     bool f64_2pass = false;  // NXG_F64_2PASS=1: the two-pass count/emit f64 decoder
+    // f64 decoder choice: the length-run decoder (nxg_decode_f64_run.hip) unless the frames of
+    // this connection have record lengths that vary record to record; then the persistent
+    // single-pass decoder for the next kIrregularCalls calls (NXG_F64_PATH=1p forces it)
+    uint8_t* rdesc = nullptr;  // length-run decoder: 16-byte tile descriptors
+    size_t rdesc_cap = 0;
+    uint32_t irregular_left = 0;
+    bool force_1p = false;
+    uint32_t f64r_flags = 0;  // NXG_F64R_FLAGS (tests): 1 every tile exact, 2 never hand over
     uint8_t* dframe = nullptr;
     size_t dframe_cap = 0;
     uint64_t* escratch = nullptr;
@@ -86,6 +95,7 @@ struct NxgCtx {
         uint64_t len;
         NxgColumns* cols;
         uint64_t* len_out;
+        uint64_t cap;  // encode: the output capacity
         DevStatus* st;
         uint32_t slot;
     };
@@ -100,18 +110,30 @@ bool set_device(NxgCtx* c, NetidxError* err) {
     return true;
 }
 
-// Next status slot + epoch for one call. Slot k is zeroed by block 0 of the call that used
-// slot k - kStatusRing/2 (nxg_zero_slot), so at most kStatusRing/2 calls may be in flight.
+// Next status slot + epoch for one call. Slot k is zeroed by the call that used slot
+// k - kStatusRing/2 (nxg_zero_slot: block 0 of its kernel, or end_call when it launched none), so
+// at most kStatusRing/2 calls may be in flight. Every begin_call is paired with an end_call.
 bool begin_call(NxgCtx* c, DevStatus** st, uint32_t* slot, NetidxError* err) {
     *slot = c->calls % kStatusRing;
     *st = c->dst + *slot;
     nxg_zero_slot = c->dst + (c->calls + kStatusRing / 2) % kStatusRing;
+    nxg_zero_used = false;
     c->calls++;
     c->epoch++;
     if (c->epoch > kEpochMax) {  // wrap: stale words could alias epoch 1 again
         c->epoch = 1;
         if (c->tstat) HIPCHK(hipMemsetAsync(c->tstat, 0, c->tstat_words * 8, c->stream));
     }
+    return true;
+}
+
+// After a call's launches (or a failure to launch): if no kernel took the zero-ahead slot (an
+// empty frame or batch launches nothing), clear it here, so that the call kStatusRing/2 later
+// does not inherit this ring lap's status bits.
+bool end_call(NxgCtx* c, NetidxError* err) {
+    if (nxg_zero_used) return true;
+    nxg_zero_used = true;
+    HIPCHK(hipMemsetAsync(nxg_zero_slot, 0, sizeof(DevStatus), c->stream));
     return true;
 }
 
@@ -267,8 +289,45 @@ NxgColumns staged_view(NxgCtx* c, const NxgColumns* like) {
     return v;
 }
 
+constexpr uint32_t kIrregularCalls = 64;
+
+// path codes of a homogeneous-f64 attempt (Pending::fast)
+enum { FAST_NONE = 0, FAST_RUN = 1, FAST_1P = 2 };
+
+bool ensure_rdesc(NxgCtx* c, size_t bytes, NetidxError* err) {
+    if (bytes <= c->rdesc_cap) return true;
+    size_t n = std::max(bytes, c->rdesc_cap * 2);
+    n = std::max<size_t>(n, 1 << 16);
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (c->rdesc) HIPCHK(hipFree(c->rdesc));
+    c->rdesc = nullptr;
+    HIPCHK(hipMalloc(&c->rdesc, n));
+    c->rdesc_cap = n;
+    return true;
+}
+
+// the persistent (or two-pass) decoder
+bool enqueue_dec_1p(NxgCtx* c, const uint8_t* f, uint64_t len, NxgColumns* out, DevStatus* st,
+                    NetidxError* err);
+
+// Homogeneous-f64 attempt; *path receives the FAST_* code of the decoder that was enqueued.
 bool enqueue_dec_fast(NxgCtx* c, const uint8_t* f, uint64_t len, NxgColumns* out, DevStatus* st,
-                      NetidxError* err) {
+                      int* path, NetidxError* err) {
+    if (!c->f64_2pass && !c->force_1p && c->irregular_left == 0) {
+        *path = FAST_RUN;
+        if (!ensure_tstat(c, nxg_dec_f64r_groups(len), err)) return false;
+        if (!ensure_rdesc(c, 16 * nxg_dec_f64r_tiles(len), err)) return false;
+        HIPCHK(nxg_launch_dec_f64r(f, len, out->id, out->fixed, out->cap_rows, c->rdesc,
+                                   c->tstat, c->epoch, c->f64r_flags, st, c->stream));
+        return true;
+    }
+    if (c->irregular_left) c->irregular_left--;
+    *path = FAST_1P;
+    return enqueue_dec_1p(c, f, len, out, st, err);
+}
+
+bool enqueue_dec_1p(NxgCtx* c, const uint8_t* f, uint64_t len, NxgColumns* out, DevStatus* st,
+                    NetidxError* err) {
     if (!c->f64_2pass && c->wgs_dec_f64_1p >= 2) {
         if (!ensure_tstat(c, 2 * nxg_dec_f64_1p_tiles(len), err)) return false;
         HIPCHK(nxg_launch_dec_f64_1p(f, len, out->id, out->fixed, out->cap_rows, c->tstat,
@@ -315,11 +374,26 @@ bool finish_decode(NxgCtx* c, const uint8_t* f, uint64_t len, NxgColumns* out, i
         HIPCHK(hipStreamSynchronize(c->stream));
     }
     DevStatus h = c->hst[slot];
+    if (tried_fast == FAST_RUN && len > 0 && h.fast_fail && h.irregular) {
+        // record lengths vary record to record: the persistent decoder, for this frame and the
+        // next kIrregularCalls ones
+        c->irregular_left = kIrregularCalls;
+        DevStatus* st2;
+        uint32_t slot2;
+        if (!begin_call(c, &st2, &slot2, err)) return false;
+        const bool ok = enqueue_dec_1p(c, f, len, out, st2, err);
+        if (!end_call(c, err) || !ok) return false;
+        HIPCHK(hipMemcpyAsync(c->hst + slot2, st2, sizeof(DevStatus), hipMemcpyDeviceToHost,
+                              c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        h = c->hst[slot2];
+    }
     if (tried_fast && len > 0 && h.fast_fail) {
         DevStatus* st2;
         uint32_t slot2;
         if (!begin_call(c, &st2, &slot2, err)) return false;
-        if (!enqueue_dec_general(c, f, len, out, st2, err)) return false;
+        const bool ok = enqueue_dec_general(c, f, len, out, st2, err);
+        if (!end_call(c, err) || !ok) return false;
         HIPCHK(hipMemcpyAsync(c->hst + slot2, st2, sizeof(DevStatus), hipMemcpyDeviceToHost,
                               c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
@@ -536,6 +610,10 @@ NxgCtx* nxg_ctx_new(int device, NetidxError* err) {
     c->wgs_dec_f64_1p = nxg_dec_f64_1p_wgs(c->ncu);
     const char* f2 = getenv("NXG_F64_2PASS");
     c->f64_2pass = f2 && f2[0] == '1';
+    const char* fp = getenv("NXG_F64_PATH");
+    c->force_1p = fp && strcmp(fp, "1p") == 0;
+    const char* ff = getenv("NXG_F64R_FLAGS");
+    c->f64r_flags = ff ? (uint32_t)strtoul(ff, nullptr, 0) : 0u;
     return c;
 }
 
@@ -552,6 +630,7 @@ void nxg_ctx_destroy(NxgCtx* c) {
     if (c->dscratch) (void)hipFree(c->dscratch);
     if (c->dframe) (void)hipFree(c->dframe);
     if (c->escratch) (void)hipFree(c->escratch);
+    if (c->rdesc) (void)hipFree(c->rdesc);
     if (c->dheap) (void)hipFree(c->dheap);
     if (c->dst) (void)hipFree(c->dst);
     if (c->hst) (void)hipHostFree(c->hst);
@@ -628,12 +707,11 @@ bool nxg_decode_updates(NxgCtx* c, const uint8_t* frame, uint64_t len, NxgColumn
     DevStatus* st;
     uint32_t slot;
     if (!begin_call(c, &st, &slot, err)) return false;
-    const int fast = !(flags & NXG_DECODE_HINT_MIXED);
-    if (fast) {
-        if (!enqueue_dec_fast(c, df, len, target, st, err)) return false;
-    } else {
-        if (!enqueue_dec_general(c, df, len, target, st, err)) return false;
-    }
+    int fast = FAST_NONE;
+    const bool ok = !(flags & NXG_DECODE_HINT_MIXED)
+                        ? enqueue_dec_fast(c, df, len, target, st, &fast, err)
+                        : enqueue_dec_general(c, df, len, target, st, err);
+    if (!end_call(c, err) || !ok) return false;
     NxgStatus s;
     if (!finish_decode(c, df, len, target, fast, st, slot, &s, err)) return false;
     // result layout: F64 when the homogeneous kernel produced it (tag/aux not written)
@@ -673,16 +751,18 @@ bool nxg_decode_updates_async(NxgCtx* c, const uint8_t* dframe, uint64_t len, Nx
     DevStatus* st;
     uint32_t slot;
     if (!begin_call(c, &st, &slot, err)) return false;
-    const int fast = !(flags & NXG_DECODE_HINT_MIXED);
-    if (fast ? !enqueue_dec_fast(c, dframe, len, dout, st, err)
-             : !enqueue_dec_general(c, dframe, len, dout, st, err))
-        return false;
-    c->pending.push_back({1, fast, dframe, len, dout, nullptr, st, slot});
+    int fast = FAST_NONE;
+    const bool ok = !(flags & NXG_DECODE_HINT_MIXED)
+                        ? enqueue_dec_fast(c, dframe, len, dout, st, &fast, err)
+                        : enqueue_dec_general(c, dframe, len, dout, st, err);
+    if (!end_call(c, err) || !ok) return false;
+    c->pending.push_back({1, fast, dframe, len, dout, nullptr, 0, st, slot});
     return true;
 }
 
-// Completes every in-flight call in order; the status returned is the last call's (the first
-// failing call's, if one failed).
+// Completes every in-flight call in order (every one, even after a failure, so that each decode
+// gets its fallback and each encode its length); the status returned is the last call's, or the
+// first failing call's, and the first error is the one reported.
 bool nxg_ctx_sync(NxgCtx* c, NxgStatus* ust, NetidxError* err) {
     if (!c) {
         set_err(err, "null ctx");
@@ -692,32 +772,47 @@ bool nxg_ctx_sync(NxgCtx* c, NxgStatus* ust, NetidxError* err) {
     std::vector<NxgCtx::Pending> ps;
     ps.swap(c->pending);
     HIPCHK(hipStreamSynchronize(c->stream));
-    // every in-flight call's status in one copy (the ring is small), not one round trip each
+    // the in-flight calls used consecutive ring slots: at most two copies cover them
     if (!ps.empty()) {
-        HIPCHK(hipMemcpyAsync(c->hst, c->dst, sizeof(DevStatus) * kStatusRing,
-                              hipMemcpyDeviceToHost, c->stream));
+        const uint32_t s0 = ps.front().slot, s1 = ps.back().slot;
+        if (s0 <= s1) {
+            HIPCHK(hipMemcpyAsync(c->hst + s0, c->dst + s0, sizeof(DevStatus) * (s1 - s0 + 1),
+                                  hipMemcpyDeviceToHost, c->stream));
+        } else {
+            HIPCHK(hipMemcpyAsync(c->hst + s0, c->dst + s0, sizeof(DevStatus) * (kStatusRing - s0),
+                                  hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(hipMemcpyAsync(c->hst, c->dst, sizeof(DevStatus) * (s1 + 1),
+                                  hipMemcpyDeviceToHost, c->stream));
+        }
         HIPCHK(hipStreamSynchronize(c->stream));
     }
     if (ust) memset(ust, 0, sizeof *ust);
-    bool reported = false;
+    bool reported = false, ok = true;
     for (auto& p : ps) {
+        NetidxError e{nullptr};
+        bool r;
         if (p.kind == 1) {
             NxgStatus s;
-            if (!finish_decode(c, p.frame, p.len, p.cols, p.fast, p.st, p.slot, &s, err, true))
-                return false;
-            p.cols->layout =
-                (!mixed_capable(p.cols) || s.path == 1) ? NXG_LAYOUT_F64 : NXG_LAYOUT_MIXED;
-            if (ust && !reported) *ust = s;
-            if (s.err_kind) reported = true;
+            r = finish_decode(c, p.frame, p.len, p.cols, p.fast, p.st, p.slot, &s, &e, true);
+            if (r) {
+                p.cols->layout =
+                    (!mixed_capable(p.cols) || s.path == 1) ? NXG_LAYOUT_F64 : NXG_LAYOUT_MIXED;
+                if (ust && !reported) *ust = s;
+                if (s.err_kind) reported = true;
+            }
         } else {
             NxgColumns dummy{};
             dummy.layout = NXG_LAYOUT_F64;
-            if (!finish_encode(c, p.cols ? p.cols : &dummy, p.st, p.slot, p.len_out, ~0ull, false,
-                               err, true))
-                return false;
+            r = finish_encode(c, p.cols ? p.cols : &dummy, p.st, p.slot, p.len_out, p.cap, true,
+                              &e, true);
         }
+        if (!r && ok) {
+            ok = false;
+            set_err(err, "%s", e.msg ? e.msg : "async call failed");
+        }
+        nxg_error_free(&e);
     }
-    return true;
+    return ok;
 }
 
 static bool encode_impl(NxgCtx* c, const NxgColumns* in, const uint8_t* heap, uint8_t* out,
@@ -776,7 +871,8 @@ static bool encode_impl(NxgCtx* c, const NxgColumns* in, const uint8_t* heap, ui
     // pass 1 (sizing) when writing to a host buffer; a device buffer is written directly
     if (host && out) {
         if (!begin_call(c, &st, &slot, err)) return false;
-        if (!enqueue_encode(c, din, dheap, nullptr, 0, st, err)) return false;
+        const bool ok = enqueue_encode(c, din, dheap, nullptr, 0, st, err);
+        if (!end_call(c, err) || !ok) return false;
         if (!finish_encode(c, din, st, slot, &total, 0, false, err)) return false;
         if (total > cap) {
             set_err(err, "output buffer too small: need %llu bytes, have %llu",
@@ -795,7 +891,8 @@ static bool encode_impl(NxgCtx* c, const NxgColumns* in, const uint8_t* heap, ui
         cap = total;
     }
     if (!begin_call(c, &st, &slot, err)) return false;
-    if (!enqueue_encode(c, din, dheap, dout, out ? cap : 0, st, err)) return false;
+    const bool ok = enqueue_encode(c, din, dheap, dout, out ? cap : 0, st, err);
+    if (!end_call(c, err) || !ok) return false;
     if (!finish_encode(c, din, st, slot, &total, cap, dout != nullptr, err)) return false;
     if (host && out && total) {
         HIPCHK(hipMemcpyAsync(out, dout, total, hipMemcpyDeviceToHost, c->stream));
@@ -962,8 +1059,9 @@ bool nxg_encode_updates_async(NxgCtx* c, const NxgColumns* din, const uint8_t* d
     DevStatus* st;
     uint32_t slot;
     if (!begin_call(c, &st, &slot, err)) return false;
-    if (!enqueue_encode(c, din, dheap, dout, cap, st, err)) return false;
-    c->pending.push_back({2, 0, nullptr, 0, const_cast<NxgColumns*>(din), len_out, st, slot});
+    const bool ok = enqueue_encode(c, din, dheap, dout, cap, st, err);
+    if (!end_call(c, err) || !ok) return false;
+    c->pending.push_back({2, 0, nullptr, 0, const_cast<NxgColumns*>(din), len_out, cap, st, slot});
     return true;
 }
 

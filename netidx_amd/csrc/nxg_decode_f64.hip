@@ -172,7 +172,7 @@ hipError_t nxg_launch_dec_f64(const uint8_t* wire, uint64_t W, uint64_t* oid, ui
     uint32_t* wcnt = reinterpret_cast<uint32_t*>(scratch);
     uint32_t* gcnt = reinterpret_cast<uint32_t*>(scratch + MAX_WGS * WAVES / 2);
     hipLaunchKernelGGL(nxg_f64_count_kernel, dim3(wgs), dim3(TPB), 0, s, wire, W, nt, wcnt, gcnt,
-                       moff, st, nxg_zero_slot);
+                       moff, st, nxg_take_zero_slot());
     hipLaunchKernelGGL(nxg_f64_emit_kernel, dim3(wgs), dim3(TPB), 0, s, wire, W, nt, wcnt, gcnt,
                        moff, oid, oval, cap, st);
     return hipGetLastError();

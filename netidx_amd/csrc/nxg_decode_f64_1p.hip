@@ -327,7 +327,7 @@ hipError_t nxg_launch_dec_f64_1p(const uint8_t* wire, uint64_t W, uint64_t* oid,
     if (nt == 0) return hipSuccess;
     if (wgs < 2) return hipErrorInvalidValue;
     hipLaunchKernelGGL(nxg_f64_1p_kernel, dim3(wgs), dim3(TPB1), 0, s, wire, W, nt, oid, oval, cap,
-                       tstat, tstat + nt, epoch, st, nxg_zero_slot);
+                       tstat, tstat + nt, epoch, st, nxg_take_zero_slot());
     return hipGetLastError();
 }
 

@@ -1,0 +1,626 @@
+// nxg_decode_f64_run.hip -- homogeneous-f64 decode by length-run speculation, for gfx950.
+// Replaces the receive_batch_fn loop (netidx/src/channel.rs:504-521) for frames in which every
+// message is From::Update(Id, F64):
+//     varint(L) 04 varint(id) 09 f64be     L = lw(10 + vl(id)) = 11 + vl(id)
+// (len_wrapped_encode pack.rs:527-535, derive lib.rs:289-381, Value::encode lib.rs:404-407).
+// Ids of 1..5 varint bytes (< 2^35) are decoded here, so records are 12..16 bytes long.
+//
+// Why speculation works. Record k+1 starts at s_k + L_k: the boundaries are a pointer chain.
+// But L depends only on the id's varint width, and publisher ids come from a per-process
+// counter (netidx-core/src/utils.rs:130-134), so the ids of a batch change width only at 2^7,
+// 2^14, 2^21, 2^28: almost every 16 KiB tile is a run of records of ONE length. For such a tile
+// the record count follows from its first record alone: n = ceil((T - e) / L).
+//
+//   probe  (one lane per tile): the tile's entry e (the unique valid record start in its first
+//          16 bytes), L from that record, n, and a check of the predicted last record. A tile
+//          whose prediction fails (a width change, a false candidate) is counted exactly by the
+//          whole wave (merge points, below). Counts -> block scan -> decoupled look-back across
+//          workgroups -> each tile's first record index. Reads ~64 B per tile.
+//   emit   (one wave per tile, no inter-workgroup waits): every record of a uniform tile is at
+//          e + kL; lane j decodes records j, j+64, ... with two 16-byte loads each, checks it
+//          completely (length, variant 4, id varint width, value tag 9) and stores straight to
+//          the id / value columns (64 consecutive rows per store: coalesced). Exact tiles are
+//          re-walked from their merge points. Each tile's chain exit must equal the next
+//          tile's entry (and the last one the frame end), so a wrong speculation can cost
+//          speed, never correctness: any failed check raises fast_fail and the host reruns the
+//          frame on the general decoder.
+//
+// Merge points (exact tiles): the first record at or after a chunk start c lies in [c, c+16);
+// every valid record start in that window starts a walk, and the walks are advanced in position
+// order until they coincide. The true chain passes through the merge point, which depends only
+// on the bytes, so the lane that owns the previous chunk computes the same position.
+#include "nxg_device.h"
+
+namespace f64r {
+#ifndef NXG_F64R_T
+#define NXG_F64R_T 16384
+#endif
+constexpr uint32_t T = NXG_F64R_T;  // tile bytes (a wave's unit in the emit pass)
+constexpr uint32_t SUB = 4096;    // exact path: LDS image of 64 chunks of 64 bytes
+constexpr uint32_t HALO = 128;    // look-ahead bytes past the image (merge walks, records)
+constexpr int TPB = 256;
+constexpr uint32_t MODE_EXACT = 0;  // Desc.mode: 12..16 = uniform record length
+
+constexpr uint32_t F_FORCE_EXACT = 1;  // probe flags (tests): every tile on the exact path
+constexpr uint32_t F_NO_BAIL = 2;      //   never give up on an irregular frame
+
+// Per-tile descriptor written by the probe, read by the emit pass. A tile is one or two runs of
+// records of one length each: records [0, ks) of length L from `entry`, then records [ks, count)
+// of length L2; or an exact tile (mode 0: merge points).
+struct Desc {
+    uint64_t base;   // first record index
+    uint16_t count;  // records starting in the tile (<= T / 12)
+    uint16_t ks;     // records in the first run
+    uint16_t x;      // chain exit, relative to the tile start (next tile's entry + T)
+    uint8_t entry;   // first record start, relative to the tile start (0..15)
+    uint8_t mode;    // bits 0-2: L - 11, bits 3-5: L2 - 11; 0 = exact tile
+};
+static_assert(sizeof(Desc) == 16, "Desc is one 16-byte load");
+}  // namespace f64r
+
+namespace {
+using namespace f64r;
+
+NXG_DEV uint4 ld16r(const uint8_t* __restrict__ p) { return *reinterpret_cast<const uint4*>(p); }
+// the bytes of [off, off+16) that lie inside the frame, zero-filled (out of line: rare)
+__device__ __attribute__((noinline)) uint4 ld16_tail(const uint8_t* __restrict__ wire,
+                                                    uint64_t off, uint64_t W) {
+    uint32_t v[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < 16; k++)
+        if (off + k < W) v[k >> 2] |= (uint32_t)wire[off + k] << (8 * (k & 3));
+    return make_uint4(v[0], v[1], v[2], v[3]);
+}
+NXG_DEV uint4 ld16g(const uint8_t* __restrict__ wire, uint64_t off, uint64_t W) {
+    if (off + 16 <= W) return ld16r(wire + off);
+    return ld16_tail(wire, off, W);
+}
+
+// 16 bytes at byte s (0..15) of the 32 bytes d[0..7] (little-endian dwords), no memory access
+NXG_DEV void extract16(const uint32_t (&d)[8], uint32_t s, uint32_t& e0, uint32_t& e1,
+                       uint32_t& e2, uint32_t& e3) {
+    // two levels of selects on the dword offset q = s / 4 (masks, not a dynamic array index,
+    // which the compiler would lower to scratch memory)
+    const uint32_t r = s & 3u;
+    const uint32_t m2 = 0u - ((s >> 3) & 1u), m1 = 0u - ((s >> 2) & 1u);
+    uint32_t g[6], f[5];
+#pragma unroll
+    for (int j = 0; j < 6; j++) g[j] = d[j] ^ ((d[j] ^ d[j + 2]) & m2);
+#pragma unroll
+    for (int j = 0; j < 5; j++) f[j] = g[j] ^ ((g[j] ^ g[j + 1]) & m1);
+    e0 = alignbyte(f[1], f[0], r);
+    e1 = alignbyte(f[2], f[1], r);
+    e2 = alignbyte(f[3], f[2], r);
+    e3 = alignbyte(f[4], f[3], r);
+}
+
+// A valid f64 Update record (L in 12..16: 1..5 id bytes) at e0,e1? Returns L or 0.
+// rem = bytes from the record start to the frame end.
+NXG_DEV uint32_t rec_check16(uint32_t e0, uint32_t e1, uint64_t rem) {
+    const uint32_t L = e0 & 0xffu;
+    const bool head = (L - 12u <= 4u) && (((e0 >> 8) & 0xffu) == 4u);
+    const uint32_t sh = 8u * ((L - 11u) & 7u);  // 8 * nb
+    const uint64_t x = ((((uint64_t)e1) << 32) | e0) >> 16;  // bytes 2..7
+    const uint64_t m = (1ull << sh) - 1ull;
+    const uint64_t want = 0x8080808080ull & (m >> 8);
+    const bool var = (x & 0x808080808080ull & m) == want;  // exactly nb varint bytes
+    const uint32_t tag = (uint32_t)(x >> sh) & 0xffu;       // Value tag after the id
+    return (head && var && tag == 9u && rem >= L) ? L : 0u;
+}
+
+// id and f64 bits of a record of length L (12..16) already checked by rec_check16
+NXG_DEV void rec_decode16(uint32_t e0, uint32_t e1, uint32_t e2, uint32_t e3, uint32_t L,
+                          uint64_t& id, uint64_t& val) {
+    const uint32_t sh = 8u * ((L - 11u) & 7u);
+    const uint64_t x = ((((uint64_t)e1) << 32) | e0) >> 16;
+    const uint64_t y = x & ((1ull << sh) - 1ull) & 0x7f7f7f7f7full;
+    id = (y & 0x7full) | ((y >> 1) & 0x3f80ull) | ((y >> 2) & 0x1fc000ull) |
+         ((y >> 3) & 0xfe00000ull) | ((y >> 4) & 0x7f0000000ull);
+    const uint32_t o = L - 8u;  // value offset, 4..8
+    const uint32_t lo = o >= 8u ? e2 : alignbyte(e2, e1, o & 3u);
+    const uint32_t hi = o >= 8u ? e3 : alignbyte(e3, e2, o & 3u);
+    val = ((uint64_t)bswap32(lo) << 32) | bswap32(hi);  // big-endian f64 (pack.rs:592-598)
+}
+
+// SWAR: 0x80 in each byte of x whose value is in [12, 16] (record lengths)
+NXG_DEV uint32_t len_bytes(uint32_t x) {
+    const uint32_t y = x & 0x7f7f7f7fu;
+    return (0x90909090u - y) & ~x & (y + 0x74747474u) & 0x80808080u;
+}
+// candidate starts in positions 0..15 of d[0..4]: a byte in 12..16 followed by 0x04
+NXG_DEV uint32_t cand16(uint32_t d0, uint32_t d1, uint32_t d2, uint32_t d3, uint32_t d4) {
+    const uint32_t a = nib(len_bytes(d0)) | (nib(len_bytes(d1)) << 4) | (nib(len_bytes(d2)) << 8) |
+                       (nib(len_bytes(d3)) << 12);
+    const uint32_t b = nib(zero_bytes(d0 ^ 0x04040404u)) | (nib(zero_bytes(d1 ^ 0x04040404u)) << 4) |
+                       (nib(zero_bytes(d2 ^ 0x04040404u)) << 8) |
+                       (nib(zero_bytes(d3 ^ 0x04040404u)) << 12) |
+                       (nib(zero_bytes(d4 ^ 0x04040404u)) << 16);
+    return a & (b >> 1) & 0xffffu;
+}
+
+// 16 bytes at LDS byte offset rel (any alignment)
+NXG_DEV void lds16(const uint8_t* buf, uint32_t rel, uint32_t& e0, uint32_t& e1, uint32_t& e2,
+                   uint32_t& e3) {
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(buf + (rel & ~3u));
+    const uint32_t s = rel & 3u;
+    const uint32_t d0 = w[0], d1 = w[1], d2 = w[2], d3 = w[3], d4 = w[4];
+    e0 = alignbyte(d1, d0, s);
+    e1 = alignbyte(d2, d1, s);
+    e2 = alignbyte(d3, d2, s);
+    e3 = alignbyte(d4, d3, s);
+}
+
+constexpr uint32_t FAILX = 0xffffffffu;
+constexpr int WIN = 64;  // merge walks must coincide within 64 bytes of the chunk start
+
+// Merge point of all record walks starting in [r, r+16) of the LDS image (r 4-aligned), as a
+// position relative to the image; the END position (W - a0) for a chunk at or past the frame's
+// end; FAILX if the walks do not merge.
+NXG_DEV uint32_t merge16(const uint8_t* buf, uint32_t r, uint64_t a0, uint64_t W) {
+    const uint64_t abs_r = a0 + r;
+    if (abs_r >= W) return (uint32_t)(W - a0);
+    const uint64_t remr = W - abs_r;
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(buf + r);
+    uint32_t cand = cand16(w[0], w[1], w[2], w[3], w[4]);
+    uint64_t S = 0;
+    if (remr < 16) S |= 1ull << remr;  // the frame end is a valid (terminal) position
+    while (cand) {
+        const uint32_t p = __builtin_ctz(cand);
+        cand &= cand - 1;
+        uint32_t e0, e1, e2, e3;
+        lds16(buf, r + p, e0, e1, e2, e3);
+        if (rec_check16(e0, e1, remr - p)) S |= 1ull << p;
+    }
+    for (int it = 0; it < WIN && __popcll(S) > 1; it++) {
+        const uint32_t p = __builtin_ctzll(S);
+        S &= S - 1;
+        uint32_t e0, e1, e2, e3;
+        lds16(buf, r + p, e0, e1, e2, e3);
+        const uint32_t L = rec_check16(e0, e1, remr - p);
+        const uint32_t np = p + L;
+        if (np >= (uint32_t)WIN) return FAILX;
+        bool ok = (np == remr);
+        if (!ok) {
+            lds16(buf, r + np, e0, e1, e2, e3);
+            ok = rec_check16(e0, e1, remr - np) != 0;
+        }
+        if (ok) S |= 1ull << np;
+    }
+    if (__popcll(S) != 1) return FAILX;
+    return r + (uint32_t)__builtin_ctzll(S);
+}
+
+// Exact path for tile t, by the whole wave, in 4 KiB sub-tiles. A sub-tile at a0 owns the
+// records that START in [a0, a0 + 4096), like a uniform tile. Its LDS image holds the bytes
+// [a0 - 64, a0 + 4096 + HALO) (image offset = position - a0 + 64). Lane j walks the chain from
+// the merge point of chunk j to that of chunk j + 1; lane 0 starts one chunk earlier (the chunk
+// before a0, whose merge point precedes a0: the frame start for a0 = 0), so the walks cover
+// every record from before a0 to past a0 + 4096, and each record is counted by exactly one lane.
+// Returns (wave-uniform) the record count, the entry (first start - t0), the exit x (first start
+// at or past t0 + T, or the frame end, minus t0) and `bad`. With EMIT the records go to rows
+// base + index (a rare path: plain stores).
+constexpr uint32_t XLO = 64;            // image offset of a0
+constexpr uint32_t XHI = XLO + SUB;     // image offset of a0 + 4096
+constexpr uint32_t IMGB = XHI + HALO;   // image bytes
+template <bool EMIT>
+NXG_DEV void exact_tile(const uint8_t* __restrict__ wire, uint64_t W, uint64_t t, uint8_t* buf,
+                        uint32_t lane, uint64_t base, uint64_t* __restrict__ oid,
+                        uint64_t* __restrict__ oval, uint64_t cap, uint32_t& count,
+                        uint32_t& entry, uint32_t& x, bool& bad, bool& over) {
+    const uint64_t t0 = t * T;
+    count = 0;
+    entry = 0;
+    x = 0;
+    uint32_t prev_exit = 0;
+    for (uint32_t s = 0; s < T / SUB; s++) {
+        const uint64_t a0 = t0 + (uint64_t)s * SUB;
+        if (a0 >= W) break;
+        const uint64_t ib = a0 - XLO;  // frame position of image byte 0 (wraps for a0 = 0)
+        wave_lds_order();
+#pragma unroll
+        for (uint32_t i = 0; i < (IMGB + 1023) / 1024; i++) {
+            const uint32_t off = i * 1024 + lane * 16;
+            if (off < IMGB) {
+                uint4 v = make_uint4(0, 0, 0, 0);
+                if (a0 + off >= XLO) v = ld16g(wire, ib + off, W);  // nothing before the frame
+                *reinterpret_cast<uint4*>(buf + off) = v;
+            }
+        }
+        wave_lds_order();
+        // segment starts: lane 0 the chunk before a0, lane j >= 1 chunk j; ends: the next lane's
+        // start, lane 63 the merge point of the chunk at a0 + 4096
+        uint32_t xa;
+        if (lane == 0) xa = a0 == 0 ? XLO : merge16(buf, 0, ib, W);
+        else xa = merge16(buf, XLO + lane * 64, ib, W);
+        uint32_t xb = wave_next(xa);
+        if (lane == 63) xb = merge16(buf, XHI, ib, W);
+        bool b = xa == FAILX || xb == FAILX || xa > xb || (lane == 0 && xa > XLO);
+        // walk: count the records that start in [XLO, XHI); note the first start >= XLO (lane 0)
+        // and the first position >= XHI (the exit)
+        uint32_t n = 0, first = FAILX, ex = FAILX;
+        if (!b) {
+            uint32_t pos = xa;
+            int guard = 0;
+            while (pos < xb && guard < 24) {
+                if (pos >= XLO && first == FAILX) first = pos;
+                if (pos >= XHI) {
+                    if (ex == FAILX) ex = pos;
+                } else {
+                    uint32_t e0, e1, e2, e3;
+                    lds16(buf, pos, e0, e1, e2, e3);
+                    const uint32_t L = rec_check16(e0, e1, W - (ib + pos));
+                    if (!L) break;
+                    if (pos >= XLO) n++;
+                    pos += L;
+                    guard++;
+                    continue;
+                }
+                // past the sub-tile: step by the length byte only (the next sub-tile checks it)
+                const uint32_t L = buf[pos];
+                if (L - 12u > 4u) break;
+                pos += L;
+                guard++;
+            }
+            b = pos != xb;
+            if (pos >= XLO && first == FAILX) first = pos;  // segment end (e.g. the frame end)
+            if (pos >= XHI && ex == FAILX) ex = pos;
+        }
+        if (__any(b)) {
+            bad = true;
+            return;
+        }
+        const uint32_t f0 = (uint32_t)__builtin_amdgcn_readlane((int)first, 0);
+        const uint32_t exw = wave_min_u32(ex);
+        if (s == 0) entry = f0 - XLO;
+        else if (f0 != prev_exit) {  // the sub-tiles' chains must meet
+            bad = true;
+            return;
+        }
+        const uint32_t inc = wave_incl_scan(n);
+        if (EMIT) {
+            uint64_t row = base + count + (inc - n);
+            uint32_t pos = xa;
+            while (pos < xb && pos < XHI) {
+                uint32_t e0, e1, e2, e3;
+                lds16(buf, pos, e0, e1, e2, e3);
+                const uint32_t L = e0 & 0xffu;
+                if (pos >= XLO) {
+                    uint64_t id, val;
+                    rec_decode16(e0, e1, e2, e3, L, id, val);
+                    if (row < cap) {
+                        oid[row] = id;
+                        oval[row] = val;
+                    } else {
+                        over = true;
+                    }
+                    row++;
+                }
+                pos += L;
+            }
+        }
+        count += wave_last(inc);
+        // the chain leaves the sub-tile at exw (image offset); the frame end if it ends inside
+        const uint32_t endw = W - ib < (uint64_t)IMGB ? (uint32_t)(W - ib) : FAILX;
+        const uint32_t xo = exw != FAILX ? exw : endw;
+        if (xo == FAILX) {
+            bad = true;
+            return;
+        }
+        prev_exit = xo - SUB;  // the next sub-tile's entry, as an image offset
+        x = s * SUB + (xo - XLO);
+    }
+}
+
+}  // namespace
+
+// 32 bytes at frame offset off (16-aligned) as dwords
+NXG_DEV void ld32(const uint8_t* __restrict__ wire, uint64_t off, uint64_t W, uint32_t (&q)[8]) {
+    const uint4 a = ld16g(wire, off, W), b = ld16g(wire, off + 16, W);
+    q[0] = a.x, q[1] = a.y, q[2] = a.z, q[3] = a.w;
+    q[4] = b.x, q[5] = b.y, q[6] = b.z, q[7] = b.w;
+}
+// length of the valid record at tile-relative position p (0 if none)
+NXG_DEV uint32_t rec_len_at(const uint8_t* __restrict__ wire, uint64_t W, uint64_t t0,
+                            uint32_t p) {
+    uint32_t q[8], e0, e1, e2, e3;
+    ld32(wire, t0 + (p & ~15u), W, q);
+    extract16(q, p & 15u, e0, e1, e2, e3);
+    return rec_check16(e0, e1, W - t0 - p);
+}
+
+// Two-run search, by the whole wave, for a tile whose records do not all have the first
+// record's length L: the first k whose position e + kL holds no record of length L (64 samples,
+// then the 64 positions after the last good sample), the second run's length L2 there, and a
+// check of that run's middle and last records. Returns false if the tile is not two runs.
+NXG_DEV bool run_search(const uint8_t* __restrict__ wire, uint64_t W, uint64_t t0, uint32_t e,
+                        uint32_t L, uint32_t lim, uint32_t lane, uint32_t& ks, uint32_t& L2,
+                        uint32_t& n, uint32_t& x) {
+    const uint32_t n1 = (lim - e + L - 1) / L;  // records if the whole tile were one run
+    const uint32_t step = (n1 + 62) / 63;
+    const uint32_t ki = lane == 63 ? n1 - 1 : min(lane * step, n1 - 1);
+    const bool good = rec_len_at(wire, W, t0, e + ki * L) == L;
+    const uint64_t badm = __ballot(!good);
+    if (!badm) return false;
+    const uint32_t ib = __builtin_ctzll(badm);  // first bad sample (never lane 0: k = 0 is good)
+    const uint32_t khi = (uint32_t)__builtin_amdgcn_readlane((int)ki, ib);
+    const uint32_t klo = ib ? (uint32_t)__builtin_amdgcn_readlane((int)ki, ib - 1) + 1 : 0u;
+    const uint32_t k2 = min(klo + lane, khi);
+    const uint32_t l2 = rec_len_at(wire, W, t0, e + k2 * L);
+    const uint64_t bm2 = __ballot(l2 != L);
+    const uint32_t j = __builtin_ctzll(bm2);  // bm2 != 0: k = khi is bad
+    ks = klo + j;
+    L2 = (uint32_t)__builtin_amdgcn_readlane((int)l2, j);
+    if (L2 == 0 || L2 == L) return false;
+    const uint32_t p2 = e + ks * L;
+    const uint32_t n2 = (lim - p2 + L2 - 1) / L2;
+    // the second run: 64 samples, its last record included
+    const uint32_t kc = lane == 63 ? n2 - 1 : lane * (n2 - 1) / 63;
+    const bool ok = rec_len_at(wire, W, t0, p2 + kc * L2) == L2;
+    if (!__all(ok)) return false;
+    n = ks + n2;
+    x = p2 + n2 * L2;
+    return true;
+}
+
+// ---- probe: one lane per tile ------------------------------------------------------------------
+__global__ __launch_bounds__(TPB) void nxg_f64r_probe_kernel(
+    const uint8_t* __restrict__ wire, uint64_t W, uint64_t nt, Desc* __restrict__ desc,
+    uint64_t* tstat, uint32_t epoch, uint32_t flags, DevStatus* __restrict__ st,
+    DevStatus* zst) {
+    zero_status(zst);
+    __shared__ __attribute__((aligned(16))) uint8_t img[TPB / 64][IMGB];
+    __shared__ uint64_t scan_tmp[TPB / 64];
+    __shared__ uint64_t sh_base;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const uint64_t t = (uint64_t)blockIdx.x * TPB + tid;
+    const bool has = t < nt;
+    const uint64_t t0 = t * T;
+    const uint32_t lim = has ? (W - t0 < T ? (uint32_t)(W - t0) : T) : 0u;
+    uint32_t count = 0, e = 0, x = 0, L = 0, L2 = 0, ks = 0;
+    int state = 0;  // 0 done, 1 run search, 2 exact
+    bool bad = false;
+    if (has) {
+        const uint64_t rem0 = W - t0;
+        uint32_t d[8];
+        ld32(wire, t0, W, d);
+        uint32_t cand = cand16(d[0], d[1], d[2], d[3], d[4]);
+        uint32_t V = 0;  // valid record starts (and the frame end) in [0, 16)
+        if (rem0 < 16) V |= 1u << rem0;
+        while (cand) {
+            const uint32_t s = __builtin_ctz(cand);
+            cand &= cand - 1;
+            uint32_t e0, e1, e2, e3;
+            extract16(d, s, e0, e1, e2, e3);
+            if (rec_check16(e0, e1, rem0 - s)) V |= 1u << s;
+        }
+        // the entry is the lowest valid start; the only other start allowed in the window is
+        // its successor (a record of <= 16 bytes leaves room for one more)
+        const uint32_t s1 = V ? (uint32_t)__builtin_ctz(V) : 32u;
+        uint32_t L1 = 0;
+        if (s1 < 16 && s1 != rem0) {
+            uint32_t e0, e1, e2, e3;
+            extract16(d, s1, e0, e1, e2, e3);
+            L1 = e0 & 0xffu;
+        }
+        const uint32_t p2 = s1 + L1;
+        if (t == 0 && !(V & 1u)) {
+            bad = true;
+        } else if (s1 < 16 && s1 == rem0) {  // the frame ends here: no record starts in the tile
+            e = x = s1;
+            L = L2 = 12;
+        } else if (s1 < 16 && V == ((1u << s1) | (p2 < 16 ? 1u << p2 : 0u))) {
+            e = s1;
+            L = L2 = L1;
+            const uint32_t n = (lim - e + L - 1) / L;
+            // the prediction's records at 1/4, 1/2, 3/4 and the end must have the same length
+            const uint32_t m = n - 1;
+            const uint32_t la = rec_len_at(wire, W, t0, e + m * L);
+            const uint32_t lb = rec_len_at(wire, W, t0, e + (m / 2) * L);
+            const uint32_t lc = rec_len_at(wire, W, t0, e + (m / 4) * L);
+            const uint32_t ld = rec_len_at(wire, W, t0, e + (3 * m / 4) * L);
+            if (la == L && lb == L && lc == L && ld == L) {
+                count = ks = n;
+                x = e + n * L;
+            } else {
+                state = 1;
+            }
+        } else {
+            state = 2;  // a false candidate, or no valid start: let the merge points decide
+        }
+        if ((flags & F_FORCE_EXACT) && !bad) state = 2;
+    }
+    // an irregular frame (record lengths that change from record to record: more than 1 tile
+    // in 8 off the runs, here or in any workgroup so far) is left to the persistent decoder, which
+    // the host reruns it on
+    const int nirr = __syncthreads_count(state != 0);
+    const uint64_t ntg = nt - (uint64_t)blockIdx.x * TPB < TPB ? nt - (uint64_t)blockIdx.x * TPB
+                                                               : TPB;
+    const bool bail = !(flags & F_NO_BAIL) &&
+                      ((uint64_t)nirr * 8 > ntg || (nirr && ld_agent32(&st->irregular)));
+    if (bail) {
+        if (tid == 0) {
+            atomicOr(&st->irregular, 1u);
+            atomicOr(&st->fast_fail, 1u);
+        }
+        state = 0;
+    }
+    // width changes inside a tile: two runs, found by the whole wave
+    uint64_t em = __ballot(state == 1);
+    while (em) {
+        const uint32_t j = __builtin_ctzll(em);
+        em &= em - 1;
+        const uint64_t tj = (uint64_t)blockIdx.x * TPB + w * 64 + j;
+        const uint32_t ej = (uint32_t)__builtin_amdgcn_readlane((int)e, j);
+        const uint32_t Lj = (uint32_t)__builtin_amdgcn_readlane((int)L, j);
+        const uint32_t limj = (uint32_t)__builtin_amdgcn_readlane((int)lim, j);
+        uint32_t ksj, L2j, nj, xj;
+        const bool two = run_search(wire, W, tj * T, ej, Lj, limj, lane, ksj, L2j, nj, xj);
+        if (lane == j) {
+            if (two) {
+                state = 0;
+                ks = ksj;
+                L2 = L2j;
+                count = nj;
+                x = xj;
+            } else {
+                state = 2;
+            }
+        }
+    }
+    // anything else: counted exactly by the whole wave
+    em = __ballot(state == 2);
+    while (em) {
+        const uint32_t j = __builtin_ctzll(em);
+        em &= em - 1;
+        uint32_t c, en, xx;
+        bool b = false, ov = false;
+        exact_tile<false>(wire, W, (uint64_t)blockIdx.x * TPB + w * 64 + j, img[w], lane, 0,
+                          nullptr, nullptr, 0, c, en, xx, b, ov);
+        if (lane == j) {
+            count = c;
+            e = en;
+            x = xx;
+            L = 0;
+            bad |= b;
+        }
+        if (lane == 0) atomicAdd(&st->diag[0], 1ull);  // exact tiles (diagnostics)
+    }
+    if (__any(bad) && lane == 0) atomicOr(&st->fast_fail, 1u);
+    uint64_t total;
+    const uint64_t excl = block_excl_scan<uint64_t, TPB>(count, scan_tmp, &total);
+    if (w == 0) {
+        uint64_t base = 0;
+        if (blockIdx.x == 0) {
+            if (lane == 0) st_agent(&tstat[0], lb_word(kFlagInc, epoch, total));
+        } else {
+            if (lane == 0) st_agent(&tstat[blockIdx.x], lb_word(kFlagAgg, epoch, total));
+            bool give_up;
+            base = lookback_prefix<4>(tstat, blockIdx.x, epoch, nullptr, give_up);
+            if (give_up) {
+                if (lane == 0) {
+                    atomicOr(&st->timeout, 1u);
+                    atomicOr(&st->fast_fail, 1u);
+                }
+            } else if (lane == 0) {
+                st_agent(&tstat[blockIdx.x], lb_word(kFlagInc, epoch, base + total));
+            }
+        }
+        if (lane == 0) sh_base = base;
+    }
+    __syncthreads();
+    if (has) {
+        Desc o;
+        o.base = sh_base + excl;
+        o.count = (uint16_t)count;
+        o.ks = (uint16_t)ks;
+        o.x = (uint16_t)x;
+        o.entry = (uint8_t)e;
+        o.mode = L ? (uint8_t)((L - 11u) | ((L2 - 11u) << 3)) : (uint8_t)MODE_EXACT;
+        desc[t] = o;
+    }
+}
+
+// ---- emit: one wave per tile ---------------------------------------------------------------------
+// A run tile: record k < ks at e + kL, record k >= ks at e + ks L + (k - ks) L2; lane j decodes
+// records j, j + 64, ...; R records per lane are loaded together.
+template <bool GUARD>
+NXG_DEV bool emit_runs(const uint8_t* __restrict__ wire, uint64_t W, uint64_t t0, uint32_t e,
+                       uint32_t L, uint32_t ks, uint32_t L2, uint32_t n, uint64_t base,
+                       uint64_t* __restrict__ oid, uint64_t* __restrict__ oval, uint64_t cap,
+                       uint32_t lane, bool& over) {
+    constexpr int R = 4;
+    bool bad = false;
+    const uint64_t r1 = t0 + e, r2 = t0 + e + (uint64_t)ks * L;
+    for (uint32_t kb = 0; kb < n; kb += 64 * R) {
+        uint32_t d[R][8];
+        uint64_t p[R];
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            const uint32_t k0 = kb + r * 64 + lane;
+            const uint32_t k = k0 < n ? k0 : n - 1;  // clamp: the loads stay unconditional
+            p[r] = k < ks ? r1 + (uint64_t)k * L : r2 + (uint64_t)(k - ks) * L2;
+            const uint64_t a = p[r] & ~15ull;
+            const uint4 A = GUARD ? ld16g(wire, a, W) : ld16r(wire + a);
+            const uint4 B = GUARD ? ld16g(wire, a + 16, W) : ld16r(wire + a + 16);
+            d[r][0] = A.x, d[r][1] = A.y, d[r][2] = A.z, d[r][3] = A.w;
+            d[r][4] = B.x, d[r][5] = B.y, d[r][6] = B.z, d[r][7] = B.w;
+        }
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            const uint32_t k = kb + r * 64 + lane;
+            const uint32_t Lk = (k < n ? k : n - 1) < ks ? L : L2;
+            uint32_t e0, e1, e2, e3;
+            extract16(d[r], (uint32_t)p[r] & 15u, e0, e1, e2, e3);
+            bad |= rec_check16(e0, e1, W - p[r]) != Lk;
+            uint64_t id, val;
+            rec_decode16(e0, e1, e2, e3, Lk, id, val);
+            const uint64_t row = base + k;
+            if (k < n) {
+                if (row < cap) {
+                    oid[row] = id;
+                    oval[row] = val;
+                } else {
+                    over = true;
+                }
+            }
+        }
+    }
+    return bad;
+}
+
+__global__ __launch_bounds__(TPB) void nxg_f64r_emit_kernel(
+    const uint8_t* __restrict__ wire, uint64_t W, uint64_t nt, const Desc* __restrict__ desc,
+    uint64_t* __restrict__ oid, uint64_t* __restrict__ oval, uint64_t cap,
+    DevStatus* __restrict__ st) {
+    __shared__ __attribute__((aligned(16))) uint8_t img[TPB / 64][IMGB];
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint64_t t = (uint64_t)blockIdx.x * (TPB / 64) + w;
+    if (t >= nt) return;
+    if (st->fast_fail) return;  // the probe rejected the frame (previous launch: plain load)
+    const Desc D = desc[t];
+    const uint64_t t0 = t * T;
+    bool bad = false, over = false;
+    // the chain: this tile's exit is the next tile's entry; the last tile ends at the frame end
+    if (t + 1 < nt) bad |= (uint32_t)D.x != T + desc[t + 1].entry;
+    else bad |= t0 + D.x != W;
+    if (D.mode != MODE_EXACT) {
+        const uint32_t L = 11u + (D.mode & 7u), L2 = 11u + ((D.mode >> 3) & 7u);
+        if (t0 + T + 32 <= W)
+            bad |= emit_runs<false>(wire, W, t0, D.entry, L, D.ks, L2, D.count, D.base, oid,
+                                    oval, cap, lane, over);
+        else
+            bad |= emit_runs<true>(wire, W, t0, D.entry, L, D.ks, L2, D.count, D.base, oid,
+                                   oval, cap, lane, over);
+    } else {
+        uint32_t c, en, xx;
+        bool b = false;
+        exact_tile<true>(wire, W, t, img[w], lane, D.base, oid, oval, cap, c, en, xx, b, over);
+        bad |= b || c != D.count || en != D.entry || xx != D.x;
+    }
+    if (t == nt - 1 && lane == 0) {
+        st->n_rows = D.base + D.count;
+        st->path = 1;
+    }
+    if (__any(bad) && lane == 0) atomicOr(&st->fast_fail, 1u);
+    if (__any(over) && lane == 0) atomicOr(&st->capacity, 1u);
+}
+
+uint64_t nxg_dec_f64r_tiles(uint64_t W) { return (W + T - 1) / T; }
+uint64_t nxg_dec_f64r_groups(uint64_t W) { return (nxg_dec_f64r_tiles(W) + TPB - 1) / TPB; }
+
+// `desc` holds nxg_dec_f64r_tiles(W) 16-byte descriptors, `tstat` nxg_dec_f64r_groups(W)
+// epoch-tagged words; neither needs initialisation. flags: F_FORCE_EXACT / F_NO_BAIL (tests).
+hipError_t nxg_launch_dec_f64r(const uint8_t* wire, uint64_t W, uint64_t* oid, uint64_t* oval,
+                               uint64_t cap, void* desc, uint64_t* tstat, uint32_t epoch,
+                               uint32_t flags, DevStatus* st, hipStream_t s) {
+    const uint64_t nt = nxg_dec_f64r_tiles(W);
+    if (nt == 0) return hipSuccess;
+    const uint64_t ng = nxg_dec_f64r_groups(W);
+    const uint64_t ne = (nt + TPB / 64 - 1) / (TPB / 64);
+    if (ne > 0x7fffffffull) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(nxg_f64r_probe_kernel, dim3((uint32_t)ng), dim3(TPB), 0, s, wire, W, nt,
+                       reinterpret_cast<Desc*>(desc), tstat, epoch, flags, st, nxg_take_zero_slot());
+    hipLaunchKernelGGL(nxg_f64r_emit_kernel, dim3((uint32_t)ne), dim3(TPB), 0, s, wire, W, nt,
+                       reinterpret_cast<const Desc*>(desc), oid, oval, cap, st);
+    return hipGetLastError();
+}

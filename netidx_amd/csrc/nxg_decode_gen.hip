@@ -1174,7 +1174,7 @@ hipError_t nxg_launch_dec_gen(const uint8_t* wire, uint64_t W, const ColsDesc& c
     const uint32_t R = (uint32_t)g * WAVES;
     uint64_t* fix = reinterpret_cast<uint64_t*>(lws + 64 * nt);  // nxg_dec_gen_scratch_bytes
     hipLaunchKernelGGL(nxg_gen_count_kernel, dim3(g), dim3(TPB), 0, s, wire, W, nt, lws, runs, st,
-                       nxg_zero_slot, fix);
+                       nxg_take_zero_slot(), fix);
     hipLaunchKernelGGL(nxg_gen_resolve_kernel, dim3(1), dim3(RES_TPB), 0, s, wire, W, nt, R, lws,
                        runs, base, st);
     hipLaunchKernelGGL(nxg_gen_emit_kernel, dim3(g), dim3(TPB), 0, s, wire, W, nt, lws, base, cd,

@@ -187,7 +187,7 @@ hipError_t nxg_launch_enc_f64(const uint64_t* id, const uint64_t* val, uint64_t 
     if (nt == 0) return hipSuccess;
     const uint64_t g = grid <= 0 ? nt : (nt < (uint64_t)grid ? nt : (uint64_t)grid);
     hipLaunchKernelGGL(nxg_enc_f64_kernel, dim3(g), dim3(TPB), 0, s, id, val, n, out, cap, tstat,
-                       (uint32_t)nt, epoch, st, nxg_zero_slot);
+                       (uint32_t)nt, epoch, st, nxg_take_zero_slot());
     return hipGetLastError();
 }
 

@@ -390,8 +390,12 @@ __global__ __launch_bounds__(TPB) void nxg_enc_rows_kernel(
             }
             default: vlen = value_len(c, true, r, &err); break;
             }
+            // queue_send refuses a message longer than MAX_BATCH (channel.rs:178-181); that bound
+            // also keeps the 32-bit staged lengths exact
+            const uint64_t ml = err ? 0ull : lwlen(1 + vl64(c.id[r]) + vlen);
+            if (!err && ml > 0x3FFFFFFFull) err = NXG_TOO_BIG;
             if (err) atomicMax(&st->err_kind, err);
-            len_lds[rl] = err ? 0u : (uint32_t)lwlen(1 + vl64(c.id[r]) + vlen);
+            len_lds[rl] = err ? 0u : (uint32_t)ml;
         }
         __syncthreads();
         // 3. the tile's byte offsets: block scan, then look-back over the tiles' byte counts
@@ -551,7 +555,7 @@ hipError_t nxg_launch_enc_general(const ColsDesc& cd, const uint8_t* heap, uint8
     if (nt) {
         const uint64_t g = grid <= 0 ? nt : (nt < (uint64_t)grid ? nt : (uint64_t)grid);
         hipLaunchKernelGGL(nxg_enc_rows_kernel, dim3(g), dim3(TPB), 0, s, cd, heap, out, cap,
-                           cd.n_ctl ? ctl_pre : nullptr, row_off, tstat, (uint32_t)nt, epoch, st, nxg_zero_slot);
+                           cd.n_ctl ? ctl_pre : nullptr, row_off, tstat, (uint32_t)nt, epoch, st, nxg_take_zero_slot());
     }
     if (cd.n_ctl && out) {
         const uint64_t nb = (cd.n_ctl + TPB - 1) / TPB;

@@ -5,7 +5,7 @@
 
 #include "../../include/nxg_codec.h"
 
-// Per-call device status block (a ring slot, zeroed in-kernel 128 calls ahead: zero_status).
+// Per-call device status block (a ring slot, zeroed kStatusRing/2 = 512 calls ahead: zero_status).
 struct DevStatus {
     uint64_t n_rows, n_children, n_ctl, n_heartbeat;  // totals written by the last tile
     uint32_t err_kind;                                 // first error in wire order
@@ -17,7 +17,7 @@ struct DevStatus {
     uint32_t runs_valid;   // general decode: runs on the true chain, 0 = all (resolve -> emit)
     uint64_t total_bytes;  // encode: bytes written
     uint32_t nonf64;       // general path ran into content that F64-only columns cannot hold
-    uint32_t pad0;
+    uint32_t irregular;    // f64 run decode: record lengths vary too often (=> persistent kernel)
     // general decode: first error as ~(offset << 8 | kind), combined with atomicMax (0 = none)
     uint64_t err_key;
     uint64_t pad1;
@@ -82,12 +82,19 @@ constexpr int MAXB = TILE * 15 + 32;   // staging bytes (f64 records <= 15 B for
 
 // launchers (each defined next to its kernel)
 struct ColsDesc;
-// Every launcher takes the call's status slot `st` and `zst`, the slot that the call 128 calls
-// later will use. Block 0 zeroes `zst` on entry, so the ring needs no per-call memset.
+// Every launcher takes the call's status slot `st` and `zst`, the slot that the call 512 calls
+// later will use (nxg_take_zero_slot()). Block 0 of the kernel that receives it zeroes `zst` on
+// entry, so the ring needs no per-call memset; a call that launches no such kernel (an empty
+// frame or batch) has the host zero it instead (nxg_zero_used, nxg_api.cpp).
 __device__ inline void zero_status(DevStatus* zst) {
     if (zst && blockIdx.x == 0 && threadIdx.x == 0) *zst = DevStatus{};
 }
 extern thread_local DevStatus* nxg_zero_slot;  // host side: passed through to the kernels
+extern thread_local bool nxg_zero_used;         // a kernel of this call zeroes nxg_zero_slot
+inline DevStatus* nxg_take_zero_slot() {
+    nxg_zero_used = true;
+    return nxg_zero_slot;
+}
 // f64 decode: count pass + emit pass, `wgs` workgroups each (nxg_dec_f64_wgs). `scratch`
 // holds f64dec::SCRATCH_WORDS words and `moff` 64 bytes per tile (nxg_dec_f64_tiles(W) tiles);
 // neither needs initialisation.
@@ -103,6 +110,14 @@ hipError_t nxg_launch_dec_f64_1p(const uint8_t* wire, uint64_t W, uint64_t* oid,
                                  uint64_t cap, uint64_t* tstat, uint32_t epoch, int wgs,
                                  DevStatus* st, hipStream_t s);
 int nxg_dec_f64_1p_wgs(int ncu);
+// f64 decode by length runs (nxg_decode_f64_run.hip): probe + emit launches. `desc` holds 16 bytes
+// per tile (nxg_dec_f64r_tiles(W)), `tstat` nxg_dec_f64r_groups(W) epoch-tagged words. Sets
+// DevStatus.irregular (and fast_fail) for frames whose record lengths vary record to record.
+uint64_t nxg_dec_f64r_tiles(uint64_t W);
+uint64_t nxg_dec_f64r_groups(uint64_t W);
+hipError_t nxg_launch_dec_f64r(const uint8_t* wire, uint64_t W, uint64_t* oid, uint64_t* oval,
+                               uint64_t cap, void* desc, uint64_t* tstat, uint32_t epoch,
+                               uint32_t flags, DevStatus* st, hipStream_t s);
 uint64_t nxg_enc_f64_tiles(uint64_t n);  // tiles (and tstat words) of an f64 encode
 hipError_t nxg_launch_enc_f64(const uint64_t* id, const uint64_t* val, uint64_t n, uint8_t* out,
                               uint64_t cap, uint64_t* tstat, uint32_t epoch, DevStatus* st,

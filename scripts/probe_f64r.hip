@@ -1,0 +1,199 @@
+// probe_f64r.hip -- timing probe for the length-run f64 decode (nxg_decode_f64_run.hip) against
+// the persistent single-pass decoder (nxg_decode_f64_1p.hip) and a plain stream kernel.
+// Frames (all From::Update(Id, F64)): seq = ids 0..N-1 in order (Id::new order, BASELINE
+// configs[1]); x28 = sequential ids straddling 2^28 (4- and 5-byte varints); perm = a random
+// permutation of 0..N-1 (record lengths vary record to record); w35 = random ids in [2^28, 2^35).
+// Every decode is checked against the generator's columns.
+// Usage: probe_f64r [records] [reps]
+#include <stdio.h>
+#include <stdlib.h>
+
+#include <algorithm>
+#include <random>
+#include <vector>
+
+#include "../netidx_amd/csrc/nxg_f64_rec.h"
+
+namespace p1n {
+#include "../netidx_amd/csrc/nxg_decode_f64_1p.hip"
+}
+namespace fr {
+#include "../netidx_amd/csrc/nxg_decode_f64_run.hip"
+}
+#undef NXG_F64R_T
+#define NXG_F64R_T 8192
+namespace fr8 {
+#include "../netidx_amd/csrc/nxg_decode_f64_run.hip"
+}
+#undef NXG_F64R_T
+#define NXG_F64R_T 4096
+namespace fr4 {
+#include "../netidx_amd/csrc/nxg_decode_f64_run.hip"
+}
+thread_local DevStatus* nxg_zero_slot = nullptr;
+thread_local bool nxg_zero_used = false;
+
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
+    fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); exit(1); } } while (0)
+
+__global__ void stream_kernel(const uint4* __restrict__ in, uint64_t nin, uint4* __restrict__ out,
+                              uint64_t nout) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nout; i += stride) {
+        uint4 v = i < nin ? in[i] : make_uint4(0, 0, 0, 0);
+        out[i] = v;
+    }
+}
+
+static uint64_t splitmix(uint64_t& s) {
+    uint64_t z = (s += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+static void build(const std::vector<uint64_t>& ids, std::vector<uint64_t>& vals,
+                  std::vector<uint8_t>& w) {
+    uint64_t seed = 7;
+    w.clear();
+    w.reserve(ids.size() * 16);
+    vals.resize(ids.size());
+    for (size_t i = 0; i < ids.size(); i++) {
+        uint8_t idb[10];
+        int nb = 0;
+        uint64_t v = ids[i];
+        while (v >= 0x80) { idb[nb++] = (uint8_t)(v | 0x80); v >>= 7; }
+        idb[nb++] = (uint8_t)v;
+        w.push_back((uint8_t)(11 + nb));
+        w.push_back(4);
+        for (int k = 0; k < nb; k++) w.push_back(idb[k]);
+        w.push_back(9);
+        const uint64_t f = vals[i] = splitmix(seed);
+        for (int k = 7; k >= 0; k--) w.push_back((uint8_t)(f >> (8 * k)));
+    }
+}
+
+int main(int argc, char** argv) {
+    const uint64_t N = argc > 1 ? strtoull(argv[1], 0, 0) : 10000000ull;
+    const int reps = argc > 2 ? atoi(argv[2]) : 20;
+    int ncu = 0;
+    CK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0));
+    uint64_t *oid, *oval, *tstat;
+    uint8_t *dw, *dstream;
+    void* desc;
+    DevStatus* st;
+    const uint64_t Wmax = N * 16 + 64;
+    CK(hipMalloc(&dw, Wmax));
+    CK(hipMalloc(&dstream, N * 16 + 64));
+    CK(hipMalloc(&oid, N * 8));
+    CK(hipMalloc(&oval, N * 8));
+    CK(hipMalloc(&desc, (Wmax / 4096 + 2) * 16));
+    const size_t tsw = 2 * (Wmax / 3968 + 2) + 4096;
+    CK(hipMalloc(&tstat, tsw * 8));
+    CK(hipMemset(tstat, 0, tsw * 8));
+    CK(hipMalloc(&st, sizeof(DevStatus) * 2));
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    uint32_t epoch = 0;
+    std::vector<uint64_t> hid(N), hval(N);
+
+    auto run = [&](const char* name, const std::vector<uint64_t>& ids,
+                   const std::vector<uint64_t>& vals, uint64_t W, int which,
+                   uint32_t flags = 0) {
+        auto fn = [&]() {
+            CK(hipMemsetAsync(st, 0, sizeof(DevStatus), 0));
+            epoch++;
+            if (which == 0)
+                CK(fr::nxg_launch_dec_f64r(dw, W, oid, oval, N, desc, tstat, epoch, flags, st, 0));
+            else if (which == 8)
+                CK(fr8::nxg_launch_dec_f64r(dw, W, oid, oval, N, desc, tstat, epoch, flags, st, 0));
+            else if (which == 4)
+                CK(fr4::nxg_launch_dec_f64r(dw, W, oid, oval, N, desc, tstat, epoch, flags, st, 0));
+            else
+                CK(p1n::nxg_launch_dec_f64_1p(dw, W, oid, oval, N, tstat, epoch,
+                                              p1n::nxg_dec_f64_1p_wgs(ncu), st, 0));
+        };
+        for (int i = 0; i < 3; i++) fn();
+        CK(hipDeviceSynchronize());
+        CK(hipMemset(oid, 0xff, N * 8));
+        CK(hipMemset(oval, 0xff, N * 8));
+        fn();
+        CK(hipDeviceSynchronize());
+        DevStatus h;
+        CK(hipMemcpy(&h, st, sizeof h, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(hid.data(), oid, N * 8, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(hval.data(), oval, N * 8, hipMemcpyDeviceToHost));
+        long bad = 0;
+        for (uint64_t i = 0; i < N; i++) bad += hid[i] != ids[i] || hval[i] != vals[i];
+        CK(hipEventRecord(a, 0));
+        for (int i = 0; i < reps; i++) fn();
+        CK(hipEventRecord(b, 0));
+        CK(hipEventSynchronize(b));
+        float ms = 0;
+        CK(hipEventElapsedTime(&ms, a, b));
+        ms /= reps;
+        printf("%-14s %-5s %8.4f ms %7.1f GB/s (W+16N) %5.1f%% rows=%llu ff=%u irr=%u to=%u "
+               "cap=%u exact_tiles=%llu mismatches=%ld\n",
+               which == 1 ? "f64_1p" : which == 8 ? "f64run_T8k" : which == 4 ? "f64run_T4k"
+               : (flags & 1 ? "f64run_exact" : flags & 2 ? "f64run_nobail" : "f64run"),
+               name, ms, (W + 16.0 * N) / ms / 1e6,
+               (W + 16.0 * N) / ms / 1e6 / 8000 * 100, (unsigned long long)h.n_rows, h.fast_fail,
+               h.irregular, h.timeout, h.capacity, (unsigned long long)h.diag[0], bad);
+        fflush(stdout);
+    };
+
+    std::vector<uint64_t> ids(N), vals;
+    std::vector<uint8_t> w;
+    const char* names[4] = {"seq", "x28", "perm", "w35"};
+    for (int f = 0; f < 4; f++) {
+        if (f == 0) for (uint64_t i = 0; i < N; i++) ids[i] = i;
+        if (f == 1) for (uint64_t i = 0; i < N; i++) ids[i] = (1ull << 28) - N / 2 + i;
+        if (f == 2) {
+            for (uint64_t i = 0; i < N; i++) ids[i] = i;
+            std::mt19937_64 g(11);
+            std::shuffle(ids.begin(), ids.end(), g);
+        }
+        if (f == 3) {
+            uint64_t s = 99;
+            for (uint64_t i = 0; i < N; i++)
+                ids[i] = (1ull << 28) + splitmix(s) % ((1ull << 35) - (1ull << 28));
+        }
+        build(ids, vals, w);
+        const uint64_t W = w.size();
+        CK(hipMemcpy(dw, w.data(), W, hipMemcpyHostToDevice));
+        printf("frame %s: records=%llu wire=%llu bytes\n", names[f], (unsigned long long)N,
+               (unsigned long long)W);
+        run(names[f], ids, vals, W, 0);
+        run(names[f], ids, vals, W, 8);
+        run(names[f], ids, vals, W, 4);
+        if (f == 0 || f == 2) run(names[f], ids, vals, W, 1);
+        if (f == 2) run(names[f], ids, vals, W, 4, 3);  // exact path everywhere (4 KiB tiles)
+        if (f == 2) run(names[f], ids, vals, W, 0, 2);            // two-run search everywhere
+        if (f == 0) {
+            run(names[f], ids, vals, W, 0);
+            run(names[f], ids, vals, W, 8);
+            run(names[f], ids, vals, W, 4);
+            run(names[f], ids, vals, W, 1);
+            auto tstream = [&](const char* nm, int grid) {
+                for (int i = 0; i < 3; i++)
+                    hipLaunchKernelGGL(stream_kernel, dim3(grid), dim3(256), 0, 0,
+                                       (const uint4*)dw, W / 16, (uint4*)dstream, N);
+                CK(hipEventRecord(a, 0));
+                for (int i = 0; i < reps; i++)
+                    hipLaunchKernelGGL(stream_kernel, dim3(grid), dim3(256), 0, 0,
+                                       (const uint4*)dw, W / 16, (uint4*)dstream, N);
+                CK(hipEventRecord(b, 0));
+                CK(hipEventSynchronize(b));
+                float ms = 0;
+                CK(hipEventElapsedTime(&ms, a, b));
+                ms /= reps;
+                printf("%-14s %-5s %8.4f ms %7.1f GB/s (W+16N) %5.1f%%\n", nm, "seq", ms,
+                       (W + 16.0 * N) / ms / 1e6, (W + 16.0 * N) / ms / 1e6 / 80);
+            };
+            tstream("stream_8192", 8192);
+            tstream("stream_2048", 2048);
+        }
+    }
+    return 0;
+}

@@ -1,0 +1,220 @@
+"""Full-size parity at the BASELINE.json configs: the HIP path through the C ABI against the CPU
+oracle (oracle/nx_oracle.c) on EVERY column and EVERY byte -- no sampling, no self-comparison.
+
+  configs[1]  decode 10^7 all-f64 records          (product decode vs nxo.decode of the same bytes)
+  configs[2]  decode 10^7 mixed records            (every column, children, control spans)
+  configs[3]  encode 10^7 records, f64 and mixed   (product encode vs the oracle encoder's bytes)
+
+plus the f64 decoders' robustness cases: ids whose varints cross 2^28 (5-byte ids), ids in random
+order (record lengths vary record to record: the persistent decoder takes the frame), the
+length-run decoder's exact path on every tile, and two decodes running at once on two streams.
+Reference rules: netidx-core/src/pack.rs:504-555, netidx-value/src/lib.rs:470-506.
+"""
+import os
+import time
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def codec():
+    import torch
+    import netidx_amd
+    assert torch.cuda.is_available()
+    c = netidx_amd.Codec(0)
+    yield c
+    c.close()
+
+
+def _decode_dev(codec, wire, cols, flags=0):
+    import torch
+    dw = torch.from_numpy(np.ascontiguousarray(wire)).cuda()
+    st = codec.decode_into(dw, dw.numel(), cols, flags, check=False)
+    return st
+
+
+def _assert_f64(cols, st, wire, n):
+    import nxo
+    assert st.err_kind == 0 and st.n_rows == n and st.path == 1
+    o = nxo.decode(wire, cap_rows=n + 1, cap_children=1, cap_ctl=1).trim()
+    assert o["err_kind"] == 0 and len(o["id"]) == n and (o["tag"] == 9).all()
+    g = cols.numpy()
+    assert np.array_equal(g["id"], o["id"])
+    assert np.array_equal(g["fixed"], o["fixed"])
+
+
+def test_config2_f64_decode_10m_every_row(codec):
+    import netidx_amd
+    import nxo
+    from netidx_amd import synth
+    from netidx_amd.codec import Columns
+    n = 10_000_000
+    ids, vals = synth.f64_columns(n)
+    wire = nxo.encode_f64(ids, vals)
+    assert len(wire) == 147_886_336
+    cols = Columns(n, 0, 0, netidx_amd.LAYOUT_F64, "cuda")
+    st = _decode_dev(codec, wire, cols)
+    _assert_f64(cols, st, wire, n)
+
+
+def test_config4_f64_encode_10m_every_byte(codec):
+    import netidx_amd
+    import nxo
+    from netidx_amd import synth
+    n = 10_000_000
+    ids, vals = synth.f64_columns(n)
+    out = codec.encode_batch(netidx_amd.columns_from_arrays(ids, vals)).cpu().numpy()
+    assert np.array_equal(out, nxo.encode_f64(ids, vals))
+
+
+def _mixed(n, seed=None):
+    import nxo
+    from netidx_amd import synth
+    m = synth.mixed_columns(n) if seed is None else synth.mixed_columns(n, seed)
+    d = nxo.Decoded(n, len(m.ctag) + 1, 1)
+    for name in ("id", "tag", "fixed", "aux"):
+        getattr(d, name)[:n] = getattr(m, name)
+    d.ctag[:len(m.ctag)] = m.ctag
+    d.cfixed[:len(m.ctag)] = m.cfixed
+    d.caux[:len(m.ctag)] = m.caux
+    d.s.n_rows, d.s.n_children, d.s.n_ctl = n, len(m.ctag), 0
+    return m, np.frombuffer(nxo.encode(d, m.heap), np.uint8)
+
+
+def test_config3_mixed_decode_10m_every_column(codec):
+    import netidx_amd
+    import nxo
+    from netidx_amd.codec import Columns
+    n = 10_000_000
+    m, wire = _mixed(n)
+    nc = len(m.ctag)
+    cols = Columns(n + 1, nc + 1, 1, netidx_amd.LAYOUT_MIXED, "cuda")
+    st = _decode_dev(codec, wire, cols, netidx_amd.HINT_MIXED)
+    assert st.err_kind == 0 and st.path == 2 and st.n_rows == n
+    o = nxo.decode(wire, cap_rows=n + 1, cap_children=nc + 1, cap_ctl=1).trim()
+    assert o["err_kind"] == 0 and len(o["id"]) == n and len(o["ctag"]) == nc
+    g = cols.numpy()
+    for k in ("id", "tag", "fixed", "aux", "ctag", "cfixed", "caux", "ctl_row", "ctl_off",
+              "ctl_len", "ctl_variant"):
+        assert np.array_equal(g[k], o[k]), k
+    assert st.n_heartbeat == o["n_heartbeat"] == 0
+    # and the generator's own columns (strings are zero-copy offsets into the frame, so only
+    # the non-text columns are compared with the generator)
+    assert np.array_equal(g["id"], m.id) and np.array_equal(g["tag"], m.tag)
+    assert np.array_equal(g["ctag"], m.ctag) and np.array_equal(g["cfixed"], m.cfixed)
+
+
+def test_config4_mixed_encode_10m_every_byte(codec):
+    import netidx_amd
+    import torch
+    n = 10_000_000
+    m, wire = _mixed(n)
+    mc = netidx_amd.columns_from_arrays(m.id, m.fixed, m.tag, m.aux, m.ctag, m.cfixed, m.caux)
+    heap = torch.from_numpy(m.heap.copy()).cuda()
+    out = codec.encode_batch(mc, heap).cpu().numpy()
+    assert np.array_equal(out, wire)
+
+
+def test_f64_ids_across_2_28_on_the_fast_path(codec):
+    """Ids grow from a per-process counter (netidx-core/src/utils.rs:130-134): a long-lived
+    publisher crosses 2^28, where ids take 5 varint bytes. 10^6 records straddling it."""
+    import netidx_amd
+    import nxo
+    from netidx_amd import synth
+    from netidx_amd.codec import Columns
+    n = 1_000_000
+    ids, vals = synth.f64_columns(n, 71, id_offset=2**28 - n // 2)
+    wire = nxo.encode_f64(ids, vals)
+    cols = Columns(n, 0, 0, netidx_amd.LAYOUT_F64, "cuda")
+    _assert_f64(cols, _decode_dev(codec, wire, cols), wire, n)
+    # 5-byte ids everywhere (random order within [2^28, 2^35))
+    rng = np.random.default_rng(72)
+    ids = rng.integers(2**28, 2**35, n, dtype=np.uint64)
+    wire = nxo.encode_f64(ids, vals)
+    _assert_f64(cols, _decode_dev(codec, wire, cols), wire, n)
+
+
+def test_f64_ids_in_random_order(codec):
+    """Record lengths that vary record to record: the length-run decoder hands the frame to the
+    persistent decoder (DevStatus.irregular), still on path 1 and bit-exact."""
+    import netidx_amd
+    import nxo
+    from netidx_amd import synth
+    from netidx_amd.codec import Columns
+    n = 2_000_000
+    ids, vals = synth.f64_columns(n, 73)
+    ids = np.random.default_rng(74).permutation(ids)
+    wire = nxo.encode_f64(ids, vals)
+    cols = Columns(n, 0, 0, netidx_amd.LAYOUT_F64, "cuda")
+    for _ in range(2):  # the second frame goes straight to the persistent decoder
+        _assert_f64(cols, _decode_dev(codec, wire, cols), wire, n)
+
+
+def test_f64_run_decoder_exact_path_everywhere():
+    """NXG_F64R_FLAGS=1 (read at ctx creation) routes every tile of the length-run decoder
+    through its exact path (merge points): bit-exact on sequential, random-order and wide ids."""
+    import netidx_amd
+    import nxo
+    from netidx_amd import synth
+    from netidx_amd.codec import Columns
+    os.environ["NXG_F64R_FLAGS"] = "3"
+    try:
+        c = netidx_amd.Codec(0)
+    finally:
+        del os.environ["NXG_F64R_FLAGS"]
+    try:
+        n = 300_000
+        cols = Columns(n, 0, 0, netidx_amd.LAYOUT_F64, "cuda")
+        for k, off in enumerate((0, 2**28 - n // 2)):
+            ids, vals = synth.f64_columns(n, 80 + k, id_offset=off)
+            if k == 1:
+                ids = np.random.default_rng(81).permutation(ids)
+            wire = nxo.encode_f64(ids, vals)
+            _assert_f64(cols, _decode_dev(c, wire, cols), wire, n)
+    finally:
+        c.close()
+
+
+def test_f64_decodes_on_two_streams_at_once():
+    """Co-residency: two decodes in flight on two streams of one GPU (no workgroup of the f64
+    path waits on one that may not be resident). Both bit-exact; the pair completes within
+    2.5x the time of one decode alone."""
+    import netidx_amd
+    import torch
+    from netidx_amd import synth
+    from netidx_amd.codec import Columns
+    n = 10_000_000
+    ids, vals = synth.f64_columns(n)
+    import nxo
+    wire = torch.from_numpy(nxo.encode_f64(ids, vals)).cuda()
+    cs = [netidx_amd.Codec(0) for _ in range(2)]
+    ss = [torch.cuda.Stream() for _ in range(2)]
+    outs = [Columns(n, 0, 0, netidx_amd.LAYOUT_F64, "cuda") for _ in range(2)]
+    try:
+        for c, s in zip(cs, ss):
+            c.set_stream(s.cuda_stream)
+
+        def run(k_ctx, reps):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                for k in range(k_ctx):
+                    cs[k].decode_async(wire.data_ptr(), wire.numel(), outs[k])
+            sts = [cs[k].sync() for k in range(k_ctx)]
+            torch.cuda.synchronize()
+            return (time.perf_counter() - t0) / reps, sts
+
+        run(1, 3)
+        run(2, 3)
+        solo, _ = run(1, 20)
+        pair, sts = run(2, 20)
+        for st, o in zip(sts, outs):
+            assert st.path == 1 and st.n_rows == n
+            assert torch.equal(o.fixed[:n].cpu(), torch.from_numpy(vals.view(np.int64)))
+        assert pair < 2.5 * solo, (pair, solo)
+    finally:
+        for c in cs:
+            c.close()
