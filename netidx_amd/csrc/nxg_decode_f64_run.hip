@@ -521,6 +521,24 @@ __global__ __launch_bounds__(TPB) void nxg_f64r_probe_kernel(
 }
 
 // ---- emit: one wave per tile ---------------------------------------------------------------------
+#ifndef NXG_F64R_NT
+#define NXG_F64R_NT 0  // bit 0: nontemporal column stores, bit 1: nontemporal wire loads
+#endif
+#ifndef NXG_F64R_DPP
+#define NXG_F64R_DPP 0  // a record's second 16-byte block from the next lane (one load per record)
+#endif
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+NXG_DEV uint4 ld16s(const uint8_t* __restrict__ p) {
+    if (NXG_F64R_NT & 2) {
+        const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(p));
+        return make_uint4(v.x, v.y, v.z, v.w);
+    }
+    return ld16r(p);
+}
+NXG_DEV void st_col(uint64_t* p, uint64_t v) {
+    if (NXG_F64R_NT & 1) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
 // A run tile: record k < ks at e + kL, record k >= ks at e + ks L + (k - ks) L2; lane j decodes
 // records j, j + 64, ...; R records per lane are loaded together.
 template <bool GUARD>
@@ -540,10 +558,31 @@ NXG_DEV bool emit_runs(const uint8_t* __restrict__ wire, uint64_t W, uint64_t t0
             const uint32_t k = k0 < n ? k0 : n - 1;  // clamp: the loads stay unconditional
             p[r] = k < ks ? r1 + (uint64_t)k * L : r2 + (uint64_t)(k - ks) * L2;
             const uint64_t a = p[r] & ~15ull;
-            const uint4 A = GUARD ? ld16g(wire, a, W) : ld16r(wire + a);
-            const uint4 B = GUARD ? ld16g(wire, a + 16, W) : ld16r(wire + a + 16);
+            const uint4 A = GUARD ? ld16g(wire, a, W) : ld16s(wire + a);
             d[r][0] = A.x, d[r][1] = A.y, d[r][2] = A.z, d[r][3] = A.w;
-            d[r][4] = B.x, d[r][5] = B.y, d[r][6] = B.z, d[r][7] = B.w;
+            if (!NXG_F64R_DPP) {
+                const uint4 B = GUARD ? ld16g(wire, a + 16, W) : ld16s(wire + a + 16);
+                d[r][4] = B.x, d[r][5] = B.y, d[r][6] = B.z, d[r][7] = B.w;
+            }
+        }
+        if (NXG_F64R_DPP) {
+            // Records are <= 16 bytes and lane j + 1 holds the record after lane j's, so when
+            // lane j's record runs past its 16-byte block, the next block is exactly lane j + 1's
+            // first one; when it does not, bytes 16..31 are never read. Lane 63 and the lanes at
+            // or past the last record load their second block themselves.
+#pragma unroll
+            for (int r = 0; r < R; r++) {
+                d[r][4] = wave_next(d[r][0]);
+                d[r][5] = wave_next(d[r][1]);
+                d[r][6] = wave_next(d[r][2]);
+                d[r][7] = wave_next(d[r][3]);
+                const uint32_t k0 = kb + r * 64 + lane;
+                if (lane == 63 || k0 + 1 >= n) {
+                    const uint64_t a = (p[r] & ~15ull) + 16;
+                    const uint4 B = GUARD ? ld16g(wire, a, W) : ld16s(wire + a);
+                    d[r][4] = B.x, d[r][5] = B.y, d[r][6] = B.z, d[r][7] = B.w;
+                }
+            }
         }
 #pragma unroll
         for (int r = 0; r < R; r++) {
@@ -557,8 +596,8 @@ NXG_DEV bool emit_runs(const uint8_t* __restrict__ wire, uint64_t W, uint64_t t0
             const uint64_t row = base + k;
             if (k < n) {
                 if (row < cap) {
-                    oid[row] = id;
-                    oval[row] = val;
+                    st_col(&oid[row], id);
+                    st_col(&oval[row], val);
                 } else {
                     over = true;
                 }

@@ -20,16 +20,26 @@ namespace p1n {
 namespace fr {
 #include "../netidx_amd/csrc/nxg_decode_f64_run.hip"
 }
-#undef NXG_F64R_T
-#define NXG_F64R_T 8192
-namespace fr8 {
+#define NXG_F64R_NT 1
+namespace fr8 {  // nontemporal column stores
 #include "../netidx_amd/csrc/nxg_decode_f64_run.hip"
 }
-#undef NXG_F64R_T
-#define NXG_F64R_T 4096
-namespace fr4 {
+#undef NXG_F64R_NT
+#define NXG_F64R_NT 3
+namespace fr4 {  // nontemporal stores and loads
 #include "../netidx_amd/csrc/nxg_decode_f64_run.hip"
 }
+#undef NXG_F64R_NT
+#define NXG_F64R_DPP 1
+namespace frd {  // one load per record (second block from the next lane)
+#include "../netidx_amd/csrc/nxg_decode_f64_run.hip"
+}
+#define NXG_F64R_NT 1
+namespace frdn {  // the same + nontemporal stores
+#include "../netidx_amd/csrc/nxg_decode_f64_run.hip"
+}
+#undef NXG_F64R_NT
+#undef NXG_F64R_DPP
 thread_local DevStatus* nxg_zero_slot = nullptr;
 thread_local bool nxg_zero_used = false;
 
@@ -110,6 +120,20 @@ int main(int argc, char** argv) {
                 CK(fr8::nxg_launch_dec_f64r(dw, W, oid, oval, N, desc, tstat, epoch, flags, st, 0));
             else if (which == 4)
                 CK(fr4::nxg_launch_dec_f64r(dw, W, oid, oval, N, desc, tstat, epoch, flags, st, 0));
+            else if (which == 5)
+                CK(frd::nxg_launch_dec_f64r(dw, W, oid, oval, N, desc, tstat, epoch, flags, st, 0));
+            else if (which == 6)
+                CK(frdn::nxg_launch_dec_f64r(dw, W, oid, oval, N, desc, tstat, epoch, flags, st, 0));
+            else if (which == 20) {  // the probe kernel alone
+                const uint64_t nt = fr::nxg_dec_f64r_tiles(W);
+                hipLaunchKernelGGL(fr::nxg_f64r_probe_kernel, dim3(fr::nxg_dec_f64r_groups(W)),
+                                   dim3(256), 0, 0, dw, W, nt, (fr::f64r::Desc*)desc, tstat,
+                                   epoch, 0u, st, (DevStatus*)nullptr);
+            } else if (which == 21) {  // the emit kernel alone (descriptors of the last run)
+                const uint64_t nt = fr::nxg_dec_f64r_tiles(W);
+                hipLaunchKernelGGL(fr::nxg_f64r_emit_kernel, dim3((nt + 3) / 4), dim3(256), 0, 0,
+                                   dw, W, nt, (const fr::f64r::Desc*)desc, oid, oval, N, st);
+            }
             else
                 CK(p1n::nxg_launch_dec_f64_1p(dw, W, oid, oval, N, tstat, epoch,
                                               p1n::nxg_dec_f64_1p_wgs(ncu), st, 0));
@@ -135,7 +159,9 @@ int main(int argc, char** argv) {
         ms /= reps;
         printf("%-14s %-5s %8.4f ms %7.1f GB/s (W+16N) %5.1f%% rows=%llu ff=%u irr=%u to=%u "
                "cap=%u exact_tiles=%llu mismatches=%ld\n",
-               which == 1 ? "f64_1p" : which == 8 ? "f64run_T8k" : which == 4 ? "f64run_T4k"
+               which == 1 ? "f64_1p" : which == 8 ? "f64run_ntS" : which == 4 ? "f64run_ntSL"
+               : which == 5 ? "f64run_dpp" : which == 6 ? "f64run_dppntS"
+               : which == 20 ? "probe_only" : which == 21 ? "emit_only"
                : (flags & 1 ? "f64run_exact" : flags & 2 ? "f64run_nobail" : "f64run"),
                name, ms, (W + 16.0 * N) / ms / 1e6,
                (W + 16.0 * N) / ms / 1e6 / 8000 * 100, (unsigned long long)h.n_rows, h.fast_fail,
@@ -165,15 +191,19 @@ int main(int argc, char** argv) {
         printf("frame %s: records=%llu wire=%llu bytes\n", names[f], (unsigned long long)N,
                (unsigned long long)W);
         run(names[f], ids, vals, W, 0);
-        run(names[f], ids, vals, W, 8);
-        run(names[f], ids, vals, W, 4);
+        if (f != 2) {
+            run(names[f], ids, vals, W, 8);
+            run(names[f], ids, vals, W, 4);
+            run(names[f], ids, vals, W, 5);
+            run(names[f], ids, vals, W, 6);
+        }
         if (f == 0 || f == 2) run(names[f], ids, vals, W, 1);
-        if (f == 2) run(names[f], ids, vals, W, 4, 3);  // exact path everywhere (4 KiB tiles)
         if (f == 2) run(names[f], ids, vals, W, 0, 2);            // two-run search everywhere
         if (f == 0) {
             run(names[f], ids, vals, W, 0);
-            run(names[f], ids, vals, W, 8);
-            run(names[f], ids, vals, W, 4);
+            run(names[f], ids, vals, W, 20);
+            run(names[f], ids, vals, W, 0);
+            run(names[f], ids, vals, W, 21);
             run(names[f], ids, vals, W, 1);
             auto tstream = [&](const char* nm, int grid) {
                 for (int i = 0; i < 3; i++)
