@@ -33,9 +33,12 @@
 
 namespace f64r {
 #ifndef NXG_F64R_T
-#define NXG_F64R_T 16384
+#define NXG_F64R_T 32768
 #endif
-constexpr uint32_t T = NXG_F64R_T;  // tile bytes (a wave's unit in the emit pass)
+constexpr uint32_t T = NXG_F64R_T;  // tile bytes (the probe's unit)
+constexpr uint32_t EREC = 256;      // records per emit wave (a tile's records, in order)
+constexpr uint32_t ESUB = (T / 12 + EREC) / EREC;  // emit waves per tile (records >= 12 B)
+static_assert(T + 16 <= 65535, "Desc.x is 16 bits");
 constexpr uint32_t SUB = 4096;    // exact path: LDS image of 64 chunks of 64 bytes
 constexpr uint32_t HALO = 128;    // look-ahead bytes past the image (merge walks, records)
 constexpr int TPB = 256;
@@ -328,6 +331,18 @@ NXG_DEV uint32_t rec_len_at(const uint8_t* __restrict__ wire, uint64_t W, uint64
     return rec_check16(e0, e1, W - t0 - p);
 }
 
+// length of the valid record at tile-relative position p (0 if none) and its id
+NXG_DEV uint32_t rec_at(const uint8_t* __restrict__ wire, uint64_t W, uint64_t t0, uint32_t p,
+                        uint64_t& id) {
+    uint32_t q[8], e0, e1, e2, e3;
+    ld32(wire, t0 + (p & ~15u), W, q);
+    extract16(q, p & 15u, e0, e1, e2, e3);
+    const uint32_t L = rec_check16(e0, e1, W - t0 - p);
+    uint64_t v;
+    rec_decode16(e0, e1, e2, e3, L ? L : 12u, id, v);
+    return L;
+}
+
 // Two-run search, by the whole wave, for a tile whose records do not all have the first
 // record's length L: the first k whose position e + kL holds no record of length L (64 samples,
 // then the 64 positions after the last good sample), the second run's length L2 there, and a
@@ -411,17 +426,48 @@ __global__ __launch_bounds__(TPB) void nxg_f64r_probe_kernel(
         } else if (s1 < 16 && V == ((1u << s1) | (p2 < 16 ? 1u << p2 : 0u))) {
             e = s1;
             L = L2 = L1;
-            const uint32_t n = (lim - e + L - 1) / L;
-            // the prediction's records at 1/4, 1/2, 3/4 and the end must have the same length
+            uint32_t n = (lim - e + L - 1) / L;
+            ks = n;
+            // Ids from the publisher's counter are consecutive (utils.rs:130-134): if the first
+            // id plus n crosses the next varint width, the tile is predicted as two runs split
+            // where the ids reach it.
+            uint64_t id0;
+            {
+                uint32_t e0, e1, e2, e3;
+                extract16(d, e, e0, e1, e2, e3);
+                uint64_t v0;
+                rec_decode16(e0, e1, e2, e3, L, id0, v0);
+                const uint32_t nb = L - 11u;
+                const uint64_t next = 1ull << (7u * nb);
+                if (nb < 5 && id0 < next && id0 + n > next) {
+                    ks = (uint32_t)(next - id0);
+                    L2 = L + 1;
+                    const uint32_t q2 = e + ks * L;
+                    n = ks + (lim - q2 + L2 - 1) / L2;
+                }
+            }
+            // the prediction's last record and both sides of the split must have the predicted
+            // lengths and ids (one HBM line per sample; the emit pass checks every record)
+            auto at = [&](uint32_t k) { return k < ks ? e + k * L : e + ks * L + (k - ks) * L2; };
+            auto len = [&](uint32_t k) { return k < ks ? L : L2; };
             const uint32_t m = n - 1;
-            const uint32_t la = rec_len_at(wire, W, t0, e + m * L);
-            const uint32_t lb = rec_len_at(wire, W, t0, e + (m / 2) * L);
-            const uint32_t lc = rec_len_at(wire, W, t0, e + (m / 4) * L);
-            const uint32_t ld = rec_len_at(wire, W, t0, e + (3 * m / 4) * L);
-            if (la == L && lb == L && lc == L && ld == L) {
-                count = ks = n;
-                x = e + n * L;
+            const uint32_t ke = ks < n ? ks - 1 : m, kf = ks < n ? ks : m;
+            uint64_t ia, ie, iff;
+            const bool lok = rec_at(wire, W, t0, at(m), ia) == len(m) &&
+                             rec_at(wire, W, t0, at(ke), ie) == len(ke) &&
+                             rec_at(wire, W, t0, at(kf), iff) == len(kf);
+            bool ok = lok && ia == id0 + m && ie == id0 + ke && iff == id0 + kf;
+            if (!ok && lok && ks == n) {
+                // one length, ids not consecutive: one more sample, the middle record
+                uint64_t ib;
+                ok = rec_at(wire, W, t0, at(m / 2), ib) == L;
+            }
+            if (ok) {
+                count = n;
+                x = at(n);
             } else {
+                ks = n = (lim - e + L - 1) / L;  // back to one run for the wave's search
+                L2 = L;
                 state = 1;
             }
         } else {
@@ -522,10 +568,16 @@ __global__ __launch_bounds__(TPB) void nxg_f64r_probe_kernel(
 
 // ---- emit: one wave per tile ---------------------------------------------------------------------
 #ifndef NXG_F64R_NT
-#define NXG_F64R_NT 0  // bit 0: nontemporal column stores, bit 1: nontemporal wire loads
+#define NXG_F64R_NT 0  // bit 0: nontemporal column stores, bit 1: nontemporal wire loads,
+#endif                 // bit 2: nontemporal stores only for lines no other wave writes
+#ifndef NXG_F64R_R
+#define NXG_F64R_R 4   // records per lane loaded together
 #endif
 #ifndef NXG_F64R_DPP
-#define NXG_F64R_DPP 0  // a record's second 16-byte block from the next lane (one load per record)
+#define NXG_F64R_DPP 1  // a record's second 16-byte block from the next lane (one load per record)
+#endif
+#ifndef NXG_F64R_LDS
+#define NXG_F64R_LDS 0  // 64 records' bytes as one aligned 1 KiB load per wave, through LDS
 #endif
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 NXG_DEV uint4 ld16s(const uint8_t* __restrict__ p) {
@@ -535,52 +587,96 @@ NXG_DEV uint4 ld16s(const uint8_t* __restrict__ p) {
     }
     return ld16r(p);
 }
-NXG_DEV void st_col(uint64_t* p, uint64_t v) {
-    if (NXG_F64R_NT & 1) __builtin_nontemporal_store(v, p);
+NXG_DEV void st_col(uint64_t* p, uint64_t v, bool inner) {
+    if ((NXG_F64R_NT & 1) || ((NXG_F64R_NT & 4) && inner)) __builtin_nontemporal_store(v, p);
     else *p = v;
 }
 // A run tile: record k < ks at e + kL, record k >= ks at e + ks L + (k - ks) L2; lane j decodes
 // records j, j + 64, ...; R records per lane are loaded together.
 template <bool GUARD>
 NXG_DEV bool emit_runs(const uint8_t* __restrict__ wire, uint64_t W, uint64_t t0, uint32_t e,
-                       uint32_t L, uint32_t ks, uint32_t L2, uint32_t n, uint64_t base,
+                       uint32_t L, uint32_t ks, uint32_t L2, uint32_t klo, uint32_t n,
+                       uint64_t base,
                        uint64_t* __restrict__ oid, uint64_t* __restrict__ oval, uint64_t cap,
-                       uint32_t lane, bool& over) {
-    constexpr int R = 4;
+                       uint32_t lane, uint8_t* lbuf, bool& over) {
+    constexpr int R = NXG_F64R_R;
     bool bad = false;
     const uint64_t r1 = t0 + e, r2 = t0 + e + (uint64_t)ks * L;
-    for (uint32_t kb = 0; kb < n; kb += 64 * R) {
+    // rows in the first and last 128-byte line of the tile's rows share the line with the
+    // neighbouring tiles' rows
+    const uint64_t lfirst = (base + klo) >> 4, llast = (base + n - 1) >> 4;
+    auto pos = [&](uint32_t k) -> uint64_t {
+        return k < ks ? r1 + (uint64_t)k * L : r2 + (uint64_t)(k - ks) * L2;
+    };
+    for (uint32_t kb = klo; kb < n; kb += 64 * R) {
         uint32_t d[R][8];
         uint64_t p[R];
-#pragma unroll
-        for (int r = 0; r < R; r++) {
-            const uint32_t k0 = kb + r * 64 + lane;
-            const uint32_t k = k0 < n ? k0 : n - 1;  // clamp: the loads stay unconditional
-            p[r] = k < ks ? r1 + (uint64_t)k * L : r2 + (uint64_t)(k - ks) * L2;
-            const uint64_t a = p[r] & ~15ull;
-            const uint4 A = GUARD ? ld16g(wire, a, W) : ld16s(wire + a);
-            d[r][0] = A.x, d[r][1] = A.y, d[r][2] = A.z, d[r][3] = A.w;
-            if (!NXG_F64R_DPP) {
-                const uint4 B = GUARD ? ld16g(wire, a + 16, W) : ld16s(wire + a + 16);
-                d[r][4] = B.x, d[r][5] = B.y, d[r][6] = B.z, d[r][7] = B.w;
-            }
-        }
-        if (NXG_F64R_DPP) {
-            // Records are <= 16 bytes and lane j + 1 holds the record after lane j's, so when
-            // lane j's record runs past its 16-byte block, the next block is exactly lane j + 1's
-            // first one; when it does not, bytes 16..31 are never read. Lane 63 and the lanes at
-            // or past the last record load their second block themselves.
+        if (NXG_F64R_LDS) {
+            // the R x 64 records' bytes: one aligned, fully coalesced 1 KiB load per wave and
+            // batch (lane i: block i; lane 0 also block 64), then each lane reads the two blocks
+            // holding its record from LDS. Records are <= 16 bytes, so 64 of them starting in
+            // block 0 end by block 64.
+            uint64_t ab[R];
+            uint4 A[R], X[R];
 #pragma unroll
             for (int r = 0; r < R; r++) {
-                d[r][4] = wave_next(d[r][0]);
-                d[r][5] = wave_next(d[r][1]);
-                d[r][6] = wave_next(d[r][2]);
-                d[r][7] = wave_next(d[r][3]);
+                const uint32_t kf = kb + r * 64 < n ? kb + r * 64 : n - 1;
+                ab[r] = pos(kf) & ~15ull;
+                A[r] = GUARD ? ld16g(wire, ab[r] + 16 * lane, W) : ld16s(wire + ab[r] + 16 * lane);
+                if (lane == 0)
+                    X[r] = GUARD ? ld16g(wire, ab[r] + 1024, W) : ld16s(wire + ab[r] + 1024);
+            }
+            wave_lds_order();
+#pragma unroll
+            for (int r = 0; r < R; r++) {
+                uint4* blk = reinterpret_cast<uint4*>(lbuf + r * 1040);
+                blk[lane] = A[r];
+                if (lane == 0) blk[64] = X[r];
+            }
+            wave_lds_order();
+#pragma unroll
+            for (int r = 0; r < R; r++) {
                 const uint32_t k0 = kb + r * 64 + lane;
-                if (lane == 63 || k0 + 1 >= n) {
-                    const uint64_t a = (p[r] & ~15ull) + 16;
-                    const uint4 B = GUARD ? ld16g(wire, a, W) : ld16s(wire + a);
-                    d[r][4] = B.x, d[r][5] = B.y, d[r][6] = B.z, d[r][7] = B.w;
+                p[r] = pos(k0 < n ? k0 : n - 1);
+                const uint32_t q = (uint32_t)(p[r] - ab[r]) >> 4;
+                const uint4* blk = reinterpret_cast<const uint4*>(lbuf + r * 1040);
+                const uint4 a = blk[q], b = blk[q + 1];
+                d[r][0] = a.x, d[r][1] = a.y, d[r][2] = a.z, d[r][3] = a.w;
+                d[r][4] = b.x, d[r][5] = b.y, d[r][6] = b.z, d[r][7] = b.w;
+            }
+        } else {
+            uint4 B[R];
+#pragma unroll
+            for (int r = 0; r < R; r++) {
+                const uint32_t k0 = kb + r * 64 + lane;
+                const uint32_t k = k0 < n ? k0 : n - 1;  // clamp: the loads stay unconditional
+                p[r] = pos(k);
+                const uint64_t a = p[r] & ~15ull;
+                const uint4 A = GUARD ? ld16g(wire, a, W) : ld16s(wire + a);
+                d[r][0] = A.x, d[r][1] = A.y, d[r][2] = A.z, d[r][3] = A.w;
+                if (!NXG_F64R_DPP) {
+                    B[r] = GUARD ? ld16g(wire, a + 16, W) : ld16s(wire + a + 16);
+                } else if (lane == 63 || k0 + 1 >= n) {
+                    B[r] = GUARD ? ld16g(wire, a + 16, W) : ld16s(wire + a + 16);
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < R; r++) {
+                if (NXG_F64R_DPP) {
+                    // Records are <= 16 bytes and lane j + 1 holds the record after lane j's, so
+                    // when lane j's record runs past its 16-byte block, the next block is exactly
+                    // lane j + 1's first one; when it does not, bytes 16..31 are never read. Lane
+                    // 63 and the lanes at or past the last record loaded it themselves.
+                    const uint32_t k0 = kb + r * 64 + lane;
+                    const bool own = lane == 63 || k0 + 1 >= n;
+                    const uint32_t n0 = wave_next(d[r][0]), n1 = wave_next(d[r][1]),
+                                   n2 = wave_next(d[r][2]), n3 = wave_next(d[r][3]);
+                    d[r][4] = own ? B[r].x : n0;
+                    d[r][5] = own ? B[r].y : n1;
+                    d[r][6] = own ? B[r].z : n2;
+                    d[r][7] = own ? B[r].w : n3;
+                } else {
+                    d[r][4] = B[r].x, d[r][5] = B[r].y, d[r][6] = B[r].z, d[r][7] = B[r].w;
                 }
             }
         }
@@ -596,8 +692,9 @@ NXG_DEV bool emit_runs(const uint8_t* __restrict__ wire, uint64_t W, uint64_t t0
             const uint64_t row = base + k;
             if (k < n) {
                 if (row < cap) {
-                    st_col(&oid[row], id);
-                    st_col(&oval[row], val);
+                    const bool inner = (row >> 4) != lfirst && (row >> 4) != llast;
+                    st_col(&oid[row], id, inner);
+                    st_col(&oval[row], val, inner);
                 } else {
                     over = true;
                 }
@@ -607,38 +704,47 @@ NXG_DEV bool emit_runs(const uint8_t* __restrict__ wire, uint64_t W, uint64_t t0
     return bad;
 }
 
+// wave g: tile g / ESUB, records [EREC * (g % ESUB), EREC * (g % ESUB + 1)) of it
 __global__ __launch_bounds__(TPB) void nxg_f64r_emit_kernel(
     const uint8_t* __restrict__ wire, uint64_t W, uint64_t nt, const Desc* __restrict__ desc,
     uint64_t* __restrict__ oid, uint64_t* __restrict__ oval, uint64_t cap,
     DevStatus* __restrict__ st) {
     __shared__ __attribute__((aligned(16))) uint8_t img[TPB / 64][IMGB];
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const uint64_t t = (uint64_t)blockIdx.x * (TPB / 64) + w;
+    const uint64_t g = (uint64_t)blockIdx.x * (TPB / 64) + w;
+    const uint64_t t = g / ESUB;
+    const uint32_t sub = (uint32_t)(g % ESUB);
     if (t >= nt) return;
     if (st->fast_fail) return;  // the probe rejected the frame (previous launch: plain load)
     const Desc D = desc[t];
+    const uint32_t klo = sub * EREC;
+    if (D.mode == MODE_EXACT ? sub != 0 : klo >= D.count) return;
+    const uint32_t khi = D.count - klo < EREC ? D.count : klo + EREC;
     const uint64_t t0 = t * T;
     bool bad = false, over = false;
-    // the chain: this tile's exit is the next tile's entry; the last tile ends at the frame end
-    if (t + 1 < nt) bad |= (uint32_t)D.x != T + desc[t + 1].entry;
-    else bad |= t0 + D.x != W;
+    if (sub == 0) {
+        // the chain: this tile's exit is the next tile's entry; the last tile ends at the
+        // frame end
+        if (t + 1 < nt) bad |= (uint32_t)D.x != T + desc[t + 1].entry;
+        else bad |= t0 + D.x != W;
+        if (t == nt - 1 && lane == 0) {
+            st->n_rows = D.base + D.count;
+            st->path = 1;
+        }
+    }
     if (D.mode != MODE_EXACT) {
         const uint32_t L = 11u + (D.mode & 7u), L2 = 11u + ((D.mode >> 3) & 7u);
         if (t0 + T + 32 <= W)
-            bad |= emit_runs<false>(wire, W, t0, D.entry, L, D.ks, L2, D.count, D.base, oid,
-                                    oval, cap, lane, over);
+            bad |= emit_runs<false>(wire, W, t0, D.entry, L, D.ks, L2, klo, khi, D.base, oid,
+                                    oval, cap, lane, img[w], over);
         else
-            bad |= emit_runs<true>(wire, W, t0, D.entry, L, D.ks, L2, D.count, D.base, oid,
-                                   oval, cap, lane, over);
+            bad |= emit_runs<true>(wire, W, t0, D.entry, L, D.ks, L2, klo, khi, D.base, oid,
+                                   oval, cap, lane, img[w], over);
     } else {
         uint32_t c, en, xx;
         bool b = false;
         exact_tile<true>(wire, W, t, img[w], lane, D.base, oid, oval, cap, c, en, xx, b, over);
         bad |= b || c != D.count || en != D.entry || xx != D.x;
-    }
-    if (t == nt - 1 && lane == 0) {
-        st->n_rows = D.base + D.count;
-        st->path = 1;
     }
     if (__any(bad) && lane == 0) atomicOr(&st->fast_fail, 1u);
     if (__any(over) && lane == 0) atomicOr(&st->capacity, 1u);
@@ -655,7 +761,7 @@ hipError_t nxg_launch_dec_f64r(const uint8_t* wire, uint64_t W, uint64_t* oid, u
     const uint64_t nt = nxg_dec_f64r_tiles(W);
     if (nt == 0) return hipSuccess;
     const uint64_t ng = nxg_dec_f64r_groups(W);
-    const uint64_t ne = (nt + TPB / 64 - 1) / (TPB / 64);
+    const uint64_t ne = (nt * ESUB + TPB / 64 - 1) / (TPB / 64);
     if (ne > 0x7fffffffull) return hipErrorInvalidValue;
     hipLaunchKernelGGL(nxg_f64r_probe_kernel, dim3((uint32_t)ng), dim3(TPB), 0, s, wire, W, nt,
                        reinterpret_cast<Desc*>(desc), tstat, epoch, flags, st, nxg_take_zero_slot());

@@ -13,6 +13,10 @@
 #include <vector>
 
 #include "../netidx_amd/csrc/nxg_f64_rec.h"
+#define NXG_F64R_NT 0
+#define NXG_F64R_LDS 0
+#define NXG_F64R_DPP 0
+#define NXG_F64R_R 4
 
 namespace p1n {
 #include "../netidx_amd/csrc/nxg_decode_f64_1p.hip"
@@ -20,26 +24,38 @@ namespace p1n {
 namespace fr {
 #include "../netidx_amd/csrc/nxg_decode_f64_run.hip"
 }
-#define NXG_F64R_NT 1
-namespace fr8 {  // nontemporal column stores
+#undef NXG_F64R_NT
+#define NXG_F64R_NT 4
+namespace fr8 {  // nontemporal stores for the tile's inner lines
 #include "../netidx_amd/csrc/nxg_decode_f64_run.hip"
 }
 #undef NXG_F64R_NT
-#define NXG_F64R_NT 3
-namespace fr4 {  // nontemporal stores and loads
+#define NXG_F64R_NT 0
+#undef NXG_F64R_T
+#define NXG_F64R_T 16384
+namespace fr4 {  // 16 KiB probe tiles
 #include "../netidx_amd/csrc/nxg_decode_f64_run.hip"
 }
-#undef NXG_F64R_NT
-#define NXG_F64R_DPP 1
-namespace frd {  // one load per record (second block from the next lane)
-#include "../netidx_amd/csrc/nxg_decode_f64_run.hip"
-}
-#define NXG_F64R_NT 1
-namespace frdn {  // the same + nontemporal stores
-#include "../netidx_amd/csrc/nxg_decode_f64_run.hip"
-}
-#undef NXG_F64R_NT
+#undef NXG_F64R_T
+#define NXG_F64R_T 32768
 #undef NXG_F64R_DPP
+#define NXG_F64R_DPP 1
+namespace frdn {  // one load per record
+#include "../netidx_amd/csrc/nxg_decode_f64_run.hip"
+}
+#undef NXG_F64R_DPP
+#define NXG_F64R_DPP 0
+#undef NXG_F64R_DPP
+#define NXG_F64R_DPP 1
+#undef NXG_F64R_NT
+#define NXG_F64R_NT 4
+namespace frd {  // one load per record + inner nontemporal stores
+#include "../netidx_amd/csrc/nxg_decode_f64_run.hip"
+}
+#undef NXG_F64R_DPP
+#define NXG_F64R_DPP 0
+#undef NXG_F64R_NT
+#define NXG_F64R_NT 0
 thread_local DevStatus* nxg_zero_slot = nullptr;
 thread_local bool nxg_zero_used = false;
 
@@ -52,6 +68,36 @@ __global__ void stream_kernel(const uint4* __restrict__ in, uint64_t nin, uint4*
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nout; i += stride) {
         uint4 v = i < nin ? in[i] : make_uint4(0, 0, 0, 0);
         out[i] = v;
+    }
+}
+
+// the emit's memory pattern without parsing: lane k reads 16 B at 15 k and writes 8 B to each
+// of two columns
+__global__ void copy2col_kernel(const uint8_t* __restrict__ in, uint64_t N,
+                                uint64_t* __restrict__ a, uint64_t* __restrict__ b) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < N; i += stride) {
+        const uint4 v = *reinterpret_cast<const uint4*>(in + ((15 * i) & ~15ull));
+        a[i] = ((uint64_t)v.y << 32) | v.x;
+        b[i] = ((uint64_t)v.w << 32) | v.z;
+    }
+}
+typedef uint32_t v4p __attribute__((ext_vector_type(4)));
+__global__ void stream_nt_kernel(const v4p* __restrict__ in, uint64_t nin, v4p* __restrict__ out,
+                                 uint64_t nout) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nout; i += 4 * stride) {
+        v4p v[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint64_t j = i + k * stride;
+            v[k] = j < nin ? __builtin_nontemporal_load(in + j) : v4p{0, 0, 0, 0};
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint64_t j = i + k * stride;
+            if (j < nout) __builtin_nontemporal_store(v[k], out + j);
+        }
     }
 }
 
@@ -131,7 +177,8 @@ int main(int argc, char** argv) {
                                    epoch, 0u, st, (DevStatus*)nullptr);
             } else if (which == 21) {  // the emit kernel alone (descriptors of the last run)
                 const uint64_t nt = fr::nxg_dec_f64r_tiles(W);
-                hipLaunchKernelGGL(fr::nxg_f64r_emit_kernel, dim3((nt + 3) / 4), dim3(256), 0, 0,
+                hipLaunchKernelGGL(fr::nxg_f64r_emit_kernel, dim3((nt * fr::f64r::ESUB + 3) / 4),
+                                   dim3(256), 0, 0,
                                    dw, W, nt, (const fr::f64r::Desc*)desc, oid, oval, N, st);
             }
             else
@@ -159,8 +206,8 @@ int main(int argc, char** argv) {
         ms /= reps;
         printf("%-14s %-5s %8.4f ms %7.1f GB/s (W+16N) %5.1f%% rows=%llu ff=%u irr=%u to=%u "
                "cap=%u exact_tiles=%llu mismatches=%ld\n",
-               which == 1 ? "f64_1p" : which == 8 ? "f64run_ntS" : which == 4 ? "f64run_ntSL"
-               : which == 5 ? "f64run_dpp" : which == 6 ? "f64run_dppntS"
+               which == 1 ? "f64_1p" : which == 8 ? "f64run_ntIn" : which == 4 ? "f64run_T16k"
+               : which == 5 ? "f64run_dppntIn" : which == 6 ? "f64run_dpp"
                : which == 20 ? "probe_only" : which == 21 ? "emit_only"
                : (flags & 1 ? "f64run_exact" : flags & 2 ? "f64run_nobail" : "f64run"),
                name, ms, (W + 16.0 * N) / ms / 1e6,
@@ -222,6 +269,28 @@ int main(int argc, char** argv) {
                        (W + 16.0 * N) / ms / 1e6, (W + 16.0 * N) / ms / 1e6 / 80);
             };
             tstream("stream_8192", 8192);
+            {
+                auto t2 = [&](const char* nm, auto launch) {
+                    for (int i = 0; i < 3; i++) launch();
+                    CK(hipEventRecord(a, 0));
+                    for (int i = 0; i < reps; i++) launch();
+                    CK(hipEventRecord(b, 0));
+                    CK(hipEventSynchronize(b));
+                    float ms = 0;
+                    CK(hipEventElapsedTime(&ms, a, b));
+                    ms /= reps;
+                    printf("%-14s %-5s %8.4f ms %7.1f GB/s (W+16N) %5.1f%%\n", nm, "seq", ms,
+                           (W + 16.0 * N) / ms / 1e6, (W + 16.0 * N) / ms / 1e6 / 80);
+                };
+                t2("copy2col", [&]() {
+                    hipLaunchKernelGGL(copy2col_kernel, dim3(8192), dim3(256), 0, 0, dw, N, oid,
+                                       oval);
+                });
+                t2("stream_nt", [&]() {
+                    hipLaunchKernelGGL(stream_nt_kernel, dim3(2048), dim3(256), 0, 0,
+                                       (const v4p*)dw, W / 16, (v4p*)dstream, N);
+                });
+            }
             tstream("stream_2048", 2048);
         }
     }
