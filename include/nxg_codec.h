@@ -160,6 +160,18 @@ bool nxg_encode_updates(NxgCtx* ctx, const NxgColumns* in, const uint8_t* heap, 
 /* Async device-resident variant (len_out is written at nxg_ctx_sync time). */
 bool nxg_encode_updates_async(NxgCtx* ctx, const NxgColumns* din, const uint8_t* dheap,
                               uint8_t* dout, uint64_t cap, uint64_t* len_out, NetidxError* err);
+/* nxg_encode_updates plus the frame split of WriteChannel::queue_send + try_flush
+ * (netidx/src/channel.rs:177-202, 237-257): the payload is cut before the message that would take
+ * a frame past MAX_BATCH = 0x3FFFFFFF bytes, so `out` holds the frames' payloads back to back and
+ * chunk_len_out[0 .. *n_chunks) their lengths (each goes out behind its own u32 header,
+ * nxg_frame_header). The encode kernels record the cut themselves (the message holding byte
+ * MAX_BATCH). Batches that would need a second cut (more than MAX_BATCH + the first chunk's
+ * length, about 2 GiB) are refused: the reference then cuts before every further message
+ * (channel.rs:187 compares against the last chunk's length), which nxg_frame_split reproduces
+ * from message lengths. An empty batch gives no frame, as try_flush sends nothing. */
+bool nxg_encode_frames(NxgCtx* ctx, const NxgColumns* in, const uint8_t* heap, uint8_t* out,
+                       uint64_t cap, uint64_t* len_out, uint64_t* chunk_len_out,
+                       uint64_t cap_chunks, uint64_t* n_chunks, NetidxError* err);
 
 /* ---- dispatch: replaces ConnectionCtx::process_updates_batch (connection.rs:546-567) ------
  * The decoded Update rows fanned out to the subscriber's channels. For each row, in batch

@@ -115,6 +115,9 @@ SIGNATURES = {
     "nxg_encode_updates_async": (C.c_bool, [C.c_void_p, C.POINTER(NxgColumns), C.c_void_p,
                                             C.c_void_p, C.c_uint64, C.POINTER(C.c_uint64),
                                             C.POINTER(NetidxError)]),
+    "nxg_encode_frames": (C.c_bool, [C.c_void_p, C.POINTER(NxgColumns), C.c_void_p, C.c_void_p,
+                                     C.c_uint64, C.POINTER(C.c_uint64), C.c_void_p, C.c_uint64,
+                                     C.POINTER(C.c_uint64), C.POINTER(NetidxError)]),
     "nxg_dispatch_updates": (C.c_bool, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64,
                                         C.c_void_p, C.POINTER(NetidxError)]),
     "nxg_publish_commit": (C.c_bool, [C.c_void_p, C.c_void_p, C.POINTER(NxgColumns), C.c_void_p,
@@ -370,6 +373,17 @@ class Codec:
         m = self.encode_into(cols, heap, out.data_ptr(), n)
         assert m == n
         return out[:n]
+
+    def encode_frames(self, cols, heap, out_ptr, cap, max_frames=16):
+        """Encode into out_ptr and return (total length, [frame payload lengths]) as
+        WriteChannel::queue_send / try_flush would cut them (MAX_BATCH, channel.rs:177-257)."""
+        n, k, err = C.c_uint64(0), C.c_uint64(0), NetidxError()
+        chunks = np.zeros(max_frames, np.uint64)
+        _check(lib().nxg_encode_frames(self.ctx, C.byref(cols.s), _heap_ptr(heap),
+                                       C.c_void_p(out_ptr), cap, C.byref(n),
+                                       C.c_void_p(chunks.ctypes.data), max_frames, C.byref(k),
+                                       C.byref(err)), err)
+        return n.value, [int(x) for x in chunks[: k.value]]
 
     def encode_async(self, cols, heap, out_ptr, cap):
         """Enqueue an encode; the returned c_uint64 holds the length after sync()."""

@@ -101,6 +101,7 @@ struct NxgCtx {
     };
     std::vector<Pending> pending;
     DevStatus last{};  // last completed decode's device status (diagnostics)
+    uint64_t last_split = 0;  // last completed encode's DevStatus.split_start
 };
 
 namespace {
@@ -524,12 +525,17 @@ bool finish_encode(NxgCtx* c, const NxgColumns* in, DevStatus* st, uint32_t slot
     if (!fetched || (in->layout == NXG_LAYOUT_MIXED && in->n_ctl))
         HIPCHK(hipStreamSynchronize(c->stream));
     const DevStatus& h = c->hst[slot];
+    c->last_split = h.split_start;
     if (h.timeout) {
         set_err(err, "device look-back watchdog expired");
         return false;
     }
     if (h.err_kind) {
-        set_err(err, "encode failed: PackError kind %u", h.err_kind);
+        if (h.err_kind == NXG_TOO_BIG)
+            set_err(err, "encode failed: a message exceeds MAX_BATCH (%llu bytes) or a size "
+                         "guard (PackError::TooBig)", (unsigned long long)kMaxBatch);
+        else
+            set_err(err, "encode failed: PackError kind %u", h.err_kind);
         return false;
     }
     const uint64_t total = h.total_bytes + ctl_total;
@@ -1062,6 +1068,49 @@ bool nxg_encode_updates_async(NxgCtx* c, const NxgColumns* din, const uint8_t* d
     const bool ok = enqueue_encode(c, din, dheap, dout, cap, st, err);
     if (!end_call(c, err) || !ok) return false;
     c->pending.push_back({2, 0, nullptr, 0, const_cast<NxgColumns*>(din), len_out, cap, st, slot});
+    return true;
+}
+
+bool nxg_encode_frames(NxgCtx* c, const NxgColumns* in, const uint8_t* heap, uint8_t* out,
+                       uint64_t cap, uint64_t* len_out, uint64_t* chunk_len_out,
+                       uint64_t cap_chunks, uint64_t* n_chunks, NetidxError* err) {
+    if (!out || !n_chunks || (cap_chunks && !chunk_len_out)) {
+        set_err(err, "null argument");
+        return false;
+    }
+    uint64_t total = 0;
+    if (!encode_impl(c, in, heap, out, cap, &total, err)) return false;
+    if (len_out) *len_out = total;
+    uint64_t ch[2];
+    uint64_t k = 0;
+    if (total == 0) {
+        k = 0;
+    } else if (total <= kMaxBatch) {
+        ch[k++] = total;
+    } else {
+        if (!c->last_split) {
+            set_err(err, "frame split: the encoder recorded no boundary for a %llu-byte batch",
+                    (unsigned long long)total);
+            return false;
+        }
+        const uint64_t c1 = c->last_split - 1;
+        // the next cut is before the first message ending past MAX_BATCH + c1 (channel.rs:187)
+        if (total > kMaxBatch + c1) {
+            set_err(err, "frame split: a %llu-byte batch needs more than one cut (the reference "
+                         "then cuts before every message); split the batch or use "
+                         "nxg_frame_split with the message lengths", (unsigned long long)total);
+            return false;
+        }
+        ch[k++] = c1;
+        ch[k++] = total - c1;
+    }
+    if (k > cap_chunks) {
+        set_err(err, "frame split: %llu frames, capacity %llu", (unsigned long long)k,
+                (unsigned long long)cap_chunks);
+        return false;
+    }
+    for (uint64_t i = 0; i < k; i++) chunk_len_out[i] = ch[i];
+    *n_chunks = k;
     return true;
 }
 

@@ -133,6 +133,15 @@ __global__ __launch_bounds__(TPB) void nxg_enc_f64_kernel(
         const uint32_t phase = (uint32_t)(base & 15u);
 
         const uint64_t end = base + tbytes;
+        if (base <= kMaxBatch && kMaxBatch < end) {  // the first frame boundary is in this tile
+            uint64_t o = base + off;
+#pragma unroll
+            for (int k = 0; k < ERPT; k++)
+                if (r0 + k < n) {
+                    note_split(st, o, rec_len(ids[k]));
+                    o += rec_len(ids[k]);
+                }
+        }
         if (out && end > cap) {
             if (tid == 0) atomicOr(&st->capacity, 1u);
         } else if (out && phase + tbytes > (uint32_t)(MAXB_ALL - 16)) {

@@ -432,6 +432,8 @@ __global__ __launch_bounds__(TPB) void nxg_enc_rows_kernel(
 #pragma unroll
                 for (int k = 0; k < GRPT; k++) {
                     off_lds[tid * GRPT + k] = (uint16_t)o;
+                    if (tbase <= kMaxBatch && kMaxBatch < tbase + tot)
+                        note_split(st, tbase + off + (o - phase - (uint32_t)off), L[k]);
                     o += (uint32_t)L[k];
                 }
             }
@@ -500,6 +502,7 @@ __global__ __launch_bounds__(TPB) void nxg_enc_rows_kernel(
                 if (r < n && L[k] && out) {
                     uint64_t pos = rpos;
                     if (c.n_ctl) pos += ctl_pre[ctl_upto(c.ctl_row, c.n_ctl, r)];
+                    note_split(st, pos, L[k]);
                     if (pos + L[k] > cap) {
                         atomicOr(&st->capacity, 1u);
                     } else {
@@ -533,6 +536,7 @@ __global__ __launch_bounds__(TPB) void nxg_enc_ctl_write_kernel(
         const uint64_t rb = r < c.n_rows ? row_off[r] : rows_total;
         const uint64_t pos = rb + ctl_pre[k];
         const uint64_t len = c.ctl_len[k];
+        note_split(stw, pos, len);
         if (pos + len > cap) {
             atomicOr(&stw->capacity, 1u);
             continue;

@@ -20,7 +20,9 @@ struct DevStatus {
     uint32_t irregular;    // f64 run decode: record lengths vary too often (=> persistent kernel)
     // general decode: first error as ~(offset << 8 | kind), combined with atomicMax (0 = none)
     uint64_t err_key;
-    uint64_t pad1;
+    // encode: 1 + the start offset of the message that holds byte MAX_BATCH, i.e. where
+    // WriteChannel::queue_send records its first frame boundary (channel.rs:187-191); 0 = none
+    uint64_t split_start;
     // diagnostics (general decode): 0 redo tiles, 1 look-back fallbacks, 2 repair rounds,
     // 3 lane walks, 4 speculation attempts, 5 tiles without a speculated entry,
     // 6 exhausted (budgeted) walks, 7 work-list entries of the emit pass
@@ -38,6 +40,12 @@ constexpr uint64_t kFlagMask = 3ull << 62;
 constexpr int kEpochShift = 44;
 constexpr uint64_t kEpochMax = (1ull << 18) - 1;
 constexpr uint64_t kValMask = (1ull << kEpochShift) - 1;
+constexpr uint64_t kMaxBatch = 0x3FFFFFFF;  // MAX_BATCH, netidx/src/channel.rs:34
+// encode: note the message [pos, pos + len) if it holds byte MAX_BATCH (exactly one does, in a
+// frame longer than MAX_BATCH)
+__device__ inline void note_split(DevStatus* st, uint64_t pos, uint64_t len) {
+    if (pos <= kMaxBatch && kMaxBatch < pos + len) st->split_start = pos + 1;
+}
 __host__ __device__ inline uint64_t lb_word(uint64_t flag, uint32_t epoch, uint64_t v) {
     return flag | ((uint64_t)epoch << kEpochShift) | (v & kValMask);
 }

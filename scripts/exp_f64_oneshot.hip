@@ -187,6 +187,6 @@ hipError_t nxg_launch_dec_f64_os(const uint8_t* wire, uint64_t W, uint64_t* oid,
     if (nb == 0) return hipSuccess;
     if (nb > 0xffffffffull) return hipErrorInvalidValue;
     hipLaunchKernelGGL(nxg_f64_os_kernel, dim3((uint32_t)nb), dim3(TPBO), 0, s, wire, W, nt, oid,
-                       oval, cap, tstat, epoch, st, nxg_zero_slot);
+                       oval, cap, tstat, epoch, st, nxg_take_zero_slot());
     return hipGetLastError();
 }

@@ -11,6 +11,7 @@
 
 #include "../netidx_amd/csrc/nxg_device.h"
 thread_local DevStatus* nxg_zero_slot = nullptr;
+thread_local bool nxg_zero_used = false;
 
 #define NXG_ENC_RPT 4
 #define NXG_ENC_STGB 21

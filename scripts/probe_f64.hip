@@ -39,6 +39,7 @@ namespace posnt {  // one-shot decoder, nontemporal column stores
 }
 #undef NXG_OS_NT
 thread_local DevStatus* nxg_zero_slot = nullptr;
+thread_local bool nxg_zero_used = false;
 
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
     fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); exit(1); } } while (0)

@@ -11,7 +11,7 @@ export TMPDIR=/tmp
 OUT=$R/gpurun_out/prof
 mkdir -p $OUT
 cd /tmp
-ARGS="--steps 20 --warmup 3 --no-extras --cpu-seconds 0.2"
+ARGS="--steps 20 --warmup 3 --no-extras --cpu-seconds 0.2 --records ${RECORDS:-10000000}"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o trace -- python3 $R/bench.py $ARGS > $OUT/trace_bench.json 2> $OUT/trace.err \
  && timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o fetch -- python3 $R/bench.py $ARGS > $OUT/fetch_bench.json 2> $OUT/fetch.err \
  && timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o write -- python3 $R/bench.py $ARGS > $OUT/write_bench.json 2> $OUT/write.err \

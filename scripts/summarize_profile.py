@@ -21,7 +21,7 @@ import sys
 from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-DEC = ("nxg_f64_1p_kernel",)
+DEC = ("nxg_f64r_probe_kernel", "nxg_f64r_emit_kernel")  # one decode = both launches
 
 
 def rows(pattern):
@@ -85,7 +85,8 @@ def main():
            "hbm_bytes_per_launch": int(fetch + write),
            "read_bytes": int(fetch), "write_bytes_raw": int(write),
            "source": f"profiles/{tag}_dec_f64_profile.json (FETCH_SIZE x2 per gfx950 note)"}
-    json.dump(pmc, open(os.path.join(prof, "pmc_dec_f64.json"), "w"), indent=1)
+    name = "pmc_dec_f64.json" if records == 10_000_000 else f"pmc_dec_f64_{records}.json"
+    json.dump(pmc, open(os.path.join(prof, name), "w"), indent=1)
     print(json.dumps(summary, indent=1))
 
 

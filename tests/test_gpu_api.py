@@ -1,0 +1,140 @@
+"""C-ABI behaviour on the GPU: the MAX_BATCH frame split of the encode seam, async calls and the
+status ring.
+
+- nxg_encode_frames cuts the payload exactly as WriteChannel::queue_send + try_flush
+  (netidx/src/channel.rs:177-202, 237-257): checked against nxg_frame_split over the oracle's
+  message lengths, at 10^8 records (1.498 GB > MAX_BATCH: the reference's two frames).
+- async encode into a buffer that is too small fails at nxg_ctx_sync (no frame with holes).
+- a call that launches no kernel (an empty frame) still clears the status slot the call 512
+  later uses, so a capacity failure two ring laps back cannot leak into a good decode.
+- one nxg_ctx_sync finishes every pending call: a decode that needs the general fallback and an
+  encode after it both complete.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def codec():
+    import torch
+    import netidx_amd
+    assert torch.cuda.is_available()
+    c = netidx_amd.Codec(0)
+    yield c
+    c.close()
+
+
+def _vl(ids):
+    ids = np.asarray(ids, np.uint64)
+    n = np.ones(len(ids), np.int64)
+    for k in range(1, 10):
+        n += ids >= np.uint64(1 << (7 * k))
+    return n
+
+
+def test_encode_frames_max_batch_split_1e8(codec):
+    import netidx_amd
+    import nxo
+    import torch
+    from netidx_amd import synth
+    n = 100_000_000
+    ids, vals = synth.f64_columns(n, synth.SEED_8GPU)
+    cols = netidx_amd.columns_from_arrays(ids, vals)
+    out = torch.empty(1_497_886_336 + 64, dtype=torch.uint8, device="cuda")
+    total, chunks = codec.encode_frames(cols, None, out.data_ptr(), out.numel())
+    assert total == 1_497_886_336
+    # the reference's cut: queue_send over the oracle's message lengths (11 + varint_len(id))
+    ref_chunks = netidx_amd.frame_split(11 + _vl(ids))
+    assert chunks == list(ref_chunks) and len(chunks) == 2 and sum(chunks) == total
+    assert chunks[0] <= 0x3FFFFFFF
+    del cols
+    got = out[:total].cpu().numpy()
+    ref = nxo.encode_f64(ids, vals)
+    assert np.array_equal(got, ref)
+    # the second frame starts with a message (ids near 7.2e7 take 4 varint bytes: L = 15)
+    c0 = chunks[0]
+    assert ref[c0] == 15 and ref[c0 + 1] == 4
+
+
+def test_encode_frames_small_and_empty(codec):
+    import netidx_amd
+    import torch
+    from netidx_amd import synth
+    ids, vals = synth.f64_columns(1000, 5)
+    cols = netidx_amd.columns_from_arrays(ids, vals)
+    out = torch.empty(16000, dtype=torch.uint8, device="cuda")
+    total, chunks = codec.encode_frames(cols, None, out.data_ptr(), out.numel())
+    assert chunks == [total] and total == int((11 + _vl(ids)).sum())
+    empty = netidx_amd.columns_from_arrays(np.zeros(0, np.uint64), np.zeros(0, np.uint64))
+    total, chunks = codec.encode_frames(empty, None, out.data_ptr(), out.numel())
+    assert total == 0 and chunks == []
+
+
+def test_async_encode_too_small_fails_at_sync(codec):
+    import netidx_amd
+    import torch
+    from netidx_amd import synth
+    ids, vals = synth.f64_columns(50_000, 6)
+    cols = netidx_amd.columns_from_arrays(ids, vals)
+    need = int((11 + _vl(ids)).sum())
+    out = torch.empty(need - 100, dtype=torch.uint8, device="cuda")
+    codec.encode_async(cols, None, out.data_ptr(), out.numel())
+    with pytest.raises(netidx_amd.CodecError):
+        codec.sync()
+    # the ctx stays usable
+    big = torch.empty(need + 16, dtype=torch.uint8, device="cuda")
+    ln = codec.encode_async(cols, None, big.data_ptr(), big.numel())
+    codec.sync()
+    assert ln.value == need
+
+
+def test_status_ring_empty_call_clears_its_slot(codec):
+    """Call i fails with a capacity error; call i + 512 launches nothing (empty frame); call
+    i + 1024 reuses call i's slot and must not inherit its bits."""
+    import netidx_amd
+    import nxo
+    import torch
+    from netidx_amd import synth
+    from netidx_amd.codec import Columns
+    ids, vals = synth.f64_columns(2000, 7)
+    wire = torch.from_numpy(nxo.encode_f64(ids, vals)).cuda()
+    small = Columns(100, 0, 0, netidx_amd.LAYOUT_F64, "cuda")
+    good = Columns(2000, 0, 0, netidx_amd.LAYOUT_F64, "cuda")
+    st = codec.decode_into(wire, wire.numel(), small, check=False)
+    assert st.err_kind == netidx_amd.CAPACITY
+    for k in range(1, 1025):
+        if k == 512:
+            st = codec.decode_into(wire, 0, good, check=False)
+            assert st.err_kind == 0 and st.n_rows == 0
+        else:
+            st = codec.decode_into(wire, wire.numel(), good, check=False)
+            assert st.err_kind == 0 and st.n_rows == 2000, (k, st.err_kind)
+
+
+def test_sync_finishes_every_pending_call(codec):
+    import netidx_amd
+    import nxo
+    import torch
+    from netidx_amd import synth
+    from netidx_amd.codec import Columns
+    ids, vals = synth.f64_columns(30_000, 8)
+    w = nxo.encode_f64(ids, vals).tobytes()
+    hb = w[:12 * 1000] + b"\x02\x05" + w[12 * 1000:]  # a Heartbeat: the general fallback
+    d_plain = torch.from_numpy(np.frombuffer(w, np.uint8).copy()).cuda()
+    d_hb = torch.from_numpy(np.frombuffer(hb, np.uint8).copy()).cuda()
+    outs = [Columns.for_frame(len(x), netidx_amd.LAYOUT_MIXED, "cuda") for x in (w, hb, w)]
+    cols = netidx_amd.columns_from_arrays(ids, vals)
+    eout = torch.empty(len(w) + 16, dtype=torch.uint8, device="cuda")
+    codec.decode_async(d_plain.data_ptr(), len(w), outs[0])
+    codec.decode_async(d_hb.data_ptr(), len(hb), outs[1])
+    ln = codec.encode_async(cols, None, eout.data_ptr(), eout.numel())
+    codec.decode_async(d_plain.data_ptr(), len(w), outs[2])
+    codec.sync()
+    for o, x in zip(outs, (w, hb, w)):
+        ref = nxo.decode(x).trim()
+        g = o.numpy()
+        assert np.array_equal(g["id"], ref["id"]) and np.array_equal(g["fixed"], ref["fixed"])
+    assert outs[1].s.n_heartbeat == 1
+    assert ln.value == len(w) and eout[: len(w)].cpu().numpy().tobytes() == w
