@@ -8,7 +8,7 @@ set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=${1:-r01}
 export TMPDIR=/tmp
-OUT=$R/gpurun_out/prof
+OUT=$R/gpurun_out/prof_$TAG
 mkdir -p $OUT
 cd /tmp
 ARGS="--steps 20 --warmup 3 --no-extras --cpu-seconds 0.2 --records ${RECORDS:-10000000}"

@@ -121,7 +121,7 @@ def test_sync_finishes_every_pending_call(codec):
     from netidx_amd.codec import Columns
     ids, vals = synth.f64_columns(30_000, 8)
     w = nxo.encode_f64(ids, vals).tobytes()
-    hb = w[:12 * 1000] + b"\x02\x05" + w[12 * 1000:]  # a Heartbeat: the general fallback
+    hb = w[:12 * 100] + b"\x02\x05" + w[12 * 100:]  # a Heartbeat between records 99 and 100
     d_plain = torch.from_numpy(np.frombuffer(w, np.uint8).copy()).cuda()
     d_hb = torch.from_numpy(np.frombuffer(hb, np.uint8).copy()).cuda()
     outs = [Columns.for_frame(len(x), netidx_amd.LAYOUT_MIXED, "cuda") for x in (w, hb, w)]
