@@ -599,51 +599,103 @@ def extras_single_gpu(codec, stream, steps, warmup):
     return ex
 
 
-def extras_multi_gpu(codec, world, rank, stream):
-    """N > 1. Config 5: 10^8 records sharded by record; each rank encodes its shard, then an
-    RCCL all-gather (padded to the longest shard, netidx_amd/shard.py) assembles the full frame
-    on every GPU -- the path's only collective. Then the same 10^8 records decoded sharded by
-    record (strong scaling), and config 3 (mixed) at 10^7 records per GPU (weak scaling); times
-    are the slowest rank's kernel time (HIP events)."""
+def make_comm(codec, world, rank):
+    """The library's RCCL communicator (nxg_comm_init; its id broadcast over torch.distributed),
+    or None where RCCL cannot serve (gloo rehearsals with ranks sharing one GPU): then the
+    torch.distributed mirrors of netidx_amd/shard.py run the same protocols."""
     import netidx_amd
+    import torch.distributed as dist
+    if BACKEND == "gloo":
+        return None
+    obj = [netidx_amd.Comm.unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(obj, src=0)
+    return netidx_amd.Comm(codec, world, rank, obj[0])
+
+
+def extras_multi_gpu(codec, world, rank, stream):
+    """N > 1. Config 5: 10^8 records sharded by record; each rank encodes its shard straight
+    into its place in the full frame and grouped send/recv over RCCL deliver every shard to every
+    GPU (nxg_encode_allgather: one 8-byte all-gather of the sizes, no padding or copies). Then
+    that one frame is decoded in N byte ranges, one per GPU (nxg_decode_sharded: each GPU takes
+    the messages that start in its range, the ranges' summaries are all-gathered and linked),
+    and config 3 (mixed) runs at 10^7 records per GPU (weak scaling). Times: the slowest rank's
+    wall clock (barrier + device sync on both sides)."""
+    import netidx_amd
+    import numpy as np
     import torch
     from netidx_amd import shard, synth
+    from netidx_amd.codec import Columns
     total = 100_000_000
     b, e = shard.shard_range(total, world, rank)
     n = e - b
     ids, vals = synth.f64_columns(n, synth.SEED_8GPU, id_offset=b)
     cols = netidx_amd.columns_from_arrays(ids, vals)
-    dout = torch.empty(21 * n + 64, dtype=torch.uint8, device="cuda")
+    cap = 15 * total + 64
+    dout = torch.empty(cap, dtype=torch.uint8, device="cuda")
+    comm = make_comm(codec, world, rank)
+    via = "rccl (nxg_encode_allgather)" if comm else "torch.distributed mirror (shard.py)"
+
+    def encode_gather():
+        if comm:
+            return comm.encode_allgather(cols, None, dout.data_ptr(), cap)
+        ln = codec.encoded_len(cols)
+        off = shard.shard_offsets(ln, world, coll_device())
+        codec.encode_into(cols, None, dout.data_ptr() + int(off[rank]), cap - int(off[rank]))
+        if coll_device() == "cuda":
+            shard.allgather_at_offsets(dout, off, rank, world)
+        else:
+            host = dout[: int(off[-1])].cpu()
+            shard.allgather_at_offsets(host, off, rank, world)
+            dout[: int(off[-1])].copy_(host)
+        return int(off[-1]), [int(x) for x in off[:-1]]
+
     times = []
     for it in range(3):
         barrier(world)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        ln = codec.encode_async(cols, None, dout.data_ptr(), dout.numel())
-        codec.sync()
-        src = dout if coll_device() == "cuda" else dout.cpu()
-        full, lengths = shard.gather_frames(src, ln.value, world)
+        W, offs = encode_gather()
         torch.cuda.synchronize()
         times.append(time.perf_counter() - t0)
     t = max_over_ranks(min(times), world)
-    ex = {"encode_allgather_1e8": {"records": total, "wire_bytes": int(full.numel()),
-                                   "world": world, "encode_allgather_ms": round(t * 1e3, 3),
+    # check: this rank's shard where it belongs, and the frame's length is the whole batch's
+    assert W == 1_497_886_336, W
+    ex = {"encode_allgather_1e8": {"records": total, "wire_bytes": W, "world": world, "via": via,
+                                   "encode_allgather_ms": round(t * 1e3, 3),
                                    "M_updates_s": round(total / t / 1e6, 1)}}
-    del cols, dout, full
-    # the same 10^8-record f64 batch decoded sharded by record (strong scaling): each rank
-    # decodes the frame of its own records; the job's time is the slowest rank's
-    from netidx_amd.codec import Columns
-    wire = codec.encode_batch(netidx_amd.columns_from_arrays(ids, vals))
-    out = Columns(n, 0, 0, netidx_amd.LAYOUT_F64, "cuda")
-    wall, kms, st = time_decode(codec, wire, out, n, 10, 2, world, stream)
-    assert st.path == 1 and st.n_rows == n and st.err_kind == 0, st
-    got = out.fixed[:n].cpu().numpy().view("uint64")
-    assert (got == vals).all(), "sharded decode is not bit-exact"
-    kmax = max_over_ranks(kms, world)
-    ex["decode_f64_1e8_sharded"] = {
-        "records": total, "world": world, "records_per_gpu_max": total - total * (world - 1) // world,
-        "kernel_ms_slowest_rank": round(kmax, 4), "M_updates_s": round(total / (kmax / 1e3) / 1e6, 1)}
-    del wire, out
+    del cols
+    # the one frame decoded in byte ranges (strong scaling)
+    out = Columns(n + 2 * total // world // 100 + 1024, 0, 0, netidx_amd.LAYOUT_F64, "cuda")
+
+    def decode_ranges():
+        if comm:
+            return comm.decode_sharded(dout, W, out)
+        return shard.decode_sharded(
+            lambda bb, ee: codec.decode_range(dout, W, bb, ee, out), W, rank, world)
+
+    decode_ranges()
+    times = []
+    for it in range(5):
+        barrier(world)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        row_off, rng = decode_ranges()
+        torch.cuda.synchronize()
+        times.append(time.perf_counter() - t0)
+    t = max_over_ranks(min(times), world)
+    nr = int(rng[4] if isinstance(rng, tuple) else rng.n_rows)
+    # checker: rows [row_off, row_off + nr) of the batch (ids are the global row numbers)
+    got_id = out.id[:nr].cpu().numpy().view(np.uint64)
+    got_val = out.fixed[:nr].cpu().numpy().view(np.uint64)
+    assert np.array_equal(got_id, np.arange(row_off, row_off + nr, dtype=np.uint64))
+    _, want_val = synth.f64_columns(nr, synth.SEED_8GPU, id_offset=row_off)
+    assert np.array_equal(got_val, want_val), "range decode is not bit-exact"
+    ex["decode_f64_1e8_byte_ranges"] = {
+        "records": total, "world": world, "via": via.replace("nxg_encode_allgather",
+                                                              "nxg_decode_sharded"),
+        "ms_slowest_rank": round(t * 1e3, 4), "M_updates_s": round(total / t / 1e6, 1)}
+    del dout, out
+    torch.cuda.empty_cache()
     # config 3 per GPU (weak scaling): each rank decodes its own 10^7-record mixed batch
     nm = 10_000_000
     m = synth.mixed_columns(nm)
@@ -659,6 +711,8 @@ def extras_multi_gpu(codec, world, rank, stream):
     ex["decode_mixed_1e7_per_gpu"] = {
         "records_per_gpu": nm, "world": world, "kernel_ms_slowest_rank": round(kmax, 4),
         "M_updates_s": round(world * nm / (kmax / 1e3) / 1e6, 1)}
+    if comm:
+        comm.close()
     return ex
 
 

@@ -173,6 +173,52 @@ bool nxg_encode_frames(NxgCtx* ctx, const NxgColumns* in, const uint8_t* heap, u
                        uint64_t cap, uint64_t* len_out, uint64_t* chunk_len_out,
                        uint64_t cap_chunks, uint64_t* n_chunks, NetidxError* err);
 
+/* ---- multi-GPU: one frame decoded in byte ranges, one batch encoded in shards -------------
+ * One process per GPU. A frame of W bytes is cut into contiguous byte ranges; each GPU decodes
+ * the messages that START in its range, reading past the range end as needed (messages never
+ * straddle frames, channel.rs:187-201, but they do straddle ranges). A range's summary says
+ * where its chain enters (the first message start >= begin) and leaves (the first start >= end,
+ * or the frame end); nxg_range_link checks that consecutive ranges meet and numbers their rows.
+ * Homogeneous-f64 frames only (the length-run decoder); others report ok = 0. */
+typedef struct NxgRange {
+    uint64_t begin, end; /* the byte range [begin, end) of the frame */
+    uint64_t entry;      /* first message start >= begin (absolute byte offset) */
+    uint64_t exit;       /* first message start >= end, or the frame end */
+    uint64_t n_rows;     /* rows decoded from the range (at dout rows 0 .. n_rows) */
+    uint32_t ok;         /* 1: decoded; 0: not a homogeneous-f64 range (decode the frame) */
+    uint32_t err_kind;   /* NxgErrKind when ok = 1 but the columns overflowed, else 0 */
+} NxgRange;
+/* Device frame and device columns; synchronous. */
+bool nxg_decode_range(NxgCtx* ctx, const uint8_t* dframe, uint64_t frame_len, uint64_t begin,
+                      uint64_t end, NxgColumns* dout, NxgRange* rng, NetidxError* err);
+/* Ranges in frame order, contiguous from 0 to frame_len: checks ranges[0].entry == 0,
+ * ranges[i].exit == ranges[i+1].entry and the last exit == frame_len; row_off[i] = rows before
+ * range i. Returns false (and *bad = the first range whose entry is off the chain) otherwise. */
+bool nxg_range_link(const NxgRange* ranges, uint32_t n, uint64_t frame_len, uint64_t* row_off,
+                    uint32_t* bad, NetidxError* err);
+
+/* RCCL communicator (librccl, over xGMI) for the sharded calls. nxg_comm_unique_id on one rank,
+ * its 128 bytes sent to every rank by the caller (as ncclGetUniqueId's id), nxg_comm_init on
+ * every rank (collective). */
+typedef struct NxgComm NxgComm;
+bool nxg_comm_unique_id(uint8_t id[128], NetidxError* err);
+NxgComm* nxg_comm_init(NxgCtx* ctx, int nranks, int rank, const uint8_t id[128],
+                       NetidxError* err);
+void nxg_comm_destroy(NxgComm* comm);
+/* BASELINE configs[4]: every rank encodes its shard of the batch (rows in rank order) straight
+ * into its place in the full frame (an 8-byte all-gather of the shard sizes first), then grouped
+ * send/recv deliver every shard into the same offsets on every rank: no padding, no compaction.
+ * *len_out = the full frame length; shard_off[0 .. nranks) = each shard's byte offset (may be
+ * NULL). Device columns and buffers. */
+bool nxg_encode_allgather(NxgCtx* ctx, NxgComm* comm, const NxgColumns* din, const uint8_t* dheap,
+                          uint8_t* dout, uint64_t cap, uint64_t* len_out, uint64_t* shard_off,
+                          NetidxError* err);
+/* One frame (on every rank's device) decoded in nranks byte ranges: rank r decodes range r,
+ * the summaries are all-gathered and linked; a range whose guessed entry is off the chain is
+ * decoded again from its predecessor's exit. *row_off = this rank's first global row. */
+bool nxg_decode_sharded(NxgCtx* ctx, NxgComm* comm, const uint8_t* dframe, uint64_t frame_len,
+                        NxgColumns* dout, uint64_t* row_off, NxgRange* rng, NetidxError* err);
+
 /* ---- dispatch: replaces ConnectionCtx::process_updates_batch (connection.rs:546-567) ------
  * The decoded Update rows fanned out to the subscriber's channels. For each row, in batch
  * order: the subscription of its Id, found by a dense table (publisher Ids come from a counter

@@ -63,6 +63,19 @@ class NxgColumns(C.Structure):
     ]
 
 
+class NxgRange(C.Structure):
+    _fields_ = [("begin", C.c_uint64), ("end", C.c_uint64), ("entry", C.c_uint64),
+                ("exit", C.c_uint64), ("n_rows", C.c_uint64), ("ok", C.c_uint32),
+                ("err_kind", C.c_uint32)]
+
+    def tuple(self):
+        return (self.begin, self.end, self.entry, self.exit, self.n_rows, self.ok, self.err_kind)
+
+    @classmethod
+    def of(cls, t):
+        return cls(*t)
+
+
 class NxgSubTable(C.Structure):
     _fields_ = [("n_ids", C.c_uint64), ("slot_of_id", C.c_void_p), ("n_slots", C.c_uint64),
                 ("slot_sub_id", C.c_void_p), ("slot_stream_off", C.c_void_p),
@@ -118,6 +131,22 @@ SIGNATURES = {
     "nxg_encode_frames": (C.c_bool, [C.c_void_p, C.POINTER(NxgColumns), C.c_void_p, C.c_void_p,
                                      C.c_uint64, C.POINTER(C.c_uint64), C.c_void_p, C.c_uint64,
                                      C.POINTER(C.c_uint64), C.POINTER(NetidxError)]),
+    "nxg_decode_range": (C.c_bool, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint64,
+                                    C.POINTER(NxgColumns), C.POINTER(NxgRange),
+                                    C.POINTER(NetidxError)]),
+    "nxg_range_link": (C.c_bool, [C.POINTER(NxgRange), C.c_uint32, C.c_uint64, C.c_void_p,
+                                  C.POINTER(C.c_uint32), C.POINTER(NetidxError)]),
+    "nxg_comm_unique_id": (C.c_bool, [C.c_void_p, C.POINTER(NetidxError)]),
+    "nxg_comm_init": (C.c_void_p, [C.c_void_p, C.c_int, C.c_int, C.c_void_p,
+                                   C.POINTER(NetidxError)]),
+    "nxg_comm_destroy": (None, [C.c_void_p]),
+    "nxg_encode_allgather": (C.c_bool, [C.c_void_p, C.c_void_p, C.POINTER(NxgColumns),
+                                        C.c_void_p, C.c_void_p, C.c_uint64,
+                                        C.POINTER(C.c_uint64), C.c_void_p,
+                                        C.POINTER(NetidxError)]),
+    "nxg_decode_sharded": (C.c_bool, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64,
+                                      C.POINTER(NxgColumns), C.POINTER(C.c_uint64),
+                                      C.POINTER(NxgRange), C.POINTER(NetidxError)]),
     "nxg_dispatch_updates": (C.c_bool, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64,
                                         C.c_void_p, C.POINTER(NetidxError)]),
     "nxg_publish_commit": (C.c_bool, [C.c_void_p, C.c_void_p, C.POINTER(NxgColumns), C.c_void_p,
@@ -374,6 +403,15 @@ class Codec:
         assert m == n
         return out[:n]
 
+    def decode_range(self, dframe, frame_len, begin, end, cols):
+        """Decode the messages that start in [begin, end) of a device frame (rows at cols[0:]);
+        returns the NxgRange summary (entry / exit / n_rows / ok)."""
+        ptr = dframe.data_ptr() if hasattr(dframe, "data_ptr") else int(dframe)
+        rng, err = NxgRange(), NetidxError()
+        _check(lib().nxg_decode_range(self.ctx, C.c_void_p(ptr), frame_len, begin, end,
+                                      C.byref(cols.s), C.byref(rng), C.byref(err)), err)
+        return rng
+
     def encode_frames(self, cols, heap, out_ptr, cap, max_frames=16):
         """Encode into out_ptr and return (total length, [frame payload lengths]) as
         WriteChannel::queue_send / try_flush would cut them (MAX_BATCH, channel.rs:177-257)."""
@@ -558,6 +596,67 @@ class FrameReader:
 
     def buffered(self):
         return lib().nxg_frame_reader_buffered(self.r)
+
+
+def range_link(ranges, frame_len):
+    """nxg_range_link: row offsets of consecutive byte-range summaries, or (None, bad_index)
+    when range `bad_index` does not enter the chain where its predecessor leaves it."""
+    n = len(ranges)
+    arr = (NxgRange * max(n, 1))(*[r if isinstance(r, NxgRange) else NxgRange.of(r)
+                                   for r in ranges])
+    offs = np.zeros(max(n, 1), np.uint64)
+    bad, err = C.c_uint32(0), NetidxError()
+    ok = lib().nxg_range_link(arr, n, frame_len, C.c_void_p(offs.ctypes.data), C.byref(bad),
+                              C.byref(err))
+    if err.msg:
+        lib().nxg_error_free(C.byref(err))
+    return (offs[:n], None) if ok else (None, int(bad.value))
+
+
+class Comm:
+    """RCCL communicator of the sharded calls (one process per GPU)."""
+
+    @staticmethod
+    def unique_id():
+        buf, err = (C.c_uint8 * 128)(), NetidxError()
+        _check(lib().nxg_comm_unique_id(C.byref(buf), C.byref(err)), err)
+        return bytes(buf)
+
+    def __init__(self, codec, nranks, rank, uid):
+        err = NetidxError()
+        b = (C.c_uint8 * 128).from_buffer_copy(uid)
+        self.h = lib().nxg_comm_init(codec.ctx, nranks, rank, C.byref(b), C.byref(err))
+        _check(self.h is not None, err)
+        self.codec, self.nranks, self.rank = codec, nranks, rank
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().nxg_comm_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def encode_allgather(self, cols, heap, out_ptr, cap):
+        """Every rank's shard into one frame on every rank; returns (length, shard offsets)."""
+        n, err = C.c_uint64(0), NetidxError()
+        offs = np.zeros(self.nranks, np.uint64)
+        _check(lib().nxg_encode_allgather(self.codec.ctx, self.h, C.byref(cols.s),
+                                          _heap_ptr(heap), C.c_void_p(out_ptr), cap, C.byref(n),
+                                          C.c_void_p(offs.ctypes.data), C.byref(err)), err)
+        return n.value, [int(x) for x in offs]
+
+    def decode_sharded(self, dframe, frame_len, cols):
+        """This rank's byte range of one frame; returns (first global row, NxgRange)."""
+        ptr = dframe.data_ptr() if hasattr(dframe, "data_ptr") else int(dframe)
+        off, rng, err = C.c_uint64(0), NxgRange(), NetidxError()
+        _check(lib().nxg_decode_sharded(self.codec.ctx, self.h, C.c_void_p(ptr), frame_len,
+                                        C.byref(cols.s), C.byref(off), C.byref(rng),
+                                        C.byref(err)), err)
+        return off.value, rng
 
 
 def frame_split(msg_lens):

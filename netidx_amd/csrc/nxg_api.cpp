@@ -318,7 +318,7 @@ bool enqueue_dec_fast(NxgCtx* c, const uint8_t* f, uint64_t len, NxgColumns* out
         *path = FAST_RUN;
         if (!ensure_tstat(c, nxg_dec_f64r_groups(len), err)) return false;
         if (!ensure_rdesc(c, 16 * nxg_dec_f64r_tiles(len), err)) return false;
-        HIPCHK(nxg_launch_dec_f64r(f, len, out->id, out->fixed, out->cap_rows, c->rdesc,
+        HIPCHK(nxg_launch_dec_f64r(f, len, 0, len, out->id, out->fixed, out->cap_rows, c->rdesc,
                                    c->tstat, c->epoch, c->f64r_flags, st, c->stream));
         return true;
     }
@@ -1111,6 +1111,112 @@ bool nxg_encode_frames(NxgCtx* c, const NxgColumns* in, const uint8_t* heap, uin
     }
     for (uint64_t i = 0; i < k; i++) chunk_len_out[i] = ch[i];
     *n_chunks = k;
+    return true;
+}
+
+// ---- byte-range decode (multi-GPU) ---------------------------------------------------------------
+bool nxg_decode_range(NxgCtx* c, const uint8_t* dframe, uint64_t W, uint64_t begin, uint64_t end,
+                      NxgColumns* out, NxgRange* rng, NetidxError* err) {
+    if (!c || !out || !rng || (!dframe && W)) {
+        set_err(err, "null argument");
+        return false;
+    }
+    if (begin > end || end > W) {
+        set_err(err, "bad range [%llu, %llu) of a %llu-byte frame", (unsigned long long)begin,
+                (unsigned long long)end, (unsigned long long)W);
+        return false;
+    }
+    if (!c->pending.empty()) {
+        set_err(err, "an async operation is pending on this ctx; call nxg_ctx_sync first");
+        return false;
+    }
+    if (out->mem != NXG_MEM_DEVICE || !is_device_ptr(dframe)) {
+        set_err(err, "range decode needs a device frame and device columns");
+        return false;
+    }
+    if (!set_device(c, err)) return false;
+    memset(rng, 0, sizeof *rng);
+    rng->begin = begin;
+    rng->end = end;
+    if (begin == end) {  // an empty range: the chain passes through; linked as identity
+        rng->entry = rng->exit = ~0ull;
+        rng->ok = 1;
+        return true;
+    }
+    const uint64_t R = end - begin;
+    DevStatus* st;
+    uint32_t slot;
+    if (!begin_call(c, &st, &slot, err)) return false;
+    bool ok = ensure_tstat(c, nxg_dec_f64r_groups(R), err) &&
+              ensure_rdesc(c, 16 * nxg_dec_f64r_tiles(R), err);
+    if (ok) {
+        const hipError_t e = nxg_launch_dec_f64r(dframe, W, begin, end, out->id, out->fixed,
+                                                 out->cap_rows, c->rdesc, c->tstat, c->epoch,
+                                                 c->f64r_flags, st, c->stream);
+        if (e != hipSuccess) {
+            set_err(err, "range decode launch: %s", hipGetErrorString(e));
+            ok = false;
+        }
+    }
+    if (!end_call(c, err) || !ok) return false;
+    const uint64_t nt = nxg_dec_f64r_tiles(R);
+    uint8_t d0[16], dl[16];
+    HIPCHK(hipMemcpyAsync(c->hst + slot, st, sizeof(DevStatus), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(d0, c->rdesc, 16, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(dl, c->rdesc + 16 * (nt - 1), 16, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    const DevStatus& h = c->hst[slot];
+    if (h.timeout) {
+        set_err(err, "device look-back watchdog expired");
+        return false;
+    }
+    if (h.fast_fail) return true;  // ok = 0: not a homogeneous-f64 range
+    // Desc: base u64 | count u16 | ks u16 | x u16 | entry u8 | mode u8 (nxg_decode_f64_run.hip)
+    uint16_t xl;
+    memcpy(&xl, dl + 12, 2);
+    rng->entry = begin + d0[14];
+    rng->exit = begin + (nt - 1) * nxg_dec_f64r_tile_bytes() + xl;
+    rng->n_rows = h.n_rows;
+    rng->ok = 1;
+    rng->err_kind = h.capacity ? NXG_CAPACITY : 0;
+    out->n_rows = h.n_rows;
+    out->layout = NXG_LAYOUT_F64;
+    return true;
+}
+
+bool nxg_range_link(const NxgRange* r, uint32_t n, uint64_t W, uint64_t* row_off, uint32_t* bad,
+                    NetidxError* err) {
+    if (!r || (n && !row_off)) {
+        set_err(err, "null argument");
+        return false;
+    }
+    uint64_t at = 0, rows = 0;  // where the chain is, rows so far
+    uint64_t expect_begin = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        if (r[i].begin != expect_begin || r[i].end < r[i].begin || !r[i].ok) {
+            if (bad) *bad = i;
+            set_err(err, "range %u is not the next contiguous, decoded range", i);
+            return false;
+        }
+        expect_begin = r[i].end;
+        row_off[i] = rows;
+        if (r[i].begin == r[i].end) continue;  // empty: the chain passes through
+        if (r[i].entry != at) {
+            if (bad) *bad = i;
+            set_err(err, "range %u enters the chain at %llu, its predecessor leaves at %llu", i,
+                    (unsigned long long)r[i].entry, (unsigned long long)at);
+            return false;
+        }
+        at = r[i].exit;
+        rows += r[i].n_rows;
+    }
+    if (expect_begin != W || at != W) {
+        if (bad) *bad = n ? n - 1 : 0;
+        set_err(err, "the ranges cover [0, %llu) and the chain ends at %llu; the frame has %llu "
+                     "bytes", (unsigned long long)expect_begin, (unsigned long long)at,
+                (unsigned long long)W);
+        return false;
+    }
     return true;
 }
 

@@ -46,6 +46,8 @@ constexpr uint32_t MODE_EXACT = 0;  // Desc.mode: 12..16 = uniform record length
 
 constexpr uint32_t F_FORCE_EXACT = 1;  // probe flags (tests): every tile on the exact path
 constexpr uint32_t F_NO_BAIL = 2;      //   never give up on an irregular frame
+constexpr uint32_t F_FIRST = 4;        // the decoded range starts at the frame's first byte
+constexpr uint32_t F_LAST = 8;         // the decoded range ends at the frame's last byte
 
 // Per-tile descriptor written by the probe, read by the emit pass. A tile is one or two runs of
 // records of one length each: records [0, ks) of length L from `entry`, then records [ks, count)
@@ -160,9 +162,10 @@ constexpr int WIN = 64;  // merge walks must coincide within 64 bytes of the chu
 // position relative to the image; the END position (W - a0) for a chunk at or past the frame's
 // end; FAILX if the walks do not merge.
 NXG_DEV uint32_t merge16(const uint8_t* buf, uint32_t r, uint64_t a0, uint64_t W) {
-    const uint64_t abs_r = a0 + r;
-    if (abs_r >= W) return (uint32_t)(W - a0);
-    const uint64_t remr = W - abs_r;
+    // positions are signed: an exact tile at the start of a byte range images 64 bytes before it
+    const int64_t abs_r = (int64_t)a0 + (int64_t)r;
+    if (abs_r >= (int64_t)W) return (uint32_t)((int64_t)W - (int64_t)a0);
+    const uint64_t remr = (uint64_t)((int64_t)W - abs_r);
     const uint32_t* w = reinterpret_cast<const uint32_t*>(buf + r);
     uint32_t cand = cand16(w[0], w[1], w[2], w[3], w[4]);
     uint64_t S = 0;
@@ -205,11 +208,25 @@ NXG_DEV uint32_t merge16(const uint8_t* buf, uint32_t r, uint64_t a0, uint64_t W
 constexpr uint32_t XLO = 64;            // image offset of a0
 constexpr uint32_t XHI = XLO + SUB;     // image offset of a0 + 4096
 constexpr uint32_t IMGB = XHI + HALO;   // image bytes
+// the bytes of the 16 at `pos` (signed, relative to wire) that lie in [-pre, W), zero-filled
+__device__ __attribute__((noinline)) uint4 ld16_pre(const uint8_t* __restrict__ wire,
+                                                   int64_t pos, uint64_t W, uint64_t pre) {
+    uint32_t v[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const int64_t q = pos + k;
+        if (q >= -(int64_t)pre && q < (int64_t)W)
+            v[k >> 2] |= (uint32_t)wire[q] << (8 * (k & 3));
+    }
+    return make_uint4(v[0], v[1], v[2], v[3]);
+}
+
+// `pre`: bytes readable before wire[0] (a byte range that does not start the frame)
 template <bool EMIT>
-NXG_DEV void exact_tile(const uint8_t* __restrict__ wire, uint64_t W, uint64_t t, uint8_t* buf,
-                        uint32_t lane, uint64_t base, uint64_t* __restrict__ oid,
-                        uint64_t* __restrict__ oval, uint64_t cap, uint32_t& count,
-                        uint32_t& entry, uint32_t& x, bool& bad, bool& over) {
+NXG_DEV void exact_tile(const uint8_t* __restrict__ wire, uint64_t W, uint64_t R, bool first,
+                        uint64_t pre, uint64_t t, uint8_t* buf, uint32_t lane, uint64_t base,
+                        uint64_t* __restrict__ oid, uint64_t* __restrict__ oval, uint64_t cap,
+                        uint32_t& count, uint32_t& entry, uint32_t& x, bool& bad, bool& over) {
     const uint64_t t0 = t * T;
     count = 0;
     entry = 0;
@@ -217,15 +234,17 @@ NXG_DEV void exact_tile(const uint8_t* __restrict__ wire, uint64_t W, uint64_t t
     uint32_t prev_exit = 0;
     for (uint32_t s = 0; s < T / SUB; s++) {
         const uint64_t a0 = t0 + (uint64_t)s * SUB;
-        if (a0 >= W) break;
+        if (a0 >= R) break;
+        // records that START before the range end are this range's (a range decode: R < W)
+        const uint32_t xhi = XLO + (R - a0 < SUB ? (uint32_t)(R - a0) : SUB);
         const uint64_t ib = a0 - XLO;  // frame position of image byte 0 (wraps for a0 = 0)
         wave_lds_order();
 #pragma unroll
         for (uint32_t i = 0; i < (IMGB + 1023) / 1024; i++) {
             const uint32_t off = i * 1024 + lane * 16;
             if (off < IMGB) {
-                uint4 v = make_uint4(0, 0, 0, 0);
-                if (a0 + off >= XLO) v = ld16g(wire, ib + off, W);  // nothing before the frame
+                const int64_t pos = (int64_t)a0 - (int64_t)XLO + (int64_t)off;
+                const uint4 v = pos >= 0 ? ld16g(wire, (uint64_t)pos, W) : ld16_pre(wire, pos, W, pre);
                 *reinterpret_cast<uint4*>(buf + off) = v;
             }
         }
@@ -233,20 +252,20 @@ NXG_DEV void exact_tile(const uint8_t* __restrict__ wire, uint64_t W, uint64_t t
         // segment starts: lane 0 the chunk before a0, lane j >= 1 chunk j; ends: the next lane's
         // start, lane 63 the merge point of the chunk at a0 + 4096
         uint32_t xa;
-        if (lane == 0) xa = a0 == 0 ? XLO : merge16(buf, 0, ib, W);
+        if (lane == 0) xa = (a0 == 0 && first) ? XLO : merge16(buf, 0, ib, W);
         else xa = merge16(buf, XLO + lane * 64, ib, W);
         uint32_t xb = wave_next(xa);
         if (lane == 63) xb = merge16(buf, XHI, ib, W);
         bool b = xa == FAILX || xb == FAILX || xa > xb || (lane == 0 && xa > XLO);
-        // walk: count the records that start in [XLO, XHI); note the first start >= XLO (lane 0)
-        // and the first position >= XHI (the exit)
-        uint32_t n = 0, first = FAILX, ex = FAILX;
+        // walk: count the records that start in [XLO, xhi); note the first start >= XLO (lane 0)
+        // and the first position >= xhi (the exit)
+        uint32_t n = 0, fst = FAILX, ex = FAILX;
         if (!b) {
             uint32_t pos = xa;
             int guard = 0;
             while (pos < xb && guard < 24) {
-                if (pos >= XLO && first == FAILX) first = pos;
-                if (pos >= XHI) {
+                if (pos >= XLO && fst == FAILX) fst = pos;
+                if (pos >= xhi) {
                     if (ex == FAILX) ex = pos;
                 } else {
                     uint32_t e0, e1, e2, e3;
@@ -265,14 +284,14 @@ NXG_DEV void exact_tile(const uint8_t* __restrict__ wire, uint64_t W, uint64_t t
                 guard++;
             }
             b = pos != xb;
-            if (pos >= XLO && first == FAILX) first = pos;  // segment end (e.g. the frame end)
-            if (pos >= XHI && ex == FAILX) ex = pos;
+            if (pos >= XLO && fst == FAILX) fst = pos;  // segment end (e.g. the frame end)
+            if (pos >= xhi && ex == FAILX) ex = pos;
         }
         if (__any(b)) {
             bad = true;
             return;
         }
-        const uint32_t f0 = (uint32_t)__builtin_amdgcn_readlane((int)first, 0);
+        const uint32_t f0 = (uint32_t)__builtin_amdgcn_readlane((int)fst, 0);
         const uint32_t exw = wave_min_u32(ex);
         if (s == 0) entry = f0 - XLO;
         else if (f0 != prev_exit) {  // the sub-tiles' chains must meet
@@ -283,7 +302,7 @@ NXG_DEV void exact_tile(const uint8_t* __restrict__ wire, uint64_t W, uint64_t t
         if (EMIT) {
             uint64_t row = base + count + (inc - n);
             uint32_t pos = xa;
-            while (pos < xb && pos < XHI) {
+            while (pos < xb && pos < xhi) {
                 uint32_t e0, e1, e2, e3;
                 lds16(buf, pos, e0, e1, e2, e3);
                 const uint32_t L = e0 & 0xffu;
@@ -310,6 +329,10 @@ NXG_DEV void exact_tile(const uint8_t* __restrict__ wire, uint64_t W, uint64_t t
             return;
         }
         prev_exit = xo - SUB;  // the next sub-tile's entry, as an image offset
+        if (xhi < XHI && exw != FAILX) {  // the range ends inside this sub-tile
+            x = s * SUB + (xo - XLO);
+            break;
+        }
         x = s * SUB + (xo - XLO);
     }
 }
@@ -378,10 +401,12 @@ NXG_DEV bool run_search(const uint8_t* __restrict__ wire, uint64_t W, uint64_t t
 }
 
 // ---- probe: one lane per tile ------------------------------------------------------------------
+// wire: the decoded range's first byte; W: bytes from there to the frame end; R (<= W): the
+// range's length (records that START before R are the range's; the rest is look-ahead)
 __global__ __launch_bounds__(TPB) void nxg_f64r_probe_kernel(
-    const uint8_t* __restrict__ wire, uint64_t W, uint64_t nt, Desc* __restrict__ desc,
-    uint64_t* tstat, uint32_t epoch, uint32_t flags, DevStatus* __restrict__ st,
-    DevStatus* zst) {
+    const uint8_t* __restrict__ wire, uint64_t W, uint64_t R, uint64_t pre, uint64_t nt,
+    Desc* __restrict__ desc, uint64_t* tstat, uint32_t epoch, uint32_t flags,
+    DevStatus* __restrict__ st, DevStatus* zst) {
     zero_status(zst);
     __shared__ __attribute__((aligned(16))) uint8_t img[TPB / 64][IMGB];
     __shared__ uint64_t scan_tmp[TPB / 64];
@@ -390,7 +415,8 @@ __global__ __launch_bounds__(TPB) void nxg_f64r_probe_kernel(
     const uint64_t t = (uint64_t)blockIdx.x * TPB + tid;
     const bool has = t < nt;
     const uint64_t t0 = t * T;
-    const uint32_t lim = has ? (W - t0 < T ? (uint32_t)(W - t0) : T) : 0u;
+    const uint32_t lim = has ? (R - t0 < T ? (uint32_t)(R - t0) : T) : 0u;
+    const bool first = flags & F_FIRST;
     uint32_t count = 0, e = 0, x = 0, L = 0, L2 = 0, ks = 0;
     int state = 0;  // 0 done, 1 run search, 2 exact
     bool bad = false;
@@ -418,9 +444,10 @@ __global__ __launch_bounds__(TPB) void nxg_f64r_probe_kernel(
             L1 = e0 & 0xffu;
         }
         const uint32_t p2 = s1 + L1;
-        if (t == 0 && !(V & 1u)) {
+        if (t == 0 && first && !(V & 1u)) {
             bad = true;
-        } else if (s1 < 16 && s1 == rem0) {  // the frame ends here: no record starts in the tile
+        } else if (s1 < 16 && (s1 == rem0 || s1 >= lim)) {
+            // the frame (or the range) ends here: no record of this range starts in the tile
             e = x = s1;
             L = L2 = 12;
         } else if (s1 < 16 && V == ((1u << s1) | (p2 < 16 ? 1u << p2 : 0u))) {
@@ -520,8 +547,8 @@ __global__ __launch_bounds__(TPB) void nxg_f64r_probe_kernel(
         em &= em - 1;
         uint32_t c, en, xx;
         bool b = false, ov = false;
-        exact_tile<false>(wire, W, (uint64_t)blockIdx.x * TPB + w * 64 + j, img[w], lane, 0,
-                          nullptr, nullptr, 0, c, en, xx, b, ov);
+        exact_tile<false>(wire, W, R, first, pre, (uint64_t)blockIdx.x * TPB + w * 64 + j,
+                          img[w], lane, 0, nullptr, nullptr, 0, c, en, xx, b, ov);
         if (lane == j) {
             count = c;
             e = en;
@@ -706,9 +733,9 @@ NXG_DEV bool emit_runs(const uint8_t* __restrict__ wire, uint64_t W, uint64_t t0
 
 // wave g: tile g / ESUB, records [EREC * (g % ESUB), EREC * (g % ESUB + 1)) of it
 __global__ __launch_bounds__(TPB) void nxg_f64r_emit_kernel(
-    const uint8_t* __restrict__ wire, uint64_t W, uint64_t nt, const Desc* __restrict__ desc,
-    uint64_t* __restrict__ oid, uint64_t* __restrict__ oval, uint64_t cap,
-    DevStatus* __restrict__ st) {
+    const uint8_t* __restrict__ wire, uint64_t W, uint64_t R, uint64_t pre, uint64_t nt,
+    const Desc* __restrict__ desc, uint64_t* __restrict__ oid, uint64_t* __restrict__ oval,
+    uint64_t cap, uint32_t flags, DevStatus* __restrict__ st) {
     __shared__ __attribute__((aligned(16))) uint8_t img[TPB / 64][IMGB];
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const uint64_t g = (uint64_t)blockIdx.x * (TPB / 64) + w;
@@ -726,7 +753,7 @@ __global__ __launch_bounds__(TPB) void nxg_f64r_emit_kernel(
         // the chain: this tile's exit is the next tile's entry; the last tile ends at the
         // frame end
         if (t + 1 < nt) bad |= (uint32_t)D.x != T + desc[t + 1].entry;
-        else bad |= t0 + D.x != W;
+        else if (flags & F_LAST) bad |= t0 + D.x != W;  // a range's exit is linked by the host
         if (t == nt - 1 && lane == 0) {
             st->n_rows = D.base + D.count;
             st->path = 1;
@@ -743,7 +770,8 @@ __global__ __launch_bounds__(TPB) void nxg_f64r_emit_kernel(
     } else {
         uint32_t c, en, xx;
         bool b = false;
-        exact_tile<true>(wire, W, t, img[w], lane, D.base, oid, oval, cap, c, en, xx, b, over);
+        exact_tile<true>(wire, W, R, flags & F_FIRST, pre, t, img[w], lane, D.base, oid, oval,
+                         cap, c, en, xx, b, over);
         bad |= b || c != D.count || en != D.entry || xx != D.x;
     }
     if (__any(bad) && lane == 0) atomicOr(&st->fast_fail, 1u);
@@ -751,21 +779,32 @@ __global__ __launch_bounds__(TPB) void nxg_f64r_emit_kernel(
 }
 
 uint64_t nxg_dec_f64r_tiles(uint64_t W) { return (W + T - 1) / T; }
+uint64_t nxg_dec_f64r_tile_bytes() { return T; }
 uint64_t nxg_dec_f64r_groups(uint64_t W) { return (nxg_dec_f64r_tiles(W) + TPB - 1) / TPB; }
 
-// `desc` holds nxg_dec_f64r_tiles(W) 16-byte descriptors, `tstat` nxg_dec_f64r_groups(W)
-// epoch-tagged words; neither needs initialisation. flags: F_FORCE_EXACT / F_NO_BAIL (tests).
-hipError_t nxg_launch_dec_f64r(const uint8_t* wire, uint64_t W, uint64_t* oid, uint64_t* oval,
-                               uint64_t cap, void* desc, uint64_t* tstat, uint32_t epoch,
-                               uint32_t flags, DevStatus* st, hipStream_t s) {
-    const uint64_t nt = nxg_dec_f64r_tiles(W);
+// Decodes the records that start in [begin, end) of a frame of W bytes (a whole frame: 0, W).
+// `desc` holds nxg_dec_f64r_tiles(end - begin) 16-byte descriptors, `tstat`
+// nxg_dec_f64r_groups(end - begin) epoch-tagged words; neither needs initialisation.
+// flags: F_FORCE_EXACT / F_NO_BAIL (tests); F_FIRST / F_LAST are set here.
+hipError_t nxg_launch_dec_f64r(const uint8_t* wire, uint64_t W, uint64_t begin, uint64_t end,
+                               uint64_t* oid, uint64_t* oval, uint64_t cap, void* desc,
+                               uint64_t* tstat, uint32_t epoch, uint32_t flags, DevStatus* st,
+                               hipStream_t s) {
+    if (begin > end || end > W) return hipErrorInvalidValue;
+    const uint64_t R = end - begin;
+    const uint64_t nt = nxg_dec_f64r_tiles(R);
     if (nt == 0) return hipSuccess;
-    const uint64_t ng = nxg_dec_f64r_groups(W);
+    const uint64_t ng = nxg_dec_f64r_groups(R);
     const uint64_t ne = (nt * ESUB + TPB / 64 - 1) / (TPB / 64);
     if (ne > 0x7fffffffull) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(nxg_f64r_probe_kernel, dim3((uint32_t)ng), dim3(TPB), 0, s, wire, W, nt,
-                       reinterpret_cast<Desc*>(desc), tstat, epoch, flags, st, nxg_take_zero_slot());
-    hipLaunchKernelGGL(nxg_f64r_emit_kernel, dim3((uint32_t)ne), dim3(TPB), 0, s, wire, W, nt,
-                       reinterpret_cast<const Desc*>(desc), oid, oval, cap, st);
+    flags = (flags & (F_FORCE_EXACT | F_NO_BAIL)) | (begin == 0 ? F_FIRST : 0u) |
+            (end == W ? F_LAST : 0u);
+    const uint64_t pre = begin < 64 ? begin : 64;
+    hipLaunchKernelGGL(nxg_f64r_probe_kernel, dim3((uint32_t)ng), dim3(TPB), 0, s, wire + begin,
+                       W - begin, R, pre, nt, reinterpret_cast<Desc*>(desc), tstat, epoch, flags,
+                       st, nxg_take_zero_slot());
+    hipLaunchKernelGGL(nxg_f64r_emit_kernel, dim3((uint32_t)ne), dim3(TPB), 0, s, wire + begin,
+                       W - begin, R, pre, nt, reinterpret_cast<const Desc*>(desc), oid, oval, cap,
+                       flags, st);
     return hipGetLastError();
 }

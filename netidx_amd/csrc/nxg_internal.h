@@ -122,10 +122,13 @@ int nxg_dec_f64_1p_wgs(int ncu);
 // per tile (nxg_dec_f64r_tiles(W)), `tstat` nxg_dec_f64r_groups(W) epoch-tagged words. Sets
 // DevStatus.irregular (and fast_fail) for frames whose record lengths vary record to record.
 uint64_t nxg_dec_f64r_tiles(uint64_t W);
+uint64_t nxg_dec_f64r_tile_bytes();
 uint64_t nxg_dec_f64r_groups(uint64_t W);
-hipError_t nxg_launch_dec_f64r(const uint8_t* wire, uint64_t W, uint64_t* oid, uint64_t* oval,
-                               uint64_t cap, void* desc, uint64_t* tstat, uint32_t epoch,
-                               uint32_t flags, DevStatus* st, hipStream_t s);
+// Records starting in [begin, end) of a W-byte frame (the whole frame: begin 0, end W).
+hipError_t nxg_launch_dec_f64r(const uint8_t* wire, uint64_t W, uint64_t begin, uint64_t end,
+                               uint64_t* oid, uint64_t* oval, uint64_t cap, void* desc,
+                               uint64_t* tstat, uint32_t epoch, uint32_t flags, DevStatus* st,
+                               hipStream_t s);
 uint64_t nxg_enc_f64_tiles(uint64_t n);  // tiles (and tstat words) of an f64 encode
 hipError_t nxg_launch_enc_f64(const uint64_t* id, const uint64_t* val, uint64_t n, uint8_t* out,
                               uint64_t cap, uint64_t* tstat, uint32_t epoch, DevStatus* st,

@@ -1,20 +1,26 @@
-"""Sharding of a batch over ranks (one process per GPU), for bench.py and the multi-rank tests.
+"""Sharding over ranks (one process per GPU): torch.distributed mirrors of the library's RCCL
+calls (include/nxg_codec.h: nxg_encode_allgather, nxg_decode_sharded), for gloo on CPU (the
+multi-rank tests), for ranks that share one GPU (rehearsals: RCCL refuses two ranks on a
+device), and as bench.py's fallback when librccl cannot be opened.
 
-The decode path shards with no data-path collective: each rank owns a contiguous range of the
-records (a frame of its own, ids disjoint) and decodes it alone ("weak" scaling). The only
-exchange is config 5's: each rank encodes its shard and an all-gather assembles the full frame
-on every rank. A netidx frame payload is a plain sequence of length-wrapped messages
-(netidx/src/channel.rs:177-202 writes them back to back), so the concatenation of the shards'
-payloads in rank order is the payload of the whole batch.
-
-Everything here is device-agnostic torch.distributed code: RCCL ("nccl") with GPU tensors in
-bench.py, gloo with CPU tensors in tests/test_multirank_cpu.py.
+- Encode (BASELINE configs[4]): shards are encoded in rank order; after one all-gather of the
+  shard sizes, every rank places its shard at its final byte offset and grouped point-to-point
+  transfers deliver every shard to the same offsets on every rank. No padding, no compaction, one
+  host read of the sizes. A netidx frame payload is a plain sequence of
+  length-wrapped messages (netidx/src/channel.rs:177-202), so the shards in rank order are the
+  batch's payload.
+- Decode: one frame, cut into contiguous byte ranges. Each rank decodes the
+  messages that START in its range (reading past its end); the ranges' summaries (entry, exit,
+  rows) are all-gathered and linked by nxg_range_link; a range whose guessed entry is off the
+  chain decodes again from its predecessor's exit (a true message start).
 """
+import numpy as np
 
 
 def shard_range(total, world, rank):
     """[begin, end) of the records rank `rank` owns when `total` records go to `world` ranks
-    (contiguous, balanced: sizes differ by at most one)."""
+    (contiguous, balanced: sizes differ by at most one). Byte ranges of a frame use the same
+    split."""
     if world <= 0 or not 0 <= rank < world:
         raise ValueError(f"rank {rank} of world {world}")
     return total * rank // world, total * (rank + 1) // world
@@ -31,24 +37,76 @@ def max_over_ranks(x, world, device="cpu"):
     return float(t.item())
 
 
-def gather_frames(local, length, world):
-    """All-gather of per-rank frame payloads of different lengths.
-
-    `local` is a uint8 tensor holding this rank's payload in its first `length` bytes (it may
-    be longer). Returns (full, lengths): `full` is a uint8 tensor on local's device with the
-    payloads of ranks 0..world-1 back to back, `lengths` the per-rank byte counts. The payloads
-    travel padded to the longest one, in one all-gather."""
+def shard_offsets(length, world, device="cpu"):
+    """All-gather of the per-rank shard lengths; returns the byte offsets (world + 1 entries)."""
     import torch
     import torch.distributed as dist
-    dev = local.device
-    mine = torch.tensor([int(length)], dtype=torch.int64, device=dev)
-    lens = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
-    dist.all_gather(lens, mine)
-    lengths = [int(t.item()) for t in lens]
-    mx = max(lengths)
-    send = torch.zeros(mx, dtype=torch.uint8, device=dev)
-    send[:length] = local[:length]
-    parts = [torch.empty(mx, dtype=torch.uint8, device=dev) for _ in range(world)]
-    dist.all_gather(parts, send)
-    full = torch.cat([p[:n] for p, n in zip(parts, lengths)])
-    return full, lengths
+    mine = torch.tensor([int(length)], dtype=torch.int64, device=device)
+    lens = torch.empty(world, dtype=torch.int64, device=device)
+    dist.all_gather_into_tensor(lens, mine) if device != "cpu" else \
+        dist.all_gather(list(lens.split(1)), mine)
+    off = np.zeros(world + 1, np.int64)
+    off[1:] = np.cumsum(lens.cpu().numpy())
+    return off
+
+
+def allgather_at_offsets(out, off, rank, world):
+    """`out` holds this rank's shard at [off[rank], off[rank+1]); afterwards it holds every
+    shard at its offset (grouped send/recv, the same pattern as nxg_encode_allgather)."""
+    import torch.distributed as dist
+    ops = []
+    mine = out[int(off[rank]):int(off[rank + 1])]
+    for p in range(world):
+        if p == rank:
+            continue
+        if len(mine):
+            ops.append(dist.P2POp(dist.isend, mine, p))
+        theirs = out[int(off[p]):int(off[p + 1])]
+        if len(theirs):
+            ops.append(dist.P2POp(dist.irecv, theirs, p))
+    if ops:
+        for req in dist.batch_isend_irecv(ops):
+            req.wait()
+    return out
+
+
+def link_ranges(mine, world):
+    """All-gather of the ranges' summaries (NxgRange tuples) and nxg_range_link over them.
+    Returns (row offsets, None) or (None, index of the first range off the chain)."""
+    import torch.distributed as dist
+    from . import codec
+    allr = [None] * world
+    dist.all_gather_object(allr, tuple(int(x) for x in mine))
+    offs, bad = codec.range_link(allr, allr[-1][1])
+    return offs, bad, allr
+
+
+def decode_sharded(decode_range, frame_len, rank, world):
+    """The byte-range decode protocol of nxg_decode_sharded over torch.distributed.
+
+    decode_range(begin, end) decodes the messages that start in [begin, end) and returns its
+    summary (NxgRange or a tuple: begin, end, entry, exit, n_rows, ok, err_kind). Returns
+    (this rank's first global row, its final summary)."""
+    def summary(r):
+        return tuple(int(x) for x in (r.tuple() if hasattr(r, "tuple") else r))
+
+    b, e = shard_range(frame_len, world, rank)
+    mine = summary(decode_range(b, e))
+    for _ in range(world + 1):
+        offs, bad, allr = link_ranges(mine, world)
+        if offs is not None:
+            return int(offs[rank]), mine
+        if any(r[5] == 0 for r in allr):
+            raise RuntimeError("a range is not a homogeneous-f64 range: decode the whole frame")
+        if bad == rank:
+            if rank == 0:
+                raise RuntimeError("the frame does not start with a message")
+            at = 0
+            for r in allr[:rank]:
+                if r[0] != r[1]:
+                    at = r[3]
+            if at >= e:  # no message starts in this range: the chain passes through
+                mine = (b, e, at, at, 0, 1, 0)
+            else:
+                mine = (b, e) + summary(decode_range(at, e))[2:]
+    raise RuntimeError("the byte ranges of the frame do not link into one chain")

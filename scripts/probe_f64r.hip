@@ -161,25 +161,26 @@ int main(int argc, char** argv) {
             CK(hipMemsetAsync(st, 0, sizeof(DevStatus), 0));
             epoch++;
             if (which == 0)
-                CK(fr::nxg_launch_dec_f64r(dw, W, oid, oval, N, desc, tstat, epoch, flags, st, 0));
+                CK(fr::nxg_launch_dec_f64r(dw, W, 0, W, oid, oval, N, desc, tstat, epoch, flags, st, 0));
             else if (which == 8)
-                CK(fr8::nxg_launch_dec_f64r(dw, W, oid, oval, N, desc, tstat, epoch, flags, st, 0));
+                CK(fr8::nxg_launch_dec_f64r(dw, W, 0, W, oid, oval, N, desc, tstat, epoch, flags, st, 0));
             else if (which == 4)
-                CK(fr4::nxg_launch_dec_f64r(dw, W, oid, oval, N, desc, tstat, epoch, flags, st, 0));
+                CK(fr4::nxg_launch_dec_f64r(dw, W, 0, W, oid, oval, N, desc, tstat, epoch, flags, st, 0));
             else if (which == 5)
-                CK(frd::nxg_launch_dec_f64r(dw, W, oid, oval, N, desc, tstat, epoch, flags, st, 0));
+                CK(frd::nxg_launch_dec_f64r(dw, W, 0, W, oid, oval, N, desc, tstat, epoch, flags, st, 0));
             else if (which == 6)
-                CK(frdn::nxg_launch_dec_f64r(dw, W, oid, oval, N, desc, tstat, epoch, flags, st, 0));
+                CK(frdn::nxg_launch_dec_f64r(dw, W, 0, W, oid, oval, N, desc, tstat, epoch, flags, st, 0));
             else if (which == 20) {  // the probe kernel alone
                 const uint64_t nt = fr::nxg_dec_f64r_tiles(W);
                 hipLaunchKernelGGL(fr::nxg_f64r_probe_kernel, dim3(fr::nxg_dec_f64r_groups(W)),
-                                   dim3(256), 0, 0, dw, W, nt, (fr::f64r::Desc*)desc, tstat,
-                                   epoch, 0u, st, (DevStatus*)nullptr);
+                                   dim3(256), 0, 0, dw, W, W, (uint64_t)0, nt,
+                                   (fr::f64r::Desc*)desc, tstat, epoch, 12u, st,
+                                   (DevStatus*)nullptr);
             } else if (which == 21) {  // the emit kernel alone (descriptors of the last run)
                 const uint64_t nt = fr::nxg_dec_f64r_tiles(W);
                 hipLaunchKernelGGL(fr::nxg_f64r_emit_kernel, dim3((nt * fr::f64r::ESUB + 3) / 4),
-                                   dim3(256), 0, 0,
-                                   dw, W, nt, (const fr::f64r::Desc*)desc, oid, oval, N, st);
+                                   dim3(256), 0, 0, dw, W, W, (uint64_t)0, nt,
+                                   (const fr::f64r::Desc*)desc, oid, oval, N, 12u, st);
             }
             else
                 CK(p1n::nxg_launch_dec_f64_1p(dw, W, oid, oval, N, tstat, epoch,
