@@ -271,10 +271,16 @@ bool nxg_dispatch_updates(NxgCtx* ctx, const NxgSubTable* tab, const uint64_t* i
  *   NXG_PUB_UPDATE_CLIENT   Update(Some(cl), id, v) (update_subscriber): to client cl only.
  * Ids that are not published are dropped (counted in n_unmatched). The table (device memory):
  * by_id as a dense slot table, each slot's subscribed clients as a CSR, and each slot's current
- * value (cur_tag NULL: all F64; text bytes at cur_heap + cur_fixed). Output in NxgDispatch: per
- * client c, entries [chan_off[c], chan_off[c+1]) of (ent_sub = Id, ent_row = row); last_row[slot]
- * = 1 + the row that became current (0: unchanged). Synchronous; false on misuse, HIP failure,
- * capacity, or NXG_UNSUPPORTED (err->msg says which). */
+ * value (cur_tag NULL: all F64; text, Decimal and Abstract bytes at cur_heap + cur_fixed; the
+ * elements of Array/Map/Error(Value) current values at cur_ctag/cur_cfixed/cur_caux slots
+ * cur_fixed .., as NxgColumns children; the batch's children are the batch's NxgColumns
+ * children). Equality is Value::eq on every variant: floats NaN == NaN, Decimal numerically
+ * (rust_decimal's PartialEq: scale-independent, every zero equal), containers element by element
+ * (Map entries in column order -- the reference's encoder writes them sorted and unique),
+ * Abstract by its bytes. Output in NxgDispatch: per client c, entries [chan_off[c], chan_off[c+1])
+ * of (ent_sub = Id, ent_row = row); last_row[slot] = 1 + the row that became current (0:
+ * unchanged). Synchronous; false on misuse, HIP failure, capacity, or NXG_UNSUPPORTED (a value
+ * nested deeper than 32 levels; err->msg says which). */
 enum NxgPubKind { NXG_PUB_UPDATE = 0, NXG_PUB_UPDATE_CHANGED = 1, NXG_PUB_UPDATE_CLIENT = 2 };
 typedef struct NxgPubTable {
     uint64_t n_ids;                   /* slot_of_id covers Ids [0, n_ids) */
@@ -287,10 +293,19 @@ typedef struct NxgPubTable {
     const uint64_t* cur_fixed;
     const uint32_t* cur_aux;          /* NULL: 0 */
     const uint8_t* cur_heap;
+    const uint8_t* cur_ctag;          /* children of the current values (NULL: none) */
+    const uint64_t* cur_cfixed;
+    const uint32_t* cur_caux;
 } NxgPubTable;
 bool nxg_publish_commit(NxgCtx* ctx, const NxgPubTable* tab, const NxgColumns* batch,
                         const uint8_t* heap, const uint8_t* kind, const uint32_t* to_client,
                         NxgDispatch* out, NetidxError* err);
+/* The commit's unsubscribes (publisher/mod.rs:820-832): the queued (client, Id) pairs, in queue
+ * order, onto each client's From::Unsubscribed list; clients >= n_clients are dropped
+ * (pb.clients.get(&cl) is None). Output: chan_off[n_clients + 1] and ent_sub (the Ids) in `out`;
+ * ent_row = the pair's index in the queue; last_row unused (may be NULL). Synchronous. */
+bool nxg_publish_unsubscribes(NxgCtx* ctx, const uint64_t* id, const uint32_t* client,
+                              uint64_t n, uint32_t n_clients, NxgDispatch* out, NetidxError* err);
 
 /* ---- host framing (netidx/src/channel.rs) ------------------------------------------------
  * Frame boundaries exactly as WriteChannel::queue_send/try_flush split the buffer. The split

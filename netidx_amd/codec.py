@@ -93,7 +93,8 @@ class NxgPubTable(C.Structure):
     _fields_ = [("n_ids", C.c_uint64), ("slot_of_id", C.c_void_p), ("n_slots", C.c_uint64),
                 ("slot_client_off", C.c_void_p), ("client", C.c_void_p), ("n_clients", C.c_uint32),
                 ("cur_tag", C.c_void_p), ("cur_fixed", C.c_void_p), ("cur_aux", C.c_void_p),
-                ("cur_heap", C.c_void_p)]
+                ("cur_heap", C.c_void_p), ("cur_ctag", C.c_void_p), ("cur_cfixed", C.c_void_p),
+                ("cur_caux", C.c_void_p)]
 
 
 class NxgStatus(C.Structure):
@@ -152,6 +153,8 @@ SIGNATURES = {
     "nxg_publish_commit": (C.c_bool, [C.c_void_p, C.c_void_p, C.POINTER(NxgColumns), C.c_void_p,
                                       C.c_void_p, C.c_void_p, C.c_void_p,
                                       C.POINTER(NetidxError)]),
+    "nxg_publish_unsubscribes": (C.c_bool, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64,
+                                            C.c_uint32, C.c_void_p, C.POINTER(NetidxError)]),
     "nxg_frame_reader_new": (C.c_void_p, [C.POINTER(NetidxError)]),
     "nxg_frame_reader_free": (None, [C.c_void_p]),
     "nxg_frame_reader_push": (C.c_bool, [C.c_void_p, C.c_void_p, C.c_uint64,
@@ -353,7 +356,8 @@ class Codec:
                         out.n_entries, out.n_unmatched)
 
     def publish_commit(self, table, batch, kind, to_client=None, heap=None, cap=None):
-        """UpdateBatch::commit on device columns: `batch` (Columns: id, tag, fixed, aux), per-row
+        """UpdateBatch::commit on device columns: `batch` (Columns: id, tag, fixed, aux and the
+        children of its Array/Map/Error(Value) values), per-row
         `kind` (PUB_UPDATE / PUB_UPDATE_CHANGED / PUB_UPDATE_CLIENT, uint8 tensor) and
         `to_client` (int32 tensor, for PUB_UPDATE_CLIENT rows). Returns a Dispatch whose
         channels are the clients and whose entries are (Id, row); last_row[slot] = 1 + the row
@@ -381,6 +385,24 @@ class Codec:
                                         C.byref(err)), err)
         return Dispatch(chan_off, ent_id, ent_row, last_row[:n_slots], out.n_entries,
                         out.n_unmatched)
+
+    def publish_unsubscribes(self, ids, clients, n_clients):
+        """The commit's unsubscribes (publisher/mod.rs:820-832): device tensors of Ids (int64)
+        and clients (int32), in queue order. Returns a Dispatch whose channels are the clients
+        and whose entries are (Id, index in the queue)."""
+        import torch
+        n = ids.numel()
+        dev = ids.device
+        chan_off = torch.zeros(n_clients + 1, dtype=torch.int64, device=dev)
+        ent_id = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
+        ent_row = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
+        out = NxgDispatch(n, chan_off.data_ptr(), ent_id.data_ptr(), ent_row.data_ptr(), None,
+                          0, 0)
+        err = NetidxError()
+        _check(lib().nxg_publish_unsubscribes(self.ctx, C.c_void_p(ids.data_ptr()),
+                                              C.c_void_p(clients.data_ptr()), n, n_clients,
+                                              C.byref(out), C.byref(err)), err)
+        return Dispatch(chan_off, ent_id, ent_row, chan_off[:0], out.n_entries, 0)
 
     def encoded_len(self, cols, heap=None):
         n, err = C.c_uint64(0), NetidxError()
@@ -506,10 +528,12 @@ PUB_UPDATE, PUB_UPDATE_CHANGED, PUB_UPDATE_CLIENT = 0, 1, 2
 class PubTable:
     """Device-resident publisher state for UpdateBatch::commit (netidx/src/publisher/mod.rs:
     776-845): pb.by_id as a dense slot table (Id -> slot), each slot's subscribed clients (CSR)
-    and current value (tag/fixed/aux columns; text bytes in cur_heap)."""
+    and current value (tag/fixed/aux columns; text, Decimal and Abstract bytes in cur_heap; the
+    elements of container values in cur_ctag/cur_cfixed/cur_caux)."""
 
     def __init__(self, slot_of_id, slot_client_off, client, n_clients, cur_tag, cur_fixed,
-                 cur_aux=None, cur_heap=None, device="cuda"):
+                 cur_aux=None, cur_heap=None, device="cuda", cur_ctag=None, cur_cfixed=None,
+                 cur_caux=None):
         import torch
 
         def t(a, dt):
@@ -523,6 +547,9 @@ class PubTable:
         self.cur_fixed = t(cur_fixed, np.uint64).view(torch.int64)
         self.cur_aux = None if cur_aux is None else t(cur_aux, np.uint32).view(torch.int32)
         self.cur_heap = None if cur_heap is None else t(cur_heap, np.uint8)
+        self.cur_ctag = None if cur_ctag is None else t(cur_ctag, np.uint8)
+        self.cur_cfixed = None if cur_cfixed is None else t(cur_cfixed, np.uint64).view(torch.int64)
+        self.cur_caux = None if cur_caux is None else t(cur_caux, np.uint32).view(torch.int32)
 
     def c_struct(self):
         def p(x):
@@ -530,7 +557,8 @@ class PubTable:
         return NxgPubTable(self.slot_of_id.numel(), p(self.slot_of_id),
                            self.slot_client_off.numel() - 1, p(self.slot_client_off),
                            p(self.client), self.n_clients, p(self.cur_tag), p(self.cur_fixed),
-                           p(self.cur_aux), p(self.cur_heap))
+                           p(self.cur_aux), p(self.cur_heap), p(self.cur_ctag),
+                           p(self.cur_cfixed), p(self.cur_caux))
 
 
 def _heap_ptr(heap):

@@ -988,7 +988,8 @@ bool nxg_publish_commit(NxgCtx* c, const NxgPubTable* tab, const NxgColumns* bat
         HIPCHK(hipMalloc(&c->dscratch, sz));
         c->dscratch_cap = sz;
     }
-    const NxgPubBatch b{batch->id, batch->tag, batch->fixed, batch->aux, heap, kind, n};
+    const NxgPubBatch b{batch->id,    batch->tag,   batch->fixed, batch->aux, batch->ctag,
+                        batch->cfixed, batch->caux, heap,         kind,       n};
     HIPCHK(nxg_launch_pub_stage1(*tab, b, c->dscratch, c->stream));
     uint32_t flags[3] = {0, 0, 0};
     HIPCHK(hipMemcpyAsync(flags, nxg_pub_flags(c->dscratch), 12, hipMemcpyDeviceToHost, c->stream));
@@ -1001,8 +1002,9 @@ bool nxg_publish_commit(NxgCtx* c, const NxgPubTable* tab, const NxgColumns* bat
                               c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
         if (flags[2]) {
-            set_err(err, "NXG_UNSUPPORTED: an UpdateChanged compares a Decimal, Array, Map, "
-                         "Error(Value) or Abstract value");
+            set_err(err, "NXG_UNSUPPORTED: an UpdateChanged compares values nested deeper than "
+                         "%d levels, or a container whose columns have no children",
+                    NXG_MAX_DEPTH);
             return false;
         }
     } else {
@@ -1026,6 +1028,50 @@ bool nxg_publish_commit(NxgCtx* c, const NxgPubTable* tab, const NxgColumns* bat
     out->n_unmatched = res[1];
     if (res[0] > out->cap_entries) {
         set_err(err, "publish needs %llu entries, capacity is %llu", (unsigned long long)res[0],
+                (unsigned long long)out->cap_entries);
+        return false;
+    }
+    return true;
+}
+
+// the commit's unsubscribes (publisher/mod.rs:820-832): every pair routes to its client (row
+// mode 2 of the dispatch), so each client's list keeps queue order
+bool nxg_publish_unsubscribes(NxgCtx* c, const uint64_t* id, const uint32_t* client, uint64_t n,
+                              uint32_t n_clients, NxgDispatch* out, NetidxError* err) {
+    if (!c || !out || !out->chan_off || (n && (!id || !client)) ||
+        (out->cap_entries && (!out->ent_sub || !out->ent_row))) {
+        set_err(err, "null argument");
+        return false;
+    }
+    if (n >= 0xffffffffull) {
+        set_err(err, "unsubscribe lists are limited to 2^32 - 1 pairs");
+        return false;
+    }
+    HIPCHK(hipSetDevice(c->device));
+    const size_t mode_bytes = (n + 255) & ~uint64_t(255);
+    const size_t need = mode_bytes + 64 + nxg_disp_scratch_bytes(n, n_clients);
+    if (need > c->dscratch_cap) {
+        HIPCHK(hipStreamSynchronize(c->stream));
+        if (c->dscratch) HIPCHK(hipFree(c->dscratch));
+        c->dscratch = nullptr;
+        const size_t sz = std::max(need, c->dscratch_cap * 2);
+        HIPCHK(hipMalloc(&c->dscratch, sz));
+        c->dscratch_cap = sz;
+    }
+    uint8_t* mode = c->dscratch;
+    if (n) HIPCHK(hipMemsetAsync(mode, 2, n, c->stream));
+    const NxgSubTable st{0, nullptr, 0, nullptr, nullptr, nullptr, nullptr, n_clients};
+    uint8_t* ds = c->dscratch + mode_bytes;
+    uint64_t* um = reinterpret_cast<uint64_t*>(ds);
+    HIPCHK(nxg_launch_dispatch(st, id, n, ds + 64, out->chan_off, out->ent_sub, out->ent_row,
+                               out->cap_entries, nullptr, um, c->ncu, c->stream, mode, client));
+    uint64_t total = 0;
+    HIPCHK(hipMemcpyAsync(&total, out->chan_off + n_clients, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    out->n_entries = total;
+    out->n_unmatched = 0;
+    if (total > out->cap_entries) {
+        set_err(err, "unsubscribes need %llu entries, capacity is %llu", (unsigned long long)total,
                 (unsigned long long)out->cap_entries);
         return false;
     }

@@ -163,6 +163,9 @@ struct NxgPubBatch {
     const uint8_t* tag;
     const uint64_t* fixed;
     const uint32_t* aux;
+    const uint8_t* ctag;  // the batch's children (Array/Map/Error(Value) elements)
+    const uint64_t* cfixed;
+    const uint32_t* caux;
     const uint8_t* heap;
     const uint8_t* kind;
     uint64_t n_rows;

@@ -15,9 +15,11 @@
 // value when there is none. prev() is found by a stable LSD radix sort of (slot, row) -- only
 // when some slot occurs twice in a batch that has UpdateChanged rows.
 //
-// Equality on the columns covers the scalar tags and text (String, Bytes, Error(String)). A
-// comparison involving Decimal (numeric equality), Array, Map, Error(Value) or Abstract raises
-// `unsupported` (the call fails with NXG_UNSUPPORTED) instead of guessing.
+// Equality is Value::eq on every variant, over the columnar contract: text, Decimal and Abstract
+// bytes in the heap, the elements of Array / Map / Error(Value) as child slots. Containers are
+// compared by an explicit stack (no device recursion), off the scalar path. Map entries are
+// compared in column order: the reference's encoder writes a map's entries sorted by key and
+// unique, so two encodings of equal maps hold the same entries in the same order.
 #include "nxg_device.h"
 #include "nxg_internal.h"
 
@@ -28,44 +30,176 @@ constexpr int WAVES = TPB / 64;
 constexpr uint32_t NONE = 0xffffffffu;
 constexpr uint32_t SEG = 1024;  // radix pass: items per wave segment (64 per step)
 constexpr uint32_t BINS = 256;
+constexpr int MAX_DEPTH = 32;  // NXG_MAX_DEPTH: deeper values fail the call (NXG_UNSUPPORTED)
 
-// Value::eq on (tag, fixed, aux, text at heap + fixed): 1 equal, 0 different, -1 unsupported
-NXG_DEV int val_eq(uint32_t ta, uint64_t fa, uint32_t aa, const uint8_t* ha, uint32_t tb,
-                   uint64_t fb, uint32_t ab, const uint8_t* hb) {
-    auto opaque = [](uint32_t t) { return t == 19 || t == 20 || t == 21 || t == 22 || t == 27; };
-    if (opaque(ta) || opaque(tb)) return -1;
-    if (ta != tb) return 0;  // different Typ, or Bool(true) vs Bool(false)
-    switch (ta) {
-    case 8: {  // F32: NaN == NaN, otherwise IEEE ==
+// a source of values: top-level slots (tag null: all F64, aux null: 0) and their child slots
+struct VSrc {
+    const uint8_t* tag;
+    const uint64_t* fixed;
+    const uint32_t* aux;
+    const uint8_t* ctag;
+    const uint64_t* cfixed;
+    const uint32_t* caux;
+    const uint8_t* heap;
+};
+
+NXG_DEV bool heavy(uint32_t t) { return t == 19 || t == 20 || t == 21 || t == 22 || t == 27; }
+
+NXG_DEV int float_eq(uint32_t t, uint64_t fa, uint64_t fb) {
+    if (t == 8) {  // F32: NaN == NaN, otherwise IEEE == (+0 == -0)
         const float l = __uint_as_float((uint32_t)fa), r = __uint_as_float((uint32_t)fb);
         return (l != l && r != r) || l == r;
     }
-    case 9: {
-        const double l = __longlong_as_double((long long)fa), r = __longlong_as_double((long long)fb);
-        return (l != l && r != r) || l == r;
-    }
+    const double l = __longlong_as_double((long long)fa), r = __longlong_as_double((long long)fb);
+    return (l != l && r != r) || l == r;
+}
+
+NXG_DEV int bytes_eq(const uint8_t* p, const uint8_t* q, uint32_t n) {
+    for (uint32_t k = 0; k < n; k++)
+        if (p[k] != q[k]) return 0;
+    return 1;
+}
+
+// Value::eq for the scalar tags (no Decimal, container or Abstract): 1 equal, 0 different
+NXG_DEV int scalar_eq(uint32_t ta, uint64_t fa, uint32_t aa, const uint8_t* ha, uint32_t tb,
+                      uint64_t fb, uint32_t ab, const uint8_t* hb) {
+    if (ta == 17) ta = 16;  // the old Ok decodes to Null
+    if (tb == 17) tb = 16;
+    if (ta != tb) return 0;  // different Typ, or Bool(true) vs Bool(false)
+    switch (ta) {
+    case 8: case 9: return float_eq(ta, fa, fb);
     case 10: case 11: return fa == fb && aa == ab;  // DateTime / Duration
-    case 12: case 13: case 18: {                    // String / Bytes / Error(String): contents
-        if (aa != ab) return 0;
-        const uint8_t* p = ha + fa;
-        const uint8_t* q = hb + fb;
-        for (uint32_t k = 0; k < aa; k++)
-            if (p[k] != q[k]) return 0;
-        return 1;
-    }
+    case 12: case 13: case 18: return aa == ab && bytes_eq(ha + fa, hb + fb, aa);
     case 14: case 15: case 16: return 1;
     default: return fa == fb;  // integers (signed sign-extended), V32/Z32 as stored
     }
 }
 
+NXG_DEV uint32_t le32(const uint8_t* p) {
+    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+
+// rust_decimal's PartialEq (Decimal::serialize bytes: flags, lo, mid, hi little-endian; scale =
+// flags bits 16..23, sign = bit 31): numeric equality, exact for any scale byte -- a mantissa
+// below 2^96 < 10^29 cannot equal a non-zero one scaled by 10^29 or more.
+NXG_DEV int decimal_eq(const uint8_t* a, const uint8_t* b) {
+    const uint32_t fa = le32(a), fb = le32(b);
+    uint32_t ma0 = le32(a + 4), ma1 = le32(a + 8), ma2 = le32(a + 12);
+    uint32_t mb0 = le32(b + 4), mb1 = le32(b + 8), mb2 = le32(b + 12);
+    const bool za = !(ma0 | ma1 | ma2), zb = !(mb0 | mb1 | mb2);
+    if (za || zb) return za && zb;
+    if ((fa >> 31) != (fb >> 31)) return 0;
+    uint32_t sa = (fa >> 16) & 0xffu, sb = (fb >> 16) & 0xffu;
+    if (sa > sb) {  // scale the smaller-scale side: m_small * 10^d == m_large
+        uint32_t t = ma0; ma0 = mb0; mb0 = t;
+        t = ma1; ma1 = mb1; mb1 = t;
+        t = ma2; ma2 = mb2; mb2 = t;
+        t = sa; sa = sb; sb = t;
+    }
+    const uint32_t d = sb - sa;
+    if (d > 28) return 0;
+    uint64_t w0 = ma0, w1 = ma1, w2 = ma2, w3 = 0;  // 128 bits suffice: m < 2^96, 10^28 < 2^94
+    for (uint32_t k = 0; k < d; k++) {                 // but the product may reach 2^190: keep
+        uint64_t x = w0 * 10;                          // the top limb saturating
+        w0 = x & 0xffffffffu;
+        x = w1 * 10 + (x >> 32);
+        w1 = x & 0xffffffffu;
+        x = w2 * 10 + (x >> 32);
+        w2 = x & 0xffffffffu;
+        w3 = (x >> 32) | (w3 ? 1u : 0u);  // any bit above 96 makes the product unequal
+    }
+    return w0 == mb0 && w1 == mb1 && w2 == mb2 && !w3;
+}
+
+NXG_DEV void slot_at(const VSrc& s, bool child, uint64_t i, uint32_t& t, uint64_t& f, uint32_t& a) {
+    if (child) {
+        t = s.ctag[i];
+        f = s.cfixed[i];
+        a = s.caux[i];
+    } else {
+        t = s.tag ? s.tag[i] : 9u;
+        f = s.fixed[i];
+        a = s.aux ? s.aux[i] : 0u;
+    }
+}
+
+// Error(String) has two spellings in the columns: tag 18, or tag 22 over a String child
+NXG_DEV void norm_error(const VSrc& s, uint32_t& t, uint64_t& f, uint32_t& a) {
+    if (t == 22 && s.ctag && s.ctag[f] == 12) {
+        const uint64_t c = f;
+        t = 18;
+        f = s.cfixed[c];
+        a = s.caux[c];
+    }
+}
+
+// one node of the comparison: 0 different, 1 equal, 2 equal so far with `n` child pairs to
+// compare at child slots fa.., fb..; -1 a container whose source has no child columns
+NXG_DEV int node_eq(const VSrc& A, uint32_t ta, uint64_t fa, uint32_t aa, const VSrc& B,
+                    uint32_t tb, uint64_t fb, uint32_t ab, uint64_t& n) {
+    if (ta == 22) norm_error(A, ta, fa, aa);
+    if (tb == 22) norm_error(B, tb, fb, ab);
+    if (!heavy(ta) && !heavy(tb)) return scalar_eq(ta, fa, aa, A.heap, tb, fb, ab, B.heap);
+    if (ta != tb) return 0;
+    switch (ta) {
+    case 20: return decimal_eq(A.heap + fa, B.heap + fb);
+    case 27: return aa == ab && bytes_eq(A.heap + fa, B.heap + fb, aa);  // Abstract: its bytes
+    case 19: case 21:  // Array elements / Map entries (key, value) in column order
+        if (aa != ab) return 0;
+        if (aa && (!A.ctag || !B.ctag)) return -1;  // no child columns: the call fails
+        n = ta == 19 ? (uint64_t)aa : 2ull * aa;
+        return 2;
+    default:  // Error(Value): the inner value
+        if (!A.ctag || !B.ctag) return -1;
+        n = 1;
+        return 2;
+    }
+}
+
+// Value::eq with containers: 1 equal, 0 different, -1 nested deeper than MAX_DEPTH (or no
+// child columns)
+__attribute__((noinline)) NXG_DEV int deep_eq(const VSrc& A, uint64_t ia, const VSrc& B,
+                                              uint64_t ib) {
+    uint64_t sa[MAX_DEPTH + 1], sb[MAX_DEPTH + 1], sn[MAX_DEPTH + 1];  // pending child ranges
+    int sp = 0;
+    uint32_t ta, aa, tb, ab;
+    uint64_t fa, fb, n = 0;
+    slot_at(A, false, ia, ta, fa, aa);
+    slot_at(B, false, ib, tb, fb, ab);
+    int r = node_eq(A, ta, fa, aa, B, tb, fb, ab, n);
+    if (r < 2) return r;
+    sa[0] = fa, sb[0] = fb, sn[0] = n, sp = 1;
+    while (sp > 0) {
+        const int k = sp - 1;
+        if (sn[k] == 0) {
+            sp--;
+            continue;
+        }
+        if (sp > MAX_DEPTH) return -1;  // the next child sits at depth sp
+        const uint64_t ca = sa[k]++, cb = sb[k]++;
+        sn[k]--;
+        slot_at(A, true, ca, ta, fa, aa);
+        slot_at(B, true, cb, tb, fb, ab);
+        r = node_eq(A, ta, fa, aa, B, tb, fb, ab, n);
+        if (r <= 0) return r;
+        if (r == 2) sa[sp] = fa, sb[sp] = fb, sn[sp] = n, sp++;
+    }
+    return 1;
+}
+
+// Value::eq of top-level slot ia of A and ib of B: scalars inline, the rest by deep_eq
+NXG_DEV int val_eq(const VSrc& A, uint64_t ia, const VSrc& B, uint64_t ib) {
+    const uint32_t ta = A.tag ? A.tag[ia] : 9u, tb = B.tag ? B.tag[ib] : 9u;
+    if (heavy(ta) || heavy(tb)) return deep_eq(A, ia, B, ib);
+    return scalar_eq(ta, A.fixed[ia], A.aux ? A.aux[ia] : 0u, A.heap, tb, B.fixed[ib],
+                     B.aux ? B.aux[ib] : 0u, B.heap);
+}
+
 struct PubIn {
     const uint64_t* id;
-    const uint8_t* tag;  // null: all F64 (tag 9)
-    const uint64_t* fixed;
-    const uint32_t* aux;  // null: 0
-    const uint8_t* heap;
     const uint8_t* kind;
     uint64_t n;
+    VSrc v;  // the batch's values
 };
 
 NXG_DEV uint32_t slot_of(const NxgPubTable& tb, uint64_t x) {
@@ -75,7 +209,7 @@ NXG_DEV uint32_t slot_of(const NxgPubTable& tb, uint64_t x) {
 }  // namespace
 
 // flags[0]: some slot occurs twice among the non-directed rows; flags[1]: UpdateChanged rows
-// exist; flags[2]: unsupported comparison
+// exist; flags[2]: a value nested deeper than MAX_DEPTH, or a container without child columns
 __global__ __launch_bounds__(TPB) void nxg_pub_count_kernel(NxgPubTable tb, PubIn in,
                                                             uint32_t* __restrict__ cnt,
                                                             uint32_t* __restrict__ flags) {
@@ -186,17 +320,15 @@ __global__ __launch_bounds__(TPB) void nxg_pub_mode_kernel(NxgPubTable tb, PubIn
     if (kd == NXG_PUB_UPDATE_CHANGED) {
         const uint32_t s = slot_of(tb, in.id[i]);
         if (s != NONE) {  // unpublished Ids stay 0: no slot, counted as unmatched
-            const uint32_t ti = in.tag ? in.tag[i] : 9u;
-            const uint32_t ai = in.aux ? in.aux[i] : 0u;
             const uint32_t j = prev ? prev[i] : NONE;
             int eq;
-            if (j != NONE)
-                eq = val_eq(in.tag ? in.tag[j] : 9u, in.fixed[j], in.aux ? in.aux[j] : 0u, in.heap,
-                            ti, in.fixed[i], ai, in.heap);
-            else
-                eq = val_eq(tb.cur_tag ? tb.cur_tag[s] : 9u, tb.cur_fixed[s],
-                            tb.cur_aux ? tb.cur_aux[s] : 0u, tb.cur_heap, ti, in.fixed[i], ai,
-                            in.heap);
+            if (j != NONE) {
+                eq = val_eq(in.v, j, in.v, i);
+            } else {
+                const VSrc cur{tb.cur_tag, tb.cur_fixed, tb.cur_aux, tb.cur_ctag,
+                               tb.cur_cfixed, tb.cur_caux, tb.cur_heap};
+                eq = val_eq(cur, s, in.v, i);
+            }
             if (eq < 0 && !ld_agent32(&flags[2])) atomicOr(&flags[2], 1u);
             m = eq > 0 ? 1u : 0u;
         }
@@ -283,7 +415,7 @@ static PubScratch pub_layout(uint8_t* p, uint64_t n, uint64_t n_slots) {
 hipError_t nxg_launch_pub_stage1(const NxgPubTable& tb, const NxgPubBatch& b, uint8_t* scratch,
                                  hipStream_t s) {
     PubScratch sc = pub_layout(scratch, b.n_rows, tb.n_slots);
-    const PubIn in{b.id, b.tag, b.fixed, b.aux, b.heap, b.kind, b.n_rows};
+    const PubIn in{b.id, b.kind, b.n_rows, {b.tag, b.fixed, b.aux, b.ctag, b.cfixed, b.caux, b.heap}};
     hipError_t e;
     if ((e = hipMemsetAsync(sc.flags, 0, 64, s)) != hipSuccess) return e;
     if (tb.n_slots && (e = hipMemsetAsync(sc.cnt, 0, 4 * tb.n_slots, s)) != hipSuccess) return e;
@@ -301,7 +433,7 @@ hipError_t nxg_launch_pub_stage2(const NxgPubTable& tb, const NxgPubBatch& b, ui
                                  bool dup, bool changed, int ncu, hipStream_t s,
                                  const uint8_t** mode_out) {
     PubScratch sc = pub_layout(scratch, b.n_rows, tb.n_slots);
-    const PubIn in{b.id, b.tag, b.fixed, b.aux, b.heap, b.kind, b.n_rows};
+    const PubIn in{b.id, b.kind, b.n_rows, {b.tag, b.fixed, b.aux, b.ctag, b.cfixed, b.caux, b.heap}};
     const uint64_t n = b.n_rows;
     const uint32_t gi = (uint32_t)((n + TPB - 1) / TPB);
     *mode_out = nullptr;

@@ -639,43 +639,146 @@ int64_t nxo_dispatch(const uint64_t* id, uint64_t n_rows, uint64_t n_ids,
 }
 
 /* ---- publisher commit (publisher/mod.rs:776-845) ------------------------------------------- */
-/* Value::eq (netidx-value/src/op.rs:133-172) on (tag, fixed, aux, text bytes); -1: unsupported */
-static int val_eq(uint8_t ta, uint64_t fa, uint32_t aa, const uint8_t* ha, uint8_t tb, uint64_t fb,
-                  uint32_t ab, const uint8_t* hb) {
-    if (ta == 20 || ta == 19 || ta == 21 || ta == 22 || ta == 27) return -1;
-    if (tb == 20 || tb == 19 || tb == 21 || tb == 22 || tb == 27) return -1;
-    if (ta != tb) return 0; /* different Typ, or Bool(true) vs Bool(false) */
-    switch (ta) {
-    case 8: { /* F32: NaN == NaN, otherwise IEEE == */
+/* Value::eq (netidx-value/src/op.rs:133-172) over the columnar contract: a value is a slot
+ * (tag, fixed, aux) of a column set, its text/Decimal/Abstract bytes at heap + fixed, its
+ * children (Array elements, Map key/value pairs, Error(Value)'s inner value) at child slots
+ * fixed .. fixed + count. */
+typedef struct {
+    const uint8_t* tag; /* NULL: every top-level slot is F64 (tag 9) */
+    const uint64_t* fixed;
+    const uint32_t* aux; /* NULL: 0 */
+    const uint8_t* ctag;
+    const uint64_t* cfixed;
+    const uint32_t* caux;
+    const uint8_t* heap;
+} NxoVSrc;
+
+static uint32_t le32(const uint8_t* p) {
+    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+
+/* rust_decimal (Decimal::serialize: flags, lo, mid, hi as little-endian u32; scale = flags bits
+ * 16..23, sign = bit 31) compared numerically, as Decimal's PartialEq (via cmp) does: equal
+ * values at different scales are equal, and every zero is equal. Exact for any scale byte: a
+ * mantissa below 2^96 < 10^29 cannot equal a non-zero one scaled by 10^29 or more. */
+int nxo_decimal_eq(const uint8_t* a, const uint8_t* b) {
+    const uint32_t fa = le32(a), fb = le32(b);
+    uint32_t ma[3] = {le32(a + 4), le32(a + 8), le32(a + 12)};
+    uint32_t mb[3] = {le32(b + 4), le32(b + 8), le32(b + 12)};
+    const int za = !(ma[0] | ma[1] | ma[2]), zb = !(mb[0] | mb[1] | mb[2]);
+    if (za || zb) return za && zb;
+    if ((fa >> 31) != (fb >> 31)) return 0;
+    uint32_t sa = (fa >> 16) & 0xff, sb = (fb >> 16) & 0xff;
+    if (sa > sb) { /* scale the smaller-scale side up: m_small * 10^d == m_large */
+        uint32_t t[3] = {ma[0], ma[1], ma[2]};
+        memcpy(ma, mb, sizeof t);
+        memcpy(mb, t, sizeof t);
+        const uint32_t u = sa;
+        sa = sb;
+        sb = u;
+    }
+    const uint32_t d = sb - sa;
+    if (d > 28) return 0;
+    uint64_t w[6] = {ma[0], ma[1], ma[2], 0, 0, 0}; /* 192 bits in 32-bit limbs */
+    for (uint32_t k = 0; k < d; k++) {
+        uint64_t carry = 0;
+        for (int i = 0; i < 6; i++) {
+            const uint64_t x = w[i] * 10 + carry;
+            w[i] = x & 0xffffffffu;
+            carry = x >> 32;
+        }
+    }
+    return w[0] == mb[0] && w[1] == mb[1] && w[2] == mb[2] && !(w[3] | w[4] | w[5]);
+}
+
+static int nxo_f_eq(uint8_t t, uint64_t fa, uint64_t fb) {
+    if (t == 8) { /* F32: NaN == NaN, otherwise IEEE == (+0 == -0) */
         float l, r;
         uint32_t lb = (uint32_t)fa, rb = (uint32_t)fb;
         memcpy(&l, &lb, 4);
         memcpy(&r, &rb, 4);
         return (l != l && r != r) || l == r;
     }
-    case 9: {
-        double l, r;
-        memcpy(&l, &fa, 8);
-        memcpy(&r, &fb, 8);
-        return (l != l && r != r) || l == r;
+    double l, r;
+    memcpy(&l, &fa, 8);
+    memcpy(&r, &fb, 8);
+    return (l != l && r != r) || l == r;
+}
+
+/* one slot of a source: top level (child = 0) or a child slot */
+static void nxo_slot(const NxoVSrc* s, int child, uint64_t i, uint8_t* t, uint64_t* f,
+                     uint32_t* a) {
+    if (child) {
+        *t = s->ctag[i];
+        *f = s->cfixed[i];
+        *a = s->caux[i];
+    } else {
+        *t = s->tag ? s->tag[i] : 9;
+        *f = s->fixed[i];
+        *a = s->aux ? s->aux[i] : 0;
     }
+}
+
+/* Error(String) has two spellings in the columns: tag 18, or tag 22 over a String child */
+static void nxo_norm_error(const NxoVSrc* s, uint8_t* t, uint64_t* f, uint32_t* a) {
+    if (*t == 22 && s->ctag && s->ctag[*f] == 12) {
+        const uint64_t c = *f;
+        *t = 18;
+        *f = s->cfixed[c];
+        *a = s->caux[c];
+    }
+}
+
+/* 1 equal, 0 different, -1 nested deeper than NXG_MAX_DEPTH (32) or a container without child
+ * columns */
+static int nxo_val_eq_at(const NxoVSrc* A, int ca, uint64_t ia, const NxoVSrc* B, int cb,
+                         uint64_t ib, int depth) {
+    uint8_t ta, tb;
+    uint64_t fa, fb;
+    uint32_t aa, ab;
+    nxo_slot(A, ca, ia, &ta, &fa, &aa);
+    nxo_slot(B, cb, ib, &tb, &fb, &ab);
+    if (depth > 32) return -1;
+    if (ta == 22) nxo_norm_error(A, &ta, &fa, &aa);
+    if (tb == 22) nxo_norm_error(B, &tb, &fb, &ab);
+    if (ta == 17) ta = 16; /* Null */
+    if (tb == 17) tb = 16;
+    if (ta != tb) return 0; /* different Typ, or Bool(true) vs Bool(false) */
+    switch (ta) {
+    case 8: case 9: return nxo_f_eq(ta, fa, fb);
     case 10: case 11: return fa == fb && aa == ab; /* DateTime / Duration */
-    case 12: case 13: case 18: /* String / Bytes / Error(String): contents */
-        return aa == ab && memcmp(ha + fa, hb + fb, aa) == 0;
+    case 12: case 13: case 18: case 27: /* String / Bytes / Error(String) / Abstract bytes */
+        return aa == ab && memcmp(A->heap + fa, B->heap + fb, aa) == 0;
+    case 20: return nxo_decimal_eq(A->heap + fa, B->heap + fb);
     case 14: case 15: case 16: return 1;
+    case 19: case 21: case 22: { /* Array, Map (entries in order), Error(Value) */
+        const uint64_t n = ta == 19 ? aa : ta == 21 ? 2ull * aa : 1;
+        if (ta != 22 && aa != ab) return 0;
+        if (n && (!A->ctag || !B->ctag)) return -1; /* no child columns */
+        for (uint64_t k = 0; k < n; k++) {
+            const int e = nxo_val_eq_at(A, 1, fa + k, B, 1, fb + k, depth + 1);
+            if (e <= 0) return e;
+        }
+        return 1;
+    }
     default: return fa == fb; /* integers (sign-extended), V32/Z32 as u32 */
     }
 }
 
-int64_t nxo_publish_commit(const uint64_t* id, const uint8_t* tag, const uint64_t* fixed,
-                           const uint32_t* aux, const uint8_t* heap, const uint8_t* kind,
-                           const uint32_t* to_client, uint64_t n_rows, uint64_t n_ids,
-                           const uint32_t* slot_of_id, uint64_t n_slots,
-                           const uint32_t* slot_client_off, const uint32_t* client,
-                           uint32_t n_clients, const uint8_t* cur_tag, const uint64_t* cur_fixed,
-                           const uint32_t* cur_aux, const uint8_t* cur_heap, uint64_t* client_off,
-                           uint64_t* ent_id, uint64_t* ent_row, uint64_t cap, uint64_t* cur_row,
-                           uint64_t* n_unmatched) {
+int64_t nxo_publish_commit2(const uint64_t* id, const uint8_t* tag, const uint64_t* fixed,
+                            const uint32_t* aux, const uint8_t* ctag, const uint64_t* cfixed,
+                            const uint32_t* caux, const uint8_t* heap, const uint8_t* kind,
+                            const uint32_t* to_client, uint64_t n_rows, uint64_t n_ids,
+                            const uint32_t* slot_of_id, uint64_t n_slots,
+                            const uint32_t* slot_client_off, const uint32_t* client,
+                            uint32_t n_clients, const uint8_t* cur_tag, const uint64_t* cur_fixed,
+                            const uint32_t* cur_aux, const uint8_t* cur_ctag,
+                            const uint64_t* cur_cfixed, const uint32_t* cur_caux,
+                            const uint8_t* cur_heap, uint64_t* client_off, uint64_t* ent_id,
+                            uint64_t* ent_row, uint64_t cap, uint64_t* cur_row,
+                            uint64_t* n_unmatched) {
+    const NxoVSrc BS = {tag, fixed, aux, ctag, cfixed, caux, heap};
+    const NxoVSrc CS = {cur_tag, cur_fixed, cur_aux, cur_ctag, cur_cfixed, cur_caux, cur_heap};
     /* current value of each slot: the table's, or the batch row that replaced it */
     uint64_t* cur = (uint64_t*)malloc((n_slots ? n_slots : 1) * sizeof(uint64_t));
     uint8_t* emit = (uint8_t*)malloc(n_rows ? n_rows : 1);
@@ -701,13 +804,8 @@ int64_t nxo_publish_commit(const uint64_t* id, const uint8_t* tag, const uint64_
         }
         if (kind[i] == NXO_PUB_UPDATE_CHANGED) { /* if pbl.current != v */
             int eq;
-            if (cur[s]) {
-                const uint64_t j = cur[s] - 1;
-                eq = val_eq(tag[j], fixed[j], aux[j], heap, tag[i], fixed[i], aux[i], heap);
-            } else {
-                eq = val_eq(cur_tag[s], cur_fixed[s], cur_aux[s], cur_heap, tag[i], fixed[i],
-                            aux[i], heap);
-            }
+            if (cur[s]) eq = nxo_val_eq_at(&BS, 0, cur[s] - 1, &BS, 0, i, 0);
+            else eq = nxo_val_eq_at(&CS, 0, s, &BS, 0, i, 0);
             if (eq < 0) {
                 rc = -NXO_UNSUPPORTED;
                 break;
@@ -749,4 +847,37 @@ int64_t nxo_publish_commit(const uint64_t* id, const uint8_t* tag, const uint64_
     free(cur);
     free(emit);
     return rc;
+}
+
+int64_t nxo_publish_commit(const uint64_t* id, const uint8_t* tag, const uint64_t* fixed,
+                           const uint32_t* aux, const uint8_t* heap, const uint8_t* kind,
+                           const uint32_t* to_client, uint64_t n_rows, uint64_t n_ids,
+                           const uint32_t* slot_of_id, uint64_t n_slots,
+                           const uint32_t* slot_client_off, const uint32_t* client,
+                           uint32_t n_clients, const uint8_t* cur_tag, const uint64_t* cur_fixed,
+                           const uint32_t* cur_aux, const uint8_t* cur_heap, uint64_t* client_off,
+                           uint64_t* ent_id, uint64_t* ent_row, uint64_t cap, uint64_t* cur_row,
+                           uint64_t* n_unmatched) {
+    return nxo_publish_commit2(id, tag, fixed, aux, NULL, NULL, NULL, heap, kind, to_client,
+                               n_rows, n_ids, slot_of_id, n_slots, slot_client_off, client,
+                               n_clients, cur_tag, cur_fixed, cur_aux, NULL, NULL, NULL, cur_heap,
+                               client_off, ent_id, ent_row, cap, cur_row, n_unmatched);
+}
+
+/* UpdateBatch::commit's unsubscribes (publisher/mod.rs:820-832): each (client, id), in queue
+ * order, onto that client's Update.unsubscribes. client_off[n_clients + 1] (CSR), ent_id[n].
+ * Clients >= n_clients are dropped (pb.clients.get(&cl) is None). Returns the entries kept. */
+int64_t nxo_publish_unsubscribes(const uint64_t* id, const uint32_t* cl, uint64_t n,
+                                 uint32_t n_clients, uint64_t* client_off, uint64_t* ent_id) {
+    for (uint32_t c = 0; c <= n_clients; c++) client_off[c] = 0;
+    for (uint64_t i = 0; i < n; i++)
+        if (cl[i] < n_clients) client_off[cl[i] + 1]++;
+    for (uint32_t c = 0; c < n_clients; c++) client_off[c + 1] += client_off[c];
+    uint64_t* pos = (uint64_t*)malloc((n_clients ? n_clients : 1) * sizeof(uint64_t));
+    if (!pos) return -NXO_CAPACITY;
+    for (uint32_t c = 0; c < n_clients; c++) pos[c] = client_off[c];
+    for (uint64_t i = 0; i < n; i++)
+        if (cl[i] < n_clients) ent_id[pos[cl[i]]++] = id[i];
+    free(pos);
+    return (int64_t)client_off[n_clients];
 }

@@ -139,6 +139,24 @@ int64_t nxo_publish_commit(const uint64_t* id, const uint8_t* tag, const uint64_
                            uint64_t* ent_id, uint64_t* ent_row, uint64_t cap, uint64_t* cur_row,
                            uint64_t* n_unmatched);
 
+/* commit with child columns (Array/Map/Error(Value) equality) for the batch and the current
+ * values; children may be NULL when no value has any */
+int64_t nxo_publish_commit2(const uint64_t* id, const uint8_t* tag, const uint64_t* fixed,
+                            const uint32_t* aux, const uint8_t* ctag, const uint64_t* cfixed,
+                            const uint32_t* caux, const uint8_t* heap, const uint8_t* kind,
+                            const uint32_t* to_client, uint64_t n_rows, uint64_t n_ids,
+                            const uint32_t* slot_of_id, uint64_t n_slots,
+                            const uint32_t* slot_client_off, const uint32_t* client,
+                            uint32_t n_clients, const uint8_t* cur_tag, const uint64_t* cur_fixed,
+                            const uint32_t* cur_aux, const uint8_t* cur_ctag,
+                            const uint64_t* cur_cfixed, const uint32_t* cur_caux,
+                            const uint8_t* cur_heap, uint64_t* client_off, uint64_t* ent_id,
+                            uint64_t* ent_row, uint64_t cap, uint64_t* cur_row,
+                            uint64_t* n_unmatched);
+int nxo_decimal_eq(const uint8_t* a, const uint8_t* b);
+int64_t nxo_publish_unsubscribes(const uint64_t* id, const uint32_t* cl, uint64_t n,
+                                 uint32_t n_clients, uint64_t* client_off, uint64_t* ent_id);
+
 #ifdef __cplusplus
 }
 #endif

@@ -62,6 +62,16 @@ def lib():
                                                             C.c_uint64, C.c_void_p, C.c_void_p,
                                                             C.c_uint32] + [C.c_void_p] * 7 + \
             [C.c_uint64, C.c_void_p, C.c_void_p]
+        L.nxo_publish_commit2.restype = C.c_int64
+        L.nxo_publish_commit2.argtypes = [C.c_void_p] * 10 + [C.c_uint64, C.c_uint64, C.c_void_p,
+                                                              C.c_uint64, C.c_void_p, C.c_void_p,
+                                                              C.c_uint32] + [C.c_void_p] * 10 + \
+            [C.c_uint64, C.c_void_p, C.c_void_p]
+        L.nxo_decimal_eq.restype = C.c_int
+        L.nxo_decimal_eq.argtypes = [C.c_void_p, C.c_void_p]
+        L.nxo_publish_unsubscribes.restype = C.c_int64
+        L.nxo_publish_unsubscribes.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32,
+                                               C.c_void_p, C.c_void_p]
         L.nxo_dispatch.restype = C.c_int64
         L.nxo_dispatch.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_void_p, C.c_uint64,
                                    C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
@@ -175,16 +185,24 @@ UNSUPPORTED = 10
 
 
 def publish_commit(id, tag, fixed, aux, heap, kind, to_client, slot_of_id, slot_client_off,
-                   client, n_clients, cur_tag, cur_fixed, cur_aux, cur_heap):
-    """nxo_publish_commit (UpdateBatch::commit, publisher/mod.rs:776-845) on numpy arrays.
-    Returns (client_off, ent_id, ent_row, cur_row, n_unmatched), or raises ValueError(code)."""
+                   client, n_clients, cur_tag, cur_fixed, cur_aux, cur_heap, children=None,
+                   cur_children=None):
+    """nxo_publish_commit2 (UpdateBatch::commit, publisher/mod.rs:776-845) on numpy arrays.
+    children / cur_children: (ctag, cfixed, caux) of the batch's / the current values'
+    Array/Map/Error(Value) elements, or None. Returns (client_off, ent_id, ent_row, cur_row,
+    n_unmatched), or raises ValueError(code)."""
     a = {}
+    ch = children if children is not None else ([], [], [])
+    cch = cur_children if cur_children is not None else ([], [], [])
     for k, v, dt in [("id", id, np.uint64), ("tag", tag, np.uint8), ("fixed", fixed, np.uint64),
                      ("aux", aux, np.uint32), ("heap", heap, np.uint8), ("kind", kind, np.uint8),
                      ("to", to_client, np.uint32), ("soi", slot_of_id, np.uint32),
                      ("off", slot_client_off, np.uint32), ("cl", client, np.uint32),
                      ("ctag", cur_tag, np.uint8), ("cfix", cur_fixed, np.uint64),
-                     ("caux", cur_aux, np.uint32), ("cheap", cur_heap, np.uint8)]:
+                     ("caux", cur_aux, np.uint32), ("cheap", cur_heap, np.uint8),
+                     ("bct", ch[0], np.uint8), ("bcf", ch[1], np.uint64), ("bca", ch[2], np.uint32),
+                     ("cct", cch[0], np.uint8), ("ccf", cch[1], np.uint64),
+                     ("cca", cch[2], np.uint32)]:
         a[k] = np.ascontiguousarray(v if len(v) else np.zeros(1), dt)
     n = len(id)
     n_slots = len(slot_client_off) - 1
@@ -196,11 +214,37 @@ def publish_commit(id, tag, fixed, aux, heap, kind, to_client, slot_of_id, slot_
     cur_row = np.zeros(max(n_slots, 1), np.uint64)
     um = np.zeros(1, np.uint64)
     d = lambda k: a[k].ctypes.data
-    r = lib().nxo_publish_commit(d("id"), d("tag"), d("fixed"), d("aux"), d("heap"), d("kind"),
-                                 d("to"), n, len(slot_of_id), d("soi"), n_slots, d("off"), d("cl"),
-                                 n_clients, d("ctag"), d("cfix"), d("caux"), d("cheap"),
-                                 client_off.ctypes.data, ent_id.ctypes.data, ent_row.ctypes.data,
-                                 cap, cur_row.ctypes.data, um.ctypes.data)
+    dc = lambda k, have: a[k].ctypes.data if have else None
+    hb, hc = children is not None, cur_children is not None
+    r = lib().nxo_publish_commit2(d("id"), d("tag"), d("fixed"), d("aux"), dc("bct", hb),
+                                  dc("bcf", hb), dc("bca", hb), d("heap"), d("kind"), d("to"), n,
+                                  len(slot_of_id), d("soi"), n_slots, d("off"), d("cl"),
+                                  n_clients, d("ctag"), d("cfix"), d("caux"), dc("cct", hc),
+                                  dc("ccf", hc), dc("cca", hc), d("cheap"),
+                                  client_off.ctypes.data, ent_id.ctypes.data, ent_row.ctypes.data,
+                                  cap, cur_row.ctypes.data, um.ctypes.data)
     if r < 0:
         raise ValueError(-r)
     return client_off, ent_id[:r], ent_row[:r], cur_row[:n_slots], int(um[0])
+
+
+def decimal_eq(a, b):
+    """nxo_decimal_eq on two 16-byte rust_decimal encodings."""
+    a = np.frombuffer(bytes(a), np.uint8).copy()
+    b = np.frombuffer(bytes(b), np.uint8).copy()
+    assert len(a) == len(b) == 16
+    return bool(lib().nxo_decimal_eq(a.ctypes.data, b.ctypes.data))
+
+
+def publish_unsubscribes(ids, clients, n_clients):
+    """nxo_publish_unsubscribes: returns (client_off, ent_id)."""
+    ids = np.ascontiguousarray(ids, np.uint64)
+    cl = np.ascontiguousarray(clients, np.uint32)
+    off = np.zeros(n_clients + 1, np.uint64)
+    ent = np.zeros(max(len(ids), 1), np.uint64)
+    r = lib().nxo_publish_unsubscribes(ids.ctypes.data if len(ids) else None,
+                                       cl.ctypes.data if len(cl) else None, len(ids), n_clients,
+                                       off.ctypes.data, ent.ctypes.data)
+    if r < 0:
+        raise ValueError(-r)
+    return off, ent[:r]
