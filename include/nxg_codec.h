@@ -307,6 +307,25 @@ bool nxg_publish_commit(NxgCtx* ctx, const NxgPubTable* tab, const NxgColumns* b
 bool nxg_publish_unsubscribes(NxgCtx* ctx, const uint64_t* id, const uint32_t* client,
                               uint64_t n, uint32_t n_clients, NxgDispatch* out, NetidxError* err);
 
+/* ---- archive batches: replaces <GPooled<Vec<BatchItem>> as Pack>::decode ------------------
+ * (netidx-archive/src/logfile/reader.rs:449/475 over logfile/mod.rs:150-205 BatchItem and
+ * netidx/src/subscriber/mod.rs:154-177 Event). `buf` (device memory, `len` bytes) starts with the
+ * batch: varint count, then count items of varint Id (as u32) and an Event that is not
+ * length-wrapped (0x40 = Unsubscribed, else a bare Value). Bytes after the batch are not read
+ * (the uncompressed reader decodes from the record to the end of the mmap).
+ * Output: MIXED-layout columns (nxg_columns_alloc), one row per item: id = the u32 Id, the
+ * Event's Value in tag/fixed/aux (+ children; text offsets index `buf`), Unsubscribed as tag
+ * NXG_TAG_UNSUBSCRIBED with fixed 0, aux 0. status: n_rows (= count), n_children, err_kind /
+ * err_offset (the failing item's start, 0 for the count and the size guard) with the reference's
+ * PackError kinds; path = NXG_PATH_ARCHIVE. *consumed = the batch's length in bytes.
+ * Deviation: Event::decode on an empty buffer panics in the reference; here it is
+ * NXG_BUFFER_SHORT. Synchronous; false on misuse or a HIP failure. A decode error is reported in
+ * `status` (as nxg_decode_updates does), with n_rows = n_children = 0. */
+#define NXG_TAG_UNSUBSCRIBED 0x40
+#define NXG_PATH_ARCHIVE 3
+bool nxg_decode_archive_batch(NxgCtx* ctx, const uint8_t* buf, uint64_t len, NxgColumns* out,
+                              NxgStatus* status, uint64_t* consumed, NetidxError* err);
+
 /* ---- host framing (netidx/src/channel.rs) ------------------------------------------------
  * Frame boundaries exactly as WriteChannel::queue_send/try_flush split the buffer. The split
  * happens at MAX_BATCH = 0x3FFFFFFF (channel.rs:34, 187-191) and is recorded between messages.

@@ -155,6 +155,9 @@ SIGNATURES = {
                                       C.POINTER(NetidxError)]),
     "nxg_publish_unsubscribes": (C.c_bool, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64,
                                             C.c_uint32, C.c_void_p, C.POINTER(NetidxError)]),
+    "nxg_decode_archive_batch": (C.c_bool, [C.c_void_p, C.c_void_p, C.c_uint64,
+                                            C.POINTER(NxgColumns), C.POINTER(NxgStatus),
+                                            C.POINTER(C.c_uint64), C.POINTER(NetidxError)]),
     "nxg_frame_reader_new": (C.c_void_p, [C.POINTER(NetidxError)]),
     "nxg_frame_reader_free": (None, [C.c_void_p]),
     "nxg_frame_reader_push": (C.c_bool, [C.c_void_p, C.c_void_p, C.c_uint64,
@@ -310,6 +313,17 @@ class Codec:
         if check and st.err_kind:
             raise PackError(st.err_kind, st.err_offset)
         return st
+
+    def decode_archive(self, buf, nbytes, cols, check=True):
+        """An archive batch (Vec<BatchItem>, netidx-archive logfile/mod.rs:150-205) in device
+        memory into MIXED device columns. Returns (NxgStatus, bytes consumed)."""
+        ptr = buf.data_ptr() if hasattr(buf, "data_ptr") else int(buf)
+        st, err, used = NxgStatus(), NetidxError(), C.c_uint64(0)
+        _check(lib().nxg_decode_archive_batch(self.ctx, C.c_void_p(ptr), nbytes, C.byref(cols.s),
+                                              C.byref(st), C.byref(used), C.byref(err)), err)
+        if check and st.err_kind:
+            raise PackError(st.err_kind, st.err_offset)
+        return st, used.value
 
     def decode_batch(self, frame, layout=LAYOUT_MIXED, flags=0, device="cuda"):
         """Decode one frame payload; returns (Columns, NxgStatus)."""
@@ -523,6 +537,7 @@ class Dispatch:
 
 
 PUB_UPDATE, PUB_UPDATE_CHANGED, PUB_UPDATE_CLIENT = 0, 1, 2
+TAG_UNSUBSCRIBED = 0x40  # archive rows: Event::Unsubscribed
 
 
 class PubTable:

@@ -908,6 +908,56 @@ static bool encode_impl(NxgCtx* c, const NxgColumns* in, const uint8_t* heap, ui
     return true;
 }
 
+// ---- archive batches (netidx-archive logfile/mod.rs:150-205) ---------------------------------
+bool nxg_decode_archive_batch(NxgCtx* c, const uint8_t* buf, uint64_t len, NxgColumns* out,
+                              NxgStatus* ust, uint64_t* consumed, NetidxError* err) {
+    if (!c || !out || (!buf && len)) {
+        set_err(err, "null argument");
+        return false;
+    }
+    if (!c->pending.empty()) {
+        set_err(err, "an async operation is pending on this ctx; call nxg_ctx_sync first");
+        return false;
+    }
+    if (len >= (1ull << 40)) {
+        set_err(err, "batch too large (%llu bytes)", (unsigned long long)len);
+        return false;
+    }
+    if (out->mem != NXG_MEM_DEVICE || !mixed_capable(out) || !out->id) {
+        set_err(err, "archive batches decode into device MIXED-layout columns");
+        return false;
+    }
+    if (!set_device(c, err)) return false;
+    const uint8_t* df;
+    if (!frame_to_device(c, buf, len, &df, err)) return false;
+    const size_t need = 64 + nxg_arch_scratch_bytes(len);
+    if (need > c->dscratch_cap) {
+        HIPCHK(hipStreamSynchronize(c->stream));
+        if (c->dscratch) HIPCHK(hipFree(c->dscratch));
+        c->dscratch = nullptr;
+        const size_t sz = std::max(need, c->dscratch_cap * 2);
+        HIPCHK(hipMalloc(&c->dscratch, sz));
+        c->dscratch_cap = sz;
+    }
+    uint32_t* cap_flag = reinterpret_cast<uint32_t*>(c->dscratch);
+    HIPCHK(hipMemsetAsync(cap_flag, 0, 4, c->stream));
+    NxgArchResult r{};
+    HIPCHK(nxg_arch_decode(df, len, desc_of(out), c->dscratch + 64, cap_flag, 8, &r, c->stream));
+    NxgStatus s{};
+    s.n_rows = r.n_rows;
+    s.n_children = r.n_children;
+    s.err_kind = (int32_t)r.err_kind;
+    s.err_offset = r.err_offset;
+    s.path = NXG_PATH_ARCHIVE;
+    out->n_rows = r.n_rows;
+    out->n_children = r.n_children;
+    out->n_ctl = 0;
+    out->layout = NXG_LAYOUT_MIXED;
+    if (ust) *ust = s;
+    if (consumed) *consumed = r.consumed;
+    return true;
+}
+
 // ---- dispatch (connection.rs:546-567) --------------------------------------------------------
 bool nxg_dispatch_updates(NxgCtx* c, const NxgSubTable* tab, const uint64_t* id, uint64_t n_rows,
                           NxgDispatch* out, NetidxError* err) {

@@ -177,6 +177,18 @@ const uint32_t* nxg_pub_flags(uint8_t* scratch);
 hipError_t nxg_launch_pub_stage2(const NxgPubTable& tb, const NxgPubBatch& b, uint8_t* scratch,
                                  bool dup, bool changed, int ncu, hipStream_t s,
                                  const uint8_t** mode_out);
+// exclusive sums of M u32 counts into u64 offsets (nxg_publish.hip); bsum: M / 4096 + 2 words
+hipError_t nxg_scan_u32(const uint32_t* hist, uint64_t M, uint64_t* off, uint64_t* bsum,
+                        hipStream_t s);
+// archive batches (nxg_archive.hip): Vec<BatchItem> decode. Synchronous on `s`.
+struct NxgArchResult {
+    uint64_t count, n_rows, n_children, consumed, err_offset;
+    uint32_t err_kind;
+    int rounds;  // chain rounds run (-1: the serial fallback)
+};
+uint64_t nxg_arch_scratch_bytes(uint64_t W);
+hipError_t nxg_arch_decode(const uint8_t* buf, uint64_t W, const ColsDesc& cols, uint8_t* scratch,
+                           uint32_t* cap_flag, int max_rounds, NxgArchResult* res, hipStream_t s);
 int nxg_occupancy_enc_f64();
 int nxg_occupancy_enc_general();
 

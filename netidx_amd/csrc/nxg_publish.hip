@@ -345,15 +345,17 @@ __global__ void nxg_disp_scan_top_kernel(uint64_t* __restrict__ bsum, uint64_t n
 namespace {
 constexpr uint32_t SCAN_B = 256 * 16;  // = nxg_dispatch.hip's scan block
 
-hipError_t exclusive_scan(const uint32_t* hist, uint64_t M, uint64_t* off, uint64_t* bsum,
-                          hipStream_t s);
 __global__ __launch_bounds__(TPB) void add_block_kernel(uint64_t* __restrict__ off, uint64_t M,
                                                         const uint64_t* __restrict__ bsum) {
     const uint64_t i = (uint64_t)blockIdx.x * TPB + threadIdx.x;
     if (i < M) off[i] += bsum[i / SCAN_B];
 }
-hipError_t exclusive_scan(const uint32_t* hist, uint64_t M, uint64_t* off, uint64_t* bsum,
-                          hipStream_t s) {
+}  // namespace
+
+// exclusive sums of M u32 counts into u64 offsets; bsum holds M / 4096 + 2 words
+hipError_t nxg_scan_u32(const uint32_t* hist, uint64_t M, uint64_t* off, uint64_t* bsum,
+                        hipStream_t s) {
+    if (M == 0) return hipSuccess;
     const uint64_t nb = (M + SCAN_B - 1) / SCAN_B;
     hipLaunchKernelGGL(nxg_disp_scan_block_kernel, dim3((uint32_t)nb), dim3(256), 0, s, hist, M, off,
                        bsum);
@@ -362,7 +364,6 @@ hipError_t exclusive_scan(const uint32_t* hist, uint64_t M, uint64_t* off, uint6
                        M, bsum);
     return hipGetLastError();
 }
-}  // namespace
 
 uint64_t nxg_pub_scratch_bytes(uint64_t n, uint64_t n_slots) {
     const uint64_t n_seg = (n + SEG - 1) / SEG;
@@ -455,7 +456,7 @@ hipError_t nxg_launch_pub_stage2(const NxgPubTable& tb, const NxgPubBatch& b, ui
         for (uint32_t shift = 0; shift < bits; shift += 8) {
             hipLaunchKernelGGL(nxg_radix_count_kernel, dim3(g), dim3(TPB), 0, s, ka, n, shift,
                                n_seg, sc.hist);
-            if ((e = exclusive_scan(sc.hist, M, sc.off, sc.bsum, s)) != hipSuccess) return e;
+            if ((e = nxg_scan_u32(sc.hist, M, sc.off, sc.bsum, s)) != hipSuccess) return e;
             hipLaunchKernelGGL(nxg_radix_scatter_kernel, dim3(g), dim3(TPB), 0, s, ka, va, n, shift,
                                n_seg, sc.off, kb, vb);
             uint32_t* t = ka; ka = kb; kb = t;

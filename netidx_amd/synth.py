@@ -111,3 +111,19 @@ def mixed_columns(n, seed=SEED_MIXED):
     fixed[m] = astart.astype(np.uint64)
     aux[m] = alen.astype(np.uint32)
     return MixedColumns(ids, tag, fixed, aux, ctag, cfixed.astype(np.uint64), caux, heap)
+
+
+SEED_ARCHIVE = 0x5EED0006
+
+
+def archive_columns(n, seed=SEED_ARCHIVE, p_unsub=0.05):
+    """Rows of an archive batch (Vec<BatchItem>, netidx-archive logfile/mod.rs:150-205): the
+    config-3 value mix with u32 Ids, and about p_unsub of the scalar rows turned into
+    Event::Unsubscribed (tag 0x40)."""
+    m = mixed_columns(n, seed)
+    rng = np.random.default_rng(seed + 1)
+    un = (rng.random(n) < p_unsub) & (m.tag != 19)
+    m.tag[un] = 0x40
+    m.fixed[un] = 0
+    m.aux[un] = 0
+    return m

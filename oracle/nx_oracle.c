@@ -451,6 +451,65 @@ int nxo_decode_frame(const uint8_t* w, uint64_t len, NxoCols* c) {
 }
 
 /* ---------------------------------------------------------------------------------------------
+ * Archive batches: <GPooled<Vec<BatchItem>> as Pack> (pack.rs:167-185 -> Vec<T>, pack.rs:934-973)
+ * with BatchItem(Id, Event) (netidx-archive/src/logfile/mod.rs:150-205) and Event::decode
+ * (netidx/src/subscriber/mod.rs:154-177): varint count, check_sz!(count, remaining, BatchItem),
+ * then per item varint(id) as u32 and an Event that is NOT length-wrapped -- byte 0x40 is
+ * Unsubscribed, anything else a bare Value. Boundaries follow from the values' tags alone.
+ * size_of::<BatchItem>() is taken as 24 (Id u32 + Event 16 with its niche in Value's repr(u32)
+ * tag, align 8): parity unpinned, it only sets the TooBig guard. Deviation: Event::decode on an
+ * empty buffer indexes chunk()[0] and panics in the reference; here it is BufferShort.
+ * Rows: id = the u32 Id, the value (Unsubscribed: tag NXO_TAG_UNSUBSCRIBED, 0, 0). Returns the
+ * bytes consumed (trailing bytes after the count items are not read), or -kind with err_offset =
+ * the failing item's start (0 for the count and the size guard).
+ * ------------------------------------------------------------------------------------------- */
+#define BATCH_ITEM_SIZE 24
+
+int64_t nxo_decode_archive(const uint8_t* w, uint64_t len, NxoCols* c) {
+    c->n_rows = c->n_children = c->n_ctl = c->n_heartbeat = 0;
+    c->err_kind = 0;
+    c->err_offset = 0;
+    Ctx x = {c, 1};
+    Buf b = {w, 0, len};
+    uint64_t count, start = 0, id;
+    int e;
+    if ((e = dvar(&b, &count))) goto fail;
+    {
+        const uint64_t sz = count > UINT64_MAX / BATCH_ITEM_SIZE ? UINT64_MAX : count * BATCH_ITEM_SIZE;
+        if (sz > MAX_VEC || sz > (rem(&b) << 8)) {
+            e = NXO_TOO_BIG;
+            goto fail;
+        }
+    }
+    for (uint64_t i = 0; i < count; i++) {
+        start = b.pos;
+        if (c->n_rows >= c->cap_rows) {
+            e = NXO_CAPACITY;
+            goto fail;
+        }
+        const uint64_t r = c->n_rows;
+        if ((e = dvar(&b, &id))) goto fail;
+        if (rem(&b) == 0) {
+            e = NXO_BUFFER_SHORT;
+            goto fail;
+        }
+        if (w[b.pos] == NXO_TAG_UNSUBSCRIBED) {
+            b.pos++;
+            put_slot(&x, 1, r, NXO_TAG_UNSUBSCRIBED, 0, 0);
+        } else if ((e = dvalue(&x, &b, 1, r, 0))) {
+            goto fail;
+        }
+        c->id[r] = (uint32_t)id;
+        c->n_rows++;
+    }
+    return (int64_t)b.pos;
+fail:
+    c->err_kind = e;
+    c->err_offset = start;
+    return -(int64_t)e;
+}
+
+/* ---------------------------------------------------------------------------------------------
  * Encode (lib.rs:361-468, array.rs:583-593, pack.rs:1212-1223, abstract_type.rs:272-278)
  * ------------------------------------------------------------------------------------------- */
 static uint32_t zz32(int32_t n) { return ((uint32_t)n << 1) ^ (uint32_t)(n >> 31); }
@@ -880,4 +939,30 @@ int64_t nxo_publish_unsubscribes(const uint64_t* id, const uint32_t* cl, uint64_
         if (cl[i] < n_clients) ent_id[pos[cl[i]]++] = id[i];
     free(pos);
     return (int64_t)client_off[n_clients];
+}
+
+/* <Vec<BatchItem> as Pack>::encode (pack.rs:941-952): varint(count), then per row varint(id)
+ * and the Event (tag NXO_TAG_UNSUBSCRIBED: the byte 0x40; else the bare Value). out == NULL:
+ * the length only. TooBig if count * size_of::<BatchItem>() > MAX_VEC. */
+int64_t nxo_encode_archive(const NxoCols* c, const uint8_t* heap, uint8_t* out, uint64_t cap) {
+    if (c->n_rows > MAX_VEC / BATCH_ITEM_SIZE) return -NXO_TOO_BIG;
+    uint64_t total = nxo_varint_len(c->n_rows);
+    for (uint64_t r = 0; r < c->n_rows; r++) {
+        int64_t l = 1;
+        if (c->tag[r] != NXO_TAG_UNSUBSCRIBED) {
+            l = vlen(c, 1, r, 0);
+            if (l < 0) return l;
+        }
+        total += nxo_varint_len((uint32_t)c->id[r]) + (uint64_t)l;
+    }
+    if (!out) return (int64_t)total;
+    if (total > cap) return -NXO_CAPACITY;
+    uint8_t* o = out;
+    putvar(&o, c->n_rows);
+    for (uint64_t r = 0; r < c->n_rows; r++) {
+        putvar(&o, (uint32_t)c->id[r]);
+        if (c->tag[r] == NXO_TAG_UNSUBSCRIBED) *o++ = NXO_TAG_UNSUBSCRIBED;
+        else venc(c, heap, 1, r, &o);
+    }
+    return (int64_t)total;
 }

@@ -154,6 +154,11 @@ int64_t nxo_publish_commit2(const uint64_t* id, const uint8_t* tag, const uint64
                             uint64_t* ent_row, uint64_t cap, uint64_t* cur_row,
                             uint64_t* n_unmatched);
 int nxo_decimal_eq(const uint8_t* a, const uint8_t* b);
+
+/* archive batches (netidx-archive logfile/mod.rs:188-205): see nx_oracle.c */
+#define NXO_TAG_UNSUBSCRIBED 0x40
+int64_t nxo_decode_archive(const uint8_t* w, uint64_t len, NxoCols* c);
+int64_t nxo_encode_archive(const NxoCols* c, const uint8_t* heap, uint8_t* out, uint64_t cap);
 int64_t nxo_publish_unsubscribes(const uint64_t* id, const uint32_t* cl, uint64_t n,
                                  uint32_t n_clients, uint64_t* client_off, uint64_t* ent_id);
 

@@ -393,11 +393,75 @@ def edge_ok():
     return out
 
 
+# --- archive batches ---------------------------------------------------------------------------
+# <Vec<BatchItem> as Pack> (pack.rs:934-973): varint count, then per item varint(Id u32) and an
+# Event (netidx/src/subscriber/mod.rs:154-177): 0x40 = Unsubscribed, else a bare Value -- not
+# length-wrapped (netidx-archive/src/logfile/mod.rs:150-205).
+UNSUB = 0x40
+
+
+def archive(items, trailing=b""):
+    """items: [(id, value or None for Unsubscribed)]. Returns wire, cols (rows carry the u32
+    Id), consumed."""
+    wire = bytearray(enc_varint(len(items)))
+    cols = Cols()
+    for i, v in items:
+        wire += enc_varint(i)
+        if v is None:
+            cols.rows.append((i & 0xFFFFFFFF, UNSUB, 0, 0))
+            wire.append(UNSUB)
+        else:
+            slot = flatten(cols, v, len(wire) + 1)
+            cols.rows.append((i & 0xFFFFFFFF,) + slot)
+            wire += enc_value(v)
+    return bytes(wire) + trailing, cols, len(wire)
+
+
+def archive_batches():
+    rng = random.Random(0x5EED0002)
+    out = [
+        # netidx-archive/src/logfile/test.rs:10-43: every item Event::Update(Value::U64(42))
+        ("ref_basic", [(0, (4, 42)), (1, (4, 42))], b""),
+        ("empty", [], b""),
+        ("unsub_only", [(7, None), (2**32 - 1, None)], b""),
+        ("mixed", [(rng.getrandbits(32), None if rng.random() < 0.1 else rand_value(rng))
+                   for _ in range(500)], b""),
+        ("long", [(3, (12, b"x" * 5000)), (4, (13, bytes(range(256)) * 40)), (5, None),
+                  (6, (19, [(9, f64bits(float(k))) for k in range(300)])),
+                  (7, (12, "\u00e9".encode() * 3000)), (8, (16, None))], b""),
+        # bytes after the batch (the rest of an mmap'd file) are not read
+        ("trailing", [(1, (9, f64bits(2.5))), (2, (16, None))], b"\xff\x1c\x00junk"),
+    ]
+    return out
+
+
+def archive_errors():
+    """(name, wire, kind, offset): offset = the failing item's start (0: count / size guard)."""
+    one = enc_varint(5) + enc_value((4, 42))
+    return [
+        ("count_short", b"", 4, 0),                                   # decode_varint on empty
+        ("toobig", enc_varint(1000) + one, 2, 0),                     # check_sz: 24000 > 10<<8
+        ("event_empty", enc_varint(1) + enc_varint(9), 4, 1),         # chunk()[0] panic -> Short
+        ("fewer_items", enc_varint(3) + one + one, 4, 1 + 2 * len(one)),
+        ("bad_tag", enc_varint(2) + one + enc_varint(6) + b"\x1c", 1, 1 + len(one)),
+        ("bad_utf8", enc_varint(1) + enc_varint(6) + b"\x0c\x02\xc3\x28", 3, 1),
+        ("id_varint_10", enc_varint(1) + b"\xff" * 10 + b"\x10", 3, 1),
+        ("string_toobig", enc_varint(1) + enc_varint(6) + b"\x0c\x09ab", 2, 1),
+    ]
+
+
+def archive_edge_ok():
+    """Accepted non-canonical inputs: an Id varint wider than u32 is truncated (Id(v as u32))."""
+    w = enc_varint(1) + enc_varint(2**40 + 7) + enc_value((16, None))
+    return [("id_truncated", w, [(7, 16, 0, 0)], len(w))]
+
+
 def main():
     kat = kats()
     with open(os.path.join(HERE, "kat.json"), "w") as f:
         json.dump(kat, f, indent=1)
-    manifest = {"batches": [], "errors": [], "edge_ok": []}
+    manifest = {"batches": [], "errors": [], "edge_ok": [], "archive": [],
+                "archive_errors": [], "archive_edge_ok": []}
     for name, msgs in batches():
         wire, cols = batch(msgs)
         fn = f"batch_{name}.bin"
@@ -410,10 +474,25 @@ def main():
     for name, wire, rows in edge_ok():
         manifest["edge_ok"].append({"name": name, "hex": wire.hex(),
                                     "rows": [list(r) for r in rows]})
+    for name, items, trailing in archive_batches():
+        wire, cols, consumed = archive(items, trailing)
+        fn = f"archive_{name}.bin"
+        with open(os.path.join(HERE, fn), "wb") as f:
+            f.write(wire)
+        manifest["archive"].append({"name": name, "file": fn, "len": len(wire),
+                                    "consumed": consumed, "expect": cols_json(cols)})
+    for name, wire, kind, off in archive_errors():
+        manifest["archive_errors"].append({"name": name, "hex": wire.hex(), "kind": kind,
+                                           "offset": off})
+    for name, wire, rows, consumed in archive_edge_ok():
+        manifest["archive_edge_ok"].append({"name": name, "hex": wire.hex(), "consumed": consumed,
+                                            "rows": [list(r) for r in rows]})
     with open(os.path.join(HERE, "manifest.json"), "w") as f:
         json.dump(manifest, f, indent=1)
     print("wrote", len(kat), "KATs,", len(manifest["batches"]), "batches,",
-          len(manifest["errors"]), "error cases,", len(manifest["edge_ok"]), "edge cases")
+          len(manifest["errors"]), "error cases,", len(manifest["edge_ok"]), "edge cases,",
+          len(manifest["archive"]), "archive batches,", len(manifest["archive_errors"]),
+          "archive error cases")
 
 
 if __name__ == "__main__":

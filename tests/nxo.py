@@ -72,6 +72,10 @@ def lib():
         L.nxo_publish_unsubscribes.restype = C.c_int64
         L.nxo_publish_unsubscribes.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32,
                                                C.c_void_p, C.c_void_p]
+        L.nxo_decode_archive.restype = C.c_int64
+        L.nxo_decode_archive.argtypes = [C.c_void_p, C.c_uint64, C.POINTER(NxoCols)]
+        L.nxo_encode_archive.restype = C.c_int64
+        L.nxo_encode_archive.argtypes = [C.POINTER(NxoCols), C.c_void_p, C.c_void_p, C.c_uint64]
         L.nxo_dispatch.restype = C.c_int64
         L.nxo_dispatch.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_void_p, C.c_uint64,
                                    C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
@@ -136,6 +140,34 @@ def encode(d, heap):
         raise ValueError(f"encode error {-n}")
     out = np.zeros(max(n, 1), np.uint8)
     m = lib().nxo_encode(C.byref(d.s), heap.ctypes.data, out.ctypes.data, n)
+    assert m == n, (m, n)
+    return out[:n].tobytes()
+
+
+TAG_UNSUBSCRIBED = 0x40
+
+
+def decode_archive(buf, cap_rows=None, cap_children=None):
+    """nxo_decode_archive (an archive batch, Vec<BatchItem>). Returns (Decoded, consumed or
+    -kind)."""
+    buf = np.frombuffer(bytes(buf), np.uint8) if not isinstance(buf, np.ndarray) else buf
+    n = len(buf)
+    d = Decoded(cap_rows if cap_rows is not None else n // 2 + 1,
+                cap_children if cap_children is not None else n + 1, 1)
+    r = lib().nxo_decode_archive(buf.ctypes.data if n else None, n, C.byref(d.s))
+    d.wire = buf
+    return d, int(r)
+
+
+def encode_archive(d, heap):
+    """nxo_encode_archive of the rows of `d` (Decoded-shaped columns) with text at `heap`."""
+    heap = np.frombuffer(bytes(heap), np.uint8) if not isinstance(heap, np.ndarray) else heap
+    hp = heap.ctypes.data if len(heap) else None
+    n = lib().nxo_encode_archive(C.byref(d.s), hp, None, 0)
+    if n < 0:
+        raise ValueError(f"encode error {-n}")
+    out = np.zeros(max(n, 1), np.uint8)
+    m = lib().nxo_encode_archive(C.byref(d.s), hp, out.ctypes.data, n)
     assert m == n, (m, n)
     return out[:n].tobytes()
 

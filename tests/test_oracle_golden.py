@@ -87,6 +87,38 @@ def test_golden_edge_ok(c):
     assert rows == c["rows"]
 
 
+@pytest.mark.parametrize("b", MANIFEST["archive"], ids=lambda b: b["name"])
+def test_golden_archive(b):
+    """Archive batches (Vec<BatchItem>, netidx-archive/src/logfile/mod.rs:188-205): every row and
+    child against the twin's expected decode, the bytes consumed, and the re-encode."""
+    wire = open(os.path.join(GOLD, b["file"]), "rb").read()
+    d, consumed = nxo.decode_archive(wire)
+    t = d.trim()
+    e = b["expect"]
+    assert t["err_kind"] == 0 and consumed == b["consumed"]
+    rows = [list(map(int, r)) for r in zip(t["id"], t["tag"], t["fixed"], t["aux"])]
+    assert rows == e["rows"]
+    ch = [list(map(int, r)) for r in zip(t["ctag"], t["cfixed"], t["caux"])]
+    assert ch == e["children"]
+    assert nxo.encode_archive(d, wire) == wire[:consumed]
+
+
+@pytest.mark.parametrize("c", MANIFEST["archive_errors"], ids=lambda c: c["name"])
+def test_golden_archive_errors(c):
+    d, r = nxo.decode_archive(bytes.fromhex(c["hex"]))
+    t = d.trim()
+    assert (t["err_kind"], t["err_offset"]) == (c["kind"], c["offset"]) and r == -c["kind"]
+
+
+@pytest.mark.parametrize("c", MANIFEST["archive_edge_ok"], ids=lambda c: c["name"])
+def test_golden_archive_edge_ok(c):
+    d, consumed = nxo.decode_archive(bytes.fromhex(c["hex"]))
+    t = d.trim()
+    assert t["err_kind"] == 0 and consumed == c["consumed"]
+    rows = [list(map(int, r)) for r in zip(t["id"], t["tag"], t["fixed"], t["aux"])]
+    assert rows == c["rows"]
+
+
 def test_encode_f64_matches_decode():
     rng = np.random.default_rng(7)
     ids = rng.integers(0, 2**63, 5000, dtype=np.uint64)
