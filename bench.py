@@ -163,6 +163,31 @@ def oracle_check_encode(out_bytes, ids, vals=None, mixed=None):
     return len(ref)
 
 
+def oracle_check_archive(buf, cols, m):
+    """Checker for the archive legs: the product's encoded batch == the oracle encoder's bytes for
+    the same columns, and the product's decode == the oracle's decode, every column."""
+    import numpy as np
+    nxo = _nxo()
+    n = len(m.id)
+    d = nxo.Decoded(n, len(m.ctag) + 1, 1)
+    for name in ("id", "tag", "fixed", "aux"):
+        getattr(d, name)[:n] = getattr(m, name)
+    d.ctag[:len(m.ctag)] = m.ctag
+    d.cfixed[:len(m.ctag)] = m.cfixed
+    d.caux[:len(m.ctag)] = m.caux
+    d.s.n_rows, d.s.n_children = n, len(m.ctag)
+    ref = np.frombuffer(nxo.encode_archive(d, m.heap), np.uint8)
+    got = buf.cpu().numpy()
+    assert np.array_equal(got, ref), "archive encode differs from the oracle"
+    o, used = nxo.decode_archive(got, cap_rows=n + 1, cap_children=len(m.ctag) + 1)
+    o = o.trim()
+    assert o["err_kind"] == 0 and used == len(got)
+    g = cols.numpy()
+    for k in ("id", "tag", "fixed", "aux", "ctag", "cfixed", "caux"):
+        assert np.array_equal(g[k][: len(o[k])], o[k]), f"archive decode differs in {k}"
+    return n
+
+
 def host_cpu():
     model = "unknown"
     try:
@@ -307,6 +332,45 @@ def extras_single_gpu(codec, stream, steps, warmup):
         torch.cuda.empty_cache()
     except Exception as e:
         ex["decode_mixed_1e7"] = {"error": repr(e)}
+    # (b1) archive batches (Vec<BatchItem>): 10^7 items of the config-3 value
+    # mix with 5 % Event::Unsubscribed; the product encoder writes the batch, the product decoder
+    # reads it back; both checked once against the oracle. Wall clock per synchronous call.
+    try:
+        n = 10_000_000
+        m = synth.archive_columns(n)
+        mc = netidx_amd.columns_from_arrays(m.id, m.fixed, m.tag, m.aux, m.ctag, m.cfixed, m.caux)
+        heap = torch.from_numpy(m.heap.copy()).cuda()
+        buf = codec.encode_archive(mc, heap)
+        out = Columns(n + 1, len(m.ctag) + 1, 1, netidx_amd.LAYOUT_MIXED, "cuda")
+        k = max(3, steps // 4)
+        for _ in range(2):
+            codec.encode_archive(mc, heap, buf)
+            st, used = codec.decode_archive(buf, buf.numel(), out)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(k):
+            codec.encode_archive(mc, heap, buf)
+        torch.cuda.synchronize()
+        t_enc = (time.perf_counter() - t0) / k
+        t0 = time.perf_counter()
+        for _ in range(k):
+            st, used = codec.decode_archive(buf, buf.numel(), out)
+        torch.cuda.synchronize()
+        t_dec = (time.perf_counter() - t0) / k
+        assert st.n_rows == n and used == buf.numel()
+        checked = oracle_check_archive(buf, out, m)
+        b = buf.numel() + n * (8 + 1 + 8 + 4) + 13 * len(m.ctag)
+        ex["archive_1e7"] = {"items": n, "batch_bytes": buf.numel(),
+                             "decode_ms": round(t_dec * 1e3, 3),
+                             "decode_M_items_s": round(n / t_dec / 1e6, 1),
+                             "decode_hbm_frac": round(b / t_dec / 1e9 / HBM_PEAK_GBS, 4),
+                             "encode_ms": round(t_enc * 1e3, 3),
+                             "encode_M_items_s": round(n / t_enc / 1e6, 1),
+                             "oracle_items_checked": checked}
+        del mc, heap, buf, out
+        torch.cuda.empty_cache()
+    except Exception as e:
+        ex["archive_1e7"] = {"error": repr(e)}
     # (b2) the socket-buffer path: host (pinned) frame -> device decode -> host (pinned) columns,
     # through the same synchronous call (nxg_decode_updates stages H2D and D2H itself); wall
     # clock, so PCIe Gen5 transfers are included. Never the bench `value`.

@@ -325,6 +325,13 @@ bool nxg_publish_unsubscribes(NxgCtx* ctx, const uint64_t* id, const uint32_t* c
 #define NXG_PATH_ARCHIVE 3
 bool nxg_decode_archive_batch(NxgCtx* ctx, const uint8_t* buf, uint64_t len, NxgColumns* out,
                               NxgStatus* status, uint64_t* consumed, NetidxError* err);
+/* Replaces <GPooled<Vec<BatchItem>> as Pack>::encode (writer.rs:423-428, pack.rs:941-952):
+ * device MIXED-layout columns in the same form (id = the u32 Id, tag NXG_TAG_UNSUBSCRIBED for
+ * Event::Unsubscribed; text at heap + fixed, device memory; no control messages) to `out`
+ * (device memory, `cap` bytes; NULL: *len_out = the length only). Synchronous. TooBig when
+ * count * size_of::<BatchItem>() exceeds MAX_VEC or a value violates a size guard. */
+bool nxg_encode_archive_batch(NxgCtx* ctx, const NxgColumns* in, const uint8_t* heap,
+                              uint8_t* out, uint64_t cap, uint64_t* len_out, NetidxError* err);
 
 /* ---- host framing (netidx/src/channel.rs) ------------------------------------------------
  * Frame boundaries exactly as WriteChannel::queue_send/try_flush split the buffer. The split

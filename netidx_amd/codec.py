@@ -158,6 +158,9 @@ SIGNATURES = {
     "nxg_decode_archive_batch": (C.c_bool, [C.c_void_p, C.c_void_p, C.c_uint64,
                                             C.POINTER(NxgColumns), C.POINTER(NxgStatus),
                                             C.POINTER(C.c_uint64), C.POINTER(NetidxError)]),
+    "nxg_encode_archive_batch": (C.c_bool, [C.c_void_p, C.POINTER(NxgColumns), C.c_void_p,
+                                            C.c_void_p, C.c_uint64, C.POINTER(C.c_uint64),
+                                            C.POINTER(NetidxError)]),
     "nxg_frame_reader_new": (C.c_void_p, [C.POINTER(NetidxError)]),
     "nxg_frame_reader_free": (None, [C.c_void_p]),
     "nxg_frame_reader_push": (C.c_bool, [C.c_void_p, C.c_void_p, C.c_uint64,
@@ -324,6 +327,24 @@ class Codec:
         if check and st.err_kind:
             raise PackError(st.err_kind, st.err_offset)
         return st, used.value
+
+    def encode_archive(self, cols, heap=None, out=None):
+        """Device MIXED columns -> an archive batch (Vec<BatchItem>). Returns a uint8 tensor on
+        the device (out=None), or the length written into `out` (a device tensor)."""
+        import torch
+        err, n = NetidxError(), C.c_uint64(0)
+        if out is None:
+            _check(lib().nxg_encode_archive_batch(self.ctx, C.byref(cols.s), _heap_ptr(heap),
+                                                  None, 0, C.byref(n), C.byref(err)), err)
+            out = torch.empty(max(n.value, 1), dtype=torch.uint8, device=cols.id.device)
+            _check(lib().nxg_encode_archive_batch(self.ctx, C.byref(cols.s), _heap_ptr(heap),
+                                                  C.c_void_p(out.data_ptr()), out.numel(),
+                                                  C.byref(n), C.byref(err)), err)
+            return out[: n.value]
+        _check(lib().nxg_encode_archive_batch(self.ctx, C.byref(cols.s), _heap_ptr(heap),
+                                              C.c_void_p(out.data_ptr()), out.numel(), C.byref(n),
+                                              C.byref(err)), err)
+        return n.value
 
     def decode_batch(self, frame, layout=LAYOUT_MIXED, flags=0, device="cuda"):
         """Decode one frame payload; returns (Columns, NxgStatus)."""

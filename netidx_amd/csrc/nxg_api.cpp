@@ -909,6 +909,61 @@ static bool encode_impl(NxgCtx* c, const NxgColumns* in, const uint8_t* heap, ui
 }
 
 // ---- archive batches (netidx-archive logfile/mod.rs:150-205) ---------------------------------
+// <Vec<BatchItem> as Pack>::encode (pack.rs:941-952): the count varint here, the items by the
+// general encoder's rows kernel in archive mode
+bool nxg_encode_archive_batch(NxgCtx* c, const NxgColumns* in, const uint8_t* heap, uint8_t* out,
+                              uint64_t cap, uint64_t* len_out, NetidxError* err) {
+    if (!c || !in) {
+        set_err(err, "null argument");
+        return false;
+    }
+    if (!c->pending.empty()) {
+        set_err(err, "an async operation is pending on this ctx; call nxg_ctx_sync first");
+        return false;
+    }
+    if (in->mem != NXG_MEM_DEVICE || !mixed_capable(in) || in->n_ctl ||
+        (in->n_rows && (!in->id || !is_device_ptr(in->id)))) {
+        set_err(err, "archive batches encode from device MIXED-layout columns without control "
+                     "messages");
+        return false;
+    }
+    if (in->n_rows > kMaxVecBytes / kBatchItemSize) {  // Vec::encode's guard (pack.rs:943-945)
+        set_err(err, "encode failed: %llu items exceed MAX_VEC (PackError::TooBig)",
+                (unsigned long long)in->n_rows);
+        return false;
+    }
+    if (!set_device(c, err)) return false;
+    uint8_t hdr[10];
+    uint32_t hl = 0;
+    for (uint64_t v = in->n_rows;; v >>= 7) {
+        if (v < 0x80) {
+            hdr[hl++] = (uint8_t)v;
+            break;
+        }
+        hdr[hl++] = (uint8_t)((v & 0x7f) | 0x80);
+    }
+    if (out && cap < hl) {
+        set_err(err, "output buffer too small: need at least %u bytes", hl);
+        return false;
+    }
+    if (out) HIPCHK(hipMemcpyAsync(out, hdr, hl, hipMemcpyHostToDevice, c->stream));
+    const uint64_t nt = nxg_enc_general_tiles(in->n_rows);
+    if (!ensure_tstat(c, nt, err) || !ensure_escratch(c, 1, err)) return false;
+    DevStatus* st;
+    uint32_t slot;
+    if (!begin_call(c, &st, &slot, err)) return false;
+    const hipError_t le = nxg_launch_enc_general(desc_of(in), heap, out, out ? cap : 0, c->escratch,
+                                                 c->tstat, c->epoch, st, c->grid_enc_gen,
+                                                 c->stream, hl);
+    if (!end_call(c, err)) return false;
+    HIPCHK(le);
+    uint64_t total = 0;
+    if (!finish_encode(c, in, st, slot, &total, cap, out != nullptr, err)) return false;
+    if (in->n_rows == 0) total = hl;
+    if (len_out) *len_out = total;
+    return true;
+}
+
 bool nxg_decode_archive_batch(NxgCtx* c, const uint8_t* buf, uint64_t len, NxgColumns* out,
                               NxgStatus* ust, uint64_t* consumed, NetidxError* err) {
     if (!c || !out || (!buf && len)) {

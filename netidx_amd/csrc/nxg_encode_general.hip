@@ -20,6 +20,11 @@
 //    sized and written without the explicit stack; Map, Error and nested containers take the
 //    general walk.
 // 3. ctl_write: copies each control span to its position.
+//
+// Archive mode (arch_base > 0, nxg_encode_archive_batch): the rows of an archive batch
+// (<Vec<BatchItem> as Pack>::encode, pack.rs:941-952; BatchItem logfile/mod.rs:188-205): each row
+// is varint(Id as u32) and its Event -- the byte 0x40 for Unsubscribed (tag 0x40), else the bare
+// Value -- after the count varint the host writes at [0, arch_base). No length prefix, no variant.
 #include "nxg_device.h"
 
 namespace {
@@ -305,7 +310,8 @@ __global__ __launch_bounds__(TPB) void nxg_enc_rows_kernel(
     ColsDesc c, const uint8_t* __restrict__ heap, uint8_t* __restrict__ out, uint64_t cap,
     const uint64_t* __restrict__ ctl_pre, uint64_t* __restrict__ row_off,
     uint64_t* __restrict__ tstat, uint32_t ntiles, uint32_t epoch, DevStatus* __restrict__ st,
-    DevStatus* zst) {
+    DevStatus* zst, uint64_t arch_base) {
+    const bool arch = arch_base != 0;
     zero_status(zst);
     __shared__ uint64_t tmp[4];
     __shared__ uint64_t sh_base;
@@ -329,7 +335,8 @@ __global__ __launch_bounds__(TPB) void nxg_enc_rows_kernel(
 #pragma unroll
         for (int k = 0; k < GRPT; k++) {
             const uint64_t r = r0 + k;
-            cls[k] = r < n ? value_class(c.tag[r]) : NCLS;
+            const uint32_t tg = r < n ? c.tag[r] : 0u;
+            cls[k] = r < n ? (arch && tg == 0x40u ? (uint32_t)CLS_SCAL : value_class(tg)) : NCLS;
             pos[k] = 0;
 #pragma unroll
             for (uint32_t q = 0; q < NCLS; q++) {
@@ -373,7 +380,7 @@ __global__ __launch_bounds__(TPB) void nxg_enc_rows_kernel(
             case CLS_TEXT: vlen = 1 + vl64(v.aux) + v.aux; break;
             case CLS_TIME: vlen = 13; break;
             case CLS_SCAL:
-                vlen = scalar_len(v);
+                vlen = arch && v.tag == 0x40u ? 1 : scalar_len(v);
                 if (!vlen) {  // a tag the encoder does not write (17): the walk reports it
                     cls_lds[rl] = CLS_GEN;
                     vlen = value_len(c, true, r, &err);
@@ -392,8 +399,10 @@ __global__ __launch_bounds__(TPB) void nxg_enc_rows_kernel(
             }
             // queue_send refuses a message longer than MAX_BATCH (channel.rs:178-181); that bound
             // also keeps the 32-bit staged lengths exact
-            const uint64_t ml = err ? 0ull : lwlen(1 + vl64(c.id[r]) + vlen);
-            if (!err && ml > 0x3FFFFFFFull) err = NXG_TOO_BIG;
+            const uint64_t ml = err    ? 0ull
+                                : arch ? vl64((uint32_t)c.id[r]) + vlen
+                                       : lwlen(1 + vl64(c.id[r]) + vlen);
+            if (!err && ml > (arch ? 0xFFFFFFFFull : 0x3FFFFFFFull)) err = NXG_TOO_BIG;
             if (err) atomicMax(&st->err_kind, err);
             len_lds[rl] = err ? 0u : (uint32_t)ml;
         }
@@ -420,7 +429,7 @@ __global__ __launch_bounds__(TPB) void nxg_enc_rows_kernel(
             if (lane == 0) sh_base = base;
         }
         __syncthreads();
-        const uint64_t tbase = sh_base;
+        const uint64_t tbase = sh_base + arch_base;
         const uint32_t phase = (uint32_t)(tbase & 15u);
         const bool staged = out && c.n_ctl == 0 && phase + tot <= (uint64_t)(GSTG - 16) &&
                             tbase + tot <= cap;
@@ -432,7 +441,7 @@ __global__ __launch_bounds__(TPB) void nxg_enc_rows_kernel(
 #pragma unroll
                 for (int k = 0; k < GRPT; k++) {
                     off_lds[tid * GRPT + k] = (uint16_t)o;
-                    if (tbase <= kMaxBatch && kMaxBatch < tbase + tot)
+                    if (!arch && tbase <= kMaxBatch && kMaxBatch < tbase + tot)
                         note_split(st, tbase + off + (o - phase - (uint32_t)off), L[k]);
                     o += (uint32_t)L[k];
                 }
@@ -444,9 +453,13 @@ __global__ __launch_bounds__(TPB) void nxg_enc_rows_kernel(
                 if (!len) continue;
                 const uint64_t r = rt + rl;
                 Out w{stg, off_lds[rl]};
-                w.var(len);
-                w.b(4);
-                w.var(c.id[r]);
+                if (arch) {
+                    w.var((uint32_t)c.id[r]);
+                } else {
+                    w.var(len);
+                    w.b(4);
+                    w.var(c.id[r]);
+                }
                 switch (cls_lds[rl]) {
                 case CLS_FIX8: {
                     const Slot v = get_slot(c, true, r);
@@ -502,14 +515,18 @@ __global__ __launch_bounds__(TPB) void nxg_enc_rows_kernel(
                 if (r < n && L[k] && out) {
                     uint64_t pos = rpos;
                     if (c.n_ctl) pos += ctl_pre[ctl_upto(c.ctl_row, c.n_ctl, r)];
-                    note_split(st, pos, L[k]);
+                    if (!arch) note_split(st, pos, L[k]);
                     if (pos + L[k] > cap) {
                         atomicOr(&st->capacity, 1u);
                     } else {
                         Out w{out, pos};
-                        w.var(L[k]);
-                        w.b(4);
-                        w.var(c.id[r]);
+                        if (arch) {
+                            w.var((uint32_t)c.id[r]);
+                        } else {
+                            w.var(L[k]);
+                            w.b(4);
+                            w.var(c.id[r]);
+                        }
                         if (cls_lds[tid * GRPT + k] != CLS_GEN) row_write_flat(c, heap, r, w);
                         else value_write(c, heap, true, r, w);
                     }
@@ -518,7 +535,7 @@ __global__ __launch_bounds__(TPB) void nxg_enc_rows_kernel(
             }
         }
         if (tile == ntiles - 1 && tid == 0) {
-            st->total_bytes = sh_base + tot;  // rows only; ctl bytes added by the host
+            st->total_bytes = sh_base + tot + arch_base;  // rows (+ archive header); ctl: host
             st->n_rows = n;
         }
         __syncthreads();
@@ -550,7 +567,8 @@ uint64_t nxg_enc_general_tiles(uint64_t n) { return (n + GTILE - 1) / GTILE; }
 
 hipError_t nxg_launch_enc_general(const ColsDesc& cd, const uint8_t* heap, uint8_t* out,
                                   uint64_t cap, uint64_t* scratch, uint64_t* tstat,
-                                  uint32_t epoch, DevStatus* st, int grid, hipStream_t s) {
+                                  uint32_t epoch, DevStatus* st, int grid, hipStream_t s,
+                                  uint64_t arch_base) {
     // scratch layout: ctl_pre[n_ctl + 1] | row_off[n_rows]  (only when n_ctl > 0)
     uint64_t* ctl_pre = scratch;
     uint64_t* row_off = cd.n_ctl ? scratch + cd.n_ctl + 1 : nullptr;
@@ -559,7 +577,8 @@ hipError_t nxg_launch_enc_general(const ColsDesc& cd, const uint8_t* heap, uint8
     if (nt) {
         const uint64_t g = grid <= 0 ? nt : (nt < (uint64_t)grid ? nt : (uint64_t)grid);
         hipLaunchKernelGGL(nxg_enc_rows_kernel, dim3(g), dim3(TPB), 0, s, cd, heap, out, cap,
-                           cd.n_ctl ? ctl_pre : nullptr, row_off, tstat, (uint32_t)nt, epoch, st, nxg_take_zero_slot());
+                           cd.n_ctl ? ctl_pre : nullptr, row_off, tstat, (uint32_t)nt, epoch, st, nxg_take_zero_slot(),
+                           arch_base);
     }
     if (cd.n_ctl && out) {
         const uint64_t nb = (cd.n_ctl + TPB - 1) / TPB;

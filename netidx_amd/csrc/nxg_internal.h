@@ -41,6 +41,8 @@ constexpr int kEpochShift = 44;
 constexpr uint64_t kEpochMax = (1ull << 18) - 1;
 constexpr uint64_t kValMask = (1ull << kEpochShift) - 1;
 constexpr uint64_t kMaxBatch = 0x3FFFFFFF;  // MAX_BATCH, netidx/src/channel.rs:34
+constexpr uint64_t kMaxVecBytes = 2ull * 1024 * 1024 * 1024;  // MAX_VEC, pack.rs:917
+constexpr uint64_t kBatchItemSize = 24;  // size_of::<BatchItem>() (logfile/mod.rs:188; unpinned)
 // encode: note the message [pos, pos + len) if it holds byte MAX_BATCH (exactly one does, in a
 // frame longer than MAX_BATCH)
 __device__ inline void note_split(DevStatus* st, uint64_t pos, uint64_t len) {
@@ -134,9 +136,11 @@ hipError_t nxg_launch_enc_f64(const uint64_t* id, const uint64_t* val, uint64_t 
                               uint64_t cap, uint64_t* tstat, uint32_t epoch, DevStatus* st,
                               int grid, hipStream_t s);
 uint64_t nxg_enc_general_tiles(uint64_t n);  // tiles (and tstat words) of a general encode
+// arch_base > 0: archive-batch rows after an arch_base-byte count header (nxg_encode_general.hip)
 hipError_t nxg_launch_enc_general(const ColsDesc& cols, const uint8_t* heap, uint8_t* out,
                                   uint64_t cap, uint64_t* scratch, uint64_t* tstat,
-                                  uint32_t epoch, DevStatus* st, int grid, hipStream_t s);
+                                  uint32_t epoch, DevStatus* st, int grid, hipStream_t s,
+                                  uint64_t arch_base = 0);
 // general decode: count + resolve + emit + fix. `lws` holds nxg_dec_gen_scratch_bytes(W) bytes
 // (64 u32 lane words per tile, then the emit pass's work list), `runs` gdec2::MAX_RUNS *
 // RUN_WORDS u64, `base` gdec2::MAX_RUNS * 4 u64; none needs zeroing.

@@ -196,3 +196,24 @@ def test_archive_capacity(codec):
     assert st.err_kind == 7
     cols, st, used = gpu_decode(codec, buf, cap_rows=10_000)
     assert st.err_kind == 0 and st.n_rows == 10_000
+
+
+@pytest.mark.parametrize("n", [0, 1, 1000, 1_000_000])
+def test_archive_encode_vs_oracle(codec, n):
+    """nxg_encode_archive_batch (<Vec<BatchItem> as Pack>::encode, pack.rs:941-952) byte-identical
+    to the oracle's encoder, and decoded back to the same columns."""
+    import torch
+    import netidx_amd
+    from netidx_amd import synth
+    m = synth.archive_columns(max(n, 1), seed=200 + n % 89)
+    if n == 0:
+        m = type(m)(m.id[:0], m.tag[:0], m.fixed[:0], m.aux[:0], m.ctag[:0], m.cfixed[:0],
+                    m.caux[:0], m.heap)
+    ref = archive_bytes(m)
+    cols = netidx_amd.columns_from_arrays(m.id, m.fixed, m.tag, m.aux, m.ctag, m.cfixed, m.caux)
+    heap = torch.from_numpy(m.heap.copy()).cuda()
+    got = codec.encode_archive(cols, heap).cpu().numpy()
+    assert np.array_equal(got, ref)
+    if n:
+        st = assert_matches_oracle(codec, got)
+        assert st.n_rows == n
