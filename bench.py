@@ -456,69 +456,56 @@ def extras_single_gpu(codec, stream, steps, warmup):
         torch.cuda.empty_cache()
     except Exception as e:
         ex["decode_f64_1e7_host_pipelined"] = {"error": repr(e)}
-    # (b4) end to end through a loopback TCP socket: the publisher thread encodes on the GPU,
-    # copies the frame to host memory and sends it (flush_buf framing); the subscriber receives
-    # into a socket buffer, reassembles the frame (read_task logic, nxg_frame_reader_*) and
-    # decodes it from host memory (H2D + decode + D2H of the columns). Wall clock per frame.
+    # (b4) end to end through a loopback TCP socket, all in the library's C++ sessions
+    # (nxg_session_*): handshake + To::Subscribe / From::Subscribed, then per frame the publisher
+    # encodes on the GPU (nxg_encode_frames), copies to pinned memory and writes the frame; the
+    # subscriber reads the socket into a pinned buffer, copies the frame to the device and
+    # decodes it (device-resident columns). Wall clock per frame, F frames back to back.
     try:
-        import socket
         import threading
         n = 10_000_000
         cols, wire = make_f64_wire(codec, n, 0)
         W = wire.numel()
-        F = 3
+        F = 6
         pub = netidx_amd.Codec(0)
-        dwire = torch.empty(W + 64, dtype=torch.uint8, device="cuda")
-        hwire = torch.empty(W, dtype=torch.uint8).pin_memory()
-        hout = Columns(n, 0, 0, netidx_amd.LAYOUT_F64, "cpu")
-        srv = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
-        srv.bind(("127.0.0.1", 0))
-        srv.listen(1)
-        port = srv.getsockname()[1]
+        dout = Columns(n, 0, 0, netidx_amd.LAYOUT_F64, "cuda")
+        lst = netidx_amd.Session.listen()
+        res = {}
 
         def publisher():
-            c = socket.create_connection(("127.0.0.1", port))
-            c.setsockopt(socket.SOL_SOCKET, socket.SO_SNDBUF, 8 << 20)
-            for _ in range(F):
-                ln = pub.encode_async(cols, None, dwire.data_ptr(), dwire.numel())
-                pub.sync()
-                hwire[: ln.value].copy_(dwire[: ln.value])
-                c.sendall(netidx_amd.frame_header(ln.value))
-                c.sendall(memoryview(hwire.numpy())[: ln.value])
-            c.close()
+            try:
+                s = lst.accept()
+                netidx_amd.msg_parse(s.recv_frame(), to=True)
+                s.send(netidx_amd.msg_subscribed("/local/bench/0", 0, 16))
+                for _ in range(F):
+                    s.publish(pub, cols)
+                s.close()
+            except Exception as e:
+                res["err"] = repr(e)
 
         th = threading.Thread(target=publisher)
-        t0 = time.perf_counter()
         th.start()
-        conn, _ = srv.accept()
-        conn.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 8 << 20)
-        r = netidx_amd.FrameReader()
-        rbuf = bytearray(8 << 20)
-        frames = 0
-        while True:
-            k = conn.recv_into(rbuf)
-            if not k:
-                break
-            r.feed(rbuf, k)
-            while True:
-                v = r.next_view()
-                if v is None:
-                    break
-                st = codec.decode_into(v[0], v[1], hout)
-                assert st.path == 1 and st.n_rows == n
-                frames += 1
+        sub = netidx_amd.Session.connect("127.0.0.1", lst.port)
+        sub.send(netidx_amd.msg_subscribe("/local/bench/0"))
+        netidx_amd.msg_parse(sub.recv_frame())
+        sub.recv_decode(codec, dout)  # the first frame (buffers sized, pages touched)
+        t0 = time.perf_counter()
+        for _ in range(F - 1):
+            st, flen = sub.recv_decode(codec, dout)
+            assert st.path == 1 and st.n_rows == n and flen == W
+        dt = (time.perf_counter() - t0) / (F - 1)
         th.join()
-        dt = (time.perf_counter() - t0) / F
-        conn.close()
-        srv.close()
+        sub.close()
+        lst.close()
         pub.close()
-        assert frames == F and torch.equal(hout.fixed[:n], cols.fixed[:n].cpu())
+        assert "err" not in res, res.get("err")
+        assert torch.equal(dout.fixed[:n], cols.fixed[:n])
         ex["socket_e2e_f64_1e7"] = {
-            "records": n, "frames": F, "ms_per_frame": round(dt * 1e3, 2),
-            "M_updates_s": round(n / dt / 1e6, 1),
-            "path": "GPU encode -> D2H -> TCP loopback -> frame reassembly -> H2D -> GPU decode "
-                    "-> D2H columns"}
-        del cols, wire, dwire, hwire, hout
+            "records": n, "frames": F - 1, "frame_bytes": W, "ms_per_frame": round(dt * 1e3, 2),
+            "M_updates_s": round(n / dt / 1e6, 1), "GB_s_socket": round(W / dt / 1e9, 2),
+            "path": "C++ sessions: GPU encode -> D2H pinned -> TCP loopback -> pinned recv -> "
+                    "H2D -> GPU decode (device columns)"}
+        del cols, wire, dout
         torch.cuda.empty_cache()
     except Exception as e:
         ex["socket_e2e_f64_1e7"] = {"error": repr(e)}

@@ -333,6 +333,70 @@ bool nxg_decode_archive_batch(NxgCtx* ctx, const uint8_t* buf, uint64_t len, Nxg
 bool nxg_encode_archive_batch(NxgCtx* ctx, const NxgColumns* in, const uint8_t* heap,
                               uint8_t* out, uint64_t cap, uint64_t* len_out, NetidxError* err);
 
+/* ---- the publisher <-> subscriber connection (BASELINE configs[0]) ------------------------
+ * Replaces hello_publisher (netidx/src/subscriber/connection.rs:120-140), ClientCtx::hello
+ * (publisher/server.rs:367-381), read_task / flush_buf (channel.rs:107-126, 379-443) and the
+ * To::Subscribe -> From::Subscribed exchange (publisher/server.rs:60-137, 506-516), anonymous
+ * authentication only. Raw handshake messages are a u32 big-endian length + the packed value
+ * (channel.rs:63-105): u64 3 both ways, then Hello::Anonymous both ways. After the handshake
+ * the connection is a Channel of frames (nxg_frame_header) holding len-wrapped messages.
+ * Sessions are blocking sockets; one thread per session. */
+typedef struct NxgSession NxgSession;
+/* subscriber side: connect and run the handshake */
+NxgSession* nxg_session_connect(const char* ipv4, uint16_t port, NetidxError* err);
+/* publisher side: a listening socket (port 0: any; *bound_port receives it), then one accepted,
+ * handshaken connection per nxg_session_accept */
+NxgSession* nxg_session_listen(const char* ipv4, uint16_t port, uint16_t* bound_port,
+                               NetidxError* err);
+NxgSession* nxg_session_accept(NxgSession* listener, NetidxError* err);
+void nxg_session_close(NxgSession* s);
+/* frames_in, bytes_in, frames_out, bytes_out */
+void nxg_session_stats(const NxgSession* s, uint64_t out[4]);
+/* one frame out: u32 header (channel.rs:107-126) + payload (<= MAX_BATCH) */
+bool nxg_session_send(NxgSession* s, const uint8_t* payload, uint64_t len, NetidxError* err);
+/* the next complete frame in (read_task, channel.rs:379-443): *payload stays valid until the
+ * next receive on this session; encrypted frames are refused */
+bool nxg_session_recv_frame(NxgSession* s, const uint8_t** payload, uint64_t* len,
+                            NetidxError* err);
+/* the data path, subscriber side: the next frame, read into page-locked memory, decoded on the
+ * device into `out` as nxg_decode_updates does (status, flags likewise) */
+bool nxg_session_recv_decode(NxgSession* s, NxgCtx* ctx, NxgColumns* out, uint32_t flags,
+                             NxgStatus* status, uint64_t* frame_len, NetidxError* err);
+/* the data path, publisher side: device columns encoded on the GPU (nxg_encode_frames: the
+ * MAX_BATCH cuts), copied to page-locked memory and written as frames */
+bool nxg_session_publish(NxgSession* s, NxgCtx* ctx, const NxgColumns* cols, const uint8_t* heap,
+                         uint64_t* bytes_sent, NetidxError* err);
+/* Control messages (len-wrapped derived enums, netidx-derive lib.rs:289-381). Builders return
+ * the message length (out NULL: the length only) or -NXG_CAPACITY / -NXG_UNKNOWN_TAG. */
+/* To::Subscribe { path, resolver: SocketAddr::V4, timestamp, permissions, token }
+ * (netproto publisher.rs:57-63) */
+int64_t nxg_msg_subscribe(const char* path, uint64_t path_len, uint32_t resolver_ipv4,
+                          uint16_t resolver_port, uint64_t timestamp, uint32_t permissions,
+                          const uint8_t* token, uint64_t token_len, uint8_t* out, uint64_t cap);
+/* From::Subscribed(path, id, value) with a scalar value (tag/fixed/aux as NxgColumns; String and
+ * Bytes bytes at `text`) */
+int64_t nxg_msg_subscribed(const char* path, uint64_t path_len, uint64_t id, uint8_t tag,
+                           uint64_t fixed, uint32_t aux, const uint8_t* text, uint8_t* out,
+                           uint64_t cap);
+/* From::Heartbeat (2 bytes) */
+int64_t nxg_msg_heartbeat(uint8_t* out, uint64_t cap);
+/* One control message parsed: to = 0 a publisher::From, 1 a publisher::To. Offsets index `buf`.
+ * value_fixed holds scalar payloads as read (big-endian integers, varints as decoded, zigzag
+ * not undone); other values are reported by tag and span. */
+typedef struct NxgCtlMsg {
+    uint64_t msg_len; /* the message's bytes (len-wrapped region) */
+    uint32_t variant;
+    uint32_t permissions;
+    uint64_t id;
+    uint64_t path_off, path_len;
+    uint64_t timestamp;
+    uint64_t token_off, token_len;
+    uint64_t value_off, value_len; /* the value's bytes, tag included */
+    uint64_t value_fixed;
+    uint32_t value_tag, value_aux;
+} NxgCtlMsg;
+bool nxg_msg_parse(const uint8_t* buf, uint64_t len, int to, NxgCtlMsg* m, NetidxError* err);
+
 /* ---- host framing (netidx/src/channel.rs) ------------------------------------------------
  * Frame boundaries exactly as WriteChannel::queue_send/try_flush split the buffer. The split
  * happens at MAX_BATCH = 0x3FFFFFFF (channel.rs:34, 187-191) and is recorded between messages.

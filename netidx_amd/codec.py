@@ -97,6 +97,14 @@ class NxgPubTable(C.Structure):
                 ("cur_caux", C.c_void_p)]
 
 
+class NxgCtlMsg(C.Structure):
+    _fields_ = [("msg_len", C.c_uint64), ("variant", C.c_uint32), ("permissions", C.c_uint32),
+                ("id", C.c_uint64), ("path_off", C.c_uint64), ("path_len", C.c_uint64),
+                ("timestamp", C.c_uint64), ("token_off", C.c_uint64), ("token_len", C.c_uint64),
+                ("value_off", C.c_uint64), ("value_len", C.c_uint64), ("value_fixed", C.c_uint64),
+                ("value_tag", C.c_uint32), ("value_aux", C.c_uint32)]
+
+
 class NxgStatus(C.Structure):
     _fields_ = [
         ("n_rows", C.c_uint64), ("n_children", C.c_uint64), ("n_ctl", C.c_uint64),
@@ -161,6 +169,28 @@ SIGNATURES = {
     "nxg_encode_archive_batch": (C.c_bool, [C.c_void_p, C.POINTER(NxgColumns), C.c_void_p,
                                             C.c_void_p, C.c_uint64, C.POINTER(C.c_uint64),
                                             C.POINTER(NetidxError)]),
+    "nxg_session_connect": (C.c_void_p, [C.c_char_p, C.c_uint16, C.POINTER(NetidxError)]),
+    "nxg_session_listen": (C.c_void_p, [C.c_char_p, C.c_uint16, C.POINTER(C.c_uint16),
+                                        C.POINTER(NetidxError)]),
+    "nxg_session_accept": (C.c_void_p, [C.c_void_p, C.POINTER(NetidxError)]),
+    "nxg_session_close": (None, [C.c_void_p]),
+    "nxg_session_stats": (None, [C.c_void_p, C.POINTER(C.c_uint64)]),
+    "nxg_session_send": (C.c_bool, [C.c_void_p, C.c_void_p, C.c_uint64, C.POINTER(NetidxError)]),
+    "nxg_session_recv_frame": (C.c_bool, [C.c_void_p, C.POINTER(C.c_void_p),
+                                          C.POINTER(C.c_uint64), C.POINTER(NetidxError)]),
+    "nxg_session_recv_decode": (C.c_bool, [C.c_void_p, C.c_void_p, C.POINTER(NxgColumns),
+                                           C.c_uint32, C.POINTER(NxgStatus),
+                                           C.POINTER(C.c_uint64), C.POINTER(NetidxError)]),
+    "nxg_session_publish": (C.c_bool, [C.c_void_p, C.c_void_p, C.POINTER(NxgColumns), C.c_void_p,
+                                       C.POINTER(C.c_uint64), C.POINTER(NetidxError)]),
+    "nxg_msg_subscribe": (C.c_int64, [C.c_char_p, C.c_uint64, C.c_uint32, C.c_uint16, C.c_uint64,
+                                      C.c_uint32, C.c_void_p, C.c_uint64, C.c_void_p,
+                                      C.c_uint64]),
+    "nxg_msg_subscribed": (C.c_int64, [C.c_char_p, C.c_uint64, C.c_uint64, C.c_uint8, C.c_uint64,
+                                       C.c_uint32, C.c_void_p, C.c_void_p, C.c_uint64]),
+    "nxg_msg_heartbeat": (C.c_int64, [C.c_void_p, C.c_uint64]),
+    "nxg_msg_parse": (C.c_bool, [C.c_void_p, C.c_uint64, C.c_int, C.POINTER(NxgCtlMsg),
+                                 C.POINTER(NetidxError)]),
     "nxg_frame_reader_new": (C.c_void_p, [C.POINTER(NetidxError)]),
     "nxg_frame_reader_free": (None, [C.c_void_p]),
     "nxg_frame_reader_push": (C.c_bool, [C.c_void_p, C.c_void_p, C.c_uint64,
@@ -660,6 +690,116 @@ class FrameReader:
 
     def buffered(self):
         return lib().nxg_frame_reader_buffered(self.r)
+
+
+def _msg(fn, *args):
+    n = fn(*args, None, 0)
+    if n < 0:
+        raise CodecError(f"message builder failed ({-n})")
+    out = (C.c_uint8 * max(n, 1))()
+    m = fn(*args, out, n)
+    assert m == n
+    return bytes(out[:n])
+
+
+def msg_subscribe(path, timestamp=0, permissions=0, token=b"", resolver=(0, 0)):
+    """To::Subscribe (netproto publisher.rs:57-63) as one len-wrapped message."""
+    p = path.encode() if isinstance(path, str) else path
+    tok = (C.c_uint8 * max(len(token), 1)).from_buffer_copy(token + b"\0")
+    return _msg(lib().nxg_msg_subscribe, p, len(p), resolver[0], resolver[1], timestamp,
+                permissions, tok, len(token))
+
+
+def msg_subscribed(path, id, tag, fixed=0, aux=0, text=b""):
+    """From::Subscribed(path, id, scalar value)."""
+    p = path.encode() if isinstance(path, str) else path
+    t = (C.c_uint8 * max(len(text), 1)).from_buffer_copy(text + b"\0")
+    return _msg(lib().nxg_msg_subscribed, p, len(p), id, tag, fixed, aux, t)
+
+
+def msg_heartbeat():
+    return _msg(lib().nxg_msg_heartbeat)
+
+
+def msg_parse(buf, to=False):
+    """Parse one control message (publisher::From, or To with to=True); returns NxgCtlMsg."""
+    b = bytes(buf)
+    a = (C.c_uint8 * max(len(b), 1)).from_buffer_copy(b + b"\0")
+    m, err = NxgCtlMsg(), NetidxError()
+    _check(lib().nxg_msg_parse(a, len(b), 1 if to else 0, C.byref(m), C.byref(err)), err)
+    return m
+
+
+class Session:
+    """One publisher<->subscriber connection (nxg_session_*, include/nxg_codec.h): the handshake,
+    frames, the device data path. Blocking; use one thread per session."""
+
+    def __init__(self, handle):
+        self.h = handle
+
+    @classmethod
+    def connect(cls, ip, port):
+        err = NetidxError()
+        h = lib().nxg_session_connect(ip.encode(), port, C.byref(err))
+        _check(bool(h), err)
+        return cls(h)
+
+    @classmethod
+    def listen(cls, ip="127.0.0.1", port=0):
+        err, bp = NetidxError(), C.c_uint16(0)
+        h = lib().nxg_session_listen(ip.encode(), port, C.byref(bp), C.byref(err))
+        _check(bool(h), err)
+        s = cls(h)
+        s.port = bp.value
+        return s
+
+    def accept(self):
+        err = NetidxError()
+        h = lib().nxg_session_accept(self.h, C.byref(err))
+        _check(bool(h), err)
+        return Session(h)
+
+    def close(self):
+        if self.h:
+            lib().nxg_session_close(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def stats(self):
+        a = (C.c_uint64 * 4)()
+        lib().nxg_session_stats(self.h, a)
+        return dict(zip(("frames_in", "bytes_in", "frames_out", "bytes_out"), list(a)))
+
+    def send(self, payload):
+        b = bytes(payload)
+        a = (C.c_uint8 * max(len(b), 1)).from_buffer_copy(b + b"\0")
+        err = NetidxError()
+        _check(lib().nxg_session_send(self.h, a, len(b), C.byref(err)), err)
+
+    def recv_frame(self):
+        """The next frame's payload (a copy)."""
+        p, n, err = C.c_void_p(), C.c_uint64(), NetidxError()
+        _check(lib().nxg_session_recv_frame(self.h, C.byref(p), C.byref(n), C.byref(err)), err)
+        return C.string_at(p.value, n.value) if n.value else b""
+
+    def recv_decode(self, codec, cols, flags=0):
+        """The next frame decoded on the device; returns (NxgStatus, frame length)."""
+        st, n, err = NxgStatus(), C.c_uint64(), NetidxError()
+        _check(lib().nxg_session_recv_decode(self.h, codec.ctx, C.byref(cols.s), flags,
+                                             C.byref(st), C.byref(n), C.byref(err)), err)
+        return st, n.value
+
+    def publish(self, codec, cols, heap=None):
+        """Device columns encoded on the GPU and written as frames; returns the bytes sent."""
+        n, err = C.c_uint64(), NetidxError()
+        _check(lib().nxg_session_publish(self.h, codec.ctx, C.byref(cols.s), _heap_ptr(heap),
+                                         C.byref(n), C.byref(err)), err)
+        return n.value
 
 
 def range_link(ranges, frame_len):

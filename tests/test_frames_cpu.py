@@ -58,39 +58,147 @@ def test_reader_rejects_encrypted_frames():
         next(it)
 
 
-def test_config1_loopback_one_f64_path():
-    """simple_publisher / simple_subscriber (BASELINE configs[0]) reduced to the data path: the
-    publisher sends From::Update(Id(0), F64(x)) for a series of values, one batch per update, as
-    flush_buf frames them; the subscriber reassembles frames with read_task's logic and decodes."""
-    vals = [1.0, -0.0, 2.5, float("inf"), 1e-300, 3.25]
+VERSION_RAW = bytes.fromhex("00000008" "0000000000000003")  # write_raw(&3u64), channel.rs:63-80
+HELLO_ANON_RAW = bytes.fromhex("00000002" "0200")          # Hello::Anonymous: lw(1)=2, variant 0
+
+
+def recv_exact(c, n):
+    b = b""
+    while len(b) < n:
+        k = c.recv(n - len(b))
+        assert k, "connection closed"
+        b += k
+    return b
+
+
+def test_handshake_bytes_subscriber_side():
+    """A hand-written publisher (the bytes of ClientCtx::hello, publisher/server.rs:367-381)
+    against the library's subscriber (hello_publisher, subscriber/connection.rs:120-140)."""
     srv = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
     srv.bind(("127.0.0.1", 0))
     srv.listen(1)
     port = srv.getsockname()[1]
+    got = {}
 
     def publisher():
-        c = socket.create_connection(("127.0.0.1", port))
-        for v in vals:
-            bits = np.array([struct.unpack("<Q", struct.pack("<d", v))[0]], np.uint64)
-            wire = nxo.encode_f64(np.array([0], np.uint64), bits).tobytes()
-            c.sendall(netidx_amd.frame_header(len(wire)) + wire)
+        c, _ = srv.accept()
+        c.sendall(VERSION_RAW)
+        got["version"] = recv_exact(c, 12)
+        got["hello"] = recv_exact(c, 6)
+        c.sendall(HELLO_ANON_RAW)
+        # the channel: the subscriber's first frame is To::Subscribe
+        n = struct.unpack(">I", recv_exact(c, 4))[0]
+        got["subscribe"] = recv_exact(c, n)
         c.close()
 
     t = threading.Thread(target=publisher)
     t.start()
-    conn, _ = srv.accept()
-    r = netidx_amd.FrameReader()
-    got = []
-    while True:
-        data = conn.recv(7)  # small reads: frames arrive in pieces
-        if not data:
-            break
-        r.feed(data)
-        for f in r.frames():
-            d = nxo.decode(f)
-            assert d.s.err_kind == 0 and d.s.n_rows == 1 and d.id[0] == 0
-            got.append(struct.unpack("<d", struct.pack("<Q", int(d.fixed[0])))[0])
+    s = netidx_amd.Session.connect("127.0.0.1", port)
+    s.send(netidx_amd.msg_subscribe("/foo/bar", timestamp=7, permissions=3))
     t.join()
-    conn.close()
+    s.close()
     srv.close()
-    assert [struct.pack("<d", x) for x in got] == [struct.pack("<d", x) for x in vals]
+    assert got["version"] == VERSION_RAW and got["hello"] == HELLO_ANON_RAW
+    # To::Subscribe {path, resolver V4 0.0.0.0:0, timestamp u64, permissions u32, token Bytes}
+    body = (b"\x00" + b"\x08/foo/bar" + b"\x00" + bytes(6) + struct.pack(">QI", 7, 3) + b"\x00")
+    assert got["subscribe"] == bytes([len(body) + 1]) + body
+    m = netidx_amd.msg_parse(got["subscribe"], to=True)
+    assert (m.variant, m.timestamp, m.permissions, m.path_len) == (0, 7, 3, 8)
+
+
+def test_handshake_bytes_publisher_side():
+    """A hand-written subscriber against the library's publisher: the version and Hello bytes,
+    and a Hello other than Anonymous refused."""
+    lst = netidx_amd.Session.listen()
+    res = {}
+
+    def accept():
+        try:
+            res["s"] = lst.accept()
+        except netidx_amd.CodecError as e:
+            res["err"] = str(e)
+
+    for hello, ok in ((HELLO_ANON_RAW, True), (bytes.fromhex("00000002" "0202"), False)):
+        res.clear()
+        t = threading.Thread(target=accept)
+        t.start()
+        c = socket.create_connection(("127.0.0.1", lst.port))
+        assert recv_exact(c, 12) == VERSION_RAW
+        c.sendall(VERSION_RAW + hello)
+        if ok:
+            assert recv_exact(c, 6) == HELLO_ANON_RAW
+        t.join()
+        c.close()
+        if ok:
+            res["s"].close()
+        else:
+            assert "not supported" in res["err"]
+    lst.close()
+
+
+def test_control_messages():
+    """From::Subscribed / Heartbeat built and parsed by the library; every byte derived from the
+    derive rules (lib.rs:289-381) and Value::encode (value lib.rs:361-468)."""
+    m = netidx_amd.msg_subscribed("/a", 5, 9, struct.unpack("<Q", struct.pack("<d", 1.5))[0])
+    # body: variant 1 + path 3 + id 1 + value 9 = 14 bytes; lw(14) = 15
+    assert m == bytes([15, 3, 2]) + b"/a" + b"\x05\x09" + struct.pack(">d", 1.5)
+    p = netidx_amd.msg_parse(m)
+    assert (p.variant, p.id, p.value_tag, p.path_off, p.path_len) == (3, 5, 9, 3, 2)
+    assert struct.pack(">Q", p.value_fixed) == struct.pack(">d", 1.5)
+    assert netidx_amd.msg_heartbeat() == b"\x02\x05"
+    assert netidx_amd.msg_parse(b"\x02\x05").variant == 5
+    s = netidx_amd.msg_subscribed("/s", 1, 12, 0, 3, b"abc")
+    p = netidx_amd.msg_parse(s)
+    assert p.value_tag == 12 and s[p.value_fixed:p.value_fixed + p.value_aux] == b"abc"
+    # agrees with the oracle's decode of the same message as a control span
+    d = nxo.decode(m).trim()
+    assert len(d["ctl_variant"]) == 1 and d["ctl_variant"][0] == 3 and d["ctl_len"][0] == len(m)
+
+
+def test_config1_loopback_one_f64_path():
+    """simple_publisher / simple_subscriber (BASELINE configs[0], examples/examples/
+    simple_publisher.rs:21-47) over loopback TCP through the library's sessions: handshake,
+    To::Subscribe, From::Subscribed with the current value, then one From::Update per value and
+    Heartbeats, each in its own frame. No GPU in this config: the update payloads are made by the
+    oracle encoder (test infrastructure) and checked two ways, by the library's message parser
+    and by the oracle's decode."""
+    vals = [1.0, -0.0, 2.5, float("inf"), 1e-300, 3.25]
+    bits = [struct.unpack("<Q", struct.pack("<d", v))[0] for v in vals]
+    lst = netidx_amd.Session.listen()
+    done = {}
+
+    def publisher():
+        s = lst.accept()
+        sub = netidx_amd.msg_parse(s.recv_frame(), to=True)
+        done["path"] = sub.variant, sub.path_len
+        s.send(netidx_amd.msg_subscribed("/local/bench/0", 0, 9, bits[0]))
+        for k, b in enumerate(bits[1:]):
+            if k % 2:
+                s.send(netidx_amd.msg_heartbeat())
+            s.send(nxo.encode_f64(np.array([0], np.uint64), np.array([b], np.uint64)).tobytes())
+        done["stats"] = s.stats()
+        s.close()
+
+    t = threading.Thread(target=publisher)
+    t.start()
+    sub = netidx_amd.Session.connect("127.0.0.1", lst.port)
+    sub.send(netidx_amd.msg_subscribe("/local/bench/0"))
+    first = netidx_amd.msg_parse(sub.recv_frame())
+    assert first.variant == 3 and first.id == 0 and first.value_tag == 9
+    got, hb = [first.value_fixed], 0
+    while len(got) < len(vals):
+        f = sub.recv_frame()
+        m = netidx_amd.msg_parse(f)
+        if m.variant == 5:
+            hb += 1
+            continue
+        assert m.variant == 4 and m.id == 0 and m.value_tag == 9 and m.msg_len == len(f)
+        d = nxo.decode(f).trim()
+        assert d["err_kind"] == 0 and int(d["fixed"][0]) == m.value_fixed
+        got.append(m.value_fixed)
+    t.join()
+    st = sub.stats()
+    sub.close()
+    lst.close()
+    assert got == bits and hb == 2 and done["path"] == (0, len("/local/bench/0"))
+    assert st["frames_in"] == len(vals) + hb and done["stats"]["frames_out"] == len(vals) + hb

@@ -57,3 +57,77 @@ def test_loopback_mixed_batches():
         assert torch.equal(cols.id[:n], mc.id[:n]) and torch.equal(cols.tag[:n], mc.tag[:n])
         frame = torch.from_numpy(np.frombuffer(f, np.uint8).copy()).cuda()
         assert sub.encode_batch(cols, frame).cpu().numpy().tobytes() == wire
+
+
+def _config1_pub(lst, pub, batches, heaps, res):
+    """The publisher side of a session: accept + handshake, To::Subscribe -> From::Subscribed,
+    then each batch of device columns encoded on the GPU and written as frames."""
+    import netidx_amd
+    try:
+        s = lst.accept()
+        m = netidx_amd.msg_parse(s.recv_frame(), to=True)
+        res["sub"] = (m.variant, m.path_len)
+        s.send(netidx_amd.msg_subscribed("/local/bench/0", 0, 16))
+        for cols, heap in zip(batches, heaps):
+            s.publish(pub, cols, heap)
+        res["stats"] = s.stats()
+        s.close()
+    except Exception as e:  # surfaced by the test
+        res["err"] = repr(e)
+
+
+@pytest.mark.parametrize("kind", ["f64", "mixed"])
+def test_session_end_to_end(kind):
+    """BASELINE configs[0]'s data path through the library only: nxg_session_* handshake and
+    subscription, nxg_session_publish (GPU encode -> pinned -> socket) and
+    nxg_session_recv_decode (socket -> pinned -> GPU decode). The decoded device columns equal the
+    generator's columns; each frame's bytes equal the oracle encoder's."""
+    import torch
+    import netidx_amd
+    import nxo
+    from netidx_amd import synth
+    from netidx_amd.codec import Columns
+    pub, sub = netidx_amd.Codec(0), netidx_amd.Codec(0)
+    batches, heaps, ref = [], [], []
+    for k in range(3):
+        n = 200_000 + 7 * k
+        if kind == "f64":
+            ids, vals = synth.f64_columns(n, 300 + k)
+            batches.append(netidx_amd.columns_from_arrays(ids, vals))
+            heaps.append(None)
+            ref.append((ids, vals, None))
+        else:
+            m = synth.mixed_columns(n, 400 + k)
+            batches.append(netidx_amd.columns_from_arrays(m.id, m.fixed, m.tag, m.aux, m.ctag,
+                                                          m.cfixed, m.caux))
+            heaps.append(torch.from_numpy(m.heap.copy()).cuda())
+            ref.append((m.id, m.fixed, m))
+    lst = netidx_amd.Session.listen()
+    res = {}
+    t = threading.Thread(target=_config1_pub, args=(lst, pub, batches, heaps, res))
+    t.start()
+    s = netidx_amd.Session.connect("127.0.0.1", lst.port)
+    s.send(netidx_amd.msg_subscribe("/local/bench/0"))
+    first = netidx_amd.msg_parse(s.recv_frame())
+    assert first.variant == 3 and first.value_tag == 16
+    for k, (ids, vals, m) in enumerate(ref):
+        n = len(ids)
+        layout = netidx_amd.LAYOUT_F64 if m is None else netidx_amd.LAYOUT_MIXED
+        out = Columns(n + 1, (len(m.ctag) + 1) if m is not None else 0, 1, layout, "cuda")
+        st, flen = s.recv_decode(sub, out, 0 if m is None else netidx_amd.HINT_MIXED)
+        assert st.err_kind == 0 and st.n_rows == n
+        g = out.numpy()
+        assert np.array_equal(g["id"][:n], ids)
+        if m is None:
+            assert np.array_equal(g["fixed"][:n], vals)
+            assert flen == len(nxo.encode_f64(ids, vals))
+        else:
+            assert np.array_equal(g["tag"][:n], m.tag)
+            assert np.array_equal(g["ctag"][:len(m.ctag)], m.ctag)
+            plain = (m.tag != 12) & (m.tag != 19)
+            assert np.array_equal(g["fixed"][:n][plain], m.fixed[plain])
+    t.join()
+    s.close()
+    lst.close()
+    assert "err" not in res, res.get("err")
+    assert res["sub"] == (0, len("/local/bench/0")) and res["stats"]["frames_out"] == 4
