@@ -1096,16 +1096,26 @@ bool nxg_publish_commit(NxgCtx* c, const NxgPubTable* tab, const NxgColumns* bat
     const NxgPubBatch b{batch->id,    batch->tag,   batch->fixed, batch->aux, batch->ctag,
                         batch->cfixed, batch->caux, heap,         kind,       n};
     HIPCHK(nxg_launch_pub_stage1(*tab, b, c->dscratch, c->stream));
-    uint32_t flags[3] = {0, 0, 0};
+    uint32_t flags[4] = {0, 0, 0, 0};
     HIPCHK(hipMemcpyAsync(flags, nxg_pub_flags(c->dscratch), 12, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     const uint8_t* mode = nullptr;
     HIPCHK(nxg_launch_pub_stage2(*tab, b, c->dscratch, flags[0] != 0, flags[1] != 0, c->ncu,
                                  c->stream, &mode));
     if (flags[1]) {
-        HIPCHK(hipMemcpyAsync(&flags[2], nxg_pub_flags(c->dscratch) + 2, 4, hipMemcpyDeviceToHost,
+        uint32_t f23[2] = {0, 0};
+        HIPCHK(hipMemcpyAsync(f23, nxg_pub_flags(c->dscratch) + 2, 8, hipMemcpyDeviceToHost,
                               c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
+        if (f23[1]) {  // Decimal / container / Abstract comparisons: the stack-walk kernel
+            const uint32_t* prev =
+                flags[0] ? nxg_pub_prev(c->dscratch, n, tab->n_slots) : nullptr;
+            HIPCHK(nxg_launch_pub_deep(*tab, b, c->dscratch, prev, c->ncu, c->stream));
+            HIPCHK(hipMemcpyAsync(f23, nxg_pub_flags(c->dscratch) + 2, 4, hipMemcpyDeviceToHost,
+                                  c->stream));
+            HIPCHK(hipStreamSynchronize(c->stream));
+        }
+        flags[2] = f23[0];
         if (flags[2]) {
             set_err(err, "NXG_UNSUPPORTED: an UpdateChanged compares values nested deeper than "
                          "%d levels, or a container whose columns have no children",

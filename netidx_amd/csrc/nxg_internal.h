@@ -181,6 +181,11 @@ const uint32_t* nxg_pub_flags(uint8_t* scratch);
 hipError_t nxg_launch_pub_stage2(const NxgPubTable& tb, const NxgPubBatch& b, uint8_t* scratch,
                                  bool dup, bool changed, int ncu, hipStream_t s,
                                  const uint8_t** mode_out);
+// stage 3, when flags[3] is set: the UpdateChanged comparisons that need the stack walk
+// (prev_used: nxg_pub_prev(scratch) if stage 2 sorted, else null)
+hipError_t nxg_launch_pub_deep(const NxgPubTable& tb, const NxgPubBatch& b, uint8_t* scratch,
+                               const uint32_t* prev_used, int ncu, hipStream_t s);
+const uint32_t* nxg_pub_prev(uint8_t* scratch, uint64_t n, uint64_t n_slots);
 // exclusive sums of M u32 counts into u64 offsets (nxg_publish.hip); bsum: M / 4096 + 2 words
 hipError_t nxg_scan_u32(const uint32_t* hist, uint64_t M, uint64_t* off, uint64_t* bsum,
                         hipStream_t s);

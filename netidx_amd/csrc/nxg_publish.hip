@@ -209,7 +209,8 @@ NXG_DEV uint32_t slot_of(const NxgPubTable& tb, uint64_t x) {
 }  // namespace
 
 // flags[0]: some slot occurs twice among the non-directed rows; flags[1]: UpdateChanged rows
-// exist; flags[2]: a value nested deeper than MAX_DEPTH, or a container without child columns
+// exist; flags[2]: a value nested deeper than MAX_DEPTH, or a container without child columns;
+// flags[3]: some UpdateChanged row compares a Decimal, container or Abstract (nxg_pub_deep_kernel)
 __global__ __launch_bounds__(TPB) void nxg_pub_count_kernel(NxgPubTable tb, PubIn in,
                                                             uint32_t* __restrict__ cnt,
                                                             uint32_t* __restrict__ flags) {
@@ -309,31 +310,63 @@ __global__ __launch_bounds__(TPB) void nxg_pub_prev_kernel(const uint32_t* __res
 }
 
 // routing of every row (nxg_dispatch.hip Route): 0 through the slot, 1 not pushed, 2 one client
+// the comparison of UpdateChanged row i: 1 equal, 0 different, -1 too deep; 2 (DEEP) when a
+// side is a Decimal, container or Abstract and `deep` is false (left to nxg_pub_deep_kernel, so
+// that this kernel needs no stack)
+constexpr int DEEP = 2;
+template <bool ALLOW_DEEP>
+NXG_DEV int changed_eq(const NxgPubTable& tb, const PubIn& in, const uint32_t* prev, uint64_t i,
+                       uint32_t s) {
+    const uint32_t j = prev ? prev[i] : NONE;
+    const VSrc cur{tb.cur_tag, tb.cur_fixed, tb.cur_aux, tb.cur_ctag, tb.cur_cfixed, tb.cur_caux,
+                   tb.cur_heap};
+    const VSrc& A = j != NONE ? in.v : cur;
+    const uint64_t ia = j != NONE ? j : s;
+    const uint32_t ta = A.tag ? A.tag[ia] : 9u, tb_ = in.v.tag ? in.v.tag[i] : 9u;
+    if (heavy(ta) || heavy(tb_)) {
+        if (!ALLOW_DEEP) return DEEP;
+        return deep_eq(A, ia, in.v, i);
+    }
+    return scalar_eq(ta, A.fixed[ia], A.aux ? A.aux[ia] : 0u, A.heap, tb_, in.v.fixed[i],
+                     in.v.aux ? in.v.aux[i] : 0u, in.v.heap);
+}
+
+// routing of every row (nxg_dispatch.hip Route): 0 through the slot, 1 not pushed, 2 one client;
+// 3: an UpdateChanged whose comparison needs the stack walk (flags[3] set)
 __global__ __launch_bounds__(TPB) void nxg_pub_mode_kernel(NxgPubTable tb, PubIn in,
                                                            const uint32_t* __restrict__ prev,
                                                            uint8_t* __restrict__ mode,
                                                            uint32_t* __restrict__ flags) {
     const uint64_t i = (uint64_t)blockIdx.x * TPB + threadIdx.x;
-    if (i >= in.n) return;
-    const uint32_t kd = in.kind[i];
-    uint32_t m = kd == NXG_PUB_UPDATE_CLIENT ? 2u : 0u;
-    if (kd == NXG_PUB_UPDATE_CHANGED) {
-        const uint32_t s = slot_of(tb, in.id[i]);
-        if (s != NONE) {  // unpublished Ids stay 0: no slot, counted as unmatched
-            const uint32_t j = prev ? prev[i] : NONE;
-            int eq;
-            if (j != NONE) {
-                eq = val_eq(in.v, j, in.v, i);
-            } else {
-                const VSrc cur{tb.cur_tag, tb.cur_fixed, tb.cur_aux, tb.cur_ctag,
-                               tb.cur_cfixed, tb.cur_caux, tb.cur_heap};
-                eq = val_eq(cur, s, in.v, i);
+    bool deep = false;
+    if (i < in.n) {
+        const uint32_t kd = in.kind[i];
+        uint32_t m = kd == NXG_PUB_UPDATE_CLIENT ? 2u : 0u;
+        if (kd == NXG_PUB_UPDATE_CHANGED) {
+            const uint32_t s = slot_of(tb, in.id[i]);
+            if (s != NONE) {  // unpublished Ids stay 0: no slot, counted as unmatched
+                const int eq = changed_eq<false>(tb, in, prev, i, s);
+                deep = eq == DEEP;
+                m = deep ? 3u : eq > 0 ? 1u : 0u;
             }
-            if (eq < 0 && !ld_agent32(&flags[2])) atomicOr(&flags[2], 1u);
-            m = eq > 0 ? 1u : 0u;
         }
+        mode[i] = (uint8_t)m;
     }
-    mode[i] = (uint8_t)m;
+    if (__any(deep) && (threadIdx.x & 63) == 0 && !ld_agent32(&flags[3])) atomicOr(&flags[3], 1u);
+}
+
+// the rows left at mode 3: Value::eq with the stack walk (containers, Decimal, Abstract)
+__global__ __launch_bounds__(TPB) void nxg_pub_deep_kernel(NxgPubTable tb, PubIn in,
+                                                           const uint32_t* __restrict__ prev,
+                                                           uint8_t* __restrict__ mode,
+                                                           uint32_t* __restrict__ flags) {
+    for (uint64_t i = (uint64_t)blockIdx.x * TPB + threadIdx.x; i < in.n;
+         i += (uint64_t)gridDim.x * TPB) {
+        if (mode[i] != 3u) continue;
+        const int eq = changed_eq<true>(tb, in, prev, i, slot_of(tb, in.id[i]));
+        if (eq < 0 && !ld_agent32(&flags[2])) atomicOr(&flags[2], 1u);
+        mode[i] = eq > 0 ? 1u : 0u;
+    }
 }
 
 // ---- launch (host) ------------------------------------------------------------------------------
@@ -469,4 +502,21 @@ hipError_t nxg_launch_pub_stage2(const NxgPubTable& tb, const NxgPubBatch& b, ui
                        sc.flags);
     *mode_out = sc.mode;
     return hipGetLastError();
+}
+
+// Stage 3 (after the host read flags[3]): the comparisons that need the stack walk
+hipError_t nxg_launch_pub_deep(const NxgPubTable& tb, const NxgPubBatch& b, uint8_t* scratch,
+                               const uint32_t* prev_used, int ncu, hipStream_t s) {
+    PubScratch sc = pub_layout(scratch, b.n_rows, tb.n_slots);
+    const PubIn in{b.id, b.kind, b.n_rows, {b.tag, b.fixed, b.aux, b.ctag, b.cfixed, b.caux, b.heap}};
+    const uint64_t want = (b.n_rows + TPB - 1) / TPB;
+    const uint32_t g = (uint32_t)(want < (uint64_t)ncu * 16 ? want : (uint64_t)ncu * 16);
+    if (g)
+        hipLaunchKernelGGL(nxg_pub_deep_kernel, dim3(g), dim3(TPB), 0, s, tb, in, prev_used,
+                           sc.mode, sc.flags);
+    return hipGetLastError();
+}
+
+const uint32_t* nxg_pub_prev(uint8_t* scratch, uint64_t n, uint64_t n_slots) {
+    return pub_layout(scratch, n, n_slots).prev;
 }
