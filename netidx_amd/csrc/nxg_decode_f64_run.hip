@@ -400,6 +400,100 @@ NXG_DEV bool run_search(const uint8_t* __restrict__ wire, uint64_t W, uint64_t t
     return true;
 }
 
+// The probe's fast path for tile t (one lane): the entry, the run model (one or two runs of one
+// record length each, split where consecutive ids change width) and samples that confirm it.
+// state 0: the model holds (count, x set); 1: one length, the split not found (run_search);
+// 2: no unique entry or forced (exact path). `bad`: the frame cannot be decoded from here.
+NXG_DEV void probe_fast(const uint8_t* __restrict__ wire, uint64_t W, uint64_t t, uint32_t lim,
+                        bool first, uint32_t flags, int& state, uint32_t& e, uint32_t& L,
+                        uint32_t& L2, uint32_t& ks, uint32_t& count, uint32_t& x, bool& bad) {
+    const uint64_t t0 = t * T;
+    const uint64_t rem0 = W - t0;
+    uint32_t d[8];
+    ld32(wire, t0, W, d);
+    uint32_t cand = cand16(d[0], d[1], d[2], d[3], d[4]);
+    uint32_t V = 0;  // valid record starts (and the frame end) in [0, 16)
+    if (rem0 < 16) V |= 1u << rem0;
+    while (cand) {
+        const uint32_t s = __builtin_ctz(cand);
+        cand &= cand - 1;
+        uint32_t e0, e1, e2, e3;
+        extract16(d, s, e0, e1, e2, e3);
+        if (rec_check16(e0, e1, rem0 - s)) V |= 1u << s;
+    }
+    // the entry is the lowest valid start; the only other start allowed in the window is
+    // its successor (a record of <= 16 bytes leaves room for one more)
+    const uint32_t s1 = V ? (uint32_t)__builtin_ctz(V) : 32u;
+    uint32_t L1 = 0;
+    if (s1 < 16 && s1 != rem0) {
+        uint32_t e0, e1, e2, e3;
+        extract16(d, s1, e0, e1, e2, e3);
+        L1 = e0 & 0xffu;
+    }
+    const uint32_t p2 = s1 + L1;
+    if (t == 0 && first && !(V & 1u)) {
+        bad = true;
+    } else if (s1 < 16 && (s1 == rem0 || s1 >= lim)) {
+        // the frame (or the range) ends here: no record of this range starts in the tile
+        e = x = s1;
+        L = L2 = 12;
+    } else if (s1 < 16 && V == ((1u << s1) | (p2 < 16 ? 1u << p2 : 0u))) {
+        e = s1;
+        L = L2 = L1;
+        uint32_t n = (lim - e + L - 1) / L;
+        ks = n;
+        // Ids from the publisher's counter are consecutive (utils.rs:130-134): if the first
+        // id plus n crosses the next varint width, the tile is predicted as two runs split
+        // where the ids reach it.
+        uint64_t id0;
+        {
+            uint32_t e0, e1, e2, e3;
+            extract16(d, e, e0, e1, e2, e3);
+            uint64_t v0;
+            rec_decode16(e0, e1, e2, e3, L, id0, v0);
+            const uint32_t nb = L - 11u;
+            const uint64_t next = 1ull << (7u * nb);
+            if (nb < 5 && id0 < next && id0 + n > next) {
+                ks = (uint32_t)(next - id0);
+                L2 = L + 1;
+                const uint32_t q2 = e + ks * L;
+                n = ks + (lim - q2 + L2 - 1) / L2;
+            }
+        }
+        // the prediction's last record and both sides of the split must have the predicted
+        // lengths and ids (one HBM line per sample; the emit pass checks every record)
+        auto at = [&](uint32_t k) { return k < ks ? e + k * L : e + ks * L + (k - ks) * L2; };
+        auto len = [&](uint32_t k) { return k < ks ? L : L2; };
+        const uint32_t m = n - 1;
+        const uint32_t ke = ks < n ? ks - 1 : m, kf = ks < n ? ks : m;
+        // the three samples are independent: loaded together (one memory round trip)
+        uint64_t ia, ie, iff;
+        const uint32_t la = rec_at(wire, W, t0, at(m), ia);
+        const uint32_t le = rec_at(wire, W, t0, at(ke), ie);
+        const uint32_t lf = rec_at(wire, W, t0, at(kf), iff);
+        const bool lok =
+            ((int)(la == len(m)) & (int)(le == len(ke)) & (int)(lf == len(kf))) != 0;
+        bool ok = lok && ia == id0 + m && ie == id0 + ke && iff == id0 + kf;
+        if (!ok && lok && ks == n) {
+            // one length, ids not consecutive: one more sample, the middle record
+            uint64_t ib;
+            ok = rec_at(wire, W, t0, at(m / 2), ib) == L;
+        }
+        if (ok) {
+            count = n;
+            x = at(n);
+        } else {
+            ks = n = (lim - e + L - 1) / L;  // back to one run for the wave's search
+            L2 = L;
+            state = 1;
+        }
+    } else {
+        state = 2;  // a false candidate, or no valid start: let the merge points decide
+    }
+    if ((flags & F_FORCE_EXACT) && !bad) state = 2;
+
+}
+
 // ---- probe: one lane per tile ------------------------------------------------------------------
 // wire: the decoded range's first byte; W: bytes from there to the frame end; R (<= W): the
 // range's length (records that START before R are the range's; the rest is look-ahead)
@@ -420,88 +514,7 @@ __global__ __launch_bounds__(TPB) void nxg_f64r_probe_kernel(
     uint32_t count = 0, e = 0, x = 0, L = 0, L2 = 0, ks = 0;
     int state = 0;  // 0 done, 1 run search, 2 exact
     bool bad = false;
-    if (has) {
-        const uint64_t rem0 = W - t0;
-        uint32_t d[8];
-        ld32(wire, t0, W, d);
-        uint32_t cand = cand16(d[0], d[1], d[2], d[3], d[4]);
-        uint32_t V = 0;  // valid record starts (and the frame end) in [0, 16)
-        if (rem0 < 16) V |= 1u << rem0;
-        while (cand) {
-            const uint32_t s = __builtin_ctz(cand);
-            cand &= cand - 1;
-            uint32_t e0, e1, e2, e3;
-            extract16(d, s, e0, e1, e2, e3);
-            if (rec_check16(e0, e1, rem0 - s)) V |= 1u << s;
-        }
-        // the entry is the lowest valid start; the only other start allowed in the window is
-        // its successor (a record of <= 16 bytes leaves room for one more)
-        const uint32_t s1 = V ? (uint32_t)__builtin_ctz(V) : 32u;
-        uint32_t L1 = 0;
-        if (s1 < 16 && s1 != rem0) {
-            uint32_t e0, e1, e2, e3;
-            extract16(d, s1, e0, e1, e2, e3);
-            L1 = e0 & 0xffu;
-        }
-        const uint32_t p2 = s1 + L1;
-        if (t == 0 && first && !(V & 1u)) {
-            bad = true;
-        } else if (s1 < 16 && (s1 == rem0 || s1 >= lim)) {
-            // the frame (or the range) ends here: no record of this range starts in the tile
-            e = x = s1;
-            L = L2 = 12;
-        } else if (s1 < 16 && V == ((1u << s1) | (p2 < 16 ? 1u << p2 : 0u))) {
-            e = s1;
-            L = L2 = L1;
-            uint32_t n = (lim - e + L - 1) / L;
-            ks = n;
-            // Ids from the publisher's counter are consecutive (utils.rs:130-134): if the first
-            // id plus n crosses the next varint width, the tile is predicted as two runs split
-            // where the ids reach it.
-            uint64_t id0;
-            {
-                uint32_t e0, e1, e2, e3;
-                extract16(d, e, e0, e1, e2, e3);
-                uint64_t v0;
-                rec_decode16(e0, e1, e2, e3, L, id0, v0);
-                const uint32_t nb = L - 11u;
-                const uint64_t next = 1ull << (7u * nb);
-                if (nb < 5 && id0 < next && id0 + n > next) {
-                    ks = (uint32_t)(next - id0);
-                    L2 = L + 1;
-                    const uint32_t q2 = e + ks * L;
-                    n = ks + (lim - q2 + L2 - 1) / L2;
-                }
-            }
-            // the prediction's last record and both sides of the split must have the predicted
-            // lengths and ids (one HBM line per sample; the emit pass checks every record)
-            auto at = [&](uint32_t k) { return k < ks ? e + k * L : e + ks * L + (k - ks) * L2; };
-            auto len = [&](uint32_t k) { return k < ks ? L : L2; };
-            const uint32_t m = n - 1;
-            const uint32_t ke = ks < n ? ks - 1 : m, kf = ks < n ? ks : m;
-            uint64_t ia, ie, iff;
-            const bool lok = rec_at(wire, W, t0, at(m), ia) == len(m) &&
-                             rec_at(wire, W, t0, at(ke), ie) == len(ke) &&
-                             rec_at(wire, W, t0, at(kf), iff) == len(kf);
-            bool ok = lok && ia == id0 + m && ie == id0 + ke && iff == id0 + kf;
-            if (!ok && lok && ks == n) {
-                // one length, ids not consecutive: one more sample, the middle record
-                uint64_t ib;
-                ok = rec_at(wire, W, t0, at(m / 2), ib) == L;
-            }
-            if (ok) {
-                count = n;
-                x = at(n);
-            } else {
-                ks = n = (lim - e + L - 1) / L;  // back to one run for the wave's search
-                L2 = L;
-                state = 1;
-            }
-        } else {
-            state = 2;  // a false candidate, or no valid start: let the merge points decide
-        }
-        if ((flags & F_FORCE_EXACT) && !bad) state = 2;
-    }
+    if (has) probe_fast(wire, W, t, lim, first, flags, state, e, L, L2, ks, count, x, bad);
     // an irregular frame (record lengths that change from record to record: more than 1 tile
     // in 8 off the runs, here or in any workgroup so far) is left to the persistent decoder, which
     // the host reruns it on
