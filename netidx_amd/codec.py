@@ -18,7 +18,8 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libnxg_codec.so")
+# NXG_LIB: another build of the same library (A/B experiments, scripts/ab_variants.sh)
+LIB_PATH = os.environ.get("NXG_LIB") or os.path.join(HERE, "lib", "libnxg_codec.so")
 
 # NxgErrKind (include/nxg_codec.h) = PackError (netidx-core/src/pack.rs:89-95) + codec kinds
 OK, UNKNOWN_TAG, TOO_BIG, INVALID_FORMAT, BUFFER_SHORT = 0, 1, 2, 3, 4

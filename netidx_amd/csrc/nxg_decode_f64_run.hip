@@ -36,7 +36,10 @@ namespace f64r {
 #define NXG_F64R_T 32768
 #endif
 constexpr uint32_t T = NXG_F64R_T;  // tile bytes (the probe's unit)
-constexpr uint32_t EREC = 256;      // records per emit wave (a tile's records, in order)
+#ifndef NXG_F64R_EREC
+#define NXG_F64R_EREC 256
+#endif
+constexpr uint32_t EREC = NXG_F64R_EREC;  // records per emit wave (a tile's records, in order)
 constexpr uint32_t ESUB = (T / 12 + EREC) / EREC;  // emit waves per tile (records >= 12 B)
 static_assert(T + 16 <= 65535, "Desc.x is 16 bits");
 constexpr uint32_t SUB = 4096;    // exact path: LDS image of 64 chunks of 64 bytes
