@@ -290,7 +290,7 @@ def extras_single_gpu(codec, stream, steps, warmup):
         out = Columns(n + 1, len(m.ctag) + 1, 1, netidx_amd.LAYOUT_MIXED, "cuda")
         wall, kms, st = time_decode(codec, wire, out, n, max(3, steps // 4), 1, 1, stream,
                                     flags=netidx_amd.HINT_MIXED)
-        assert st.path == 2 and st.n_rows == n and st.err_kind == 0
+        assert st.path == 4 and st.n_rows == n and st.err_kind == 0
         checked = oracle_check_decode(wire, out, n, len(m.ctag))
         nd = int((m.tag == 10).sum())
         ns = int((m.tag == 12).sum())
@@ -756,7 +756,7 @@ def extras_multi_gpu(codec, world, rank, stream):
     out = Columns(nm + 1, len(m.ctag) + 1, 1, netidx_amd.LAYOUT_MIXED, "cuda")
     wall, kms, st = time_decode(codec, wire, out, nm, 5, 1, world, stream,
                                 flags=netidx_amd.HINT_MIXED)
-    assert st.path == 2 and st.n_rows == nm and st.err_kind == 0, st
+    assert st.path == 4 and st.n_rows == nm and st.err_kind == 0, st
     assert torch.equal(out.id[:nm], mc.id[:nm]) and torch.equal(out.tag[:nm], mc.tag[:nm])
     kmax = max_over_ranks(kms, world)
     ex["decode_mixed_1e7_per_gpu"] = {

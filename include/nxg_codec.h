@@ -112,7 +112,7 @@ typedef struct NxgColumns {
 typedef struct NxgStatus {
     uint64_t n_rows, n_children, n_ctl, n_heartbeat;
     int32_t err_kind;    /* NxgErrKind of the FIRST failing message (reference is sequential) */
-    uint32_t path;       /* 1 = homogeneous-f64 kernel, 2 = general kernel */
+    uint32_t path;       /* 1 = homogeneous-f64 kernel, 2 = general kernel, 4 = fast mixed kernel */
     uint64_t err_offset; /* byte offset of the first failing message */
 } NxgStatus;
 

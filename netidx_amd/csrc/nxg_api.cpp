@@ -78,6 +78,11 @@ struct NxgCtx {
     size_t rdesc_cap = 0;
     uint32_t irregular_left = 0;
     bool force_1p = false;
+    // mixed decode: the fast decoder (nxg_decode_mixed.hip) unless it rejected a recent frame of
+    // this connection; then the general decoder for the next kMixFailCalls calls
+    // (NXG_MIXED_PATH=general: always the general decoder)
+    uint32_t mix_left = 0;
+    bool no_fmx = false;
     uint32_t f64r_flags = 0;  // NXG_F64R_FLAGS (tests): 1 every tile exact, 2 never hand over
     uint8_t* dframe = nullptr;
     size_t dframe_cap = 0;
@@ -291,9 +296,10 @@ NxgColumns staged_view(NxgCtx* c, const NxgColumns* like) {
 }
 
 constexpr uint32_t kIrregularCalls = 64;
+constexpr uint32_t kMixFailCalls = 16;
 
-// path codes of a homogeneous-f64 attempt (Pending::fast)
-enum { FAST_NONE = 0, FAST_RUN = 1, FAST_1P = 2 };
+// path codes of a fast attempt (Pending::fast): homogeneous f64 (RUN, 1P) or mixed (MIX)
+enum { FAST_NONE = 0, FAST_RUN = 1, FAST_1P = 2, FAST_MIX = 3 };
 
 bool ensure_rdesc(NxgCtx* c, size_t bytes, NetidxError* err) {
     if (bytes <= c->rdesc_cap) return true;
@@ -363,6 +369,24 @@ bool enqueue_dec_general(NxgCtx* c, const uint8_t* f, uint64_t len, NxgColumns* 
     return true;
 }
 
+// Mixed decode: the fast decoder for frames of short Update messages (it raises fast_fail on
+// anything else and finish_decode reruns the frame on the general decoder).
+bool enqueue_dec_mixed(NxgCtx* c, const uint8_t* f, uint64_t len, NxgColumns* out, DevStatus* st,
+                       int* path, NetidxError* err) {
+    const ColsDesc d = desc_of(out);
+    if (len > 0 && d.tag && d.ctag && !c->no_fmx && c->mix_left == 0) {
+        *path = FAST_MIX;
+        // one buffer for both, so that a fallback does not reallocate
+        const uint64_t need = std::max(nxg_fmx_scratch_bytes(len), nxg_dec_gen_scratch_bytes(len));
+        if (!ensure_glws(c, need, err)) return false;
+        HIPCHK(nxg_launch_dec_fmx(f, len, d, reinterpret_cast<uint8_t*>(c->glws), st, c->stream));
+        return true;
+    }
+    if (c->mix_left) c->mix_left--;
+    *path = FAST_NONE;
+    return enqueue_dec_general(c, f, len, out, st, err);
+}
+
 // finish a device decode: read status, fall back to the general kernel if the f64 kernel
 // rejected the frame, fill the user-visible status
 // `fetched`: the caller has already copied the status ring to c->hst after the stream drained.
@@ -389,16 +413,23 @@ bool finish_decode(NxgCtx* c, const uint8_t* f, uint64_t len, NxgColumns* out, i
         HIPCHK(hipStreamSynchronize(c->stream));
         h = c->hst[slot2];
     }
-    if (tried_fast && len > 0 && h.fast_fail) {
+    // a rejected frame: after the f64 decoders the mixed fast path (mixed columns), after that
+    // the general decoder
+    while (tried_fast && len > 0 && h.fast_fail) {
+        if (tried_fast == FAST_MIX) c->mix_left = kMixFailCalls;
         DevStatus* st2;
         uint32_t slot2;
         if (!begin_call(c, &st2, &slot2, err)) return false;
-        const bool ok = enqueue_dec_general(c, f, len, out, st2, err);
+        int next = FAST_NONE;
+        const bool ok = tried_fast == FAST_MIX
+                            ? enqueue_dec_general(c, f, len, out, st2, err)
+                            : enqueue_dec_mixed(c, f, len, out, st2, &next, err);
         if (!end_call(c, err) || !ok) return false;
         HIPCHK(hipMemcpyAsync(c->hst + slot2, st2, sizeof(DevStatus), hipMemcpyDeviceToHost,
                               c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
         h = c->hst[slot2];
+        tried_fast = next;
     }
     if (h.err_key) {  // general decode: the earliest (offset, kind) on the true chain
         h.err_kind = (uint32_t)(~h.err_key & 0xffu);
@@ -618,6 +649,8 @@ NxgCtx* nxg_ctx_new(int device, NetidxError* err) {
     c->f64_2pass = f2 && f2[0] == '1';
     const char* fp = getenv("NXG_F64_PATH");
     c->force_1p = fp && strcmp(fp, "1p") == 0;
+    const char* mp = getenv("NXG_MIXED_PATH");
+    c->no_fmx = mp && strcmp(mp, "general") == 0;
     const char* ff = getenv("NXG_F64R_FLAGS");
     c->f64r_flags = ff ? (uint32_t)strtoul(ff, nullptr, 0) : 0u;
     return c;
@@ -716,7 +749,7 @@ bool nxg_decode_updates(NxgCtx* c, const uint8_t* frame, uint64_t len, NxgColumn
     int fast = FAST_NONE;
     const bool ok = !(flags & NXG_DECODE_HINT_MIXED)
                         ? enqueue_dec_fast(c, df, len, target, st, &fast, err)
-                        : enqueue_dec_general(c, df, len, target, st, err);
+                        : enqueue_dec_mixed(c, df, len, target, st, &fast, err);
     if (!end_call(c, err) || !ok) return false;
     NxgStatus s;
     if (!finish_decode(c, df, len, target, fast, st, slot, &s, err)) return false;
@@ -760,7 +793,7 @@ bool nxg_decode_updates_async(NxgCtx* c, const uint8_t* dframe, uint64_t len, Nx
     int fast = FAST_NONE;
     const bool ok = !(flags & NXG_DECODE_HINT_MIXED)
                         ? enqueue_dec_fast(c, dframe, len, dout, st, &fast, err)
-                        : enqueue_dec_general(c, dframe, len, dout, st, err);
+                        : enqueue_dec_mixed(c, dframe, len, dout, st, &fast, err);
     if (!end_call(c, err) || !ok) return false;
     c->pending.push_back({1, fast, dframe, len, dout, nullptr, 0, st, slot});
     return true;

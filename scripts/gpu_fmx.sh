@@ -1,0 +1,18 @@
+#!/bin/bash
+# fast mixed decoder: GPU tests, then a kernel trace of the config-3 decode at 10^7 records
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$R/gpurun_out/fmx
+mkdir -p $OUT
+export TMPDIR=/tmp
+cd $R
+timeout -k 10 500 python -u -m pytest -x -v --timeout 120 --timeout-method thread \
+    tests/test_gpu_mixed_fast.py tests/test_gpu_parity.py ${EXTRA_TESTS} > $OUT/pytest.log 2>&1 \
+ && timeout -k 10 120 python3 scripts/diag_general.py 1000000 10000000 > $OUT/diag.log 2>&1 \
+ && cd /tmp && timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o trace -- python3 $R/scripts/diag_general.py 10000000 > $OUT/trace.log 2>&1
+rc=$?
+tail -5 $OUT/pytest.log
+cat $OUT/diag.log 2>/dev/null
+f=$(find $OUT/trace -name '*kernel_stats.csv' 2>/dev/null | head -1)
+[ -n "$f" ] && cut -d, -f1-6 "$f" | head -20
+exit $rc

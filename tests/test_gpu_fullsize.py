@@ -93,7 +93,7 @@ def test_config3_mixed_decode_10m_every_column(codec):
     nc = len(m.ctag)
     cols = Columns(n + 1, nc + 1, 1, netidx_amd.LAYOUT_MIXED, "cuda")
     st = _decode_dev(codec, wire, cols, netidx_amd.HINT_MIXED)
-    assert st.err_kind == 0 and st.path == 2 and st.n_rows == n
+    assert st.err_kind == 0 and st.path == 4 and st.n_rows == n
     o = nxo.decode(wire, cap_rows=n + 1, cap_children=nc + 1, cap_ctl=1).trim()
     assert o["err_kind"] == 0 and len(o["id"]) == n and len(o["ctag"]) == nc
     g = cols.numpy()

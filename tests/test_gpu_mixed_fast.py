@@ -1,0 +1,250 @@
+"""GPU parity of the fast mixed decoder (nxg_decode_mixed.hip, status path 4).
+
+Frames of short Update messages with flat values take the fast decoder; everything else must be
+rejected by it and rerun on the general decoder (path 2). Either way the columns, the first
+error and the re-encoding must equal the oracle's (nx_oracle.c nxo_decode, which restates
+netidx-netproto/src/publisher.rs:73-96 + netidx-value/src/lib.rs:470-506), and the fast decoder's
+columns must equal the general decoder's on the same frame.
+"""
+import os
+import random
+
+import numpy as np
+import pytest
+
+from test_gpu_parity import _mg, assert_same_as_oracle, gpu_decode, mixed_wire
+
+pytestmark = pytest.mark.gpu
+
+@pytest.fixture
+def codec():
+    # a fresh context per test: a rejected frame makes a context skip the fast decoder for the
+    # next calls (kMixFailCalls)
+    import torch
+    import netidx_amd
+    assert torch.cuda.is_available()
+    c = netidx_amd.Codec(0)
+    yield c
+    c.close()
+
+
+def _general_codec():
+    import netidx_amd
+    os.environ["NXG_MIXED_PATH"] = "general"
+    try:
+        return netidx_amd.Codec(0)
+    finally:
+        del os.environ["NXG_MIXED_PATH"]
+
+
+def flat_value(rng, mg, err22=False):
+    """A Value the fast decoder takes: a leaf, an Array of leaves or (err22) an Error(String) in
+    its Error(Value) spelling (tag 22 + 12, which re-encodes as tag 18), in a message shorter
+    than 128 bytes."""
+    while True:
+        if err22 and rng.random() < 0.02:
+            return (22, (12, b"err"))
+        v = mg.rand_value(rng)
+        t = v[0]
+        if t in (21, 22):
+            continue
+        if t == 19:
+            v = (19, [e for e in v[1] if e[0] not in (19, 21, 22)])
+        if len(mg.update(2**35 - 1, v)) < 128:
+            return v
+
+
+def flat_wire(n, seed, id_bits=(7, 14, 21, 30, 35), err22=False):
+    mg = _mg()
+    rng = random.Random(seed)
+    msgs = [("u", rng.getrandbits(rng.choice(id_bits)), flat_value(rng, mg, err22))
+            for _ in range(n)]
+    wire, _ = mg.batch(msgs)
+    return wire
+
+
+def hint():
+    import netidx_amd
+    return netidx_amd.HINT_MIXED
+
+
+def reencode(codec, cols, wire):
+    import torch
+    heap = torch.from_numpy(np.frombuffer(wire, np.uint8).copy()).cuda()
+    return codec.encode_batch(cols, heap).cpu().numpy().tobytes()
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 40, 63, 64, 65, 500, 4096, 30_000])
+def test_fast_every_leaf_tag(codec, n):
+    wire = flat_wire(n, 1000 + n)
+    cols, st = gpu_decode(codec, wire, flags=hint())
+    assert st.err_kind == 0 and st.path == 4, (st.path, st.err_kind)
+    assert_same_as_oracle(cols, st, wire)
+    assert reencode(codec, cols, wire) == wire
+
+
+@pytest.mark.parametrize("n", [1, 10, 5000, 200_000])
+def test_fast_config3_shape(codec, n):
+    m, wire = mixed_wire(n, 300 + n)
+    cols, st = gpu_decode(codec, wire, flags=hint())
+    assert st.err_kind == 0 and st.path == 4
+    assert_same_as_oracle(cols, st, wire)
+
+
+def test_fast_without_hint_after_f64_rejects(codec):
+    """No hint: the f64 decoder rejects the frame, the fast mixed decoder takes it."""
+    m, wire = mixed_wire(20_000, 7)
+    cols, st = gpu_decode(codec, wire)
+    assert st.err_kind == 0 and st.path == 4
+    assert_same_as_oracle(cols, st, wire)
+
+
+def test_fast_equals_general_every_column(codec):
+    gen = _general_codec()
+    try:
+        for n, seed in ((100_000, 1), (3000, 2)):
+            wire = flat_wire(n, seed, err22=True)
+            a, sa = gpu_decode(codec, wire, flags=hint())
+            b, sb = gpu_decode(gen, wire, flags=hint())
+            assert (sa.path, sb.path) == (4, 2)
+            ga, gb = a.numpy(), b.numpy()
+            assert set(ga) == set(gb)
+            for k in ga:
+                assert np.array_equal(ga[k], gb[k]), k
+            assert (sa.n_rows, sa.n_children, sa.n_ctl) == (sb.n_rows, sb.n_children, sb.n_ctl)
+    finally:
+        gen.close()
+
+
+def test_fast_tile_edges(codec):
+    """Messages of every length 4..127 around the 4 KiB tile boundaries: entries in the first
+    two chunks of a tile, messages that cover a whole chunk, a frame ending on a tile edge."""
+    mg = _mg()
+    rng = random.Random(17)
+    for total in (4096, 8192, 8192 + 37, 3 * 4096 - 5):
+        msgs, size = [], 0
+        while True:
+            ln = rng.choice([0, 1, 5, 30, 60, 90, 110])  # string bytes -> message 8..120 B
+            v = (12, b"q" * ln)
+            enc = mg.update(3, v)
+            if size + len(enc) > total:
+                break
+            msgs.append(("u", 3, v))
+            size += len(enc)
+        # pad to the exact size with a last message when it fits one
+        rest = total - size
+        if 5 <= rest <= 127:
+            msgs.append(("u", 3, (12, b"z" * (rest - 5))))
+        wire, _ = mg.batch(msgs)
+        cols, st = gpu_decode(codec, wire, flags=hint())
+        assert st.err_kind == 0 and st.path == 4, (total, len(wire))
+        assert_same_as_oracle(cols, st, wire)
+
+
+def test_fast_longest_messages(codec):
+    """127-byte messages (the longest one-byte length), back to back across tiles."""
+    mg = _mg()
+    one = mg.update(5, (12, b"x" * 122))
+    assert len(one) == 127 and one[0] == 127
+    wire, _ = mg.batch([("u", 5, (12, b"x" * 122))] * 200)
+    cols, st = gpu_decode(codec, wire, flags=hint())
+    assert st.err_kind == 0 and st.path == 4
+    assert_same_as_oracle(cols, st, wire)
+
+
+def _rejected(codec, wire, strict=True, big_caps=False):
+    cols, st = gpu_decode(codec, wire, flags=hint())
+    if strict:
+        assert st.path == 2 or st.err_kind != 0
+    assert_same_as_oracle(cols, st, wire, big_caps)
+
+
+def _with(mg, n, seed, extra_at, extra):
+    rng = random.Random(seed)
+    msgs = [("u", rng.getrandbits(14), flat_value(rng, mg)) for _ in range(n)]
+    msgs.insert(extra_at, extra)
+    return mg.batch(msgs)[0]
+
+
+@pytest.mark.parametrize("case", ["heartbeat", "unsubscribed", "long_string", "map", "nested",
+                                  "error_value", "wide_id", "abstract_long"])
+def test_rejected_frames_fall_back_exactly(codec, case):
+    mg = _mg()
+    extra = {
+        "heartbeat": ("hb",),
+        "unsubscribed": ("raw", 2, mg.enc_varint(99)),
+        "long_string": ("u", 1, (12, b"L" * 300)),
+        "map": ("u", 1, (21, [((9, 1), (12, b"k"))])),
+        "nested": ("u", 1, (19, [(19, [(9, 5)])])),
+        "error_value": ("u", 1, (22, (9, 7))),
+        "wide_id": ("u", (1 << 60) + 3, (9, 1)),
+        "abstract_long": ("u", 1, (27, bytes(range(200)))),
+    }[case]
+    for at in (0, 2500, 5000):
+        _rejected(codec, _with(mg, 5000, 11, at, extra))
+
+
+def test_errors_and_truncation_fall_back_exactly(codec):
+    wire = flat_wire(6000, 21)
+    rng = np.random.default_rng(5)
+    for cut in (1, 2, 7, 100, 4096, 5000):
+        _rejected(codec, wire[:-cut], strict=False)
+    for _ in range(12):
+        w = bytearray(wire)
+        w[int(rng.integers(0, len(w)))] ^= int(rng.integers(1, 256))
+        _rejected(codec, bytes(w), strict=False)
+    # bad UTF-8 in a string, an unknown value tag, a short DateTime
+    mg = _mg()
+    _rejected(codec, _with(mg, 3000, 3, 1500, ("raw", 4, mg.enc_varint(7) + b"\x0c\x02\xc3\x28")))
+    _rejected(codec, _with(mg, 3000, 4, 1500, ("raw", 4, mg.enc_varint(7) + b"\x1c")))
+    _rejected(codec, _with(mg, 3000, 5, 1500, ("raw", 4, mg.enc_varint(7) + b"\x0a\x00\x00")))
+
+
+def test_capacity_is_reported(codec):
+    import netidx_amd
+    from netidx_amd.codec import Columns
+    import torch
+    m, wire = mixed_wire(5000, 9)
+    frame = torch.from_numpy(np.frombuffer(wire, np.uint8).copy()).cuda()
+    cols = Columns(4000, len(m.ctag) + 1, 1, netidx_amd.LAYOUT_MIXED, "cuda")
+    st = codec.decode_into(frame, len(wire), cols, hint(), check=False)
+    assert st.err_kind == netidx_amd.CAPACITY
+
+
+def test_fuzz_small_frames(codec):
+    """Random bytes that look like short Updates: accept/reject and first error as the oracle."""
+    rng = np.random.default_rng(77)
+    for i in range(200):
+        n = int(rng.integers(1, 400))
+        w = bytearray(rng.integers(0, 30, n, dtype=np.uint8).tobytes())
+        p = 0
+        while p + 2 < n:  # sprinkle plausible headers
+            L = int(rng.integers(4, 40))
+            w[p] = L
+            w[p + 1] = 4
+            p += L
+        _rejected(codec, bytes(w), strict=False, big_caps=True)
+
+
+def test_fast_long_arrays(codec):
+    """Arrays of up to 120 one- and two-byte elements: more elements per round than the
+    lane-parallel list holds (the per-lane path), next to short ones (the list)."""
+    mg = _mg()
+    rng = random.Random(8)
+    msgs = []
+    for i in range(3000):
+        k = rng.random()
+        if k < 0.3:
+            v = (19, [(16, None)] * rng.randrange(60, 121))
+        elif k < 0.5:
+            v = (19, [(24, rng.randint(-128, 127)) for _ in range(rng.randrange(1, 55))])
+        elif k < 0.7:
+            v = (19, [(9, rng.getrandbits(64)) for _ in range(rng.randrange(0, 12))])
+        else:
+            v = flat_value(rng, mg)
+        msgs.append(("u", i, v))
+    wire, _ = mg.batch(msgs)
+    cols, st = gpu_decode(codec, wire, flags=hint())
+    assert st.err_kind == 0 and st.path == 4
+    assert_same_as_oracle(cols, st, wire)
+    assert reencode(codec, cols, wire) == wire

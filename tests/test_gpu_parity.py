@@ -46,9 +46,12 @@ def as_rows(d, n=None):
     return [list(map(int, r)) for r in zip(d["id"], d["tag"], d["fixed"], d["aux"])]
 
 
-def assert_same_as_oracle(cols, st, wire):
+def assert_same_as_oracle(cols, st, wire, big_caps=False):
+    """big_caps: the oracle gets room for every child an invalid frame may announce (16 per
+    remaining byte, the ValArray guard), so that its first error is a decode error, as the
+    reference's (which has no capacity) -- not a capacity error met on the way."""
     import nxo
-    o = nxo.decode(wire).trim()
+    o = (nxo.decode(wire, cap_children=16 * len(wire) + 16) if big_caps else nxo.decode(wire)).trim()
     assert (st.err_kind, st.err_offset if st.err_kind else 0) == (o["err_kind"], o["err_offset"])
     if st.err_kind:
         return
@@ -200,7 +203,7 @@ def mixed_wire(n, seed):
 def test_mixed_vs_oracle(codec, n):
     m, wire = mixed_wire(n, 100 + n)
     cols, st = gpu_decode(codec, wire)
-    assert st.path == 2 and st.err_kind == 0
+    assert st.path in (2, 4) and st.err_kind == 0  # 4 unless a recent frame fell back
     assert_same_as_oracle(cols, st, wire)
 
 
