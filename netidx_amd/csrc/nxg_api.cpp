@@ -83,6 +83,7 @@ struct NxgCtx {
     // (NXG_MIXED_PATH=general: always the general decoder)
     uint32_t mix_left = 0;
     bool no_fmx = false;
+    int wgs_fmx[2] = {0, 0};
     uint32_t f64r_flags = 0;  // NXG_F64R_FLAGS (tests): 1 every tile exact, 2 never hand over
     uint8_t* dframe = nullptr;
     size_t dframe_cap = 0;
@@ -379,7 +380,8 @@ bool enqueue_dec_mixed(NxgCtx* c, const uint8_t* f, uint64_t len, NxgColumns* ou
         // one buffer for both, so that a fallback does not reallocate
         const uint64_t need = std::max(nxg_fmx_scratch_bytes(len), nxg_dec_gen_scratch_bytes(len));
         if (!ensure_glws(c, need, err)) return false;
-        HIPCHK(nxg_launch_dec_fmx(f, len, d, reinterpret_cast<uint8_t*>(c->glws), st, c->stream));
+        HIPCHK(nxg_launch_dec_fmx(f, len, d, reinterpret_cast<uint8_t*>(c->glws), c->wgs_fmx, st,
+                                  c->stream));
         return true;
     }
     if (c->mix_left) c->mix_left--;
@@ -644,6 +646,7 @@ NxgCtx* nxg_ctx_new(int device, NetidxError* err) {
     const size_t gw = (size_t)gdec2::MAX_RUNS * (gdec2::RUN_WORDS + 4);
     if ((e = hipMalloc(&c->gruns, gw * 8)) != hipSuccess) return fail("hipMalloc(gruns)", e);
     c->wgs_dec_gen = nxg_dec_gen_wgs(c->ncu);
+    nxg_fmx_wgs(c->ncu, c->wgs_fmx);
     c->wgs_dec_f64_1p = nxg_dec_f64_1p_wgs(c->ncu);
     const char* f2 = getenv("NXG_F64_2PASS");
     c->f64_2pass = f2 && f2[0] == '1';

@@ -153,8 +153,9 @@ int nxg_dec_gen_wgs(int ncu);
 // fast mixed decode (nxg_decode_mixed.hip): frames of Update messages shorter than 128 bytes with
 // flat values; sets fast_fail for anything else. `scratch`: nxg_fmx_scratch_bytes(W), no zeroing.
 uint64_t nxg_fmx_scratch_bytes(uint64_t W);
+void nxg_fmx_wgs(int ncu, int* wgs);  // persistent grid sizes (count, emit)
 hipError_t nxg_launch_dec_fmx(const uint8_t* wire, uint64_t W, const ColsDesc& cols,
-                              uint8_t* scratch, DevStatus* st, hipStream_t s);
+                              uint8_t* scratch, const int* wgs, DevStatus* st, hipStream_t s);
 // subscriber dispatch (nxg_dispatch.hip): `scratch` holds nxg_disp_scratch_bytes(n, n_chans)
 // bytes (no initialisation needed); `unmatched` one u64.
 uint64_t nxg_disp_scratch_bytes(uint64_t n, uint32_t n_chans);
