@@ -184,6 +184,82 @@ NXG_DEV Cands lane_cands(const uint8_t* img, uint32_t lane, uint32_t lim) {
     return r;
 }
 
+// The tile's chain as a scan (no serial loop). The state at the boundary in front of chunk j
+// says where the next message start is: N0 / N1 = chunk j's first / second candidate, F0 / F1 =
+// chunk j+1's (chunk j lies inside one message), END = at or past the tile end, FAIL = anywhere
+// else. Chunk j maps the state in front of it to the state behind it: from N_a the chain runs to
+// x_a, which lies in chunk j+1 or j+2 (messages are < 128 bytes) and must be a first or second
+// candidate there; F_a becomes N_a; END and FAIL stay. These maps (6 states x 3 bits) compose
+// associatively, so a wave scan of them gives every chunk's entry state at once. A chain that
+// enters some chunk at a third candidate comes out FAIL here and goes to tile_chain.
+constexpr uint32_t S_N0 = 0, S_N1 = 1, S_F0 = 2, S_F1 = 3, S_FAIL = 4, S_END = 5;
+constexpr uint32_t T_ID = (0u << 0) | (1u << 3) | (2u << 6) | (3u << 9) | (4u << 12) | (5u << 15);
+NXG_DEV uint32_t tget(uint32_t T, uint32_t st) { return (T >> (3 * st)) & 7u; }
+NXG_DEV uint32_t tcompose(uint32_t later, uint32_t earlier) {
+    uint32_t c = 0;
+#pragma unroll
+    for (uint32_t st = 0; st < 6; st++) c |= tget(later, tget(earlier, st)) << (3 * st);
+    return c;
+}
+template <int CTRL, int ROWS>
+NXG_DEV uint32_t dpp_fill(uint32_t v, uint32_t fill) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)fill, (int)v, CTRL, ROWS, 0xf, false);
+}
+NXG_DEV uint32_t tscan(uint32_t T) {  // inclusive: lane j gets T_j o ... o T_0
+    T = tcompose(T, dpp_fill<0x111, 0xf>(T, T_ID));
+    T = tcompose(T, dpp_fill<0x112, 0xf>(T, T_ID));
+    T = tcompose(T, dpp_fill<0x114, 0xf>(T, T_ID));
+    T = tcompose(T, dpp_fill<0x118, 0xf>(T, T_ID));
+    T = tcompose(T, dpp_fill<0x142, 0xa>(T, T_ID));
+    T = tcompose(T, dpp_fill<0x143, 0xc>(T, T_ID));
+    return T;
+}
+
+NXG_DEV uint32_t tile_chain_scan(uint32_t e, uint32_t lim, uint32_t lane, uint32_t c0, uint32_t x0,
+                                 uint32_t c1, uint32_t x1, uint32_t& ce) {
+    ce = NONE;
+    // the candidates of chunks j+1 and j+2 (none past the tile)
+    const uint32_t c0n = dpp_fill<0x130, 0xf>(c0, FAIL), c1n = dpp_fill<0x130, 0xf>(c1, FAIL);
+    const uint32_t c0nn = dpp_fill<0x130, 0xf>(c0n, FAIL), c1nn = dpp_fill<0x130, 0xf>(c1n, FAIL);
+    auto out = [&](uint32_t x) -> uint32_t {
+        if (x == FAIL) return S_FAIL;
+        if (x >= lim) return S_END;
+        const uint32_t d = (x >> 6) - lane;
+        if (d == 1) return x == c0n ? S_N0 : (x == c1n ? S_N1 : S_FAIL);
+        if (d == 2) return x == c0nn ? S_F0 : (x == c1nn ? S_F1 : S_FAIL);
+        return S_FAIL;
+    };
+    const uint32_t T = out(x0) | (out(x1) << 3) | (S_N0 << 6) | (S_N1 << 9) | (S_FAIL << 12) |
+                       (S_END << 15);
+    // the state in front of chunk 0
+    uint32_t s0;
+    if (e >= lim) {
+        return e;  // no message starts in this tile
+    } else if (e < CH) {
+        const uint32_t a0 = (uint32_t)__builtin_amdgcn_readlane((int)c0, 0);
+        const uint32_t a1 = (uint32_t)__builtin_amdgcn_readlane((int)c1, 0);
+        s0 = e == a0 ? S_N0 : (e == a1 ? S_N1 : S_FAIL);
+    } else if (e < 2 * CH) {
+        const uint32_t a0 = (uint32_t)__builtin_amdgcn_readlane((int)c0, 1);
+        const uint32_t a1 = (uint32_t)__builtin_amdgcn_readlane((int)c1, 1);
+        s0 = e == a0 ? S_F0 : (e == a1 ? S_F1 : S_FAIL);
+    } else {
+        s0 = S_FAIL;
+    }
+    if (s0 == S_FAIL) return FAIL;
+    const uint32_t sout = tget(tscan(T), s0);          // state behind chunk j
+    const uint32_t sin = dpp_fill<0x138, 0xf>(sout, s0);  // in front of chunk j (wave_shr:1)
+    if (wave_last<uint32_t>(sout) != S_END) return FAIL;
+    if (sin == S_N0) ce = c0;
+    else if (sin == S_N1) ce = c1;
+    // the exit: the last start's chunk, whose state behind is the first END
+    const bool last = (sin == S_N0 || sin == S_N1) && sout == S_END;
+    const uint64_t lm = __ballot(last);
+    if (!lm) return FAIL;
+    const uint32_t xl = sin == S_N0 ? x0 : x1;
+    return (uint32_t)__builtin_amdgcn_readlane((int)xl, (int)__builtin_ctzll(lm));
+}
+
 // Header of the message at tile offset p: child slots (Array element count), or FAIL when the
 // message is not for the fast path. The value tag sits after the variant and the id varint.
 NXG_DEV uint32_t msg_kids(const uint8_t* img, uint32_t p) {
@@ -233,7 +309,8 @@ struct TileDesc {
 NXG_DEV TileDesc count_from(const uint8_t* img, const Cands& cd, uint32_t e, uint32_t lim,
                             bool last, uint32_t lane, uint64_t& bits) {
     uint32_t ce;
-    const uint32_t x = tile_chain(img, e, lim, lane, cd.m, cd.c0, cd.x0, cd.c1, cd.x1, ce);
+    uint32_t x = tile_chain_scan(e, lim, lane, cd.c0, cd.x0, cd.c1, cd.x1, ce);
+    if (x == FAIL) x = tile_chain(img, e, lim, lane, cd.m, cd.c0, cd.x0, cd.c1, cd.x1, ce);
     bool bad = x == FAIL || (last && x != lim);
     uint32_t n = 0, k = 0;
     bits = 0;
