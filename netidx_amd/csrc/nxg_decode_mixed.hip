@@ -35,6 +35,10 @@
 #include "nxg_internal.h"
 #include "nxg_msg.h"
 
+#ifndef NXG_FMX_SKIP
+#define NXG_FMX_SKIP 0  // timing experiments only: 1 elements, 2 text, 4 row values, 8 row stores
+#endif
+
 namespace fmx {
 constexpr uint32_t TILE = 4096;
 constexpr uint32_t CH = 64;
@@ -57,6 +61,7 @@ struct EmitLds {
     uint8_t img[IMG];
     uint16_t msg[MAXM];  // the tile's message starts
     uint32_t el[MAXC];   // a round's array elements: position | (message end - position) << 13
+    uint8_t mark[256];   // utf8_packed
 };
 
 NXG_DEV uint4 ld16(const uint8_t* __restrict__ wire, uint64_t off, uint64_t W) {
@@ -322,16 +327,21 @@ NXG_DEV TileDesc count_from(const uint8_t* img, const Cands& cd, uint32_t e, uin
 
 // ---- the emit pass's value decoder ---------------------------------------------------------------
 // Value::decode (netidx-value/src/lib.rs:470-506) for the values this path takes, restated as
-// nxg_msg.h dleaf / dcontainer do, but with every field computed from the 16 bytes after the tag
-// and selected by tag, so that a wave whose lanes hold different tags runs one instruction stream
-// (only text validation and array elements loop). Any decode error returns false: the frame
-// then goes to the general decoder, which reports it.
+// nxg_msg.h dleaf / dcontainer do. Every field is computed from the 12 bytes after the tag (three
+// words already in registers) with 32-bit tile offsets, and selected by tag, so that a wave whose
+// lanes hold different tags runs one instruction stream; only a varint longer than 4 bytes and a
+// DateTime outside +-2^42 s or with a leap second branch. Text is checked for UTF-8 by the caller
+// (ascii_ok per lane, utf8_wave for the rest). Any decode error clears ok: the frame then goes to
+// the general decoder, which reports it.
 
 // the 7-bit groups of the (up to) 8 bytes of y, least significant first
 NXG_DEV uint64_t compress7(uint64_t y) {
     const uint64_t z1 = (y & 0x007f007f007f007full) | ((y >> 1) & 0x3f803f803f803f80ull);
     const uint64_t z2 = (z1 & 0x00003fff00003fffull) | ((z1 >> 2) & 0x0fffc0000fffc000ull);
     return (z2 & 0x0fffffffull) | ((z2 >> 4) & 0x00fffffff0000000ull);
+}
+NXG_DEV uint32_t compress7_32(uint32_t y) {
+    return (y & 0x7fu) | ((y >> 1) & 0x3f80u) | ((y >> 2) & 0x1fc000u) | ((y >> 3) & 0xfe00000u);
 }
 
 // LEB128 (pack.rs:504-520) at window byte 0: its length (0: no terminator in 10 bytes); bits
@@ -352,96 +362,272 @@ NXG_DEV uint32_t wvar(uint64_t lo, uint64_t hi, uint64_t& v) {
     v = base | ((b8 & 0x7fu) << 56) | ((b9 & 1u) << 63);
     return b9 < 0x80u ? 10u : 0u;
 }
+// the same over the words w0, w1, w2 (bytes 0..11): one to four bytes without a branch
+NXG_DEV uint32_t var3(uint32_t w0, uint32_t w1, uint32_t w2, uint64_t& v) {
+    const uint32_t st = ~w0 & 0x80808080u;
+    if (__builtin_expect(st != 0u, 1)) {
+        const uint32_t nb = ((uint32_t)__builtin_ctz(st) >> 3) + 1;
+        v = compress7_32(w0 & (0xffffffffu >> (32u - 8u * nb)));
+        return nb;
+    }
+    return wvar((uint64_t)w0 | ((uint64_t)w1 << 32), w2, v);
+}
 
-struct FVal {
+// image bytes r .. r+4n-1 as n little-endian words (reads n+1 aligned words from r & ~3)
+template <int N>
+NXG_DEV void win_words(lds_bytes img, uint32_t r, uint32_t* q) {
+    lds_words w = (lds_words)(img + (r & ~3u));
+    const uint32_t sh = r & 3u;
+    uint32_t a[N + 1];
+#pragma unroll
+    for (int k = 0; k <= N; k++) a[k] = w[k];
+#pragma unroll
+    for (int k = 0; k < N; k++) q[k] = alignbyte(a[k + 1], a[k], sh);
+}
+
+struct FV {
+    uint64_t fixed;
     uint32_t tag, aux;
-    uint64_t fixed, next, kids;
+    uint32_t end;         // tile offset after the value
+    uint32_t kids;        // Array: element count
+    uint32_t soff, slen;  // text to check for UTF-8 (slen 0: none)
+    bool ok;
 };
 
-// The value whose tag t was consumed, payload at q (< lim, the message's end); arrays only when
-// `arr` (a row), with their element count in kids (the caller sets fixed to the child base).
-NXG_DEV bool fast_value(lds_bytes img, uint64_t t0, uint32_t t, uint64_t q, uint64_t lim, bool arr,
-                        FVal& o) {
-    if (t >= 28u || t == 21u || (t == 19u && !arr)) return false;
-    Win16 wn = win16(img, (uint32_t)(q - t0));
-    const bool e22 = t == 22u;
-    if (e22) {  // Error(Value) whose inner value is a String: the String after its tag (12)
-        if ((wn.lo & 0xffu) != 12u) return false;
-        wn.lo = (wn.lo >> 8) | (wn.hi << 56);
-        wn.hi >>= 8;
-        q += 1;
-    }
-    const uint64_t room = lim > q ? lim - q : 0;
+// The value with tag t whose payload starts at tile offset u; P0..P2 = its first 12 bytes; lim =
+// the message end (tile offset, >= u). Arrays only when `arr` (a row).
+// value classes as tag bit sets (bit tests, so that the compiler forms no switch on the tag)
+constexpr uint32_t B(uint32_t t) { return 1u << t; }
+constexpr uint32_t kVarTags = B(1) | B(3) | B(5) | B(7);    // V32 Z32 V64 Z64
+constexpr uint32_t kVar32 = B(1) | B(3), kZig = B(3) | B(7);
+constexpr uint32_t kTxtTags = B(12) | B(13) | B(18) | B(22);  // String Bytes Error(String)
+constexpr uint32_t kSgnTags = B(2) | B(24) | B(26);         // I32 I8 I16
+NXG_DEV FV val_decode(uint32_t t, uint32_t P0, uint32_t P1, uint32_t P2, uint32_t u, uint32_t lim,
+                      bool arr, uint64_t t0) {
+    const uint32_t bit = t < 32u ? 1u << t : 0u;
+    // Error(Value) whose inner value is a String: the String after its tag (12)
+    const bool e22 = bit & B(22);
+    const bool bad = t >= 28u || (bit & B(21)) || ((bit & B(19)) && !arr) ||
+                     (e22 && (P0 & 0xffu) != 12u);
+    P0 = e22 ? alignbyte(P1, P0, 1) : P0;
+    P1 = e22 ? alignbyte(P2, P1, 1) : P1;
+    P2 = e22 ? P2 >> 8 : P2;
+    u += e22 ? 1u : 0u;
+    const uint32_t room = lim > u ? lim - u : 0u;
     uint64_t v;
-    const uint32_t nb = wvar(wn.lo, wn.hi, v);
+    const uint32_t nb = var3(P0, P1, P2, v);
     const bool vok = nb != 0 && nb <= room;
+    const uint32_t p = u + nb;  // after a length / count varint
+    const uint32_t rest = lim > p ? lim - p : 0u;
+    const uint32_t v32 = (uint32_t)v;
+    // fixed-size payloads: n big-endian bytes (0: Bool / Null; 12: DateTime, Duration)
     const uint32_t f1 = fixed_size1(t);
-    o.tag = t == 17u ? 16u : (e22 ? 18u : t);
-    o.aux = 0;
-    o.kids = 0;
-    bool ok;
-    if (f1) {  // fixed-size payload: n big-endian bytes (0: Bool / Null; 12: DateTime, Duration)
-        const uint32_t n = f1 - 1;
-        const uint64_t be8 = __builtin_bswap64(wn.lo);
-        const uint32_t sh = 64u - 8u * min(n, 8u);
-        const uint64_t fx = n ? (be8 >> (sh & 63u)) : 0ull;
-        const uint32_t sb = t == 2u ? 32u : (t == 24u ? 8u : (t == 26u ? 16u : 0u));  // signed
-        o.fixed = t == 14u ? 1ull : (sb ? (uint64_t)((int64_t)(fx << (64u - sb)) >> (64u - sb)) : fx);
-        o.next = q + n;
-        ok = room >= n;
-        if (n == 12u) {
-            uint32_t ns = bswap32((uint32_t)wn.hi);
-            uint64_t secs = be8;
-            if (t == 10u) {
-                ok &= datetime_valid((int64_t)secs, ns);
-            } else if (ns >= 1000000000u) {  // Duration::new normalisation (dleaf case 11)
-                const uint64_t add = ns / 1000000000u;
-                ok &= secs + add >= secs;
-                secs += add;
-                ns %= 1000000000u;
-            }
-            o.fixed = secs;
-            o.aux = ns;
-        }
-    } else if (t == 1u || t == 3u || t == 5u || t == 7u) {
-        const uint32_t n32 = (uint32_t)v;
-        const int32_t z32 = (int32_t)(n32 >> 1) ^ (int32_t)(0u - (n32 & 1u));
-        o.fixed = t == 1u ? (uint64_t)n32
-                : t == 3u ? (uint64_t)(int64_t)z32
-                : t == 5u ? v : ((v >> 1) ^ (0ull - (v & 1ull)));
-        o.next = q + nb;
-        ok = vok;
-    } else if (t == 19u) {  // ValArray header (array.rs:595-612): count guard as dcontainer
-        const uint64_t p = q + nb;
-        ok = vok && v <= kMaxVec / 16 && v * 16 <= ((lim - p) << 8);
-        o.aux = (uint32_t)v;
-        o.kids = v;
-        o.next = p;
-        o.fixed = 0;
-    } else if (t == 20u) {  // Decimal: 16 bytes, not interpreted
-        ok = room >= 16;
-        o.fixed = q;
-        o.aux = 16;
-        o.next = q + 16;
-    } else if (t == 27u) {  // Abstract: len-wrapped (dleaf case 27)
-        const uint64_t p = q + nb;
-        ok = vok && v >= 1;
-        const uint64_t take = ok ? v - vl64(v) : 0;
-        const uint64_t l2 = take < lim - p ? p + take : lim;
-        ok &= l2 - p >= 16;
-        o.fixed = p;
-        o.aux = (uint32_t)(l2 - p);
-        o.next = l2;
-    } else {  // String / Bytes / Error(String): varint length, then the bytes (UTF-8 but Bytes)
-        const uint64_t off = q + nb;
-        ok = vok && v <= room - nb;
-        o.fixed = off;
-        o.aux = (uint32_t)v;
-        o.next = off + v;
-        if (ok && t != 13u) ok = utf8_ok(LdsSrc{img, t0}, off, v);
-    }
-    return ok;
+    const uint32_t n = f1 - 1u;
+    const uint32_t b0 = bswap32(P0), b1 = bswap32(P1);
+    const bool n8 = f1 >= 9u;                       // 8 or 12 bytes
+    const uint32_t sh = (32u - 8u * n) & 31u;       // 1, 2, 4 bytes: b0 >> 24, 16, 0
+    const bool sgn = bit & kSgnTags;
+    const uint32_t lo32 = f1 >= 2u ? (sgn ? (uint32_t)((int32_t)b0 >> sh) : b0 >> sh)
+                                   : ((bit & B(14)) ? 1u : 0u);
+    const uint32_t fhi = n8 ? b0 : (sgn ? (uint32_t)((int32_t)lo32 >> 31) : 0u);
+    const uint32_t flo = n8 ? b1 : lo32;
+    // DateTime::from_timestamp: |secs| < 2^42 with ns < 10^9 is always valid (no branch)
+    uint32_t ns = bswap32(P2);
+    const uint64_t secs = ((uint64_t)b0 << 32) | b1;
+    bool fok = room >= n;
+    const bool easy = ns < 1000000000u && secs + ((1ull << 42) - 1) < (1ull << 43) - 1;
+    if (__builtin_expect((bit & B(10)) && !easy, 0)) fok = fok && datetime_valid((int64_t)secs, ns);
+    // Duration::new normalisation (dleaf case 11); ns < 2^32 < 5 * 10^9
+    const bool dur = bit & B(11);
+    const uint32_t add = dur ? (uint32_t)(ns >= 1000000000u) + (ns >= 2000000000u) +
+                                   (ns >= 3000000000u) + (ns >= 4000000000u)
+                             : 0u;
+    const uint64_t s2 = secs + add;
+    fok = fok && s2 >= secs;
+    ns -= add * 1000000000u;
+    // varint scalars: V32 (truncated), Z32, V64, Z64
+    const uint32_t z32 = (v32 >> 1) ^ (0u - (v32 & 1u));
+    const uint64_t z64 = (v >> 1) ^ (0ull - (v & 1ull));
+    const bool isvar = bit & kVarTags, iszig = bit & kZig, is32 = bit & kVar32;
+    const uint64_t v32x = iszig ? (uint64_t)(int64_t)(int32_t)z32 : (uint64_t)v32;
+    const uint64_t vfix = is32 ? v32x : (iszig ? z64 : v);
+    const bool istxt = bit & kTxtTags, isarr = bit & B(19), isdec = bit & B(20);
+    const bool isfix = f1 != 0u;
+    // Abstract: len-wrapped (dleaf case 27); the wrap may claim past the message
+    const uint64_t take = v >= 1 ? v - vl64(v) : 0ull;
+    const uint32_t l2 = take < (uint64_t)rest ? p + (uint32_t)take : lim;
+    // ValArray header (array.rs:595-612): count guard as dcontainer
+    const bool aok = vok && v <= kMaxVec / 16 && v * 16 <= ((uint64_t)rest << 8);
+    const bool tok = vok && v <= (uint64_t)(room - nb);
+    const bool bok = vok && v >= 1 && l2 >= p + 16u;
+    const bool ok = isfix ? fok : (isvar ? vok : (istxt ? tok : (isarr ? aok : (isdec ? room >= 16u : bok))));
+    FV o;
+    o.tag = (bit & B(17)) ? 16u : (e22 ? 18u : t);
+    o.ok = ok && !bad;
+    const uint32_t endv = isvar || isarr ? p : (istxt ? p + v32 : (isdec ? u + 16u : l2));
+    o.end = isfix ? u + n : endv;
+    const uint64_t off = t0 + (isdec ? u : p);  // text, Decimal, Abstract: where in the frame
+    const uint64_t fval = dur ? s2 : (((uint64_t)fhi << 32) | flo);
+    o.fixed = isfix ? fval : (isvar ? vfix : (isarr ? 0ull : off));
+    const uint32_t avar = istxt || isarr ? v32 : (isdec ? 16u : (isvar ? 0u : l2 - p));
+    o.aux = isfix ? (n == 12u ? ns : 0u) : avar;
+    o.kids = isarr ? v32 : 0u;
+    o.soff = p;
+    o.slen = o.ok && istxt && !(bit & B(13)) ? v32 : 0u;
+    return o;
 }
+
+// index of the first byte >= 0x80 among bytes 0..15 of the words q[0..3] (16: none)
+NXG_DEV uint32_t first_high16(const uint32_t* q) {
+    const uint64_t lo = (((uint64_t)q[1] << 32) | q[0]) & 0x8080808080808080ull;
+    const uint64_t hi = (((uint64_t)q[3] << 32) | q[2]) & 0x8080808080808080ull;
+    return lo ? (uint32_t)__builtin_ctzll(lo) >> 3 : (hi ? 8u + ((uint32_t)__builtin_ctzll(hi) >> 3) : 16u);
+}
+// bytes [s, s + n) of the image are all ASCII: 32 bytes from one batch of LDS reads, longer text
+// (up to 127 bytes) 32 more per step
+NXG_DEV bool ascii_ok(lds_bytes img, uint32_t s, uint32_t n) {
+    bool na = false;
+#pragma unroll 1
+    for (uint32_t k = 0; k < n; k += 32) {
+        uint32_t q[8];
+        win_words<8>(img, s + k, q);
+        const uint32_t f0 = first_high16(q), f1 = 16u + first_high16(q + 4);
+        na |= min(f0, f1) < n - k;
+    }
+    return !na;
+}
+
+// inclusive max-scan over the wave (DPP, identity 0)
+NXG_DEV uint32_t wave_max_scan(uint32_t x) {
+    x = max(x, dpp0<0x111, 0xf>(x));
+    x = max(x, dpp0<0x112, 0xf>(x));
+    x = max(x, dpp0<0x114, 0xf>(x));
+    x = max(x, dpp0<0x118, 0xf>(x));
+    x = max(x, dpp0<0x142, 0xa>(x));
+    x = max(x, dpp0<0x143, 0xc>(x));
+    return x;
+}
+
+// std::str::from_utf8 (pack.rs:462) of bytes [s, s + n) of the image (s >= 3), checked by the
+// whole wave one byte per lane: a continuation byte exactly where a lead within the three bytes
+// before asks for one, no C0 / C1 / F5..FF, no overlong 3- or 4-byte form, surrogate or code
+// point past U+10FFFF (the byte after E0 / ED / F0 / F4), and every sequence ends inside the text.
+// All 64 lanes must be active.
+NXG_DEV bool utf8_wave(lds_bytes img, uint32_t s, uint32_t n, uint32_t lane) {
+    bool bad = false;
+#pragma unroll 1
+    for (uint32_t i0 = 0; i0 < n; i0 += 64) {
+        const uint32_t i = i0 + lane;
+        if (i < n) {
+            const uint32_t r = s + i - 3;
+            lds_words w = (lds_words)(img + (r & ~3u));
+            const uint32_t x = alignbyte(w[1], w[0], r & 3u);  // bytes i-3 .. i
+            const uint32_t c = x >> 24;
+            const uint32_t c1 = i >= 1 ? (x >> 16) & 0xffu : 0u;
+            const uint32_t c2 = i >= 2 ? (x >> 8) & 0xffu : 0u;
+            const uint32_t c3 = i >= 3 ? x & 0xffu : 0u;
+            const bool cont = (c & 0xc0u) == 0x80u;
+            const bool need = c1 >= 0xc0u || c2 >= 0xe0u || c3 >= 0xf0u;
+            const uint32_t L = c < 0xc0u ? 0u : (c < 0xe0u ? 2u : (c < 0xf0u ? 3u : 4u));
+            bad |= cont != need;
+            bad |= c == 0xc0u || c == 0xc1u || c >= 0xf5u;
+            bad |= (c1 == 0xe0u && c < 0xa0u) || (c1 == 0xedu && c > 0x9fu) ||
+                   (c1 == 0xf0u && c < 0x90u) || (c1 == 0xf4u && c > 0x8fu);
+            bad |= i + L > n;
+        }
+    }
+    return !__any(bad);
+}
+
+// the text of the lanes with `na` (not all ASCII), one after another by the whole wave
+NXG_DEV bool utf8_lanes(lds_bytes img, bool na, uint32_t soff, uint32_t slen, uint32_t lane) {
+    uint64_t m = __ballot(na);
+    bool good = true;
+#pragma unroll 1
+    while (m && good) {
+        const int j = (int)__builtin_ctzll(m);
+        m &= m - 1;
+        good = utf8_wave(img, (uint32_t)__builtin_amdgcn_readlane((int)soff, j),
+                         (uint32_t)__builtin_amdgcn_readlane((int)slen, j), lane);
+    }
+    return good;
+}
+
+// The same, all the texts at once: their bytes laid end to end, one per lane (64 per step), each
+// lane finding its text through `mark` (LDS, 256 bytes: the text starting at each position). More
+// than 256 bytes: utf8_lanes. The checks are utf8_wave's.
+NXG_DEV bool utf8_packed(lds_bytes img, uint8_t* mark, bool na, uint32_t soff, uint32_t slen,
+                         uint32_t lane) {
+    const uint32_t len = na ? slen : 0u;
+    const uint32_t inc = wave_incl_scan<uint32_t>(len);
+    const uint32_t pre = inc - len;
+    const uint32_t T = wave_last<uint32_t>(inc);
+    if (T == 0) return true;
+    if (T > 256u) return utf8_lanes(img, na, soff, slen, lane);
+    reinterpret_cast<uint32_t*>(mark)[lane] = 0u;
+    wave_lds_order();
+    if (len) mark[pre] = (uint8_t)(lane + 1);
+    wave_lds_order();
+    bool bad = false;
+    uint32_t carry = 0;
+#pragma unroll 1
+    for (uint32_t b0 = 0; b0 < T; b0 += 64) {
+        const uint32_t L = b0 + lane;
+        const uint32_t j1 = max(wave_max_scan(L < T ? (uint32_t)mark[L] : 0u), carry);
+        carry = wave_last<uint32_t>(j1);
+        const int j = (int)j1 - 1;  // >= 0: text 0 starts at byte 0
+        const uint32_t s = (uint32_t)__shfl((int)soff, j, 64);
+        const uint32_t n = (uint32_t)__shfl((int)len, j, 64);
+        const uint32_t i = L - (uint32_t)__shfl((int)pre, j, 64);
+        if (L < T) {
+            const uint32_t r = s + i - 3;
+            lds_words w = (lds_words)(img + (r & ~3u));
+            const uint32_t x = alignbyte(w[1], w[0], r & 3u);  // bytes i-3 .. i
+            const uint32_t c = x >> 24;
+            const uint32_t c1 = i >= 1 ? (x >> 16) & 0xffu : 0u;
+            const uint32_t c2 = i >= 2 ? (x >> 8) & 0xffu : 0u;
+            const uint32_t c3 = i >= 3 ? x & 0xffu : 0u;
+            const bool cont = (c & 0xc0u) == 0x80u;
+            const bool need = c1 >= 0xc0u || c2 >= 0xe0u || c3 >= 0xf0u;
+            const uint32_t Lq = c < 0xc0u ? 0u : (c < 0xe0u ? 2u : (c < 0xf0u ? 3u : 4u));
+            bad |= cont != need;
+            bad |= c == 0xc0u || c == 0xc1u || c >= 0xf5u;
+            bad |= (c1 == 0xe0u && c < 0xa0u) || (c1 == 0xedu && c > 0x9fu) ||
+                   (c1 == 0xf0u && c < 0x90u) || (c1 == 0xf4u && c > 0x8fu);
+            bad |= i + Lq > n;
+        }
+    }
+    wave_lds_order();
+    return !__any(bad);
+}
+
+// A fixed-size element other than DateTime / Duration (n = 0, 1, 2, 4 or 8 payload bytes): the
+// fixed-size part of val_decode alone. q: 16 bytes from the tag; e0 / elim: tile offsets of the
+// element and of its message end.
+NXG_DEV FV fixed_elem(const uint32_t* q, uint32_t e0, uint32_t elim) {
+    const uint32_t t = q[0] & 0xffu;
+    const uint32_t bit = 1u << (t & 31u);
+    const uint32_t f1 = fixed_size1(t), n = f1 - 1u;
+    const uint32_t b0 = bswap32(alignbyte(q[1], q[0], 1)), b1 = bswap32(alignbyte(q[2], q[1], 1));
+    const bool n8 = f1 == 9u;
+    const uint32_t sh = (32u - 8u * n) & 31u;
+    const bool sgn = bit & kSgnTags;
+    const uint32_t lo32 = f1 >= 2u ? (sgn ? (uint32_t)((int32_t)b0 >> sh) : b0 >> sh)
+                                   : ((bit & B(14)) ? 1u : 0u);
+    FV o;
+    o.tag = (bit & B(17)) ? 16u : t;
+    o.fixed = n8 ? (((uint64_t)b0 << 32) | b1)
+                 : (((uint64_t)(sgn ? (uint32_t)((int32_t)lo32 >> 31) : 0u) << 32) | lo32);
+    o.aux = 0;
+    o.end = e0 + f1;
+    o.kids = 0;
+    o.soff = 0;
+    o.slen = 0;
+    o.ok = elim >= e0 + f1;
+    return o;
+}
+// fixed-size element tags fixed_elem takes (not DateTime 10, Duration 11)
+NXG_DEV bool simple_fixed(uint32_t t) { return fixed_size1(t) != 0u && t != 10u && t != 11u; }
 
 }  // namespace
 
@@ -580,7 +766,11 @@ __global__ __launch_bounds__(TPB) void nxg_fmx_check_kernel(uint64_t W, uint64_t
 }
 
 // emit: one wave per tile. The message starts come from the count / fix passes (bits per
-// chunk), so the emit pass does not walk the chain again.
+// chunk), so the emit pass does not walk the chain again. Per round of 64 messages each lane
+// decodes one: the header from 20 bytes at its start (length, id varint, tag and the 12 bytes
+// after the tag), the value by val_decode; then the text of the round (ASCII per lane, the rest
+// by the wave), the rows (64 consecutive per store), and the array elements: their starts by a
+// walk per lane (by size), then one element per lane.
 __global__ __launch_bounds__(TPB) void nxg_fmx_emit_kernel(
     const uint8_t* __restrict__ wire, uint64_t W, uint64_t nt, const TileDesc* __restrict__ td,
     const uint64_t* __restrict__ rbase, const uint64_t* __restrict__ cbase,
@@ -591,8 +781,11 @@ __global__ __launch_bounds__(TPB) void nxg_fmx_emit_kernel(
     if (t >= nt) return;
     uint8_t* img = lds[w].img;
     uint16_t* msg = lds[w].msg;
+    uint32_t* el = lds[w].el;
     const lds_bytes limg = (lds_bytes)img;
     const uint64_t t0 = t * TILE;
+    // message ends past this tile offset lie past the frame
+    const uint32_t wend = (uint32_t)min<uint64_t>(W - t0, IMG);
     TileRegs g;
     tile_load(g, wire, t0, W, lane);
     uint64_t bits = starts[t * 64 + lane];
@@ -616,80 +809,196 @@ __global__ __launch_bounds__(TPB) void nxg_fmx_emit_kernel(
         const uint32_t i = k + lane;
         const bool has = i < nm;
         const uint32_t p = has ? msg[i] : 0u;
-        // header: length (one byte), Update variant, id varint, value tag
-        const uint64_t pa = t0 + p;
-        const uint64_t lim = pa + img[p];
-        const Win16 h = win16(limg, p + 2);
-        uint64_t id;
-        const uint32_t nb = wvar(h.lo, h.hi, id);
-        const uint64_t q = pa + 2 + nb;
-        bool ok = !has || (lim <= W && nb != 0 && q < lim);
-        FVal o{0, 0, 0, 0, 0};
-        if (has && ok) ok = fast_value(limg, t0, img[q - t0], q + 1, lim, true, o);
-        const uint32_t kd = has && ok ? (uint32_t)o.kids : 0u;
-        const uint32_t kpre = wave_incl_scan<uint32_t>(kd) - kd;
-        const uint64_t cb = cnext + kpre;
-        if (has && ok) {
+        // header: length, Update variant (both checked by the count pass), id varint (at most
+        // 5 bytes: the count pass), value tag, then the 12 bytes after the tag
+        uint32_t h[5];
+        win_words<5>(limg, p, h);
+        const uint32_t lim = p + (h[0] & 0xffu);
+        const uint32_t a = alignbyte(h[1], h[0], 2), b = alignbyte(h[2], h[1], 2);  // bytes 2..9
+        const uint32_t sa = ~a & 0x80808080u;
+        const uint32_t nb = sa ? ((uint32_t)__builtin_ctz(sa) >> 3) + 1 : 5u;
+        const uint64_t id = (uint64_t)compress7_32(nb >= 4u ? a : (a & ((1u << (8u * nb)) - 1u))) |
+                            (nb == 5u ? (uint64_t)(b & 0x7fu) << 28 : 0ull);
+        const uint32_t tg = (uint32_t)(((((uint64_t)b << 32) | a) >> (8u * nb)) & 0xffu);
+        const uint32_t u = 3u + nb;  // the payload, relative to p: 4..8
+        const bool up = u >= 8u;
+        const uint32_t g0 = up ? h[2] : h[1], g1 = up ? h[3] : h[2], g2 = up ? h[4] : h[3],
+                       g3 = up ? 0u : h[4];
+        const uint32_t su = u & 3u;
+        FV o = val_decode(tg, alignbyte(g1, g0, su), alignbyte(g2, g1, su),
+                          alignbyte(g3, g2, su), p + u, lim, true, t0);
+        if (NXG_FMX_SKIP & 4) o = FV{g0, tg, g1, lim, 0, 0, 0, true};
+        bool ok = !has || ((sa != 0u || !(b & 0x80u)) && u <= (lim - p) && lim <= wend && o.ok);
+        // text: the lanes with non-ASCII bytes are checked by the whole wave
+        const bool na = !(NXG_FMX_SKIP & 2) && has && ok && o.slen && !ascii_ok(limg, o.soff, o.slen);
+        bad = __any(!ok) || !utf8_packed(limg, lds[w].mark, na, o.soff, o.slen, lane);
+        if (bad) break;
+        const uint32_t kd = has ? o.kids : 0u;
+        const uint32_t kinc = wave_incl_scan<uint32_t>(kd);
+        const uint32_t kpre = kinc - kd;
+        const uint32_t rk = wave_last<uint32_t>(kinc);
+        if (has && !(NXG_FMX_SKIP & 8)) {
             const uint64_t row = rb + i;
             cols.id[row] = id;
             cols.tag[row] = (uint8_t)o.tag;
-            cols.fixed[row] = o.tag == 19u ? cb : o.fixed;
+            cols.fixed[row] = o.tag == 19u ? cnext + kpre : o.fixed;
             cols.aux[row] = o.aux;
         }
-        // array elements (non-containers): their starts (a walk by size), then one lane each
-        const uint32_t rk = wave_sum<uint32_t>(kd);
-        uint32_t* el = lds[w].el;
-        uint64_t ep = o.next;
+        if (rk == 0 || (NXG_FMX_SKIP & 1)) {
+            cnext += rk;
+            continue;
+        }
+        // array elements (non-containers)
+        // Array elements (non-containers). Stride path: an array whose first element has a fixed
+        // size is taken to be all elements of that size; element j of the round is found from
+        // its array (a max-scan over `mark`) and checked by its own tag. Any array that does not
+        // fit (a variable-size element) sends the round to the exact walk below.
+        bool strided = false;
         if (rk <= MAXC) {
+            const uint32_t ep = o.end;
+            const uint32_t f1a = kd && ep < lim ? fixed_size1(img[ep]) : 0u;
+            if (!__any(kd && f1a == 0u)) {
+                uint8_t* mark = lds[w].mark;
+                reinterpret_cast<uint32_t*>(mark)[lane] = 0u;
+                wave_lds_order();
+                if (kd) mark[kpre] = (uint8_t)(lane + 1);
+                wave_lds_order();
+                strided = true;
+                uint32_t carry = 0;
 #pragma unroll 1
-            for (uint32_t c = 0; ok && c < kd; c++) {
-                ok = ep < lim;
-                if (!ok) break;
-                el[kpre + c] = (uint32_t)(ep - t0) | ((uint32_t)(lim - ep) << 13);
-                const uint32_t et = img[ep - t0];
-                const uint32_t f1 = fixed_size1(et);  // 1 + payload bytes (0: variable size)
-                if (f1) {
-                    ep += f1;
-                } else {
-                    FVal e{0, 0, 0, 0, 0};
-                    ok = fast_value(limg, t0, et, ep + 1, lim, false, e);
-                    ep = e.next;
-                }
-            }
-            wave_lds_order();
-#pragma unroll 1
-            for (uint32_t j0 = 0; j0 < rk && !__any(!ok); j0 += 64) {
-                const uint32_t j = j0 + lane;
-                if (j < rk) {
-                    const uint32_t ev = el[j];
-                    const uint64_t e0 = t0 + (ev & 0x1fffu);
-                    FVal e{0, 0, 0, 0, 0};
-                    ok = fast_value(limg, t0, img[ev & 0x1fffu], e0 + 1, e0 + (ev >> 13), false, e);
+                for (uint32_t j0 = 0; j0 < rk; j0 += 64) {
+                    const uint32_t j = j0 + lane;
+                    const bool he = j < rk;
+                    const uint32_t a1 = max(wave_max_scan(he ? (uint32_t)mark[j] : 0u), carry);
+                    carry = wave_last<uint32_t>(a1);
+                    const int ai = (int)a1 - 1;  // mark[0] is set: the first array's kpre is 0
+                    const uint32_t fa = (uint32_t)__shfl((int)f1a, ai, 64);
+                    const uint32_t e0 = he ? (uint32_t)__shfl((int)ep, ai, 64) +
+                                                 (j - (uint32_t)__shfl((int)kpre, ai, 64)) * fa
+                                           : 8u;
+                    const uint32_t elim = he ? (uint32_t)__shfl((int)lim, ai, 64) : 16u;
+                    uint32_t q[4];
+                    win_words<4>(limg, e0, q);
+                    const uint32_t et = q[0] & 0xffu;
+                    if (!__all(!he || (e0 < elim && fixed_size1(et) == fa))) {
+                        strided = false;
+                        break;
+                    }
+                    FV e;
+                    if (__all(!he || simple_fixed(et))) {  // scalars only: no text, no branches
+                        e = fixed_elem(q, e0, elim);
+                        bad = __any(he && !e.ok);
+                    } else {  // DateTime / Duration elements
+                        e = val_decode(et, alignbyte(q[1], q[0], 1), alignbyte(q[2], q[1], 1),
+                                       alignbyte(q[3], q[2], 1), e0 + 1, elim, false, t0);
+                        bad = __any(he && !e.ok);
+                    }
+                    if (bad) break;
                     const uint64_t slot = cnext + j;
-                    if (ok && slot < cols.cap_children) {
+                    if (he && slot < cols.cap_children) {
                         cols.ctag[slot] = (uint8_t)e.tag;
                         cols.cfixed[slot] = e.fixed;
                         cols.caux[slot] = e.aux;
                     }
                 }
+                wave_lds_order();
+                if (bad) break;
+            }
+        }
+        if (strided) {
+        } else if (rk <= MAXC) {
+            // element starts: a run of elements of the first one's fixed size is confirmed 8 at
+            // a time from tags loaded together; other elements are sized by val_decode
+            uint32_t ep = o.end;
+#pragma unroll 1
+            for (uint32_t c = 0; c < kd;) {
+                if (ep >= lim) {
+                    ok = false;
+                    break;
+                }
+                const uint32_t et = img[ep];
+                const uint32_t f1 = fixed_size1(et);  // 1 + payload bytes (0: variable size)
+                if (f1) {
+                    uint32_t tg[8];
+#pragma unroll
+                    for (uint32_t r = 1; r < 8; r++) {
+                        const uint32_t x = ep + r * f1;
+                        tg[r] = c + r < kd && x < lim ? img[x] : 0xffu;
+                    }
+                    uint32_t r = 1;
+#pragma unroll
+                    for (uint32_t k = 1; k < 8; k++) r += (r == k && fixed_size1(tg[k]) == f1) ? 1u : 0u;
+#pragma unroll 1
+                    for (uint32_t k = 0; k < r; k++) {
+                        const uint32_t x = ep + k * f1;
+                        el[kpre + c + k] = x | ((lim - x) << 13);
+                    }
+                    ep += r * f1;
+                    c += r;
+                } else {
+                    el[kpre + c] = ep | ((lim - ep) << 13);
+                    uint32_t q[3];
+                    win_words<3>(limg, ep + 1, q);
+                    const FV e = val_decode(et, q[0], q[1], q[2], ep + 1, lim, false, t0);
+                    ok = e.ok;
+                    ep = e.end;
+                    c++;
+                    if (!ok) break;
+                }
+            }
+            bad = __any(!ok);
+            if (bad) break;
+            wave_lds_order();
+#pragma unroll 1
+            for (uint32_t j0 = 0; j0 < rk; j0 += 64) {
+                const uint32_t j = j0 + lane;
+                const bool he = j < rk;
+                const uint32_t ev = he ? el[j] : (8u << 13) | 8u;
+                const uint32_t e0 = ev & 0x1fffu, elim = e0 + (ev >> 13);
+                uint32_t q[4];
+                win_words<4>(limg, e0, q);
+                FV e;
+                if (__all(!he || simple_fixed(q[0] & 0xffu))) {  // scalars only: no text, no branches
+                    e = fixed_elem(q, e0, elim);
+                    bad = __any(he && !e.ok);
+                } else {
+                    e = val_decode(q[0] & 0xffu, alignbyte(q[1], q[0], 1), alignbyte(q[2], q[1], 1),
+                                   alignbyte(q[3], q[2], 1), e0 + 1, elim, false, t0);
+                    const bool eok = !he || e.ok;
+                    const bool ena = he && eok && e.slen && !ascii_ok(limg, e.soff, e.slen);
+                    bad = __any(!eok) || !utf8_packed(limg, lds[w].mark, ena, e.soff, e.slen, lane);
+                }
+                if (bad) break;
+                const uint64_t slot = cnext + j;
+                if (he && slot < cols.cap_children) {
+                    cols.ctag[slot] = (uint8_t)e.tag;
+                    cols.cfixed[slot] = e.fixed;
+                    cols.caux[slot] = e.aux;
+                }
             }
             wave_lds_order();
         } else {  // more elements than the list holds: each lane decodes its own
+            uint32_t ep = o.end;
 #pragma unroll 1
             for (uint32_t c = 0; ok && c < kd; c++) {
-                FVal e{0, 0, 0, 0, 0};
-                ok = ep < lim && fast_value(limg, t0, img[ep - t0], ep + 1, lim, false, e);
-                const uint64_t slot = cb + c;
+                ok = ep < lim;
+                if (!ok) break;
+                const uint32_t et = img[ep];
+                uint32_t q[3];
+                win_words<3>(limg, ep + 1, q);
+                const FV e = val_decode(et, q[0], q[1], q[2], ep + 1, lim, false, t0);
+                ok = e.ok && (!e.slen || utf8_ok(LdsSrc{limg, t0}, t0 + e.soff, e.slen));
+                const uint64_t slot = cnext + kpre + c;
                 if (ok && slot < cols.cap_children) {
                     cols.ctag[slot] = (uint8_t)e.tag;
                     cols.cfixed[slot] = e.fixed;
                     cols.caux[slot] = e.aux;
                 }
-                ep = e.next;
+                ep = e.end;
             }
+            bad = __any(!ok);
         }
-        bad = __any(!ok);
-        cnext += wave_sum<uint32_t>(kd);
+        cnext += rk;
     }
     if (bad && lane == 0) atomicOr(&st->fast_fail, 1u);
 }

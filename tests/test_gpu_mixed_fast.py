@@ -248,3 +248,68 @@ def test_fast_long_arrays(codec):
     assert st.err_kind == 0 and st.path == 4
     assert_same_as_oracle(cols, st, wire)
     assert reencode(codec, cols, wire) == wire
+
+
+UTF8_VALID = [
+    b"", b"a", b"\x7f", "\u0080".encode(), "߿".encode(), "ࠀ".encode(),
+    "퟿".encode(), "".encode(), "￿".encode(), "\U00010000".encode(),
+    "\U0010ffff".encode(), "é€😀Ωж".encode(), ("x" * 61 + "€").encode(),  # sequence at byte 61
+    ("€" * 40).encode(), ("y" * 63 + "😀" + "z" * 50).encode(),  # across the wave's 64 lanes
+    ("q" * 15 + "é").encode(), ("q" * 16 + "é").encode(), ("q" * 14 + "€").encode(),
+]
+UTF8_INVALID = [
+    b"\x80", b"a\xbf", b"\xc0\x80", b"\xc1\xbf", b"\xe0\x80\x80", b"\xe0\x9f\xbf",
+    b"\xed\xa0\x80", b"\xed\xbf\xbf", b"\xf0\x80\x80\x80", b"\xf0\x8f\xbf\xbf",
+    b"\xf4\x90\x80\x80", b"\xf5\x80\x80\x80", b"\xff", b"\xe2\x82", b"ab\xe2", b"\xc3",
+    b"\xc3(", b"\xe2\x28\xa1", b"\xf0\x9f\x98", b"\xc3\xa9\xa9", b"\xe2\x82\xac\x80",
+    b"x" * 62 + b"\xe2\x82", b"x" * 70 + b"\xf0\x9f\x98\x80\x80",
+]
+
+
+def _string_frame(mg, s, as_element, tag=12, n=300, seed=0):
+    rng = random.Random(seed)
+    msgs = [("u", rng.getrandbits(20), flat_value(rng, mg)) for _ in range(n)]
+    v = (19, [(9, 7), (tag, s), (6, -1)]) if as_element else (tag, s)
+    msgs.insert(n // 2, ("u", 99, v))
+    # messages of 128 bytes or more are the general decoder's
+    return mg.batch(msgs)[0], len(mg.update(99, v)) < 128
+
+
+@pytest.mark.parametrize("as_element", [False, True])
+def test_fast_utf8_valid_sequences(as_element):
+    """Text with every UTF-8 sequence length and the boundary code points, as a row and as an
+    array element: decoded on the fast path, identical to the oracle. (A fresh context per frame:
+    a frame the fast decoder declines makes a context skip it for the next calls.)"""
+    mg = _mg()
+    for k, s in enumerate(UTF8_VALID):
+        for tag in (12, 18):
+            wire, fast = _string_frame(mg, s, as_element, tag, seed=k)
+            cols, st = _decode_fresh(wire)
+            assert st.err_kind == 0 and st.path == (4 if fast else 2), (s, tag, st.path)
+            assert_same_as_oracle(cols, st, wire)
+
+
+def _decode_fresh(wire):
+    import netidx_amd
+    c = netidx_amd.Codec(0)
+    try:
+        return gpu_decode(c, wire, flags=hint())
+    finally:
+        c.close()
+
+
+@pytest.mark.parametrize("as_element", [False, True])
+def test_fast_utf8_invalid_sequences(as_element):
+    """Overlong forms, surrogates, code points past U+10FFFF, stray and missing continuation
+    bytes, sequences cut by the end of the text: the first error as the oracle's; Bytes (13)
+    with the same bytes are not text and stay on the fast path."""
+    mg = _mg()
+    for k, s in enumerate(UTF8_INVALID):
+        wire, _ = _string_frame(mg, s, as_element, seed=100 + k)
+        cols, st = _decode_fresh(wire)
+        assert st.err_kind != 0, s
+        assert_same_as_oracle(cols, st, wire)
+        wire, fast = _string_frame(mg, s, as_element, tag=13, seed=200 + k)
+        cols, st = _decode_fresh(wire)
+        assert st.err_kind == 0 and st.path == (4 if fast else 2), s
+        assert_same_as_oracle(cols, st, wire)
