@@ -38,6 +38,19 @@
 #ifndef NXG_FMX_SKIP
 #define NXG_FMX_SKIP 0  // timing experiments only: 1 elements, 2 text, 4 row values, 8 row stores
 #endif
+// timing experiments only: per-section wave clocks of the emit pass summed into DevStatus.diag
+#if NXG_FMX_PROF
+#define PMARK(k)                                          \
+    do {                                                  \
+        const uint64_t _t = __builtin_amdgcn_s_memtime(); \
+        _acc[k] += _t - _pt;                              \
+        _pt = _t;                                         \
+    } while (0)
+#else
+#define PMARK(k) \
+    do {         \
+    } while (0)
+#endif
 
 namespace fmx {
 constexpr uint32_t TILE = 4096;
@@ -491,8 +504,8 @@ NXG_DEV bool ascii_ok(lds_bytes img, uint32_t s, uint32_t n) {
     for (uint32_t k = 0; k < n; k += 32) {
         uint32_t q[8];
         win_words<8>(img, s + k, q);
-        const uint32_t f0 = first_high16(q), f1 = 16u + first_high16(q + 4);
-        na |= min(f0, f1) < n - k;
+        const uint32_t f0 = first_high16(q), f1 = first_high16(q + 4);  // 16: none
+        na |= (f0 < 16u ? f0 : (f1 < 16u ? 16u + f1 : 0xffffu)) < n - k;
     }
     return !na;
 }
@@ -599,6 +612,32 @@ NXG_DEV bool utf8_packed(lds_bytes img, uint8_t* mark, bool na, uint32_t soff, u
     }
     wave_lds_order();
     return !__any(bad);
+}
+
+// The deferred text checks of a tile: entries soff | slen << 16 in `list`, 64 per pass (ASCII per
+// lane, the rest by utf8_packed). Uniform; false on invalid UTF-8.
+NXG_DEV bool text_flush(lds_bytes img, const uint32_t* list, uint32_t ntxt, uint8_t* mark,
+                        uint32_t lane, DevStatus* st) {
+    bool good = true;
+#pragma unroll 1
+    for (uint32_t b = 0; b < ntxt && good; b += 64) {
+        const uint32_t i = b + lane;
+        const uint32_t e = i < ntxt ? list[i] : 0u;
+        const uint32_t so = e & 0xffffu, sl = e >> 16;
+        const bool na = sl && !ascii_ok(img, so, sl);
+#if NXG_FMX_PROF
+        {
+            const uint64_t nm = __ballot(na);
+            const uint32_t T = wave_sum<uint32_t>(na ? sl : 0u);
+            if (lane == 0) {
+                atomicAdd(&st->diag[4], 1ull);
+                atomicAdd(&st->diag[5], (unsigned long long)__popcll(nm) | ((unsigned long long)T << 32));
+            }
+        }
+#endif
+        good = utf8_packed(img, mark, na, so, sl, lane);
+    }
+    return good;
 }
 
 // A fixed-size element other than DateTime / Duration (n = 0, 1, 2, 4 or 8 payload bytes): the
@@ -779,6 +818,10 @@ __global__ __launch_bounds__(TPB) void nxg_fmx_emit_kernel(
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const uint64_t t = (uint64_t)blockIdx.x * (TPB / 64) + w;
     if (t >= nt) return;
+#if NXG_FMX_PROF
+    uint64_t _pt = __builtin_amdgcn_s_memtime();
+    uint64_t _acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
     uint8_t* img = lds[w].img;
     uint16_t* msg = lds[w].msg;
     uint32_t* el = lds[w].el;
@@ -804,6 +847,8 @@ __global__ __launch_bounds__(TPB) void nxg_fmx_emit_kernel(
         bits &= bits - 1;
     }
     wave_lds_order();
+    PMARK(0);
+    uint32_t ntxt = 0;  // deferred text checks in el[0, ntxt)
 #pragma unroll 1
     for (uint32_t k = 0; k < nm && !bad; k += 64) {
         const uint32_t i = k + lane;
@@ -829,9 +874,23 @@ __global__ __launch_bounds__(TPB) void nxg_fmx_emit_kernel(
                           alignbyte(g3, g2, su), p + u, lim, true, t0);
         if (NXG_FMX_SKIP & 4) o = FV{g0, tg, g1, lim, 0, 0, 0, true};
         bool ok = !has || ((sa != 0u || !(b & 0x80u)) && u <= (lim - p) && lim <= wend && o.ok);
+        PMARK(1);
         // text: the lanes with non-ASCII bytes are checked by the whole wave
-        const bool na = !(NXG_FMX_SKIP & 2) && has && ok && o.slen && !ascii_ok(limg, o.soff, o.slen);
-        bad = __any(!ok) || !utf8_packed(limg, lds[w].mark, na, o.soff, o.slen, lane);
+        // text: checked once per tile (text_flush) from a list in `el`
+        bad = __any(!ok);
+        if (!bad && !(NXG_FMX_SKIP & 2)) {
+            const bool tx = has && o.slen;
+            const uint64_t tm = __ballot(tx);
+            const uint32_t tn = (uint32_t)__popcll(tm);
+            if (ntxt + tn > MAXC) {
+                bad = !text_flush(limg, el, ntxt, lds[w].mark, lane, st);
+                ntxt = 0;
+                wave_lds_order();
+            }
+            if (tx) el[ntxt + __builtin_amdgcn_mbcnt_hi((uint32_t)(tm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)tm, 0u))] = o.soff | (o.slen << 16);
+            ntxt += tn;
+        }
+        PMARK(2);
         if (bad) break;
         const uint32_t kd = has ? o.kids : 0u;
         const uint32_t kinc = wave_incl_scan<uint32_t>(kd);
@@ -844,6 +903,7 @@ __global__ __launch_bounds__(TPB) void nxg_fmx_emit_kernel(
             cols.fixed[row] = o.tag == 19u ? cnext + kpre : o.fixed;
             cols.aux[row] = o.aux;
         }
+        PMARK(3);
         if (rk == 0 || (NXG_FMX_SKIP & 1)) {
             cnext += rk;
             continue;
@@ -857,6 +917,8 @@ __global__ __launch_bounds__(TPB) void nxg_fmx_emit_kernel(
         if (rk <= MAXC) {
             const uint32_t ep = o.end;
             const uint32_t f1a = kd && ep < lim ? fixed_size1(img[ep]) : 0u;
+#if NXG_FMX_PROF
+#endif
             if (!__any(kd && f1a == 0u)) {
                 uint8_t* mark = lds[w].mark;
                 reinterpret_cast<uint32_t*>(mark)[lane] = 0u;
@@ -872,11 +934,13 @@ __global__ __launch_bounds__(TPB) void nxg_fmx_emit_kernel(
                     const uint32_t a1 = max(wave_max_scan(he ? (uint32_t)mark[j] : 0u), carry);
                     carry = wave_last<uint32_t>(a1);
                     const int ai = (int)a1 - 1;  // mark[0] is set: the first array's kpre is 0
+                    // (ds_bpermute reads 0 from inactive lanes: all 64 take part)
                     const uint32_t fa = (uint32_t)__shfl((int)f1a, ai, 64);
-                    const uint32_t e0 = he ? (uint32_t)__shfl((int)ep, ai, 64) +
-                                                 (j - (uint32_t)__shfl((int)kpre, ai, 64)) * fa
-                                           : 8u;
-                    const uint32_t elim = he ? (uint32_t)__shfl((int)lim, ai, 64) : 16u;
+                    const uint32_t epa = (uint32_t)__shfl((int)ep, ai, 64);
+                    const uint32_t kpa = (uint32_t)__shfl((int)kpre, ai, 64);
+                    const uint32_t lma = (uint32_t)__shfl((int)lim, ai, 64);
+                    const uint32_t e0 = he ? epa + (j - kpa) * fa : 8u;
+                    const uint32_t elim = he ? lma : 16u;
                     uint32_t q[4];
                     win_words<4>(limg, e0, q);
                     const uint32_t et = q[0] & 0xffu;
@@ -904,6 +968,16 @@ __global__ __launch_bounds__(TPB) void nxg_fmx_emit_kernel(
                 wave_lds_order();
                 if (bad) break;
             }
+        }
+        PMARK(4);
+#if NXG_FMX_PROF
+        _acc[7] += strided;
+#endif
+        if (!strided && ntxt) {  // the exact walk below uses el
+            bad = !text_flush(limg, el, ntxt, lds[w].mark, lane, st);
+            ntxt = 0;
+            wave_lds_order();
+            if (bad) break;
         }
         if (strided) {
         } else if (rk <= MAXC) {
@@ -998,8 +1072,20 @@ __global__ __launch_bounds__(TPB) void nxg_fmx_emit_kernel(
             }
             bad = __any(!ok);
         }
+        PMARK(5);
         cnext += rk;
     }
+#if NXG_FMX_PROF
+    _acc[3] += (uint64_t)ntxt << 40;
+#endif
+    if (!bad && ntxt) bad = !text_flush(limg, el, ntxt, lds[w].mark, lane, st);
+#if NXG_FMX_PROF
+    _acc[6] = 1;
+    _acc[4] = 0;
+    _acc[5] = 0;
+    if (lane == 0)
+        for (int k = 0; k < 8; k++) atomicAdd(&st->diag[k], (unsigned long long)_acc[k]);
+#endif
     if (bad && lane == 0) atomicOr(&st->fast_fail, 1u);
 }
 
