@@ -375,7 +375,8 @@ bool enqueue_dec_general(NxgCtx* c, const uint8_t* f, uint64_t len, NxgColumns* 
 bool enqueue_dec_mixed(NxgCtx* c, const uint8_t* f, uint64_t len, NxgColumns* out, DevStatus* st,
                        int* path, NetidxError* err) {
     const ColsDesc d = desc_of(out);
-    if (len > 0 && d.tag && d.ctag && !c->no_fmx && c->mix_left == 0) {
+    // (frames of 4 GiB or more: the general decoder; the fast path keeps per-tile counts in 32 bits)
+    if (len > 0 && len < (1ull << 32) && d.tag && d.ctag && !c->no_fmx && c->mix_left == 0) {
         *path = FAST_MIX;
         // one buffer for both, so that a fallback does not reallocate
         const uint64_t need = std::max(nxg_fmx_scratch_bytes(len), nxg_dec_gen_scratch_bytes(len));

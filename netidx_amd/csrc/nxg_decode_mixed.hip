@@ -23,13 +23,15 @@
 // which by induction from tile 0 makes every tile's chain the true one.
 //
 //   count   per tile: entry, exit, messages, child slots (array element counts)
-//   fix     recount tiles entered off their predecessor's exit
-//   scan    prefix sums (nxg_scan_u32) -> each tile's first row and child
-//   check   the chain, the capacities, the totals
-//   emit    per tile: the message list in LDS (wave scan of the per-chunk counts), then messages
-//           k, k+64, ... per lane, decoded by fast_value (branch-light: every field from the 16
-//           bytes after the tag, selected by tag), rows written 64 at a time, children at a wave
-//           prefix of the element counts
+//   resolve one launch: recount tiles entered off their predecessor's exit, a block scan of the
+//           (messages, child slots) pairs, and the last block to arrive scans the block sums and
+//           checks the capacities (no workgroup waits on another)
+//   emit    per tile: the chain check (entry = predecessor's exit), the message list in LDS (wave
+//           scan of the per-chunk counts), then messages k, k+64, ... per lane, decoded by
+//           val_decode (every field from the bytes after the tag, selected by tag bit sets), rows
+//           written 64 at a time; text checked once per tile (ASCII per lane, the rest by one
+//           packed wave pass); array elements found by stride speculation (each element's tag
+//           confirms the size) and decoded one per lane, the exact walk as the fallback
 #include <algorithm>
 
 #include "nxg_internal.h"
@@ -723,41 +725,40 @@ __global__ __launch_bounds__(TPB) void nxg_fmx_count_kernel(const uint8_t* __res
     if (lane == 0) td[t] = d;
 }
 
-// fix pass: a tile whose entry is not its predecessor's exit is recounted from that exit. One
-// lane per tile finds them (64 tiles per wave), the wave recounts each; the others' descriptors
-// are copied. Counts go to rows[] / kids[] for the scans.
-__global__ __launch_bounds__(TPB) void nxg_fmx_fix_kernel(const uint8_t* __restrict__ wire,
-                                                          uint64_t W, uint64_t nt,
-                                                          const TileDesc* __restrict__ td,
-                                                          TileDesc* __restrict__ td2,
-                                                          uint32_t* __restrict__ rows,
-                                                          uint32_t* __restrict__ kids,
-                                                          uint64_t* __restrict__ starts) {
+// resolve: everything between the count and the emit passes in one launch (no waiting on other
+// workgroups). A lane per tile: a tile whose entry is not its predecessor's exit is recounted
+// from that exit by its wave, tile by tile; then a block scan of (rows | child slots << 32) gives
+// each tile its offset in the block (tloc), and the last block to arrive (a counter in the call's
+// status slot, DevStatus.diag[7], zeroed with the slot) scans the block sums (bpre), checks the
+// capacities and writes the totals. The chain (every entry its predecessor's exit) is checked by
+// the emit pass. Frames are shorter than 2^32 bytes here, so both halves stay in 32 bits.
+__global__ __launch_bounds__(TPB) void nxg_fmx_resolve_kernel(
+    const uint8_t* __restrict__ wire, uint64_t W, uint64_t nt, const TileDesc* __restrict__ td,
+    TileDesc* __restrict__ td2, uint64_t* __restrict__ starts, uint64_t* __restrict__ tloc,
+    uint64_t* __restrict__ bsum, uint64_t* __restrict__ bpre, uint64_t cap_rows,
+    uint64_t cap_children, DevStatus* __restrict__ st) {
     __shared__ __attribute__((aligned(16))) CountLds lds[TPB / 64];
+    __shared__ uint64_t scan_tmp[TPB / 64];
+    __shared__ uint32_t is_last;
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const uint64_t base = ((uint64_t)blockIdx.x * (TPB / 64) + w) * 64;
-    if (base >= nt) return;
-    const uint64_t tl = base + lane;
+    const uint64_t tl = (uint64_t)blockIdx.x * TPB + threadIdx.x;
+    TileDesc d{FAIL, FAIL, 0, 0};
     bool mis = false;
     if (tl < nt) {
-        const TileDesc d = td[tl];
+        d = td[tl];
         if (tl > 0) {
-            // (a failed predecessor fails the frame in the check pass)
+            // (a failed predecessor fails the frame in the emit pass's chain check)
             const uint32_t px = td[tl - 1].exit;
             mis = px != FAIL && px - TILE != d.entry;
-        }
-        if (!mis) {
-            td2[tl] = d;
-            rows[tl] = d.rows;
-            kids[tl] = d.kids;
         }
     }
     uint64_t m = __ballot(mis);
     uint8_t* img = lds[w].img;
 #pragma unroll 1
     while (m) {
-        const uint64_t t = base + (uint32_t)__builtin_ctzll(m);
+        const uint32_t j = (uint32_t)__builtin_ctzll(m);
         m &= m - 1;
+        const uint64_t t = tl - lane + j;
         const uint32_t px = td[t - 1].exit;
         const uint64_t t0 = t * TILE;
         const uint32_t lim = (uint32_t)min<uint64_t>(TILE, W - t0);
@@ -766,42 +767,45 @@ __global__ __launch_bounds__(TPB) void nxg_fmx_fix_kernel(const uint8_t* __restr
         tile_store(img, g, lane);
         const Cands cd = lane_cands(img, lane, lim);
         uint64_t bits;
-        const TileDesc d = count_from(img, cd, px - TILE, lim, t + 1 == nt, lane, bits);
+        const TileDesc r = count_from(img, cd, px - TILE, lim, t + 1 == nt, lane, bits);
         starts[t * 64 + lane] = bits;
-        if (lane == 0) {
-            td2[t] = d;
-            rows[t] = d.rows;
-            kids[t] = d.kids;
+        if (lane == j) d = r;
+    }
+    if (tl < nt) td2[tl] = d;
+    const uint64_t v = tl < nt ? (uint64_t)d.rows | ((uint64_t)d.kids << 32) : 0ull;
+    uint64_t tot;
+    const uint64_t ex = block_excl_scan<uint64_t, TPB>(v, scan_tmp, &tot);
+    if (tl < nt) tloc[tl] = ex;
+    if (threadIdx.x == 0) st_agent(&bsum[blockIdx.x], tot);
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0)
+        is_last = atomicAdd(&st->diag[7], 1ull) == (unsigned long long)gridDim.x - 1;
+    __syncthreads();
+    if (!is_last) return;
+    __threadfence();
+    const uint32_t nb = gridDim.x;
+    uint64_t run = 0;
+#pragma unroll 1
+    for (uint32_t b0 = 0; b0 < nb; b0 += TPB) {
+        const uint32_t b = b0 + threadIdx.x;
+        const uint64_t x = b < nb ? ld_agent(&bsum[b]) : 0ull;
+        uint64_t t2;
+        const uint64_t e2 = block_excl_scan<uint64_t, TPB>(x, scan_tmp, &t2);
+        if (b < nb) bpre[b] = run + e2;
+        run += t2;
+    }
+    if (threadIdx.x == 0) {
+        const uint64_t nr = run & 0xffffffffull, nc = run >> 32;
+        // columns too small: the general decoder reports the capacity error
+        if (nr > cap_rows || nc > cap_children) {
+            atomicOr(&st->fast_fail, 1u);
+        } else {
+            st->n_rows = nr;
+            st->n_children = nc;
+            st->path = 4;  // the fast mixed decoder (mixed layout)
         }
     }
-}
-
-// resolve: every tile's entry is its predecessor's exit (the first: 0); totals to the status
-__global__ __launch_bounds__(TPB) void nxg_fmx_check_kernel(uint64_t W, uint64_t nt,
-                                                            const TileDesc* __restrict__ td,
-                                                            const uint64_t* __restrict__ rbase,
-                                                            const uint64_t* __restrict__ cbase,
-                                                            uint64_t cap_rows, uint64_t cap_children,
-                                                            DevStatus* __restrict__ st) {
-    const uint64_t t = (uint64_t)blockIdx.x * TPB + threadIdx.x;
-    bool bad = false;
-    if (t < nt) {
-        const TileDesc d = td[t];
-        if (d.entry == FAIL) bad = true;
-        else if (t == 0) bad = d.entry != 0;
-        else bad = td[t - 1].exit != d.entry + TILE;
-        if (t == nt - 1) {
-            const uint64_t nr = rbase[t] + d.rows, nc = cbase[t] + d.kids;
-            // columns too small: the general decoder reports the capacity error
-            if (nr > cap_rows || nc > cap_children) bad = true;
-            if (!bad) {
-                st->n_rows = nr;
-                st->n_children = nc;
-                st->path = 4;  // the fast mixed decoder (mixed layout)
-            }
-        }
-    }
-    if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(&st->fast_fail, 1u);
 }
 
 // emit: one wave per tile. The message starts come from the count / fix passes (bits per
@@ -812,7 +816,7 @@ __global__ __launch_bounds__(TPB) void nxg_fmx_check_kernel(uint64_t W, uint64_t
 // walk per lane (by size), then one element per lane.
 __global__ __launch_bounds__(TPB) void nxg_fmx_emit_kernel(
     const uint8_t* __restrict__ wire, uint64_t W, uint64_t nt, const TileDesc* __restrict__ td,
-    const uint64_t* __restrict__ rbase, const uint64_t* __restrict__ cbase,
+    const uint64_t* __restrict__ tloc, const uint64_t* __restrict__ bpre,
     const uint64_t* __restrict__ starts, ColsDesc cols, DevStatus* __restrict__ st) {
     __shared__ __attribute__((aligned(16))) EmitLds lds[TPB / 64];
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -832,15 +836,21 @@ __global__ __launch_bounds__(TPB) void nxg_fmx_emit_kernel(
     TileRegs g;
     tile_load(g, wire, t0, W, lane);
     uint64_t bits = starts[t * 64 + lane];
-    const uint32_t nm = td[t].rows;
-    const uint64_t rb = rbase[t];
-    uint64_t cnext = cbase[t];  // first child slot of this round's messages
+    const TileDesc d = td[t];
+    // the chain: this tile is entered at its predecessor's exit (tile 0 at 0); the count pass
+    // made the last tile end exactly at W
+    const uint32_t px = t ? td[t - 1].exit : TILE;
+    const uint64_t base = bpre[t / TPB] + tloc[t];
+    const uint32_t nm = d.rows;
+    const uint64_t rb = base & 0xffffffffull;
+    uint64_t cnext = base >> 32;  // first child slot of this round's messages
     if (ld_agent32(&st->fast_fail)) return;
     tile_store(img, g, lane);
     // the message list in wire order
     const uint32_t n0 = (uint32_t)__popcll(bits);
     uint32_t at = wave_incl_scan<uint32_t>(n0) - n0;
-    bool bad = wave_last<uint32_t>(at + n0) != nm;
+    bool bad = d.entry == FAIL || px == FAIL || px - TILE != d.entry ||
+               wave_last<uint32_t>(at + n0) != nm;
 #pragma unroll 1
     while (bits) {
         msg[at++] = (uint16_t)(lane * CH + (uint32_t)__builtin_ctzll(bits));
@@ -1084,7 +1094,7 @@ __global__ __launch_bounds__(TPB) void nxg_fmx_emit_kernel(
     _acc[4] = 0;
     _acc[5] = 0;
     if (lane == 0)
-        for (int k = 0; k < 8; k++) atomicAdd(&st->diag[k], (unsigned long long)_acc[k]);
+        for (int k = 0; k < 7; k++) atomicAdd(&st->diag[k], (unsigned long long)_acc[k]);
 #endif
     if (bad && lane == 0) atomicOr(&st->fast_fail, 1u);
 }
@@ -1094,9 +1104,9 @@ uint64_t nxg_fmx_tiles(uint64_t W) { return (W + TILE - 1) / TILE; }
 
 uint64_t nxg_fmx_scratch_bytes(uint64_t W) {
     const uint64_t nt = nxg_fmx_tiles(W);
-    // 2 descs 32 B, message starts 512 B, rows + kids 8 B, rbase + cbase 16 B per tile, block
-    // sums, alignment
-    return nt * 568 + 2 * 8 * (nt / 4096 + 2) + 8 * 16;
+    // 2 descs 32 B, message starts 512 B, tloc 8 B per tile; bsum + bpre 16 B per 256 tiles;
+    // alignment
+    return nt * 552 + 16 * (nt / TPB + 1) + 6 * 16;
 }
 
 // persistent grids: every workgroup co-resident (count: [0], emit: [1])
@@ -1124,28 +1134,21 @@ hipError_t nxg_launch_dec_fmx(const uint8_t* wire, uint64_t W, const ColsDesc& c
     TileDesc* td = reinterpret_cast<TileDesc*>(take(16 * nt));
     TileDesc* td2 = reinterpret_cast<TileDesc*>(take(16 * nt));
     uint64_t* starts = reinterpret_cast<uint64_t*>(take(512 * nt));
-    uint32_t* rows = reinterpret_cast<uint32_t*>(take(4 * nt));
-    uint32_t* kids = reinterpret_cast<uint32_t*>(take(4 * nt));
-    uint64_t* rbase = reinterpret_cast<uint64_t*>(take(8 * nt));
-    uint64_t* cbase = reinterpret_cast<uint64_t*>(take(8 * nt));
-    uint64_t* bs0 = reinterpret_cast<uint64_t*>(take(8 * (nt / 4096 + 2)));
-    uint64_t* bs1 = reinterpret_cast<uint64_t*>(take(8 * (nt / 4096 + 2)));
+    uint64_t* tloc = reinterpret_cast<uint64_t*>(take(8 * nt));
+    const uint64_t nb = (nt + TPB - 1) / TPB;
+    uint64_t* bsum = reinterpret_cast<uint64_t*>(take(8 * nb));
+    uint64_t* bpre = reinterpret_cast<uint64_t*>(take(8 * nb));
     constexpr uint64_t WV = TPB / 64;  // waves per workgroup
     // one tile per wave measured faster than persistent waves with the next tile prefetched
     // (count 184 vs 237 us, emit 534 vs 653 us at 10^7 records): the passes are bound by the
     // latency of their own LDS walks, which more resident waves hide better
     (void)wgs;
-    const uint32_t gc = (uint32_t)((nt + WV - 1) / WV), ge = gc;
+    const uint32_t gc = (uint32_t)((nt + WV - 1) / WV);
     hipLaunchKernelGGL(nxg_fmx_count_kernel, dim3(gc), dim3(TPB), 0, s, wire, W, nt, td, starts,
                        nxg_take_zero_slot());
-    hipLaunchKernelGGL(nxg_fmx_fix_kernel, dim3((uint32_t)((nt + 64 * WV - 1) / (64 * WV))),
-                       dim3(TPB), 0, s, wire, W, nt, td, td2, rows, kids, starts);
-    hipError_t e;
-    if ((e = nxg_scan_u32(rows, nt, rbase, bs0, s)) != hipSuccess) return e;
-    if ((e = nxg_scan_u32(kids, nt, cbase, bs1, s)) != hipSuccess) return e;
-    hipLaunchKernelGGL(nxg_fmx_check_kernel, dim3((uint32_t)((nt + TPB - 1) / TPB)), dim3(TPB), 0,
-                       s, W, nt, td2, rbase, cbase, cols.cap_rows, cols.cap_children, st);
-    hipLaunchKernelGGL(nxg_fmx_emit_kernel, dim3(ge), dim3(TPB), 0, s, wire, W, nt, td2, rbase,
-                       cbase, starts, cols, st);
+    hipLaunchKernelGGL(nxg_fmx_resolve_kernel, dim3((uint32_t)nb), dim3(TPB), 0, s, wire, W, nt,
+                       td, td2, starts, tloc, bsum, bpre, cols.cap_rows, cols.cap_children, st);
+    hipLaunchKernelGGL(nxg_fmx_emit_kernel, dim3(gc), dim3(TPB), 0, s, wire, W, nt, td2, tloc,
+                       bpre, starts, cols, st);
     return hipGetLastError();
 }
