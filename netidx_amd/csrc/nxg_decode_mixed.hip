@@ -209,29 +209,39 @@ NXG_DEV Cands lane_cands(const uint8_t* img, uint32_t lane, uint32_t lim) {
 // chunk j+1's (chunk j lies inside one message), END = at or past the tile end, FAIL = anywhere
 // else. Chunk j maps the state in front of it to the state behind it: from N_a the chain runs to
 // x_a, which lies in chunk j+1 or j+2 (messages are < 128 bytes) and must be a first or second
-// candidate there; F_a becomes N_a; END and FAIL stay. These maps (6 states x 3 bits) compose
+// candidate there; F_a becomes N_a; END and FAIL stay. These maps (a byte per state) compose
 // associatively, so a wave scan of them gives every chunk's entry state at once. A chain that
 // enters some chunk at a third candidate comes out FAIL here and goes to tile_chain.
 constexpr uint32_t S_N0 = 0, S_N1 = 1, S_F0 = 2, S_F1 = 3, S_FAIL = 4, S_END = 5;
-constexpr uint32_t T_ID = (0u << 0) | (1u << 3) | (2u << 6) | (3u << 9) | (4u << 12) | (5u << 15);
-NXG_DEV uint32_t tget(uint32_t T, uint32_t st) { return (T >> (3 * st)) & 7u; }
-NXG_DEV uint32_t tcompose(uint32_t later, uint32_t earlier) {
-    uint32_t c = 0;
-#pragma unroll
-    for (uint32_t st = 0; st < 6; st++) c |= tget(later, tget(earlier, st)) << (3 * st);
-    return c;
+// A map is 8 bytes (states 0..7, byte s = the image of s) in two words; composing two maps is a
+// byte select of the later map by the earlier one (v_perm_b32: selector bytes 0..3 pick bytes
+// of its second operand, 4..7 of its first).
+struct SMap {
+    uint32_t lo, hi;
+};
+constexpr uint32_t ID_LO = 0x03020100u, ID_HI = 0x07060504u;
+NXG_DEV SMap scompose(SMap later, SMap earlier) {
+    return SMap{__builtin_amdgcn_perm(later.hi, later.lo, earlier.lo),
+                __builtin_amdgcn_perm(later.hi, later.lo, earlier.hi)};
+}
+NXG_DEV uint32_t sget(SMap m, uint32_t st) {
+    return ((st < 4u ? m.lo : m.hi) >> (8u * (st & 3u))) & 0xffu;
 }
 template <int CTRL, int ROWS>
 NXG_DEV uint32_t dpp_fill(uint32_t v, uint32_t fill) {
     return (uint32_t)__builtin_amdgcn_update_dpp((int)fill, (int)v, CTRL, ROWS, 0xf, false);
 }
-NXG_DEV uint32_t tscan(uint32_t T) {  // inclusive: lane j gets T_j o ... o T_0
-    T = tcompose(T, dpp_fill<0x111, 0xf>(T, T_ID));
-    T = tcompose(T, dpp_fill<0x112, 0xf>(T, T_ID));
-    T = tcompose(T, dpp_fill<0x114, 0xf>(T, T_ID));
-    T = tcompose(T, dpp_fill<0x118, 0xf>(T, T_ID));
-    T = tcompose(T, dpp_fill<0x142, 0xa>(T, T_ID));
-    T = tcompose(T, dpp_fill<0x143, 0xc>(T, T_ID));
+template <int CTRL, int ROWS>
+NXG_DEV SMap dpp_map(SMap m) {
+    return SMap{dpp_fill<CTRL, ROWS>(m.lo, ID_LO), dpp_fill<CTRL, ROWS>(m.hi, ID_HI)};
+}
+NXG_DEV SMap sscan(SMap T) {  // inclusive: lane j gets T_j o ... o T_0
+    T = scompose(T, dpp_map<0x111, 0xf>(T));
+    T = scompose(T, dpp_map<0x112, 0xf>(T));
+    T = scompose(T, dpp_map<0x114, 0xf>(T));
+    T = scompose(T, dpp_map<0x118, 0xf>(T));
+    T = scompose(T, dpp_map<0x142, 0xa>(T));
+    T = scompose(T, dpp_map<0x143, 0xc>(T));
     return T;
 }
 
@@ -249,8 +259,9 @@ NXG_DEV uint32_t tile_chain_scan(uint32_t e, uint32_t lim, uint32_t lane, uint32
         if (d == 2) return x == c0nn ? S_F0 : (x == c1nn ? S_F1 : S_FAIL);
         return S_FAIL;
     };
-    const uint32_t T = out(x0) | (out(x1) << 3) | (S_N0 << 6) | (S_N1 << 9) | (S_FAIL << 12) |
-                       (S_END << 15);
+    // F0 -> N0, F1 -> N1, FAIL and END (and the unused 6, 7) stay
+    const SMap T{out(x0) | (out(x1) << 8) | (S_N0 << 16) | (S_N1 << 24),
+                 S_FAIL | (S_END << 8) | (6u << 16) | (7u << 24)};
     // the state in front of chunk 0
     uint32_t s0;
     if (e >= lim) {
@@ -267,7 +278,7 @@ NXG_DEV uint32_t tile_chain_scan(uint32_t e, uint32_t lim, uint32_t lane, uint32
         s0 = S_FAIL;
     }
     if (s0 == S_FAIL) return FAIL;
-    const uint32_t sout = tget(tscan(T), s0);          // state behind chunk j
+    const uint32_t sout = sget(sscan(T), s0);          // state behind chunk j
     const uint32_t sin = dpp_fill<0x138, 0xf>(sout, s0);  // in front of chunk j (wave_shr:1)
     if (wave_last<uint32_t>(sout) != S_END) return FAIL;
     if (sin == S_N0) ce = c0;
@@ -753,6 +764,12 @@ __global__ __launch_bounds__(TPB) void nxg_fmx_resolve_kernel(
         }
     }
     uint64_t m = __ballot(mis);
+#if NXG_FMX_PROF
+    if (lane == 0 && m) {
+        atomicAdd(&st->diag[5], (unsigned long long)__popcll(m));
+        atomicMax(&st->diag[4], (unsigned long long)__popcll(m));
+    }
+#endif
     uint8_t* img = lds[w].img;
 #pragma unroll 1
     while (m) {
@@ -776,14 +793,16 @@ __global__ __launch_bounds__(TPB) void nxg_fmx_resolve_kernel(
     uint64_t tot;
     const uint64_t ex = block_excl_scan<uint64_t, TPB>(v, scan_tmp, &tot);
     if (tl < nt) tloc[tl] = ex;
-    if (threadIdx.x == 0) st_agent(&bsum[blockIdx.x], tot);
-    __threadfence();
-    __syncthreads();
-    if (threadIdx.x == 0)
+    // the block sum goes out with an agent-scope store and is drained before the arrival count
+    // (an agent-scope fence would write back the XCD's L2, full of the count pass's output);
+    // the last block reads the sums with agent-scope loads
+    if (threadIdx.x == 0) {
+        st_agent(&bsum[blockIdx.x], tot);
+        drain_stores();
         is_last = atomicAdd(&st->diag[7], 1ull) == (unsigned long long)gridDim.x - 1;
+    }
     __syncthreads();
     if (!is_last) return;
-    __threadfence();
     const uint32_t nb = gridDim.x;
     uint64_t run = 0;
 #pragma unroll 1
