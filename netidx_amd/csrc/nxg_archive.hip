@@ -43,7 +43,10 @@ namespace {
 
 using namespace nxgmsg;
 
-constexpr uint32_t CH = 1024;  // bytes per chunk (one lane)
+#ifndef NXG_ARCH_CH
+#define NXG_ARCH_CH 1024  // timing experiments: 512 and 256 measured slower (more breaks)
+#endif
+constexpr uint32_t CH = NXG_ARCH_CH;  // bytes per chunk (one lane)
 constexpr uint32_t TPB = 256;
 constexpr uint64_t ERR = ~0ull;       // a chunk exit after a structural decode error
 constexpr uint32_t BATCH_ITEM = 24;   // size_of::<BatchItem>() for check_sz! (parity unpinned)
