@@ -27,6 +27,10 @@
 // Value -- after the count varint the host writes at [0, arch_base). No length prefix, no variant.
 #include "nxg_device.h"
 
+#ifndef NXG_ENC_LBU
+#define NXG_ENC_LBU 1  // look-back window, 64 * NXG_ENC_LBU tiles per round trip (1, 4 and 8 measured equal)
+#endif
+
 namespace {
 
 constexpr int TPB = 256;
@@ -422,7 +426,7 @@ __global__ __launch_bounds__(TPB) void nxg_enc_rows_kernel(
             uint64_t base = 0;
             if (tile != 0) {
                 bool give_up;
-                base = lookback_prefix<1>(tstat, tile, epoch, nullptr, give_up);
+                base = lookback_prefix<NXG_ENC_LBU>(tstat, tile, epoch, nullptr, give_up);
                 if (give_up && lane == 0) atomicOr(&st->timeout, 1u);
                 if (lane == 0) st_agent(&tstat[tile], lb_word(kFlagInc, epoch, base + tot));
             }
