@@ -27,6 +27,9 @@
 // Value -- after the count varint the host writes at [0, arch_base). No length prefix, no variant.
 #include "nxg_device.h"
 
+#ifndef NXG_ENC_SKIP
+#define NXG_ENC_SKIP 0  // timing experiments only
+#endif
 #ifndef NXG_ENC_LBU
 #define NXG_ENC_LBU 1  // look-back window, 64 * NXG_ENC_LBU tiles per round trip (1, 4 and 8 measured equal)
 #endif
@@ -426,7 +429,11 @@ __global__ __launch_bounds__(TPB) void nxg_enc_rows_kernel(
             uint64_t base = 0;
             if (tile != 0) {
                 bool give_up;
+#if NXG_ENC_SKIP & 1
+                give_up = false;  // timing experiments only: no look-back (wrong offsets)
+#else
                 base = lookback_prefix<NXG_ENC_LBU>(tstat, tile, epoch, nullptr, give_up);
+#endif
                 if (give_up && lane == 0) atomicOr(&st->timeout, 1u);
                 if (lane == 0) st_agent(&tstat[tile], lb_word(kFlagInc, epoch, base + tot));
             }
