@@ -14,7 +14,7 @@ if [ "$cmd" = build ]; then
   done
   exit 0
 fi
-for rep in 1 2; do
+for rep in ${REPS:-1 2}; do
   for name in "$@"; do
     for N in 10000000 100000000; do
       lib=$R/netidx_amd/build_ab/$name/libnxg_codec.so
