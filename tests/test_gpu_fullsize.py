@@ -5,9 +5,10 @@ oracle (oracle/nx_oracle.c) on EVERY column and EVERY byte -- no sampling, no se
   configs[2]  decode 10^7 mixed records            (every column, children, control spans)
   configs[3]  encode 10^7 records, f64 and mixed   (product encode vs the oracle encoder's bytes)
 
-plus the f64 decoders' robustness cases: ids whose varints cross 2^28 (5-byte ids), ids in random
-order (record lengths vary record to record: the persistent decoder takes the frame), the
-length-run decoder's exact path on every tile, and two decodes running at once on two streams.
+plus a frame past the Infinity Cache (the XCD-ordered emit) and the f64 decoders' robustness
+cases: ids whose varints cross 2^28 (5-byte ids), ids in random order (record lengths vary record
+to record: the persistent decoder takes the frame), the length-run decoder's exact path on every
+tile, and two decodes running at once on two streams.
 Reference rules: netidx-core/src/pack.rs:504-555, netidx-value/src/lib.rs:470-506.
 """
 import os
@@ -55,6 +56,22 @@ def test_config2_f64_decode_10m_every_row(codec):
     ids, vals = synth.f64_columns(n)
     wire = nxo.encode_f64(ids, vals)
     assert len(wire) == 147_886_336
+    cols = Columns(n, 0, 0, netidx_amd.LAYOUT_F64, "cuda")
+    st = _decode_dev(codec, wire, cols)
+    _assert_f64(cols, st, wire, n)
+
+
+def test_f64_decode_past_the_infinity_cache_every_row(codec):
+    """A 2 * 10^7-record frame (296 MB, past the 256 MiB Infinity Cache): the length-run emit
+    takes its XCD-contiguous workgroup order there; every row against the oracle."""
+    import netidx_amd
+    from netidx_amd import synth
+    from netidx_amd.codec import Columns
+    n = 20_000_000
+    ids, vals = synth.f64_columns(n)
+    import nxo
+    wire = nxo.encode_f64(ids, vals)
+    assert len(wire) > 256 << 20
     cols = Columns(n, 0, 0, netidx_amd.LAYOUT_F64, "cuda")
     st = _decode_dev(codec, wire, cols)
     _assert_f64(cols, st, wire, n)
