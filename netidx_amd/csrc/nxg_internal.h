@@ -25,7 +25,8 @@ struct DevStatus {
     uint64_t split_start;
     // diagnostics (general decode): 0 redo tiles, 1 look-back fallbacks, 2 repair rounds,
     // 3 lane walks, 4 speculation attempts, 5 tiles without a speculated entry,
-    // 6 exhausted (budgeted) walks, 7 work-list entries of the emit pass
+    // 6 exhausted (budgeted) walks, 7 work-list entries of the emit pass. The fast mixed decode
+    // (path 4) uses diag[7] as its resolve pass's arrival counter (zeroed with the slot).
     unsigned long long diag[8];
 };
 static_assert(sizeof(DevStatus) == 160, "DevStatus layout");
