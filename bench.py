@@ -90,12 +90,30 @@ def make_f64_wire(codec, n, rank):
     return cols, wire
 
 
-def time_decode(codec, wire, out, n, steps, warmup, world, stream, flags=0):
-    """Returns (wall seconds max over ranks, mean kernel ms, last status)."""
+def time_decode(codec, wire, out, n, steps, warmup, world, stream, flags=0, stream_of_frames=False):
+    """Returns (wall seconds max over ranks, mean kernel ms, last status). stream_of_frames: the
+    frames go through nxg_decode_frames_async (a connection's backlog: frame j+1's probe runs in
+    frame j's emit launch), up to 500 per call; else one nxg_decode_updates_async per frame."""
     import torch
     nbytes = wire.numel()
+
+    def enqueue(k):
+        if stream_of_frames:
+            i = 0
+            while i < k:
+                m = min(500, k - i)
+                codec.decode_frames_async([wire.data_ptr()] * m, [nbytes] * m, [out] * m, flags)
+                i += m
+                if i < k:
+                    codec.sync()
+            return
+        for i in range(k):
+            codec.decode_async(wire.data_ptr(), nbytes, out, flags)
+            if (i + 1) % 500 == 0 and i + 1 < k:  # at most 512 async calls in flight
+                codec.sync()
+
     for _ in range(warmup):
-        codec.decode_async(wire.data_ptr(), nbytes, out, flags)
+        enqueue(1)
         codec.sync()
     barrier(world)
     torch.cuda.synchronize()
@@ -103,10 +121,7 @@ def time_decode(codec, wire, out, n, steps, warmup, world, stream, flags=0):
     e1 = torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     e0.record(stream)
-    for i in range(steps):
-        codec.decode_async(wire.data_ptr(), nbytes, out, flags)
-        if (i + 1) % 500 == 0 and i + 1 < steps:  # at most 512 async calls in flight
-            codec.sync()
+    enqueue(steps)
     e1.record(stream)
     st = codec.sync()
     torch.cuda.synchronize()

@@ -148,6 +148,17 @@ bool nxg_decode_updates(NxgCtx* ctx, const uint8_t* frame, uint64_t len, NxgColu
 bool nxg_decode_updates_async(NxgCtx* ctx, const uint8_t* dframe, uint64_t len, NxgColumns* dout,
                               uint32_t flags, NetidxError* err);
 bool nxg_ctx_sync(NxgCtx* ctx, NxgStatus* st, NetidxError* err);
+/* A connection's backlog of frames (read_task hands decode_task frame after frame over a
+ * channel, channel.rs:379-443 / connection.rs:209-242): n device frames, each decoded into its own
+ * device columns (outs[j]; the same columns may be passed for several frames, the later frame then
+ * overwrites them), in order, as n nxg_decode_updates_async calls would. Every frame must be
+ * complete in device memory when the call is made (work still queued on the ctx stream may not
+ * produce it). On the homogeneous-f64 path the frames are pipelined: the record-length probe of
+ * frame j + 1 runs in the same launch as the column emit of frame j. nxg_ctx_sync completes them
+ * (and reruns any frame the fast path rejected); every frame counts as one in-flight call. */
+bool nxg_decode_frames_async(NxgCtx* ctx, uint32_t n, const uint8_t* const* dframes,
+                             const uint64_t* lens, NxgColumns* const* douts, uint32_t flags,
+                             NetidxError* err);
 
 /* ---- encode: replaces handle_updates' queue_send loop (server.rs:610-612) ----------------
  * `heap` holds the bytes that string/bytes/decimal/abstract offsets and ctl spans refer to.
@@ -205,17 +216,47 @@ bool nxg_comm_unique_id(uint8_t id[128], NetidxError* err);
 NxgComm* nxg_comm_init(NxgCtx* ctx, int nranks, int rank, const uint8_t id[128],
                        NetidxError* err);
 void nxg_comm_destroy(NxgComm* comm);
+/* A caller-provided transport for the sharded calls instead of RCCL (the application's own MPI
+ * or TCP collectives; the tests' gloo), and optionally a caller-provided local codec instead of
+ * the ctx's kernels. Collective functions are called by every rank in the same order and return
+ * true on success. The protocol (nxg_encode_allgather, nxg_decode_sharded) is the same code for
+ * every transport: every rank's failure is exchanged in the next collective, so all ranks return
+ * false together (none is left waiting in a collective). */
+typedef struct NxgCommOps {
+    void* user;
+    /* collective: `bytes` bytes at `mine` (host memory) from every rank, in rank order, into
+     * `all` (host memory, nranks * bytes) */
+    bool (*allgather)(void* user, const void* mine, void* all, uint64_t bytes);
+    /* collective: `buf` (device memory; host memory with the codec hooks below) holds this
+     * rank's shard at [off[rank], off[rank + 1]); afterwards every rank's buf holds every shard
+     * at its offset (off has nranks + 1 entries) */
+    bool (*allgatherv)(void* user, uint8_t* buf, const uint64_t* off, uint32_t nranks,
+                       uint32_t rank);
+    /* local codec, all three or none (NULL: the ctx's kernels): the contracts of
+     * nxg_encoded_len, nxg_encode_updates and nxg_decode_range */
+    bool (*encoded_len)(void* user, const NxgColumns* in, const uint8_t* heap, uint64_t* len);
+    bool (*encode)(void* user, const NxgColumns* in, const uint8_t* heap, uint8_t* out,
+                   uint64_t cap, uint64_t* len);
+    bool (*decode_range)(void* user, const uint8_t* frame, uint64_t frame_len, uint64_t begin,
+                         uint64_t end, NxgColumns* out, NxgRange* rng);
+} NxgCommOps;
+/* Not collective. ctx may be NULL when ops carries the local codec. The ops struct is copied. */
+NxgComm* nxg_comm_init_ops(NxgCtx* ctx, int nranks, int rank, const NxgCommOps* ops,
+                           NetidxError* err);
 /* BASELINE configs[4]: every rank encodes its shard of the batch (rows in rank order) straight
  * into its place in the full frame (an 8-byte all-gather of the shard sizes first), then grouped
  * send/recv deliver every shard into the same offsets on every rank: no padding, no compaction.
  * *len_out = the full frame length; shard_off[0 .. nranks) = each shard's byte offset (may be
- * NULL). Device columns and buffers. */
+ * NULL). Device columns and buffers (host ones with an ops comm's local codec). A failure on any
+ * rank (its encode, a capacity short of the frame) makes every rank return false. */
 bool nxg_encode_allgather(NxgCtx* ctx, NxgComm* comm, const NxgColumns* din, const uint8_t* dheap,
                           uint8_t* dout, uint64_t cap, uint64_t* len_out, uint64_t* shard_off,
                           NetidxError* err);
 /* One frame (on every rank's device) decoded in nranks byte ranges: rank r decodes range r,
  * the summaries are all-gathered and linked; a range whose guessed entry is off the chain is
- * decoded again from its predecessor's exit. *row_off = this rank's first global row. */
+ * decoded again from its predecessor's exit. *row_off = this rank's first global row. Every rank
+ * returns the same verdict: a range that fails to decode, is not a homogeneous-f64 range, or a
+ * frame that does not link makes all of them return false. */
 bool nxg_decode_sharded(NxgCtx* ctx, NxgComm* comm, const uint8_t* dframe, uint64_t frame_len,
                         NxgColumns* dout, uint64_t* row_off, NxgRange* rng, NetidxError* err);
 

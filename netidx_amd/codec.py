@@ -131,6 +131,8 @@ SIGNATURES = {
                                             C.POINTER(NxgColumns), C.c_uint32,
                                             C.POINTER(NetidxError)]),
     "nxg_ctx_sync": (C.c_bool, [C.c_void_p, C.POINTER(NxgStatus), C.POINTER(NetidxError)]),
+    "nxg_decode_frames_async": (C.c_bool, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p,
+                                           C.c_void_p, C.c_uint32, C.POINTER(NetidxError)]),
     "nxg_encoded_len": (C.c_bool, [C.c_void_p, C.POINTER(NxgColumns), C.c_void_p,
                                    C.POINTER(C.c_uint64), C.POINTER(NetidxError)]),
     "nxg_encode_updates": (C.c_bool, [C.c_void_p, C.POINTER(NxgColumns), C.c_void_p, C.c_void_p,
@@ -149,6 +151,8 @@ SIGNATURES = {
     "nxg_comm_unique_id": (C.c_bool, [C.c_void_p, C.POINTER(NetidxError)]),
     "nxg_comm_init": (C.c_void_p, [C.c_void_p, C.c_int, C.c_int, C.c_void_p,
                                    C.POINTER(NetidxError)]),
+    "nxg_comm_init_ops": (C.c_void_p, [C.c_void_p, C.c_int, C.c_int, C.c_void_p,
+                                       C.POINTER(NetidxError)]),
     "nxg_comm_destroy": (None, [C.c_void_p]),
     "nxg_encode_allgather": (C.c_bool, [C.c_void_p, C.c_void_p, C.POINTER(NxgColumns),
                                         C.c_void_p, C.c_void_p, C.c_uint64,
@@ -388,6 +392,16 @@ class Codec:
         err = NetidxError()
         _check(lib().nxg_decode_updates_async(self.ctx, C.c_void_p(dframe_ptr), nbytes,
                                               C.byref(cols.s), flags, C.byref(err)), err)
+
+    def decode_frames_async(self, dframe_ptrs, lens, cols_list, flags=0):
+        """A backlog of device frames (nxg_decode_frames_async), decoded in order; frame j into
+        cols_list[j] (one Columns object may repeat). Complete with sync()."""
+        n = len(dframe_ptrs)
+        fp = (C.c_void_p * n)(*[int(p) for p in dframe_ptrs])
+        ln = (C.c_uint64 * n)(*[int(x) for x in lens])
+        cp = (C.c_void_p * n)(*[C.addressof(c.s) for c in cols_list])
+        err = NetidxError()
+        _check(lib().nxg_decode_frames_async(self.ctx, n, fp, ln, cp, flags, C.byref(err)), err)
 
     def sync(self, check=True):
         st, err = NxgStatus(), NetidxError()
@@ -818,8 +832,39 @@ def range_link(ranges, frame_len):
     return (offs[:n], None) if ok else (None, int(bad.value))
 
 
+_AG = C.CFUNCTYPE(C.c_bool, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64)
+_AGV = C.CFUNCTYPE(C.c_bool, C.c_void_p, C.c_void_p, C.POINTER(C.c_uint64), C.c_uint32,
+                   C.c_uint32)
+_ELEN = C.CFUNCTYPE(C.c_bool, C.c_void_p, C.POINTER(NxgColumns), C.c_void_p,
+                    C.POINTER(C.c_uint64))
+_ENC = C.CFUNCTYPE(C.c_bool, C.c_void_p, C.POINTER(NxgColumns), C.c_void_p, C.c_void_p,
+                   C.c_uint64, C.POINTER(C.c_uint64))
+_DRNG = C.CFUNCTYPE(C.c_bool, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint64,
+                    C.POINTER(NxgColumns), C.POINTER(NxgRange))
+
+
+class NxgCommOps(C.Structure):
+    _fields_ = [("user", C.c_void_p), ("allgather", _AG), ("allgatherv", _AGV),
+                ("encoded_len", _ELEN), ("encode", _ENC), ("decode_range", _DRNG)]
+
+
+def _guard(fn):
+    """A Python callback behind a C function pointer: an exception becomes `false` (the library
+    then agrees the failure with the other ranks) after it is printed."""
+    def call(*a):
+        try:
+            r = fn(*a)
+            return True if r is None else bool(r)
+        except Exception:  # noqa: BLE001 -- reported, then turned into the C failure code
+            import traceback
+            traceback.print_exc()
+            return False
+    return call
+
+
 class Comm:
-    """RCCL communicator of the sharded calls (one process per GPU)."""
+    """Communicator of the sharded calls (one process per GPU): RCCL (nxg_comm_init), or a
+    caller-provided transport and optional local codec (nxg_comm_init_ops, Comm.with_ops)."""
 
     @staticmethod
     def unique_id():
@@ -833,6 +878,51 @@ class Comm:
         self.h = lib().nxg_comm_init(codec.ctx, nranks, rank, C.byref(b), C.byref(err))
         _check(self.h is not None, err)
         self.codec, self.nranks, self.rank = codec, nranks, rank
+
+    @classmethod
+    def with_ops(cls, codec, nranks, rank, allgather, allgatherv, encoded_len=None, encode=None,
+                 decode_range=None):
+        """nxg_comm_init_ops. allgather(mine: bytes) -> bytes of every rank's, in rank order;
+        allgatherv(buf_ptr, offsets, nranks, rank) fills every shard of the buffer at its
+        offset. The optional local codec: encoded_len(NxgColumns) -> int; encode(NxgColumns,
+        out_ptr, cap) -> int; decode_range(frame_ptr, frame_len, begin, end, NxgColumns) ->
+        (begin, end, entry, exit, n_rows, ok, err_kind). codec may be None with the codec."""
+        self = cls.__new__(cls)
+
+        def ag(user, mine, all_, nbytes):
+            got = allgather(C.string_at(mine, nbytes))
+            assert len(got) == nbytes * nranks
+            C.memmove(all_, got, len(got))
+
+        def agv(user, buf, off, n, r):
+            allgatherv(int(buf or 0), [int(off[i]) for i in range(n + 1)], int(n), int(r))
+
+        fns = [_AG(_guard(ag)), _AGV(_guard(agv))]
+        if decode_range is not None:
+            def elen(user, cols, heap, out):
+                out[0] = int(encoded_len(cols.contents))
+
+            def enc(user, cols, heap, out, cap, n):
+                n[0] = int(encode(cols.contents, int(out or 0), int(cap)))
+
+            def drng(user, frame, flen, b, e, cols, rng):
+                t = decode_range(int(frame or 0), int(flen), int(b), int(e), cols.contents)
+                rng[0] = t if isinstance(t, NxgRange) else NxgRange.of(t)
+
+            fns += [_ELEN(_guard(elen)), _ENC(_guard(enc)), _DRNG(_guard(drng))]
+        else:
+            fns += [_ELEN(), _ENC(), _DRNG()]
+        self._fns = fns  # the C function pointers live as long as the communicator
+        self.ops = NxgCommOps(None, *fns)
+        err = NetidxError()
+        self.h = lib().nxg_comm_init_ops(codec.ctx if codec else None, nranks, rank,
+                                         C.byref(self.ops), C.byref(err))
+        _check(self.h is not None, err)
+        self.codec, self.nranks, self.rank = codec, nranks, rank
+        return self
+
+    def _ctx(self):
+        return self.codec.ctx if self.codec else None
 
     def close(self):
         if getattr(self, "h", None):
@@ -849,7 +939,8 @@ class Comm:
         """Every rank's shard into one frame on every rank; returns (length, shard offsets)."""
         n, err = C.c_uint64(0), NetidxError()
         offs = np.zeros(self.nranks, np.uint64)
-        _check(lib().nxg_encode_allgather(self.codec.ctx, self.h, C.byref(cols.s),
+        cs = cols.s if hasattr(cols, "s") else cols
+        _check(lib().nxg_encode_allgather(self._ctx(), self.h, C.byref(cs),
                                           _heap_ptr(heap), C.c_void_p(out_ptr), cap, C.byref(n),
                                           C.c_void_p(offs.ctypes.data), C.byref(err)), err)
         return n.value, [int(x) for x in offs]
@@ -858,8 +949,9 @@ class Comm:
         """This rank's byte range of one frame; returns (first global row, NxgRange)."""
         ptr = dframe.data_ptr() if hasattr(dframe, "data_ptr") else int(dframe)
         off, rng, err = C.c_uint64(0), NxgRange(), NetidxError()
-        _check(lib().nxg_decode_sharded(self.codec.ctx, self.h, C.c_void_p(ptr), frame_len,
-                                        C.byref(cols.s), C.byref(off), C.byref(rng),
+        cs = cols.s if hasattr(cols, "s") else cols
+        _check(lib().nxg_decode_sharded(self._ctx(), self.h, C.c_void_p(ptr), frame_len,
+                                        C.byref(cs), C.byref(off), C.byref(rng),
                                         C.byref(err)), err)
         return off.value, rng
 

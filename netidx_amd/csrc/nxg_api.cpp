@@ -59,25 +59,20 @@ struct NxgCtx {
     uint32_t epoch = 0;
     uint64_t* tstat = nullptr;
     size_t tstat_words = 0;
-    uint64_t* fscratch = nullptr;  // f64 decode: per-run / per-workgroup record counts
-    int wgs_dec_f64 = 0;
-    uint8_t* fmoff = nullptr;      // f64 decode: merge-point offsets, 64 B per tile
-    size_t fmoff_cap = 0;
     uint32_t* glws = nullptr;      // general decode: lane words, 256 B per tile
     size_t glws_cap = 0;
     uint64_t* gruns = nullptr;     // general decode: run summaries + bases
     uint8_t* dscratch = nullptr;   // dispatch: counters, offsets, block sums, unmatched count
     size_t dscratch_cap = 0;
     int wgs_dec_gen = 0;
-    int wgs_dec_f64_1p = 0;
-    bool f64_2pass = false;  // NXG_F64_2PASS=1: the two-pass count/emit f64 decoder
     // f64 decoder choice: the length-run decoder (nxg_decode_f64_run.hip) unless the frames of
-    // this connection have record lengths that vary record to record; then the persistent
-    // single-pass decoder for the next kIrregularCalls calls (NXG_F64_PATH=1p forces it)
+    // this connection have record lengths that vary record to record; then the single-pass
+    // decoder of any f64 frame (nxg_decode_f64_x.hip) for the next kIrregularCalls calls
+    // (NXG_F64_PATH=x forces it)
     uint8_t* rdesc = nullptr;  // length-run decoder: 16-byte tile descriptors
     size_t rdesc_cap = 0;
     uint32_t irregular_left = 0;
-    bool force_1p = false;
+    bool force_x = false;
     // mixed decode: the fast decoder (nxg_decode_mixed.hip) unless it rejected a recent frame of
     // this connection; then the general decoder for the next kMixFailCalls calls
     // (NXG_MIXED_PATH=general: always the general decoder)
@@ -154,18 +149,6 @@ bool ensure_tstat(NxgCtx* c, size_t words, NetidxError* err) {
     HIPCHK(hipMalloc(&c->tstat, n * 8));
     HIPCHK(hipMemsetAsync(c->tstat, 0, n * 8, c->stream));
     c->tstat_words = n;
-    return true;
-}
-
-bool ensure_fmoff(NxgCtx* c, size_t bytes, NetidxError* err) {
-    if (bytes <= c->fmoff_cap) return true;
-    size_t n = std::max(bytes, c->fmoff_cap * 2);
-    n = std::max<size_t>(n, 1 << 16);
-    HIPCHK(hipStreamSynchronize(c->stream));
-    if (c->fmoff) HIPCHK(hipFree(c->fmoff));
-    c->fmoff = nullptr;
-    HIPCHK(hipMalloc(&c->fmoff, n));
-    c->fmoff_cap = n;
     return true;
 }
 
@@ -300,7 +283,7 @@ constexpr uint32_t kIrregularCalls = 64;
 constexpr uint32_t kMixFailCalls = 16;
 
 // path codes of a fast attempt (Pending::fast): homogeneous f64 (RUN, 1P) or mixed (MIX)
-enum { FAST_NONE = 0, FAST_RUN = 1, FAST_1P = 2, FAST_MIX = 3 };
+enum { FAST_NONE = 0, FAST_RUN = 1, FAST_X = 2, FAST_MIX = 3 };
 
 bool ensure_rdesc(NxgCtx* c, size_t bytes, NetidxError* err) {
     if (bytes <= c->rdesc_cap) return true;
@@ -314,14 +297,19 @@ bool ensure_rdesc(NxgCtx* c, size_t bytes, NetidxError* err) {
     return true;
 }
 
-// the persistent (or two-pass) decoder
-bool enqueue_dec_1p(NxgCtx* c, const uint8_t* f, uint64_t len, NxgColumns* out, DevStatus* st,
-                    NetidxError* err);
+// the single-pass decoder of any f64 frame
+bool enqueue_dec_x(NxgCtx* c, const uint8_t* f, uint64_t len, NxgColumns* out, DevStatus* st,
+                   NetidxError* err) {
+    if (!ensure_tstat(c, nxg_dec_f64x_groups(len), err)) return false;
+    HIPCHK(nxg_launch_dec_f64x(f, len, out->id, out->fixed, out->cap_rows, c->tstat, c->epoch, st,
+                               c->stream));
+    return true;
+}
 
 // Homogeneous-f64 attempt; *path receives the FAST_* code of the decoder that was enqueued.
 bool enqueue_dec_fast(NxgCtx* c, const uint8_t* f, uint64_t len, NxgColumns* out, DevStatus* st,
                       int* path, NetidxError* err) {
-    if (!c->f64_2pass && !c->force_1p && c->irregular_left == 0) {
+    if (!c->force_x && c->irregular_left == 0) {
         *path = FAST_RUN;
         if (!ensure_tstat(c, nxg_dec_f64r_groups(len), err)) return false;
         if (!ensure_rdesc(c, 16 * nxg_dec_f64r_tiles(len), err)) return false;
@@ -330,22 +318,8 @@ bool enqueue_dec_fast(NxgCtx* c, const uint8_t* f, uint64_t len, NxgColumns* out
         return true;
     }
     if (c->irregular_left) c->irregular_left--;
-    *path = FAST_1P;
-    return enqueue_dec_1p(c, f, len, out, st, err);
-}
-
-bool enqueue_dec_1p(NxgCtx* c, const uint8_t* f, uint64_t len, NxgColumns* out, DevStatus* st,
-                    NetidxError* err) {
-    if (!c->f64_2pass && c->wgs_dec_f64_1p >= 2) {
-        if (!ensure_tstat(c, 2 * nxg_dec_f64_1p_tiles(len), err)) return false;
-        HIPCHK(nxg_launch_dec_f64_1p(f, len, out->id, out->fixed, out->cap_rows, c->tstat,
-                                     c->epoch, c->wgs_dec_f64_1p, st, c->stream));
-        return true;
-    }
-    if (!ensure_fmoff(c, 64 * nxg_dec_f64_tiles(len), err)) return false;
-    HIPCHK(nxg_launch_dec_f64(f, len, out->id, out->fixed, out->cap_rows, c->fscratch, c->fmoff,
-                              c->wgs_dec_f64, st, c->stream));
-    return true;
+    *path = FAST_X;
+    return enqueue_dec_x(c, f, len, out, st, err);
 }
 
 bool ensure_glws(NxgCtx* c, size_t bytes, NetidxError* err) {
@@ -403,13 +377,13 @@ bool finish_decode(NxgCtx* c, const uint8_t* f, uint64_t len, NxgColumns* out, i
     }
     DevStatus h = c->hst[slot];
     if (tried_fast == FAST_RUN && len > 0 && h.fast_fail && h.irregular) {
-        // record lengths vary record to record: the persistent decoder, for this frame and the
-        // next kIrregularCalls ones
+        // record lengths vary record to record: the single-pass decoder of any f64 frame, for
+        // this frame and the next kIrregularCalls ones
         c->irregular_left = kIrregularCalls;
         DevStatus* st2;
         uint32_t slot2;
         if (!begin_call(c, &st2, &slot2, err)) return false;
-        const bool ok = enqueue_dec_1p(c, f, len, out, st2, err);
+        const bool ok = enqueue_dec_x(c, f, len, out, st2, err);
         if (!end_call(c, err) || !ok) return false;
         HIPCHK(hipMemcpyAsync(c->hst + slot2, st2, sizeof(DevStatus), hipMemcpyDeviceToHost,
                               c->stream));
@@ -638,21 +612,13 @@ NxgCtx* nxg_ctx_new(int device, NetidxError* err) {
     if ((e = hipHostMalloc(&c->hst, sizeof(DevStatus) * kStatusRing, hipHostMallocDefault)) !=
         hipSuccess)
         return fail("hipHostMalloc(status)", e);
-    // f64 decode scratch: per-run and per-workgroup record counts
-    const size_t fw = f64dec::SCRATCH_WORDS;
-    if ((e = hipMalloc(&c->fscratch, fw * 8)) != hipSuccess) return fail("hipMalloc(fscratch)", e);
-    if ((e = hipMemset(c->fscratch, 0, fw * 8)) != hipSuccess) return fail("hipMemset(fscratch)", e);
-    c->wgs_dec_f64 = nxg_dec_f64_wgs(c->ncu);
     // general decode: run summaries + bases (no initialisation needed)
     const size_t gw = (size_t)gdec2::MAX_RUNS * (gdec2::RUN_WORDS + 4);
     if ((e = hipMalloc(&c->gruns, gw * 8)) != hipSuccess) return fail("hipMalloc(gruns)", e);
     c->wgs_dec_gen = nxg_dec_gen_wgs(c->ncu);
     nxg_fmx_wgs(c->ncu, c->wgs_fmx);
-    c->wgs_dec_f64_1p = nxg_dec_f64_1p_wgs(c->ncu);
-    const char* f2 = getenv("NXG_F64_2PASS");
-    c->f64_2pass = f2 && f2[0] == '1';
     const char* fp = getenv("NXG_F64_PATH");
-    c->force_1p = fp && strcmp(fp, "1p") == 0;
+    c->force_x = fp && strcmp(fp, "x") == 0;
     const char* mp = getenv("NXG_MIXED_PATH");
     c->no_fmx = mp && strcmp(mp, "general") == 0;
     const char* ff = getenv("NXG_F64R_FLAGS");
@@ -666,8 +632,6 @@ void nxg_ctx_destroy(NxgCtx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->dcols_valid) cols_free_impl(&c->dcols);
     if (c->tstat) (void)hipFree(c->tstat);
-    if (c->fscratch) (void)hipFree(c->fscratch);
-    if (c->fmoff) (void)hipFree(c->fmoff);
     if (c->glws) (void)hipFree(c->glws);
     if (c->gruns) (void)hipFree(c->gruns);
     if (c->dscratch) (void)hipFree(c->dscratch);
@@ -800,6 +764,67 @@ bool nxg_decode_updates_async(NxgCtx* c, const uint8_t* dframe, uint64_t len, Nx
                         : enqueue_dec_mixed(c, dframe, len, dout, st, &fast, err);
     if (!end_call(c, err) || !ok) return false;
     c->pending.push_back({1, fast, dframe, len, dout, nullptr, 0, st, slot});
+    return true;
+}
+
+bool nxg_decode_frames_async(NxgCtx* c, uint32_t n, const uint8_t* const* dframes,
+                             const uint64_t* lens, NxgColumns* const* douts, uint32_t flags,
+                             NetidxError* err) {
+    if (!c || (n && (!dframes || !lens || !douts))) {
+        set_err(err, "null argument");
+        return false;
+    }
+    if (c->pending.size() + n > kStatusRing / 2) {
+        set_err(err, "too many in-flight async calls (max %d); call nxg_ctx_sync", kStatusRing / 2);
+        return false;
+    }
+    uint64_t max_len = 0;
+    for (uint32_t j = 0; j < n; j++) {
+        if (!douts[j] || (!dframes[j] && lens[j])) {
+            set_err(err, "null frame or columns at %u", j);
+            return false;
+        }
+        if (douts[j]->mem != NXG_MEM_DEVICE || ((uintptr_t)dframes[j] & 15)) {
+            set_err(err, "async decode needs device columns and 16-byte aligned device frames");
+            return false;
+        }
+        max_len = std::max(max_len, lens[j]);
+    }
+    const bool run_path = !(flags & NXG_DECODE_HINT_MIXED) && !c->force_x &&
+                          c->irregular_left == 0 && n > 1;
+    if (!run_path) {
+        for (uint32_t j = 0; j < n; j++)
+            if (!nxg_decode_updates_async(c, dframes[j], lens[j], douts[j], flags, err))
+                return false;
+        return true;
+    }
+    if (!set_device(c, err)) return false;
+    // two descriptor arrays: frame j's probe runs beside frame j - 1's emit
+    const size_t half = (16 * nxg_dec_f64r_tiles(max_len) + 255) & ~(size_t)255;
+    if (!ensure_tstat(c, nxg_dec_f64r_groups(max_len), err)) return false;
+    if (!ensure_rdesc(c, 2 * half, err)) return false;
+    std::vector<NxgF64rFrame> fr(n);
+    uint32_t nonempty = 0;  // descriptor arrays alternate over the frames that launch
+    for (uint32_t j = 0; j < n; j++) {
+        DevStatus* st;
+        uint32_t slot;
+        if (!begin_call(c, &st, &slot, err)) return false;
+        NxgF64rFrame& f = fr[j];
+        f.wire = dframes[j];
+        f.W = lens[j];
+        f.oid = douts[j]->id;
+        f.oval = douts[j]->fixed;
+        f.cap = douts[j]->cap_rows;
+        f.desc = c->rdesc + (nonempty & 1) * half;
+        if (lens[j]) nonempty++;
+        f.epoch = c->epoch;
+        f.st = st;
+        f.zst = nxg_take_zero_slot();
+        // an empty frame launches nothing: its zero-ahead slot is cleared here
+        if (lens[j] == 0) HIPCHK(hipMemsetAsync(f.zst, 0, sizeof(DevStatus), c->stream));
+        c->pending.push_back({1, FAST_RUN, dframes[j], lens[j], douts[j], nullptr, 0, st, slot});
+    }
+    HIPCHK(nxg_launch_dec_f64r_stream(fr.data(), n, c->tstat, c->f64r_flags, c->stream));
     return true;
 }
 

@@ -29,7 +29,10 @@
 // every valid record start in that window starts a walk, and the walks are advanced in position
 // order until they coincide. The true chain passes through the merge point, which depends only
 // on the bytes, so the lane that owns the previous chunk computes the same position.
+#include <vector>
+
 #include "nxg_device.h"
+#include "nxg_f64_rec16.h"
 
 namespace f64r {
 #ifndef NXG_F64R_T
@@ -70,136 +73,7 @@ static_assert(sizeof(Desc) == 16, "Desc is one 16-byte load");
 
 namespace {
 using namespace f64r;
-
-NXG_DEV uint4 ld16r(const uint8_t* __restrict__ p) { return *reinterpret_cast<const uint4*>(p); }
-// the bytes of [off, off+16) that lie inside the frame, zero-filled (out of line: rare)
-__device__ __attribute__((noinline)) uint4 ld16_tail(const uint8_t* __restrict__ wire,
-                                                    uint64_t off, uint64_t W) {
-    uint32_t v[4] = {0, 0, 0, 0};
-#pragma unroll
-    for (int k = 0; k < 16; k++)
-        if (off + k < W) v[k >> 2] |= (uint32_t)wire[off + k] << (8 * (k & 3));
-    return make_uint4(v[0], v[1], v[2], v[3]);
-}
-NXG_DEV uint4 ld16g(const uint8_t* __restrict__ wire, uint64_t off, uint64_t W) {
-    if (off + 16 <= W) return ld16r(wire + off);
-    return ld16_tail(wire, off, W);
-}
-
-// 16 bytes at byte s (0..15) of the 32 bytes d[0..7] (little-endian dwords), no memory access
-NXG_DEV void extract16(const uint32_t (&d)[8], uint32_t s, uint32_t& e0, uint32_t& e1,
-                       uint32_t& e2, uint32_t& e3) {
-    // two levels of selects on the dword offset q = s / 4 (masks, not a dynamic array index,
-    // which the compiler would lower to scratch memory)
-    const uint32_t r = s & 3u;
-    const uint32_t m2 = 0u - ((s >> 3) & 1u), m1 = 0u - ((s >> 2) & 1u);
-    uint32_t g[6], f[5];
-#pragma unroll
-    for (int j = 0; j < 6; j++) g[j] = d[j] ^ ((d[j] ^ d[j + 2]) & m2);
-#pragma unroll
-    for (int j = 0; j < 5; j++) f[j] = g[j] ^ ((g[j] ^ g[j + 1]) & m1);
-    e0 = alignbyte(f[1], f[0], r);
-    e1 = alignbyte(f[2], f[1], r);
-    e2 = alignbyte(f[3], f[2], r);
-    e3 = alignbyte(f[4], f[3], r);
-}
-
-// A valid f64 Update record (L in 12..16: 1..5 id bytes) at e0,e1? Returns L or 0.
-// rem = bytes from the record start to the frame end.
-NXG_DEV uint32_t rec_check16(uint32_t e0, uint32_t e1, uint64_t rem) {
-    const uint32_t L = e0 & 0xffu;
-    const bool head = (L - 12u <= 4u) && (((e0 >> 8) & 0xffu) == 4u);
-    const uint32_t sh = 8u * ((L - 11u) & 7u);  // 8 * nb
-    const uint64_t x = ((((uint64_t)e1) << 32) | e0) >> 16;  // bytes 2..7
-    const uint64_t m = (1ull << sh) - 1ull;
-    const uint64_t want = 0x8080808080ull & (m >> 8);
-    const bool var = (x & 0x808080808080ull & m) == want;  // exactly nb varint bytes
-    const uint32_t tag = (uint32_t)(x >> sh) & 0xffu;       // Value tag after the id
-    return (head && var && tag == 9u && rem >= L) ? L : 0u;
-}
-
-// id and f64 bits of a record of length L (12..16) already checked by rec_check16
-NXG_DEV void rec_decode16(uint32_t e0, uint32_t e1, uint32_t e2, uint32_t e3, uint32_t L,
-                          uint64_t& id, uint64_t& val) {
-    const uint32_t sh = 8u * ((L - 11u) & 7u);
-    const uint64_t x = ((((uint64_t)e1) << 32) | e0) >> 16;
-    const uint64_t y = x & ((1ull << sh) - 1ull) & 0x7f7f7f7f7full;
-    id = (y & 0x7full) | ((y >> 1) & 0x3f80ull) | ((y >> 2) & 0x1fc000ull) |
-         ((y >> 3) & 0xfe00000ull) | ((y >> 4) & 0x7f0000000ull);
-    const uint32_t o = L - 8u;  // value offset, 4..8
-    const uint32_t lo = o >= 8u ? e2 : alignbyte(e2, e1, o & 3u);
-    const uint32_t hi = o >= 8u ? e3 : alignbyte(e3, e2, o & 3u);
-    val = ((uint64_t)bswap32(lo) << 32) | bswap32(hi);  // big-endian f64 (pack.rs:592-598)
-}
-
-// SWAR: 0x80 in each byte of x whose value is in [12, 16] (record lengths)
-NXG_DEV uint32_t len_bytes(uint32_t x) {
-    const uint32_t y = x & 0x7f7f7f7fu;
-    return (0x90909090u - y) & ~x & (y + 0x74747474u) & 0x80808080u;
-}
-// candidate starts in positions 0..15 of d[0..4]: a byte in 12..16 followed by 0x04
-NXG_DEV uint32_t cand16(uint32_t d0, uint32_t d1, uint32_t d2, uint32_t d3, uint32_t d4) {
-    const uint32_t a = nib(len_bytes(d0)) | (nib(len_bytes(d1)) << 4) | (nib(len_bytes(d2)) << 8) |
-                       (nib(len_bytes(d3)) << 12);
-    const uint32_t b = nib(zero_bytes(d0 ^ 0x04040404u)) | (nib(zero_bytes(d1 ^ 0x04040404u)) << 4) |
-                       (nib(zero_bytes(d2 ^ 0x04040404u)) << 8) |
-                       (nib(zero_bytes(d3 ^ 0x04040404u)) << 12) |
-                       (nib(zero_bytes(d4 ^ 0x04040404u)) << 16);
-    return a & (b >> 1) & 0xffffu;
-}
-
-// 16 bytes at LDS byte offset rel (any alignment)
-NXG_DEV void lds16(const uint8_t* buf, uint32_t rel, uint32_t& e0, uint32_t& e1, uint32_t& e2,
-                   uint32_t& e3) {
-    const uint32_t* w = reinterpret_cast<const uint32_t*>(buf + (rel & ~3u));
-    const uint32_t s = rel & 3u;
-    const uint32_t d0 = w[0], d1 = w[1], d2 = w[2], d3 = w[3], d4 = w[4];
-    e0 = alignbyte(d1, d0, s);
-    e1 = alignbyte(d2, d1, s);
-    e2 = alignbyte(d3, d2, s);
-    e3 = alignbyte(d4, d3, s);
-}
-
-constexpr uint32_t FAILX = 0xffffffffu;
-constexpr int WIN = 64;  // merge walks must coincide within 64 bytes of the chunk start
-
-// Merge point of all record walks starting in [r, r+16) of the LDS image (r 4-aligned), as a
-// position relative to the image; the END position (W - a0) for a chunk at or past the frame's
-// end; FAILX if the walks do not merge.
-NXG_DEV uint32_t merge16(const uint8_t* buf, uint32_t r, uint64_t a0, uint64_t W) {
-    // positions are signed: an exact tile at the start of a byte range images 64 bytes before it
-    const int64_t abs_r = (int64_t)a0 + (int64_t)r;
-    if (abs_r >= (int64_t)W) return (uint32_t)((int64_t)W - (int64_t)a0);
-    const uint64_t remr = (uint64_t)((int64_t)W - abs_r);
-    const uint32_t* w = reinterpret_cast<const uint32_t*>(buf + r);
-    uint32_t cand = cand16(w[0], w[1], w[2], w[3], w[4]);
-    uint64_t S = 0;
-    if (remr < 16) S |= 1ull << remr;  // the frame end is a valid (terminal) position
-    while (cand) {
-        const uint32_t p = __builtin_ctz(cand);
-        cand &= cand - 1;
-        uint32_t e0, e1, e2, e3;
-        lds16(buf, r + p, e0, e1, e2, e3);
-        if (rec_check16(e0, e1, remr - p)) S |= 1ull << p;
-    }
-    for (int it = 0; it < WIN && __popcll(S) > 1; it++) {
-        const uint32_t p = __builtin_ctzll(S);
-        S &= S - 1;
-        uint32_t e0, e1, e2, e3;
-        lds16(buf, r + p, e0, e1, e2, e3);
-        const uint32_t L = rec_check16(e0, e1, remr - p);
-        const uint32_t np = p + L;
-        if (np >= (uint32_t)WIN) return FAILX;
-        bool ok = (np == remr);
-        if (!ok) {
-            lds16(buf, r + np, e0, e1, e2, e3);
-            ok = rec_check16(e0, e1, remr - np) != 0;
-        }
-        if (ok) S |= 1ull << np;
-    }
-    if (__popcll(S) != 1) return FAILX;
-    return r + (uint32_t)__builtin_ctzll(S);
-}
+using namespace f64rec16;
 
 // Exact path for tile t, by the whole wave, in 4 KiB sub-tiles. A sub-tile at a0 owns the
 // records that START in [a0, a0 + 4096), like a uniform tile. Its LDS image holds the bytes
@@ -213,19 +87,6 @@ NXG_DEV uint32_t merge16(const uint8_t* buf, uint32_t r, uint64_t a0, uint64_t W
 constexpr uint32_t XLO = 64;            // image offset of a0
 constexpr uint32_t XHI = XLO + SUB;     // image offset of a0 + 4096
 constexpr uint32_t IMGB = XHI + HALO;   // image bytes
-// the bytes of the 16 at `pos` (signed, relative to wire) that lie in [-pre, W), zero-filled
-__device__ __attribute__((noinline)) uint4 ld16_pre(const uint8_t* __restrict__ wire,
-                                                   int64_t pos, uint64_t W, uint64_t pre) {
-    uint32_t v[4] = {0, 0, 0, 0};
-#pragma unroll
-    for (int k = 0; k < 16; k++) {
-        const int64_t q = pos + k;
-        if (q >= -(int64_t)pre && q < (int64_t)W)
-            v[k >> 2] |= (uint32_t)wire[q] << (8 * (k & 3));
-    }
-    return make_uint4(v[0], v[1], v[2], v[3]);
-}
-
 // `pre`: bytes readable before wire[0] (a byte range that does not start the frame)
 template <bool EMIT>
 NXG_DEV void exact_tile(const uint8_t* __restrict__ wire, uint64_t W, uint64_t R, bool first,
@@ -502,16 +363,41 @@ NXG_DEV void probe_fast(const uint8_t* __restrict__ wire, uint64_t W, uint64_t t
 // ---- probe: one lane per tile ------------------------------------------------------------------
 // wire: the decoded range's first byte; W: bytes from there to the frame end; R (<= W): the
 // range's length (records that START before R are the range's; the rest is look-ahead)
-__global__ __launch_bounds__(TPB) void nxg_f64r_probe_kernel(
-    const uint8_t* __restrict__ wire, uint64_t W, uint64_t R, uint64_t pre, uint64_t nt,
-    Desc* __restrict__ desc, uint64_t* tstat, uint32_t epoch, uint32_t flags,
-    DevStatus* __restrict__ st, DevStatus* zst) {
-    zero_status(zst);
-    __shared__ __attribute__((aligned(16))) uint8_t img[TPB / 64][IMGB];
-    __shared__ uint64_t scan_tmp[TPB / 64];
-    __shared__ uint64_t sh_base;
+// One frame's probe (or emit) launch arguments. The fused launch (nxg_f64r_fused_kernel) takes
+// one of each: the emit of frame j and the probe of frame j + 1 of a stream of frames.
+struct ProbeArgs {
+    const uint8_t* wire;
+    uint64_t W, R, pre, nt;
+    Desc* desc;
+    uint64_t* tstat;
+    uint32_t epoch, flags;
+    DevStatus* st;
+    DevStatus* zst;
+};
+struct EmitArgs {
+    const uint8_t* wire;
+    uint64_t W, R, pre, nt;
+    const Desc* desc;
+    uint64_t* oid;
+    uint64_t* oval;
+    uint64_t cap;
+    uint32_t flags, ne;  // ne: the emit's workgroups (the XCD remap's grid)
+    DevStatus* st;
+};
+
+// bid: this workgroup's probe index (the workgroups of one probe are numbered 0.. in dispatch
+// order: the look-back waits only on lower ones)
+NXG_DEV void probe_body(const ProbeArgs& a, uint32_t bid, uint8_t (*img)[IMGB],
+                        uint64_t* scan_tmp, uint64_t& sh_base) {
+    const uint8_t* __restrict__ wire = a.wire;
+    const uint64_t W = a.W, R = a.R, pre = a.pre, nt = a.nt;
+    Desc* __restrict__ desc = a.desc;
+    uint64_t* tstat = a.tstat;
+    const uint32_t epoch = a.epoch, flags = a.flags;
+    DevStatus* __restrict__ st = a.st;
+    if (bid == 0 && threadIdx.x == 0 && a.zst) *a.zst = DevStatus{};
     const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const uint64_t t = (uint64_t)blockIdx.x * TPB + tid;
+    const uint64_t t = (uint64_t)bid * TPB + tid;
     const bool has = t < nt;
     const uint64_t t0 = t * T;
     const uint32_t lim = has ? (R - t0 < T ? (uint32_t)(R - t0) : T) : 0u;
@@ -524,7 +410,7 @@ __global__ __launch_bounds__(TPB) void nxg_f64r_probe_kernel(
     // in 8 off the runs, here or in any workgroup so far) is left to the persistent decoder, which
     // the host reruns it on
     const int nirr = __syncthreads_count(state != 0);
-    const uint64_t ntg = nt - (uint64_t)blockIdx.x * TPB < TPB ? nt - (uint64_t)blockIdx.x * TPB
+    const uint64_t ntg = nt - (uint64_t)bid * TPB < TPB ? nt - (uint64_t)bid * TPB
                                                                : TPB;
     const bool bail = !(flags & F_NO_BAIL) &&
                       ((uint64_t)nirr * 8 > ntg || (nirr && ld_agent32(&st->irregular)));
@@ -540,7 +426,7 @@ __global__ __launch_bounds__(TPB) void nxg_f64r_probe_kernel(
     while (em) {
         const uint32_t j = __builtin_ctzll(em);
         em &= em - 1;
-        const uint64_t tj = (uint64_t)blockIdx.x * TPB + w * 64 + j;
+        const uint64_t tj = (uint64_t)bid * TPB + w * 64 + j;
         const uint32_t ej = (uint32_t)__builtin_amdgcn_readlane((int)e, j);
         const uint32_t Lj = (uint32_t)__builtin_amdgcn_readlane((int)L, j);
         const uint32_t limj = (uint32_t)__builtin_amdgcn_readlane((int)lim, j);
@@ -565,7 +451,7 @@ __global__ __launch_bounds__(TPB) void nxg_f64r_probe_kernel(
         em &= em - 1;
         uint32_t c, en, xx;
         bool b = false, ov = false;
-        exact_tile<false>(wire, W, R, first, pre, (uint64_t)blockIdx.x * TPB + w * 64 + j,
+        exact_tile<false>(wire, W, R, first, pre, (uint64_t)bid * TPB + w * 64 + j,
                           img[w], lane, 0, nullptr, nullptr, 0, c, en, xx, b, ov);
         if (lane == j) {
             count = c;
@@ -581,19 +467,19 @@ __global__ __launch_bounds__(TPB) void nxg_f64r_probe_kernel(
     const uint64_t excl = block_excl_scan<uint64_t, TPB>(count, scan_tmp, &total);
     if (w == 0) {
         uint64_t base = 0;
-        if (blockIdx.x == 0) {
+        if (bid == 0) {
             if (lane == 0) st_agent(&tstat[0], lb_word(kFlagInc, epoch, total));
         } else {
-            if (lane == 0) st_agent(&tstat[blockIdx.x], lb_word(kFlagAgg, epoch, total));
+            if (lane == 0) st_agent(&tstat[bid], lb_word(kFlagAgg, epoch, total));
             bool give_up;
-            base = lookback_prefix<4>(tstat, blockIdx.x, epoch, nullptr, give_up);
+            base = lookback_prefix<4>(tstat, bid, epoch, nullptr, give_up);
             if (give_up) {
                 if (lane == 0) {
                     atomicOr(&st->timeout, 1u);
                     atomicOr(&st->fast_fail, 1u);
                 }
             } else if (lane == 0) {
-                st_agent(&tstat[blockIdx.x], lb_word(kFlagInc, epoch, base + total));
+                st_agent(&tstat[bid], lb_word(kFlagInc, epoch, base + total));
             }
         }
         if (lane == 0) sh_base = base;
@@ -609,6 +495,13 @@ __global__ __launch_bounds__(TPB) void nxg_f64r_probe_kernel(
         o.mode = L ? (uint8_t)((L - 11u) | ((L2 - 11u) << 3)) : (uint8_t)MODE_EXACT;
         desc[t] = o;
     }
+}
+
+__global__ __launch_bounds__(TPB) void nxg_f64r_probe_kernel(ProbeArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t img[TPB / 64][IMGB];
+    __shared__ uint64_t scan_tmp[TPB / 64];
+    __shared__ uint64_t sh_base;
+    probe_body(a, blockIdx.x, img, scan_tmp, sh_base);
 }
 
 // ---- emit: one wave per tile ---------------------------------------------------------------------
@@ -749,21 +642,145 @@ NXG_DEV bool emit_runs(const uint8_t* __restrict__ wire, uint64_t W, uint64_t t0
     return bad;
 }
 
-// wave g: tile g / ESUB, records [EREC * (g % ESUB), EREC * (g % ESUB + 1)) of it
-__global__ __launch_bounds__(TPB) void nxg_f64r_emit_kernel(
-    const uint8_t* __restrict__ wire, uint64_t W, uint64_t R, uint64_t pre, uint64_t nt,
-    const Desc* __restrict__ desc, uint64_t* __restrict__ oid, uint64_t* __restrict__ oval,
-    uint64_t cap, uint32_t flags, DevStatus* __restrict__ st) {
-    __shared__ __attribute__((aligned(16))) uint8_t img[TPB / 64][IMGB];
+
+#ifndef NXG_F64R_PAIR
+#define NXG_F64R_PAIR 0  // 1: lane j decodes two consecutive records, one 16-byte store per column
+                         // (measured: 10^8 equal, 10^7 4 % slower than one 8-byte store per row)
+#endif
+constexpr int RP = 2;  // pair slots per lane loaded together (128 records each)
+
+// A run tile in pairs of rows (record k is row base + k). The lane of pair P decodes rows 2P and
+// 2P + 1 and writes each column's two rows with ONE 16-byte store (2P is even, so the store is
+// 16-byte aligned): a wave stores 1 KiB per instruction instead of 512 B. Its two records lie in
+// the 48 bytes from the aligned 16-byte block of the first: the lane loads blocks A and B, and
+// the third, C, is the next lane's A or B (the next lane's first record starts 24..32 bytes after
+// ours, so its aligned block is 16 or 32 bytes past ours); lane 63 and the lanes at the end of
+// the range load C themselves. Edge pairs with one row of the range store that row alone.
+template <bool GUARD>
+NXG_DEV bool emit_pairs(const uint8_t* __restrict__ wire, uint64_t W, uint64_t t0, uint32_t e,
+                        uint32_t L, uint32_t ks, uint32_t L2, uint32_t klo, uint32_t n,
+                        uint64_t base, uint64_t* __restrict__ oid, uint64_t* __restrict__ oval,
+                        uint64_t cap, uint32_t lane, bool& over) {
+    bool bad = false;
+    const uint64_t r1 = t0 + e, r2 = t0 + e + (uint64_t)ks * L;
+    auto pos = [&](uint32_t k) -> uint64_t {
+        return k < ks ? r1 + (uint64_t)k * L : r2 + (uint64_t)(k - ks) * L2;
+    };
+    const uint64_t P0 = (base + klo) >> 1, P1 = ((base + n - 1) >> 1) + 1;
+    const int64_t lo = klo, hi = (int64_t)n - 1;
+    for (uint64_t Pb = P0; Pb < P1; Pb += 64 * RP) {
+        uint32_t A[RP][4], B[RP][4], C[RP][4];
+        int64_t k0[RP];
+        uint64_t pa[RP], pb[RP], ab[RP];
+        uint32_t la[RP], lb[RP];
+        bool own[RP];
+#pragma unroll
+        for (int r = 0; r < RP; r++) {
+            k0[r] = (int64_t)(2 * (Pb + (uint64_t)r * 64 + lane)) - (int64_t)base;
+            // clamped into the range: the loads stay unconditional (edge lanes decode a
+            // neighbour again and store nothing for it)
+            const uint32_t ka = (uint32_t)min(max(k0[r], lo), hi);
+            const uint32_t kb = (uint32_t)min(max(k0[r] + 1, lo), hi);
+            pa[r] = pos(ka);
+            pb[r] = pos(kb);
+            la[r] = ka < ks ? L : L2;
+            lb[r] = kb < ks ? L : L2;
+            ab[r] = pa[r] & ~15ull;
+            const uint4 x = GUARD ? ld16g(wire, ab[r], W) : ld16s(wire + ab[r]);
+            const uint4 y = GUARD ? ld16g(wire, ab[r] + 16, W) : ld16s(wire + ab[r] + 16);
+            A[r][0] = x.x, A[r][1] = x.y, A[r][2] = x.z, A[r][3] = x.w;
+            B[r][0] = y.x, B[r][1] = y.y, B[r][2] = y.z, B[r][3] = y.w;
+            own[r] = lane == 63 || k0[r] + 2 > hi;
+            if (own[r]) {
+                const uint4 z = ld16g(wire, ab[r] + 32, W);
+                C[r][0] = z.x, C[r][1] = z.y, C[r][2] = z.z, C[r][3] = z.w;
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < RP; r++) {
+            uint32_t nA[4], nB[4];
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                nA[q] = wave_next(A[r][q]);
+                nB[q] = wave_next(B[r][q]);
+            }
+            if (!own[r]) {
+                const bool at32 = ((pb[r] + lb[r]) & ~15ull) == ab[r] + 32;
+#pragma unroll
+                for (int q = 0; q < 4; q++) C[r][q] = at32 ? nA[q] : nB[q];
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < RP; r++) {
+            const uint32_t d[8] = {A[r][0], A[r][1], A[r][2], A[r][3],
+                                   B[r][0], B[r][1], B[r][2], B[r][3]};
+            uint32_t e0, e1, e2, e3;
+            extract16(d, (uint32_t)(pa[r] - ab[r]), e0, e1, e2, e3);
+            bad |= rec_check16(e0, e1, W - pa[r]) != la[r];
+            uint64_t ida, va;
+            rec_decode16(e0, e1, e2, e3, la[r], ida, va);
+            const uint32_t sb = (uint32_t)(pb[r] - ab[r]);  // 0..31
+            const bool up = sb >= 16;
+            uint32_t d2[8];
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                d2[q] = up ? B[r][q] : A[r][q];
+                d2[q + 4] = up ? C[r][q] : B[r][q];
+            }
+            extract16(d2, sb & 15u, e0, e1, e2, e3);
+            bad |= rec_check16(e0, e1, W - pb[r]) != lb[r];
+            uint64_t idb, vb;
+            rec_decode16(e0, e1, e2, e3, lb[r], idb, vb);
+            const uint64_t row = base + (uint64_t)k0[r];  // even
+            const bool oka = k0[r] >= lo && k0[r] <= hi, okb = k0[r] + 1 >= lo && k0[r] + 1 <= hi;
+            if (oka && okb && row + 1 < cap) {
+                *reinterpret_cast<uint4*>(oid + row) =
+                    make_uint4((uint32_t)ida, (uint32_t)(ida >> 32), (uint32_t)idb,
+                               (uint32_t)(idb >> 32));
+                *reinterpret_cast<uint4*>(oval + row) =
+                    make_uint4((uint32_t)va, (uint32_t)(va >> 32), (uint32_t)vb,
+                               (uint32_t)(vb >> 32));
+            } else {
+                if (oka) {
+                    if (row < cap) {
+                        oid[row] = ida;
+                        oval[row] = va;
+                    } else {
+                        over = true;
+                    }
+                }
+                if (okb) {
+                    if (row + 1 < cap) {
+                        oid[row + 1] = idb;
+                        oval[row + 1] = vb;
+                    } else {
+                        over = true;
+                    }
+                }
+            }
+        }
+    }
+    return bad;
+}
+
+// wave g of the emit: tile g / ESUB, its records [EREC * (g % ESUB), EREC * (g % ESUB + 1)) (in
+// pair mode the inner boundaries move down by base & 1, so that every wave but the first starts
+// on an even row)
+NXG_DEV void emit_body(const EmitArgs& a, uint32_t blk, uint8_t (*img)[IMGB]) {
+    const uint8_t* __restrict__ wire = a.wire;
+    const uint64_t W = a.W, R = a.R, pre = a.pre, nt = a.nt;
+    const Desc* __restrict__ desc = a.desc;
+    const uint32_t flags = a.flags;
+    DevStatus* __restrict__ st = a.st;
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     // Workgroups go to the 8 XCDs round-robin. A frame larger than the Infinity Cache streams
     // from HBM: there each XCD takes a contiguous eighth of it (10^8 records: 0.567-0.574 vs
     // 0.579-0.583 ms over 4 interleaved runs); a cache-resident frame keeps the plain order
     // (10^7: 0.063-0.066 vs 0.062-0.063 ms).
-    uint64_t bid = blockIdx.x;
+    uint64_t bid = blk;
     if (flags & F_XCD) {
-        const uint32_t nb = gridDim.x, q = nb / 8, r = nb % 8, x = blockIdx.x % 8;
-        bid = (uint64_t)x * q + min(x, r) + blockIdx.x / 8;
+        const uint32_t nb = a.ne, q = nb / 8, r = nb % 8, x = blk % 8;
+        bid = (uint64_t)x * q + min(x, r) + blk / 8;
     }
     const uint64_t g = bid * (TPB / 64) + w;
     const uint64_t t = g / ESUB;
@@ -771,9 +788,11 @@ __global__ __launch_bounds__(TPB) void nxg_f64r_emit_kernel(
     if (t >= nt) return;
     if (st->fast_fail) return;  // the probe rejected the frame (previous launch: plain load)
     const Desc D = desc[t];
-    const uint32_t klo = sub * EREC;
-    if (D.mode == MODE_EXACT ? sub != 0 : klo >= D.count) return;
-    const uint32_t khi = D.count - klo < EREC ? D.count : klo + EREC;
+    const uint32_t shift = NXG_F64R_PAIR ? (uint32_t)(D.base & 1) : 0u;
+    const uint32_t klo = sub ? sub * EREC - shift : 0u;
+    if (D.mode == MODE_EXACT ? sub != 0 : (sub && klo >= D.count)) return;
+    const uint32_t kend = (sub + 1) * EREC - shift;
+    const uint32_t khi = D.count < kend ? D.count : kend;
     const uint64_t t0 = t * T;
     bool bad = false, over = false;
     if (sub == 0) {
@@ -787,27 +806,86 @@ __global__ __launch_bounds__(TPB) void nxg_f64r_emit_kernel(
         }
     }
     if (D.mode != MODE_EXACT) {
-        const uint32_t L = 11u + (D.mode & 7u), L2 = 11u + ((D.mode >> 3) & 7u);
-        if (t0 + T + 32 <= W)
-            bad |= emit_runs<false>(wire, W, t0, D.entry, L, D.ks, L2, klo, khi, D.base, oid,
-                                    oval, cap, lane, img[w], over);
-        else
-            bad |= emit_runs<true>(wire, W, t0, D.entry, L, D.ks, L2, klo, khi, D.base, oid,
-                                   oval, cap, lane, img[w], over);
+        if (khi > klo) {
+            const uint32_t L = 11u + (D.mode & 7u), L2 = 11u + ((D.mode >> 3) & 7u);
+            const bool guard = t0 + T + 32 > W;
+            if (NXG_F64R_PAIR) {
+                if (!guard)
+                    bad |= emit_pairs<false>(wire, W, t0, D.entry, L, D.ks, L2, klo, khi, D.base,
+                                             a.oid, a.oval, a.cap, lane, over);
+                else
+                    bad |= emit_pairs<true>(wire, W, t0, D.entry, L, D.ks, L2, klo, khi, D.base,
+                                            a.oid, a.oval, a.cap, lane, over);
+            } else {
+                if (!guard)
+                    bad |= emit_runs<false>(wire, W, t0, D.entry, L, D.ks, L2, klo, khi, D.base,
+                                            a.oid, a.oval, a.cap, lane, img[w], over);
+                else
+                    bad |= emit_runs<true>(wire, W, t0, D.entry, L, D.ks, L2, klo, khi, D.base,
+                                           a.oid, a.oval, a.cap, lane, img[w], over);
+            }
+        }
     } else {
         uint32_t c, en, xx;
         bool b = false;
-        exact_tile<true>(wire, W, R, flags & F_FIRST, pre, t, img[w], lane, D.base, oid, oval,
-                         cap, c, en, xx, b, over);
+        exact_tile<true>(wire, W, R, flags & F_FIRST, pre, t, img[w], lane, D.base, a.oid, a.oval,
+                         a.cap, c, en, xx, b, over);
         bad |= b || c != D.count || en != D.entry || xx != D.x;
     }
     if (__any(bad) && lane == 0) atomicOr(&st->fast_fail, 1u);
     if (__any(over) && lane == 0) atomicOr(&st->capacity, 1u);
 }
 
+__global__ __launch_bounds__(TPB) void nxg_f64r_emit_kernel(EmitArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t img[TPB / 64][IMGB];
+    emit_body(a, blockIdx.x, img);
+}
+
+// A stream of frames (nxg_decode_frames_async): the emit of frame j and the probe of frame j + 1
+// in ONE launch. Workgroups [0, npg) are the probe's (its real workgroups, then idle ones up to a
+// multiple of 8, so that the emit's workgroups keep their XCD), dispatched first; the probe's
+// look-back waits only on lower-numbered probe workgroups, and no emit workgroup waits on
+// anything, so every wait is on a workgroup dispatched earlier. The probe is latency-bound (about
+// one wave per 8 KiB tiles' worth of CUs): beside the streaming emit it costs the emit little,
+// and it leaves the critical path of back-to-back decodes.
+__global__ __launch_bounds__(TPB) void nxg_f64r_fused_kernel(EmitArgs ea, ProbeArgs pa,
+                                                             uint32_t npg) {
+    __shared__ __attribute__((aligned(16))) uint8_t img[TPB / 64][IMGB];
+    __shared__ uint64_t scan_tmp[TPB / 64];
+    __shared__ uint64_t sh_base;
+    if (blockIdx.x < npg) {
+        if ((uint64_t)blockIdx.x * TPB < pa.nt) probe_body(pa, blockIdx.x, img, scan_tmp, sh_base);
+        return;
+    }
+    emit_body(ea, blockIdx.x - npg, img);
+}
+
 uint64_t nxg_dec_f64r_tiles(uint64_t W) { return (W + T - 1) / T; }
 uint64_t nxg_dec_f64r_tile_bytes() { return T; }
 uint64_t nxg_dec_f64r_groups(uint64_t W) { return (nxg_dec_f64r_tiles(W) + TPB - 1) / TPB; }
+
+namespace {
+// the launch arguments of the records that start in [begin, end) of a W-byte frame
+bool f64r_args(const uint8_t* wire, uint64_t W, uint64_t begin, uint64_t end, uint64_t* oid,
+               uint64_t* oval, uint64_t cap, void* desc, uint64_t* tstat, uint32_t epoch,
+               uint32_t flags, DevStatus* st, DevStatus* zst, ProbeArgs& pa, EmitArgs& ea,
+               uint32_t& ng) {
+    if (begin > end || end > W) return false;
+    const uint64_t R = end - begin;
+    const uint64_t nt = nxg_dec_f64r_tiles(R);
+    const uint64_t ne = (nt * ESUB + TPB / 64 - 1) / (TPB / 64);
+    if (ne > 0x7fffffffull) return false;
+    flags = (flags & (F_FORCE_EXACT | F_NO_BAIL)) | (begin == 0 ? F_FIRST : 0u) |
+            (end == W ? F_LAST : 0u) | (R > kXcdMin ? F_XCD : 0u);
+    const uint64_t pre = begin < 64 ? begin : 64;
+    pa = ProbeArgs{wire + begin, W - begin, R, pre, nt, reinterpret_cast<Desc*>(desc), tstat,
+                   epoch, flags, st, zst};
+    ea = EmitArgs{wire + begin, W - begin, R, pre, nt, reinterpret_cast<const Desc*>(desc),
+                  oid, oval, cap, flags, (uint32_t)ne, st};
+    ng = (uint32_t)nxg_dec_f64r_groups(R);
+    return true;
+}
+}  // namespace
 
 // Decodes the records that start in [begin, end) of a frame of W bytes (a whole frame: 0, W).
 // `desc` holds nxg_dec_f64r_tiles(end - begin) 16-byte descriptors, `tstat`
@@ -817,21 +895,47 @@ hipError_t nxg_launch_dec_f64r(const uint8_t* wire, uint64_t W, uint64_t begin, 
                                uint64_t* oid, uint64_t* oval, uint64_t cap, void* desc,
                                uint64_t* tstat, uint32_t epoch, uint32_t flags, DevStatus* st,
                                hipStream_t s) {
-    if (begin > end || end > W) return hipErrorInvalidValue;
-    const uint64_t R = end - begin;
-    const uint64_t nt = nxg_dec_f64r_tiles(R);
-    if (nt == 0) return hipSuccess;
-    const uint64_t ng = nxg_dec_f64r_groups(R);
-    const uint64_t ne = (nt * ESUB + TPB / 64 - 1) / (TPB / 64);
-    if (ne > 0x7fffffffull) return hipErrorInvalidValue;
-    flags = (flags & (F_FORCE_EXACT | F_NO_BAIL)) | (begin == 0 ? F_FIRST : 0u) |
-            (end == W ? F_LAST : 0u) | (R > kXcdMin ? F_XCD : 0u);
-    const uint64_t pre = begin < 64 ? begin : 64;
-    hipLaunchKernelGGL(nxg_f64r_probe_kernel, dim3((uint32_t)ng), dim3(TPB), 0, s, wire + begin,
-                       W - begin, R, pre, nt, reinterpret_cast<Desc*>(desc), tstat, epoch, flags,
-                       st, nxg_take_zero_slot());
-    hipLaunchKernelGGL(nxg_f64r_emit_kernel, dim3((uint32_t)ne), dim3(TPB), 0, s, wire + begin,
-                       W - begin, R, pre, nt, reinterpret_cast<const Desc*>(desc), oid, oval, cap,
-                       flags, st);
+    ProbeArgs pa;
+    EmitArgs ea;
+    uint32_t ng;
+    if (!f64r_args(wire, W, begin, end, oid, oval, cap, desc, tstat, epoch, flags, st, nullptr, pa,
+                   ea, ng))
+        return hipErrorInvalidValue;
+    if (pa.nt == 0) return hipSuccess;
+    pa.zst = nxg_take_zero_slot();
+    hipLaunchKernelGGL(nxg_f64r_probe_kernel, dim3(ng), dim3(TPB), 0, s, pa);
+    hipLaunchKernelGGL(nxg_f64r_emit_kernel, dim3(ea.ne), dim3(TPB), 0, s, ea);
+    return hipGetLastError();
+}
+
+// A stream of whole frames, decoded in order: probe(0), then per frame j one fused launch of
+// emit(j) + probe(j + 1). Consecutive frames alternate between two descriptor arrays (fr[j].desc),
+// since probe(j + 1) runs beside emit(j). Frames of no bytes launch nothing.
+hipError_t nxg_launch_dec_f64r_stream(const NxgF64rFrame* fr, uint32_t n, uint64_t* tstat,
+                                      uint32_t flags, hipStream_t s) {
+    std::vector<ProbeArgs> pa(n);
+    std::vector<EmitArgs> ea(n);
+    std::vector<uint32_t> ng(n);
+    for (uint32_t j = 0; j < n; j++)
+        if (!f64r_args(fr[j].wire, fr[j].W, 0, fr[j].W, fr[j].oid, fr[j].oval, fr[j].cap,
+                       fr[j].desc, tstat, fr[j].epoch, flags, fr[j].st, fr[j].zst, pa[j], ea[j],
+                       ng[j]))
+            return hipErrorInvalidValue;
+    int32_t prev = -1;  // the last frame whose probe ran, its emit not yet launched
+    for (uint32_t j = 0; j <= n; j++) {
+        const bool has = j < n && pa[j].nt > 0;
+        if (j < n && !has) continue;
+        if (prev < 0) {
+            if (has) hipLaunchKernelGGL(nxg_f64r_probe_kernel, dim3(ng[j]), dim3(TPB), 0, s, pa[j]);
+        } else if (!has) {
+            hipLaunchKernelGGL(nxg_f64r_emit_kernel, dim3(ea[prev].ne), dim3(TPB), 0, s, ea[prev]);
+        } else {
+            const uint32_t npg = (ng[j] + 7u) & ~7u;
+            if ((uint64_t)npg + ea[prev].ne > 0x7fffffffull) return hipErrorInvalidValue;
+            hipLaunchKernelGGL(nxg_f64r_fused_kernel, dim3(npg + ea[prev].ne), dim3(TPB), 0, s,
+                               ea[prev], pa[j], npg);
+        }
+        prev = has ? (int32_t)j : -1;
+    }
     return hipGetLastError();
 }

@@ -1,0 +1,159 @@
+// nxg_f64_rec16.h -- From::Update(Id, F64) records of 12..16 bytes (ids of 1..5 varint bytes,
+// < 2^35) on the wire, and the record-boundary machinery shared by the homogeneous-f64 decoders
+// (nxg_decode_f64_run.hip: length runs; nxg_decode_f64_x.hip: any f64 frame, single pass):
+//     varint(L) 04 varint(id) 09 f64be     L = lw(10 + vl(id)) = 11 + vl(id)
+// (len_wrapped_encode pack.rs:527-535, derive lib.rs:289-381, Value::encode lib.rs:404-407).
+//
+// Merge points: the first record at or after a position c lies in [c, c+16); every valid record
+// start in that window starts a walk, and the walks are advanced in position order until they
+// coincide. The true chain passes through the merge point, which depends only on the bytes, so
+// the lane that owns the bytes before c computes the same position.
+#pragma once
+#include "nxg_device.h"
+
+namespace f64rec16 {
+
+NXG_DEV uint4 ld16r(const uint8_t* __restrict__ p) { return *reinterpret_cast<const uint4*>(p); }
+// the bytes of [off, off+16) that lie inside the frame, zero-filled (out of line: rare)
+__device__ __attribute__((noinline)) uint4 ld16_tail(const uint8_t* __restrict__ wire,
+                                                    uint64_t off, uint64_t W) {
+    uint32_t v[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < 16; k++)
+        if (off + k < W) v[k >> 2] |= (uint32_t)wire[off + k] << (8 * (k & 3));
+    return make_uint4(v[0], v[1], v[2], v[3]);
+}
+NXG_DEV uint4 ld16g(const uint8_t* __restrict__ wire, uint64_t off, uint64_t W) {
+    if (off + 16 <= W) return ld16r(wire + off);
+    return ld16_tail(wire, off, W);
+}
+
+// 16 bytes at byte s (0..15) of the 32 bytes d[0..7] (little-endian dwords), no memory access
+NXG_DEV void extract16(const uint32_t (&d)[8], uint32_t s, uint32_t& e0, uint32_t& e1,
+                       uint32_t& e2, uint32_t& e3) {
+    // two levels of selects on the dword offset q = s / 4 (masks, not a dynamic array index,
+    // which the compiler would lower to scratch memory)
+    const uint32_t r = s & 3u;
+    const uint32_t m2 = 0u - ((s >> 3) & 1u), m1 = 0u - ((s >> 2) & 1u);
+    uint32_t g[6], f[5];
+#pragma unroll
+    for (int j = 0; j < 6; j++) g[j] = d[j] ^ ((d[j] ^ d[j + 2]) & m2);
+#pragma unroll
+    for (int j = 0; j < 5; j++) f[j] = g[j] ^ ((g[j] ^ g[j + 1]) & m1);
+    e0 = alignbyte(f[1], f[0], r);
+    e1 = alignbyte(f[2], f[1], r);
+    e2 = alignbyte(f[3], f[2], r);
+    e3 = alignbyte(f[4], f[3], r);
+}
+
+// A valid f64 Update record (L in 12..16: 1..5 id bytes) at e0,e1? Returns L or 0.
+// rem = bytes from the record start to the frame end.
+NXG_DEV uint32_t rec_check16(uint32_t e0, uint32_t e1, uint64_t rem) {
+    const uint32_t L = e0 & 0xffu;
+    const bool head = (L - 12u <= 4u) && (((e0 >> 8) & 0xffu) == 4u);
+    const uint32_t sh = 8u * ((L - 11u) & 7u);  // 8 * nb
+    const uint64_t x = ((((uint64_t)e1) << 32) | e0) >> 16;  // bytes 2..7
+    const uint64_t m = (1ull << sh) - 1ull;
+    const uint64_t want = 0x8080808080ull & (m >> 8);
+    const bool var = (x & 0x808080808080ull & m) == want;  // exactly nb varint bytes
+    const uint32_t tag = (uint32_t)(x >> sh) & 0xffu;       // Value tag after the id
+    return (head && var && tag == 9u && rem >= L) ? L : 0u;
+}
+
+// id and f64 bits of a record of length L (12..16) already checked by rec_check16
+NXG_DEV void rec_decode16(uint32_t e0, uint32_t e1, uint32_t e2, uint32_t e3, uint32_t L,
+                          uint64_t& id, uint64_t& val) {
+    const uint32_t sh = 8u * ((L - 11u) & 7u);
+    const uint64_t x = ((((uint64_t)e1) << 32) | e0) >> 16;
+    const uint64_t y = x & ((1ull << sh) - 1ull) & 0x7f7f7f7f7full;
+    id = (y & 0x7full) | ((y >> 1) & 0x3f80ull) | ((y >> 2) & 0x1fc000ull) |
+         ((y >> 3) & 0xfe00000ull) | ((y >> 4) & 0x7f0000000ull);
+    const uint32_t o = L - 8u;  // value offset, 4..8
+    const uint32_t lo = o >= 8u ? e2 : alignbyte(e2, e1, o & 3u);
+    const uint32_t hi = o >= 8u ? e3 : alignbyte(e3, e2, o & 3u);
+    val = ((uint64_t)bswap32(lo) << 32) | bswap32(hi);  // big-endian f64 (pack.rs:592-598)
+}
+
+// SWAR: 0x80 in each byte of x whose value is in [12, 16] (record lengths)
+NXG_DEV uint32_t len_bytes(uint32_t x) {
+    const uint32_t y = x & 0x7f7f7f7fu;
+    return (0x90909090u - y) & ~x & (y + 0x74747474u) & 0x80808080u;
+}
+// candidate starts in positions 0..15 of d[0..4]: a byte in 12..16 followed by 0x04
+NXG_DEV uint32_t cand16(uint32_t d0, uint32_t d1, uint32_t d2, uint32_t d3, uint32_t d4) {
+    const uint32_t a = nib(len_bytes(d0)) | (nib(len_bytes(d1)) << 4) | (nib(len_bytes(d2)) << 8) |
+                       (nib(len_bytes(d3)) << 12);
+    const uint32_t b = nib(zero_bytes(d0 ^ 0x04040404u)) | (nib(zero_bytes(d1 ^ 0x04040404u)) << 4) |
+                       (nib(zero_bytes(d2 ^ 0x04040404u)) << 8) |
+                       (nib(zero_bytes(d3 ^ 0x04040404u)) << 12) |
+                       (nib(zero_bytes(d4 ^ 0x04040404u)) << 16);
+    return a & (b >> 1) & 0xffffu;
+}
+
+// 16 bytes at LDS byte offset rel (any alignment)
+NXG_DEV void lds16(const uint8_t* buf, uint32_t rel, uint32_t& e0, uint32_t& e1, uint32_t& e2,
+                   uint32_t& e3) {
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(buf + (rel & ~3u));
+    const uint32_t s = rel & 3u;
+    const uint32_t d0 = w[0], d1 = w[1], d2 = w[2], d3 = w[3], d4 = w[4];
+    e0 = alignbyte(d1, d0, s);
+    e1 = alignbyte(d2, d1, s);
+    e2 = alignbyte(d3, d2, s);
+    e3 = alignbyte(d4, d3, s);
+}
+
+constexpr uint32_t FAILX = 0xffffffffu;
+constexpr int WIN = 64;  // merge walks must coincide within 64 bytes of the chunk start
+
+// Merge point of all record walks starting in [r, r+16) of the LDS image (r 4-aligned), as a
+// position relative to the image; the END position (W - a0) for a chunk at or past the frame's
+// end; FAILX if the walks do not merge.
+NXG_DEV uint32_t merge16(const uint8_t* buf, uint32_t r, uint64_t a0, uint64_t W) {
+    // positions are signed: an exact tile at the start of a byte range images 64 bytes before it
+    const int64_t abs_r = (int64_t)a0 + (int64_t)r;
+    if (abs_r >= (int64_t)W) return (uint32_t)((int64_t)W - (int64_t)a0);
+    const uint64_t remr = (uint64_t)((int64_t)W - abs_r);
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(buf + r);
+    uint32_t cand = cand16(w[0], w[1], w[2], w[3], w[4]);
+    uint64_t S = 0;
+    if (remr < 16) S |= 1ull << remr;  // the frame end is a valid (terminal) position
+    while (cand) {
+        const uint32_t p = __builtin_ctz(cand);
+        cand &= cand - 1;
+        uint32_t e0, e1, e2, e3;
+        lds16(buf, r + p, e0, e1, e2, e3);
+        if (rec_check16(e0, e1, remr - p)) S |= 1ull << p;
+    }
+    for (int it = 0; it < WIN && __popcll(S) > 1; it++) {
+        const uint32_t p = __builtin_ctzll(S);
+        S &= S - 1;
+        uint32_t e0, e1, e2, e3;
+        lds16(buf, r + p, e0, e1, e2, e3);
+        const uint32_t L = rec_check16(e0, e1, remr - p);
+        const uint32_t np = p + L;
+        if (np >= (uint32_t)WIN) return FAILX;
+        bool ok = (np == remr);
+        if (!ok) {
+            lds16(buf, r + np, e0, e1, e2, e3);
+            ok = rec_check16(e0, e1, remr - np) != 0;
+        }
+        if (ok) S |= 1ull << np;
+    }
+    if (__popcll(S) != 1) return FAILX;
+    return r + (uint32_t)__builtin_ctzll(S);
+}
+
+// the bytes of the 16 at `pos` (signed, relative to wire) that lie in [-pre, W), zero-filled
+__device__ __attribute__((noinline)) uint4 ld16_pre(const uint8_t* __restrict__ wire,
+                                                   int64_t pos, uint64_t W, uint64_t pre) {
+    uint32_t v[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const int64_t q = pos + k;
+        if (q >= -(int64_t)pre && q < (int64_t)W)
+            v[k >> 2] |= (uint32_t)wire[q] << (8 * (k & 3));
+    }
+    return make_uint4(v[0], v[1], v[2], v[3]);
+}
+
+}  // namespace f64rec16

@@ -56,22 +56,6 @@ __host__ __device__ inline uint64_t lb_flag(uint64_t w, uint32_t epoch) {
     return ((w >> kEpochShift) & kEpochMax) == epoch ? (w & kFlagMask) : 0ull;
 }
 
-// ---- f64 decode geometry (nxg_decode_f64.hip) ----
-namespace f64dec {
-constexpr int TPB = 256;                 // 4 independent waves per workgroup
-constexpr int WAVES = TPB / 64;
-constexpr int CHUNK = 64;                // bytes per lane
-constexpr int IMG = 64 * CHUNK;          // 4 KiB tile image per wave (16 B x 64 lanes x 4)
-constexpr int STRIDE = IMG - CHUNK;      // tiles start 4032 B apart: lanes 0..62 own the records,
-                                         // lane 63's merge point is the next tile's first
-constexpr int TILE = IMG;                // (image size; kept for LDS sizing)
-constexpr int HALO = 128;                // look-ahead bytes loaded past the image
-constexpr int WIN = 64;                  // merge-point search bound (bits of the walk mask)
-constexpr int MAXREC = TILE / 12 + 16;   // record slots per tile (records are >= 12 bytes)
-constexpr int MAX_WGS = 2048;            // workgroups per pass (one run per wave)
-constexpr int SCRATCH_WORDS = MAX_WGS * WAVES / 2 + MAX_WGS / 2;  // wcnt + gcnt (u32)
-}  // namespace f64dec
-
 // ---- general decode geometry (nxg_decode_gen.hip) ----
 namespace gdec2 {
 constexpr int TPB = 256;            // 4 independent waves per workgroup, one run each
@@ -106,21 +90,12 @@ inline DevStatus* nxg_take_zero_slot() {
     nxg_zero_used = true;
     return nxg_zero_slot;
 }
-// f64 decode: count pass + emit pass, `wgs` workgroups each (nxg_dec_f64_wgs). `scratch`
-// holds f64dec::SCRATCH_WORDS words and `moff` 64 bytes per tile (nxg_dec_f64_tiles(W) tiles);
-// neither needs initialisation.
-uint64_t nxg_dec_f64_tiles(uint64_t W);
-hipError_t nxg_launch_dec_f64(const uint8_t* wire, uint64_t W, uint64_t* oid, uint64_t* oval,
-                              uint64_t cap, uint64_t* scratch, uint8_t* moff, int wgs,
-                              DevStatus* st, hipStream_t s);
-int nxg_dec_f64_wgs(int ncu);
-// f64 decode, single pass (nxg_decode_f64_1p.hip): `tstat` holds 2 epoch-tagged words per tile
-// (nxg_dec_f64_1p_tiles(W) tiles); `wgs` from nxg_dec_f64_1p_wgs (all co-resident).
-uint64_t nxg_dec_f64_1p_tiles(uint64_t W);
-hipError_t nxg_launch_dec_f64_1p(const uint8_t* wire, uint64_t W, uint64_t* oid, uint64_t* oval,
-                                 uint64_t cap, uint64_t* tstat, uint32_t epoch, int wgs,
-                                 DevStatus* st, hipStream_t s);
-int nxg_dec_f64_1p_wgs(int ncu);
+// f64 decode of any f64 frame in one pass (nxg_decode_f64_x.hip): `tstat` holds
+// nxg_dec_f64x_groups(W) epoch-tagged words (no initialisation needed).
+uint64_t nxg_dec_f64x_groups(uint64_t W);
+hipError_t nxg_launch_dec_f64x(const uint8_t* wire, uint64_t W, uint64_t* oid, uint64_t* oval,
+                               uint64_t cap, uint64_t* tstat, uint32_t epoch, DevStatus* st,
+                               hipStream_t s);
 // f64 decode by length runs (nxg_decode_f64_run.hip): probe + emit launches. `desc` holds 16 bytes
 // per tile (nxg_dec_f64r_tiles(W)), `tstat` nxg_dec_f64r_groups(W) epoch-tagged words. Sets
 // DevStatus.irregular (and fast_fail) for frames whose record lengths vary record to record.
@@ -132,6 +107,22 @@ hipError_t nxg_launch_dec_f64r(const uint8_t* wire, uint64_t W, uint64_t begin, 
                                uint64_t* oid, uint64_t* oval, uint64_t cap, void* desc,
                                uint64_t* tstat, uint32_t epoch, uint32_t flags, DevStatus* st,
                                hipStream_t s);
+// A stream of whole frames (nxg_decode_frames_async): probe(0), then per frame one fused launch
+// of emit(j) and probe(j + 1). Consecutive frames need different `desc` arrays; each frame has its
+// own status slot and zero slot (`zst`, zeroed by its probe).
+struct NxgF64rFrame {
+    const uint8_t* wire;
+    uint64_t W;
+    uint64_t* oid;
+    uint64_t* oval;
+    uint64_t cap;
+    void* desc;
+    uint32_t epoch;
+    DevStatus* st;
+    DevStatus* zst;
+};
+hipError_t nxg_launch_dec_f64r_stream(const NxgF64rFrame* fr, uint32_t n, uint64_t* tstat,
+                                      uint32_t flags, hipStream_t s);
 uint64_t nxg_enc_f64_tiles(uint64_t n);  // tiles (and tstat words) of an f64 encode
 hipError_t nxg_launch_enc_f64(const uint64_t* id, const uint64_t* val, uint64_t n, uint8_t* out,
                               uint64_t cap, uint64_t* tstat, uint32_t epoch, DevStatus* st,

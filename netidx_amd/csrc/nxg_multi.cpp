@@ -2,6 +2,12 @@
 // xGMI, the sharded encode of BASELINE configs[4] (shards encoded into their final offsets, then
 // grouped send/recv: SURVEY.md H5) and the byte-range sharded decode.
 //
+// The protocols are written once against a transport (RCCL, or a caller's NxgCommOps) and a
+// local codec (the ctx's kernels, or the ops' hooks), so the code that runs on an 8-GPU node is
+// the code the multi-process tests run. Every collective step carries each rank's status word:
+// a rank that fails tells the others in the next exchange and they all return false at the same
+// step (a rank that returned early would leave its peers waiting in a collective forever).
+//
 // Only the public ABI and librccl are used here. librccl is opened at nxg_comm_init with dlopen
 // (RTLD_GLOBAL, soname librccl.so.1): the codec loads on a machine without RCCL, and inside a
 // process that already has RCCL (PyTorch's torch.distributed) the same library is shared.
@@ -79,11 +85,14 @@ bool rccl(Rccl** out, NetidxError* err) {
 }  // namespace
 
 struct NxgComm {
-    Rccl* r = nullptr;
+    Rccl* r = nullptr;  // RCCL transport, or
+    bool use_ops = false;
+    NxgCommOps ops{};   // the caller's transport (and codec)
     ncclComm_t comm = nullptr;
     int nranks = 0, rank = 0;
-    hipStream_t stream = nullptr;  // the ctx's stream at init
-    uint64_t* dscratch = nullptr;  // per-rank exchange slots (sizes, range summaries)
+    NxgCtx* ctx = nullptr;
+    hipStream_t stream = nullptr;  // the ctx's stream at the last call
+    uint64_t* dscratch = nullptr;  // RCCL: per-rank exchange slots (sizes, range summaries)
 };
 
 #define NCCLCHK(expr)                                                                         \
@@ -104,11 +113,21 @@ struct NxgComm {
     } while (0)
 
 namespace {
-constexpr int kSlotWords = 8;  // one rank's exchange slot: 64 bytes (an NxgRange fits)
-static_assert(sizeof(NxgRange) <= kSlotWords * 8, "range summary fits a slot");
+constexpr int kSlotWords = 8;  // one rank's exchange slot: 64 bytes
+constexpr int kStatusWord = 7; // the slot's last word: 0 = this rank is fine, else failed
+static_assert(sizeof(NxgRange) <= (kSlotWords - 1) * 8, "range summary fits a slot");
 
-// all-gather of one 64-byte slot per rank: mine -> all[0 .. nranks)
-bool gather_slots(NxgComm* comm, const void* mine, void* all, NetidxError* err) {
+// ---- transport ------------------------------------------------------------------------------
+// all-gather of one 64-byte slot per rank (host memory): mine -> all[0 .. nranks). A transport
+// failure cannot be agreed on (the transport is what broke): it is returned as is.
+bool gather_slots(NxgComm* comm, const uint64_t* mine, uint64_t* all, NetidxError* err) {
+    if (comm->use_ops) {
+        if (!comm->ops.allgather(comm->ops.user, mine, all, kSlotWords * 8)) {
+            set_err(err, "rank %d: the transport's all-gather failed", comm->rank);
+            return false;
+        }
+        return true;
+    }
     uint64_t* d = comm->dscratch;  // [nranks + 1] slots: gathered, then the local one
     uint64_t* local = d + (size_t)comm->nranks * kSlotWords;
     HIPCHK(hipMemcpyAsync(local, mine, kSlotWords * 8, hipMemcpyHostToDevice, comm->stream));
@@ -116,6 +135,92 @@ bool gather_slots(NxgComm* comm, const void* mine, void* all, NetidxError* err) 
     HIPCHK(hipMemcpyAsync(all, d, (size_t)comm->nranks * kSlotWords * 8, hipMemcpyDeviceToHost,
                           comm->stream));
     HIPCHK(hipStreamSynchronize(comm->stream));
+    return true;
+}
+
+// every shard [off[p], off[p+1]) of `buf` to every rank, at the same offsets
+bool exchange_shards(NxgComm* comm, uint8_t* buf, const std::vector<uint64_t>& off,
+                     NetidxError* err) {
+    if (comm->use_ops) {
+        if (!comm->ops.allgatherv(comm->ops.user, buf, off.data(), (uint32_t)comm->nranks,
+                                  (uint32_t)comm->rank)) {
+            set_err(err, "rank %d: the transport's shard exchange failed", comm->rank);
+            return false;
+        }
+        return true;
+    }
+    // grouped point-to-point over xGMI: no padding to the largest shard, no compaction
+    const uint64_t my_off = off[comm->rank], my_len = off[comm->rank + 1] - my_off;
+    NCCLCHK(comm->r->GroupStart());
+    for (int p = 0; p < comm->nranks; p++) {
+        if (p == comm->rank) continue;
+        const uint64_t plen = off[p + 1] - off[p];
+        if (my_len) NCCLCHK(comm->r->Send(buf + my_off, my_len, ncclUint8, p, comm->comm,
+                                          comm->stream));
+        if (plen) NCCLCHK(comm->r->Recv(buf + off[p], plen, ncclUint8, p, comm->comm,
+                                        comm->stream));
+    }
+    NCCLCHK(comm->r->GroupEnd());
+    HIPCHK(hipStreamSynchronize(comm->stream));
+    return true;
+}
+
+// ---- local codec ----------------------------------------------------------------------------
+bool has_codec_hooks(const NxgComm* comm) { return comm->use_ops && comm->ops.decode_range; }
+
+bool local_encoded_len(NxgComm* comm, const NxgColumns* in, const uint8_t* heap, uint64_t* len,
+                       NetidxError* err) {
+    if (has_codec_hooks(comm)) {
+        if (!comm->ops.encoded_len(comm->ops.user, in, heap, len)) {
+            set_err(err, "rank %d: encoded_len failed", comm->rank);
+            return false;
+        }
+        return true;
+    }
+    return nxg_encoded_len(comm->ctx, in, heap, len, err);
+}
+bool local_encode(NxgComm* comm, const NxgColumns* in, const uint8_t* heap, uint8_t* out,
+                  uint64_t cap, uint64_t* len, NetidxError* err) {
+    if (has_codec_hooks(comm)) {
+        if (!comm->ops.encode(comm->ops.user, in, heap, out, cap, len)) {
+            set_err(err, "rank %d: encode failed", comm->rank);
+            return false;
+        }
+        return true;
+    }
+    return nxg_encode_updates(comm->ctx, in, heap, out, cap, len, err);
+}
+bool local_decode_range(NxgComm* comm, const uint8_t* f, uint64_t W, uint64_t b, uint64_t e,
+                        NxgColumns* out, NxgRange* rng, NetidxError* err) {
+    if (has_codec_hooks(comm)) {
+        if (!comm->ops.decode_range(comm->ops.user, f, W, b, e, out, rng)) {
+            set_err(err, "rank %d: decode_range failed", comm->rank);
+            return false;
+        }
+        return true;
+    }
+    return nxg_decode_range(comm->ctx, f, W, b, e, out, rng, err);
+}
+
+// After a gather: the first rank whose status word is set, or -1.
+int first_failed(const NxgComm* comm, const std::vector<uint64_t>& all) {
+    for (int i = 0; i < comm->nranks; i++)
+        if (all[(size_t)i * kSlotWords + kStatusWord]) return i;
+    return -1;
+}
+// The agreed failure: this rank keeps its own message if it is the one that failed.
+bool fail_together(NxgComm* comm, int who, const char* what, NetidxError* err) {
+    if (who != comm->rank || !err || !err->msg) set_err(err, "rank %d failed %s", who, what);
+    return false;
+}
+
+bool comm_ready(NxgCtx* ctx, NxgComm* comm, NetidxError* err) {
+    if (!comm || (!ctx && !has_codec_hooks(comm))) {
+        set_err(err, "null argument");
+        return false;
+    }
+    if (ctx) comm->ctx = ctx;
+    comm->stream = ctx ? (hipStream_t)nxg_ctx_stream(ctx) : nullptr;
     return true;
 }
 }  // namespace
@@ -152,6 +257,7 @@ NxgComm* nxg_comm_init(NxgCtx* ctx, int nranks, int rank, const uint8_t id[128],
     }
     comm->nranks = nranks;
     comm->rank = rank;
+    comm->ctx = ctx;
     comm->stream = (hipStream_t)nxg_ctx_stream(ctx);
     ncclUniqueId u;
     memcpy(&u, id, 128);
@@ -170,6 +276,30 @@ NxgComm* nxg_comm_init(NxgCtx* ctx, int nranks, int rank, const uint8_t id[128],
     return comm;
 }
 
+NxgComm* nxg_comm_init_ops(NxgCtx* ctx, int nranks, int rank, const NxgCommOps* ops,
+                           NetidxError* err) {
+    if (!ops || !ops->allgather || !ops->allgatherv || nranks < 1 || rank < 0 || rank >= nranks) {
+        set_err(err, "bad argument (nranks %d, rank %d, ops %p)", nranks, rank, (const void*)ops);
+        return nullptr;
+    }
+    const int hooks = !!ops->encoded_len + !!ops->encode + !!ops->decode_range;
+    if (hooks != 0 && hooks != 3) {
+        set_err(err, "the local codec hooks come all three or none");
+        return nullptr;
+    }
+    if (!ctx && hooks == 0) {
+        set_err(err, "a ctx is needed unless the ops carry the local codec");
+        return nullptr;
+    }
+    NxgComm* comm = new NxgComm();
+    comm->use_ops = true;
+    comm->ops = *ops;
+    comm->nranks = nranks;
+    comm->rank = rank;
+    comm->ctx = ctx;
+    return comm;
+}
+
 void nxg_comm_destroy(NxgComm* comm) {
     if (!comm) return;
     if (comm->stream) (void)hipStreamSynchronize(comm->stream);
@@ -181,74 +311,78 @@ void nxg_comm_destroy(NxgComm* comm) {
 bool nxg_encode_allgather(NxgCtx* ctx, NxgComm* comm, const NxgColumns* din, const uint8_t* dheap,
                           uint8_t* dout, uint64_t cap, uint64_t* len_out, uint64_t* shard_off,
                           NetidxError* err) {
-    if (!ctx || !comm || !din || !dout) {
-        set_err(err, "null argument");
-        return false;
-    }
-    comm->stream = (hipStream_t)nxg_ctx_stream(ctx);
-    // 1. this shard's encoded size, then every shard's (8 bytes per rank)
+    if (!comm_ready(ctx, comm, err)) return false;
+    const int n = comm->nranks;
+    std::vector<uint64_t> all((size_t)n * kSlotWords);
+    // 1. every shard's encoded size (and whether it could be sized)
     uint64_t mine[kSlotWords] = {0};
-    if (!nxg_encoded_len(ctx, din, dheap, &mine[0], err)) return false;
-    std::vector<uint64_t> all((size_t)comm->nranks * kSlotWords);
+    if (!din || !dout) {
+        set_err(err, "null argument");
+        mine[kStatusWord] = 1;
+    } else if (!local_encoded_len(comm, din, dheap, &mine[0], err)) {
+        mine[kStatusWord] = 1;
+    }
     if (!gather_slots(comm, mine, all.data(), err)) return false;
-    std::vector<uint64_t> off(comm->nranks + 1, 0);
-    for (int i = 0; i < comm->nranks; i++) off[i + 1] = off[i] + all[(size_t)i * kSlotWords];
-    const uint64_t total = off[comm->nranks];
+    int bad = first_failed(comm, all);
+    if (bad >= 0) return fail_together(comm, bad, "to size its shard", err);
+    std::vector<uint64_t> off(n + 1, 0);
+    for (int i = 0; i < n; i++) off[i + 1] = off[i] + all[(size_t)i * kSlotWords];
+    const uint64_t total = off[n];
+    // 2. the shard straight into its final place; then agree that every rank managed
+    const uint64_t my_off = off[comm->rank], my_len = mine[0];
+    uint64_t st[kSlotWords] = {0};
     if (total > cap) {
         set_err(err, "output buffer too small: the frame has %llu bytes, capacity %llu",
                 (unsigned long long)total, (unsigned long long)cap);
-        return false;
+        st[kStatusWord] = 1;
+    } else if (my_len) {
+        uint64_t wrote = 0;
+        if (!local_encode(comm, din, dheap, dout + my_off, cap - my_off, &wrote, err)) {
+            st[kStatusWord] = 1;
+        } else if (wrote != my_len) {
+            set_err(err, "shard encoded to %llu bytes, sized at %llu", (unsigned long long)wrote,
+                    (unsigned long long)my_len);
+            st[kStatusWord] = 1;
+        }
     }
-    // 2. the shard straight into its final place
-    const uint64_t my_off = off[comm->rank], my_len = mine[0];
-    uint64_t wrote = 0;
-    if (my_len &&
-        !nxg_encode_updates(ctx, din, dheap, dout + my_off, cap - my_off, &wrote, err))
-        return false;
-    if (wrote != my_len) {
-        set_err(err, "shard encoded to %llu bytes, sized at %llu", (unsigned long long)wrote,
-                (unsigned long long)my_len);
-        return false;
-    }
-    // 3. every shard to every rank, at the same offsets (grouped point-to-point over xGMI)
-    NCCLCHK(comm->r->GroupStart());
-    for (int p = 0; p < comm->nranks; p++) {
-        if (p == comm->rank) continue;
-        const uint64_t plen = off[p + 1] - off[p];
-        if (my_len) NCCLCHK(comm->r->Send(dout + my_off, my_len, ncclUint8, p, comm->comm,
-                                          comm->stream));
-        if (plen) NCCLCHK(comm->r->Recv(dout + off[p], plen, ncclUint8, p, comm->comm,
-                                        comm->stream));
-    }
-    NCCLCHK(comm->r->GroupEnd());
-    HIPCHK(hipStreamSynchronize(comm->stream));
+    if (!gather_slots(comm, st, all.data(), err)) return false;
+    bad = first_failed(comm, all);
+    if (bad >= 0) return fail_together(comm, bad, "to encode its shard", err);
+    // 3. every shard to every rank, at the same offsets
+    if (!exchange_shards(comm, dout, off, err)) return false;
     if (len_out) *len_out = total;
     if (shard_off)
-        for (int i = 0; i < comm->nranks; i++) shard_off[i] = off[i];
+        for (int i = 0; i < n; i++) shard_off[i] = off[i];
     return true;
 }
 
 bool nxg_decode_sharded(NxgCtx* ctx, NxgComm* comm, const uint8_t* dframe, uint64_t frame_len,
                         NxgColumns* dout, uint64_t* row_off, NxgRange* rng, NetidxError* err) {
-    if (!ctx || !comm || !dout || (!dframe && frame_len)) {
-        set_err(err, "null argument");
-        return false;
-    }
-    comm->stream = (hipStream_t)nxg_ctx_stream(ctx);
+    if (!comm_ready(ctx, comm, err)) return false;
     const int n = comm->nranks, r = comm->rank;
     const uint64_t b = frame_len * (uint64_t)r / (uint64_t)n;
     const uint64_t e = frame_len * (uint64_t)(r + 1) / (uint64_t)n;
-    NxgRange mine;
-    if (!nxg_decode_range(ctx, dframe, frame_len, b, e, dout, &mine, err)) return false;
+    NxgRange mine{};
+    bool failed = false;
+    if (!dout || (!dframe && frame_len)) {
+        set_err(err, "null argument");
+        failed = true;
+    } else if (!local_decode_range(comm, dframe, frame_len, b, e, dout, &mine, err)) {
+        failed = true;
+    }
     std::vector<NxgRange> all(n);
     std::vector<uint64_t> offs(n);
     std::vector<uint64_t> buf((size_t)n * kSlotWords);
     // link; a range whose entry is off the chain (a false record start guessed at its head)
-    // decodes again from its predecessor's exit, which is a true start: at most n rounds
-    for (int round = 0; round <= n; round++) {
+    // decodes again from its predecessor's exit, which is a true start: at most n rounds. Every
+    // rank sees the same summaries, so every decision below is the same on every rank.
+    for (int round = 0;; round++) {
         uint64_t slot[kSlotWords] = {0};
         memcpy(slot, &mine, sizeof mine);
+        slot[kStatusWord] = failed ? 1 : 0;
         if (!gather_slots(comm, slot, buf.data(), err)) return false;
+        const int who = first_failed(comm, buf);
+        if (who >= 0) return fail_together(comm, who, "to decode its byte range", err);
         for (int i = 0; i < n; i++) memcpy(&all[i], &buf[(size_t)i * kSlotWords], sizeof(NxgRange));
         for (int i = 0; i < n; i++)
             if (!all[i].ok) {
@@ -266,29 +400,33 @@ bool nxg_decode_sharded(NxgCtx* ctx, NxgComm* comm, const uint8_t* dframe, uint6
             set_err(err, "the byte ranges of the frame do not link into one chain");
             return false;
         }
-        // the first broken range re-decodes from its predecessor's exit (every rank agrees on
-        // `bad`: they all see the same summaries)
-        if ((int)bad == r && r > 0) {
+        if (bad == 0) {
+            set_err(err, "the frame does not start with a message");
+            return false;
+        }
+        // the first broken range re-decodes from its predecessor's exit
+        if ((int)bad == r) {
             uint64_t at = 0;  // the chain's position entering range r
             for (int i = 0; i < r; i++)
                 if (all[i].begin != all[i].end) at = all[i].exit;
             if (at < b || at > frame_len) {
                 set_err(err, "range %d: predecessor exit %llu outside the range", r,
                         (unsigned long long)at);
-                return false;
+                failed = true;
+                continue;
             }
-            NxgRange again;
-            if (!nxg_decode_range(ctx, dframe, frame_len, at < e ? at : e, e, dout, &again, err))
-                return false;
+            NxgRange again{};
+            if (!local_decode_range(comm, dframe, frame_len, at < e ? at : e, e, dout, &again,
+                                    err)) {
+                failed = true;
+                continue;
+            }
             again.begin = b;  // the same range, now entered on the chain
             if (at >= e) {    // no message starts in the range: the chain passes through
                 again.entry = again.exit = at;
                 again.n_rows = 0;
             }
             mine = again;
-        } else if ((int)bad == r && r == 0) {
-            set_err(err, "the frame does not start with a message");
-            return false;
         }
     }
     if (row_off) *row_off = offs[r];

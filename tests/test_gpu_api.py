@@ -138,3 +138,60 @@ def test_sync_finishes_every_pending_call(codec):
         assert np.array_equal(g["id"], ref["id"]) and np.array_equal(g["fixed"], ref["fixed"])
     assert outs[1].s.n_heartbeat == 1
     assert ln.value == len(w) and eout[: len(w)].cpu().numpy().tobytes() == w
+
+
+@pytest.mark.parametrize("seed", [11, 12])
+def test_decode_frames_stream(codec, seed):
+    """nxg_decode_frames_async: a backlog of frames of varied shape, each into its own columns --
+    f64 frames of odd and even record counts (the 16-byte pair stores at both row parities),
+    ids across the varint widths, an empty frame, a frame with a Heartbeat (the fast path rejects
+    it, the fallback decodes it), a frame with ids in random order (the irregular-frame path) --
+    every column against the oracle's decode of the same bytes."""
+    import netidx_amd
+    import nxo
+    import torch
+    from netidx_amd import synth
+    from netidx_amd.codec import Columns
+    rng = np.random.default_rng(seed)
+    frames = []
+    for k, n in enumerate([1, 2, 3, 129, 257, 70_001, 0, 250_000, 40_000, 100_000, 5]):
+        ids, vals = synth.f64_columns(n, seed * 100 + k, id_offset=int(rng.integers(0, 3)) * 16_000)
+        if k == 8:  # random order: record lengths vary record to record
+            ids = rng.permutation(np.arange(n, dtype=np.uint64) + np.uint64(2**21 - 20_000))
+        w = nxo.encode_f64(ids, vals).tobytes()
+        if k == 9:  # a Heartbeat between records 499 and 500
+            w = (nxo.encode_f64(ids[:500], vals[:500]).tobytes() + b"\x02\x05" +
+                 nxo.encode_f64(ids[500:], vals[500:]).tobytes())
+        frames.append(w)
+    dev = [torch.from_numpy(np.frombuffer(w, np.uint8).copy()).cuda() if w else
+           torch.empty(16, dtype=torch.uint8, device="cuda") for w in frames]
+    outs = [Columns.for_frame(max(len(w), 16), netidx_amd.LAYOUT_MIXED, "cuda") for w in frames]
+    codec.decode_frames_async([d.data_ptr() for d in dev], [len(w) for w in frames], outs)
+    codec.sync()
+    for w, o in zip(frames, outs):
+        ref = nxo.decode(w).trim()
+        g = o.numpy()
+        assert o.s.n_rows == len(ref["id"])
+        assert np.array_equal(g["id"], ref["id"]) and np.array_equal(g["fixed"], ref["fixed"])
+    assert outs[9].s.n_heartbeat == 1
+
+
+def test_decode_frames_stream_shared_columns_1e7(codec):
+    """The bench's shape: one 10^7-record f64 frame decoded 6 times as a stream into one set of
+    columns (the probe of frame j + 1 runs beside the emit of frame j), bit-exact."""
+    import netidx_amd
+    import torch
+    from netidx_amd import synth
+    from netidx_amd.codec import Columns
+    n = 10_000_000
+    ids, vals = synth.f64_columns(n, synth.SEED_F64)
+    cols = netidx_amd.columns_from_arrays(ids, vals)
+    wire = codec.encode_batch(cols)
+    out = Columns(n, 0, 0, netidx_amd.LAYOUT_F64, "cuda")
+    for rep in range(2):
+        out.id.zero_()
+        out.fixed.zero_()
+        codec.decode_frames_async([wire.data_ptr()] * 6, [wire.numel()] * 6, [out] * 6)
+        st = codec.sync()
+        assert st.path == 1 and st.n_rows == n
+        assert torch.equal(out.id[:n], cols.id[:n]) and torch.equal(out.fixed[:n], cols.fixed[:n])

@@ -7,8 +7,9 @@ oracle (oracle/nx_oracle.c) on EVERY column and EVERY byte -- no sampling, no se
 
 plus a frame past the Infinity Cache (the XCD-ordered emit) and the f64 decoders' robustness
 cases: ids whose varints cross 2^28 (5-byte ids), ids in random order (record lengths vary record
-to record: the persistent decoder takes the frame), the length-run decoder's exact path on every
-tile, and two decodes running at once on two streams.
+to record: the single-pass decoder of any f64 frame takes it), that decoder forced on every shape,
+the length-run decoder's exact path on every tile, and two decodes running at once on two streams
+(sequential ids, and ids in random order).
 Reference rules: netidx-core/src/pack.rs:504-555, netidx-value/src/lib.rs:470-506.
 """
 import os
@@ -156,7 +157,7 @@ def test_f64_ids_across_2_28_on_the_fast_path(codec):
 
 def test_f64_ids_in_random_order(codec):
     """Record lengths that vary record to record: the length-run decoder hands the frame to the
-    persistent decoder (DevStatus.irregular), still on path 1 and bit-exact."""
+    single-pass decoder (DevStatus.irregular), still on path 1 and bit-exact."""
     import netidx_amd
     import nxo
     from netidx_amd import synth
@@ -166,7 +167,7 @@ def test_f64_ids_in_random_order(codec):
     ids = np.random.default_rng(74).permutation(ids)
     wire = nxo.encode_f64(ids, vals)
     cols = Columns(n, 0, 0, netidx_amd.LAYOUT_F64, "cuda")
-    for _ in range(2):  # the second frame goes straight to the persistent decoder
+    for _ in range(2):  # the second frame goes straight to the single-pass decoder
         _assert_f64(cols, _decode_dev(codec, wire, cols), wire, n)
 
 
@@ -230,6 +231,105 @@ def test_f64_decodes_on_two_streams_at_once():
         pair, sts = run(2, 20)
         for st, o in zip(sts, outs):
             assert st.path == 1 and st.n_rows == n
+            assert torch.equal(o.fixed[:n].cpu(), torch.from_numpy(vals.view(np.int64)))
+        assert pair < 2.5 * solo, (pair, solo)
+    finally:
+        for c in cs:
+            c.close()
+
+
+def _codec_env(name, value):
+    import netidx_amd
+    os.environ[name] = value
+    try:
+        return netidx_amd.Codec(0)
+    finally:
+        del os.environ[name]
+
+
+def test_f64_single_pass_decoder_everywhere():
+    """NXG_F64_PATH=x (read at ctx creation) puts every f64 frame on the single-pass decoder
+    (nxg_decode_f64_x.hip): sequential ids, random order, 5-byte ids in random order, frames of a
+    few records, frames ending on either side of its 4 KiB and 16 KiB boundaries, and malformed
+    frames (the fallback reports the oracle's first error)."""
+    import netidx_amd
+    import nxo
+    from netidx_amd import synth
+    from netidx_amd.codec import Columns
+    c = _codec_env("NXG_F64_PATH", "x")
+    rng = np.random.default_rng(90)
+    try:
+        cases = []
+        ids, vals = synth.f64_columns(1_000_000, 91)
+        cases.append((ids, vals))
+        cases.append((rng.permutation(ids), vals))
+        cases.append((rng.integers(2**28, 2**35, 300_000, dtype=np.uint64), vals[:300_000]))
+        cases.append((rng.integers(0, 2**35, 300_000, dtype=np.uint64), vals[:300_000]))
+        for n in (1, 2, 3, 5, 64, 341, 342, 343, 1365, 1366, 1367, 4000):
+            i2, v2 = synth.f64_columns(n, 92 + n, id_offset=int(rng.integers(0, 2**20)))
+            cases.append((rng.permutation(i2), v2))
+        for ids_, vals_ in cases:
+            n = len(ids_)
+            wire = nxo.encode_f64(ids_, vals_)
+            cols = Columns(n, 0, 0, netidx_amd.LAYOUT_F64, "cuda")
+            _assert_f64(cols, _decode_dev(c, wire, cols), wire, n)
+        # frames of exactly 4096 / 16384 bytes +- one record
+        for target in (4096, 16384, 65536):
+            i3, v3 = synth.f64_columns(target // 12 + 2, 93, id_offset=200)  # 13-byte records
+            wire = nxo.encode_f64(i3, v3)
+            for n in range(target // 13 - 1, target // 13 + 2):
+                w = wire[: 13 * n]
+                cols = Columns(n, 0, 0, netidx_amd.LAYOUT_F64, "cuda")
+                _assert_f64(cols, _decode_dev(c, w, cols), w, n)
+        # malformed: a record cut short, a wrong value tag: the oracle's (kind, offset)
+        ids, vals = synth.f64_columns(20_000, 94)
+        wire = nxo.encode_f64(rng.permutation(ids), vals)
+        for bad in (wire[:-3], np.concatenate([wire[:13 * 777 + 3], [0x77], wire[13 * 777 + 4:]])):
+            bad = np.ascontiguousarray(bad, np.uint8)
+            cols = Columns.for_frame(len(bad), netidx_amd.LAYOUT_MIXED, "cuda")
+            st = _decode_dev(c, bad, cols)
+            o = nxo.decode(bad)
+            assert st.err_kind == o.s.err_kind != 0 and st.err_offset == o.s.err_offset
+    finally:
+        c.close()
+
+
+def test_f64_random_order_decodes_on_two_streams_at_once():
+    """The two-stream co-residency test on a frame with ids in random order (the single-pass
+    decoder: its workgroups wait only on lower-numbered ones)."""
+    import netidx_amd
+    import nxo
+    import torch
+    from netidx_amd import synth
+    from netidx_amd.codec import Columns
+    n = 10_000_000
+    ids, vals = synth.f64_columns(n, 95)
+    ids = np.random.default_rng(96).permutation(ids)
+    wire = torch.from_numpy(nxo.encode_f64(ids, vals)).cuda()
+    cs = [_codec_env("NXG_F64_PATH", "x") for _ in range(2)]
+    ss = [torch.cuda.Stream() for _ in range(2)]
+    outs = [Columns(n, 0, 0, netidx_amd.LAYOUT_F64, "cuda") for _ in range(2)]
+    try:
+        for c, s in zip(cs, ss):
+            c.set_stream(s.cuda_stream)
+
+        def run(k_ctx, reps):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                for k in range(k_ctx):
+                    cs[k].decode_async(wire.data_ptr(), wire.numel(), outs[k])
+            sts = [cs[k].sync() for k in range(k_ctx)]
+            torch.cuda.synchronize()
+            return (time.perf_counter() - t0) / reps, sts
+
+        run(1, 3)
+        run(2, 3)
+        solo, _ = run(1, 20)
+        pair, sts = run(2, 20)
+        for st, o in zip(sts, outs):
+            assert st.path == 1 and st.n_rows == n
+            assert torch.equal(o.id[:n].cpu(), torch.from_numpy(ids.view(np.int64)))
             assert torch.equal(o.fixed[:n].cpu(), torch.from_numpy(vals.view(np.int64)))
         assert pair < 2.5 * solo, (pair, solo)
     finally:

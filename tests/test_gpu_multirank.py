@@ -1,0 +1,103 @@
+"""The library's multi-rank protocols (nxg_multi.cpp) with 2 and 3 processes sharing device 0,
+each running the real kernels on its shard of a 10^7-record batch (BASELINE configs[4] at one
+tenth of its size).
+
+RCCL refuses two ranks on one device, so the transport is gloo behind nxg_comm_init_ops (device
+buffers staged through host memory by the test's callbacks); everything else is the product:
+each rank encodes its shard on the GPU straight into its place in the full frame
+(nxg_encode_allgather), the full frame is then decoded in byte ranges, one per rank, by the
+length-run kernels (nxg_decode_sharded), the summaries linked and the rows numbered. Checked: the
+whole frame on every rank byte for byte against the oracle's encoder, and every rank's rows
+against the batch's columns at its global row offset.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+pytestmark = [pytest.mark.gpu, pytest.mark.timeout(300)]
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _rank(rank, world, port, total, outdir):
+    import torch
+    import torch.distributed as dist
+    import netidx_amd
+    import nxo
+    from netidx_amd import shard, synth
+    from netidx_amd.codec import Columns
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        codec = netidx_amd.Codec(0)
+        b, e = shard.shard_range(total, world, rank)
+        ids, vals = synth.f64_columns(e - b, synth.SEED_8GPU, id_offset=b)
+        cols = netidx_amd.columns_from_arrays(ids, vals)
+        cap = 15 * total + 64
+        dout = torch.zeros(cap, dtype=torch.uint8, device="cuda")
+
+        def allgather(mine):
+            t = torch.frombuffer(bytearray(mine), dtype=torch.uint8)
+            out = [torch.empty_like(t) for _ in range(world)]
+            dist.all_gather(out, t)
+            return b"".join(x.numpy().tobytes() for x in out)
+
+        def allgatherv(buf_ptr, off, n, r):
+            assert buf_ptr == dout.data_ptr()
+            torch.cuda.synchronize()
+            host = dout[: off[-1]].cpu()
+            shard.allgather_at_offsets(host, off, r, n)
+            dout[: off[-1]].copy_(host)
+            torch.cuda.synchronize()
+
+        comm = netidx_amd.Comm.with_ops(codec, world, rank, allgather, allgatherv)
+        W, offs = comm.encode_allgather(cols, None, dout.data_ptr(), cap)
+        all_ids, all_vals = synth.f64_columns(total, synth.SEED_8GPU)
+        want = nxo.encode_f64(all_ids, all_vals)
+        frame_ok = W == len(want) and np.array_equal(dout[:W].cpu().numpy(), want)
+        del cols
+        out = Columns((W // world) // 12 + 1024, 0, 0, netidx_amd.LAYOUT_F64, "cuda")
+        row_off, rng = comm.decode_sharded(dout, W, out)
+        n = int(rng.n_rows)
+        got_id = out.id[:n].cpu().numpy().view(np.uint64)
+        got_val = out.fixed[:n].cpu().numpy().view(np.uint64)
+        rows_ok = np.array_equal(got_id, all_ids[row_off:row_off + n]) and \
+            np.array_equal(got_val, all_vals[row_off:row_off + n])
+        np.save(os.path.join(outdir, f"r{rank}.npy"),
+                np.array([W, int(frame_ok), row_off, n, int(rows_ok), rng.begin, rng.end,
+                          rng.entry, rng.exit] + list(offs), dtype=np.int64))
+        comm.close()
+        codec.close()
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_library_protocols_on_real_kernels(tmp_path, world):
+    import torch.multiprocessing as mp
+    from netidx_amd import shard
+    total = 10_000_000
+    mp.spawn(_rank, args=(world, _free_port(), total, str(tmp_path)), nprocs=world, join=True)
+    res = [np.load(tmp_path / f"r{r}.npy") for r in range(world)]
+    W = int(res[0][0])
+    rows = 0
+    for r, x in enumerate(res):
+        assert int(x[0]) == W and int(x[1]) == 1, f"rank {r}: the gathered frame differs"
+        assert int(x[4]) == 1, f"rank {r}: its rows differ from the batch"
+        assert int(x[2]) == rows  # row offsets number the ranges in order
+        rows += int(x[3])
+        assert (int(x[5]), int(x[6])) == shard.shard_range(W, world, r)
+        assert list(x[9:]) == list(res[0][9:])  # every rank saw the same shard offsets
+    assert rows == total
+    assert int(res[0][7]) == 0 and int(res[-1][8]) == W
+    for a, b in zip(res, res[1:]):
+        assert int(a[8]) == int(b[7])  # each range leaves where the next enters
