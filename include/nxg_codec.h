@@ -421,6 +421,12 @@ int64_t nxg_msg_subscribed(const char* path, uint64_t path_len, uint64_t id, uin
                            uint64_t cap);
 /* From::Heartbeat (2 bytes) */
 int64_t nxg_msg_heartbeat(uint8_t* out, uint64_t cap);
+/* From::Update(id, value) with a scalar value (tag/fixed/aux as NxgColumns; String and Bytes
+ * bytes at `text`): one message as Val::update + commit queue it (publisher/mod.rs:517-519,
+ * 776-845) and handle_updates encodes it (server.rs:604-629) -- the host path of a publisher
+ * that updates one value at a time (BASELINE configs[0]). */
+int64_t nxg_msg_update(uint64_t id, uint8_t tag, uint64_t fixed, uint32_t aux,
+                       const uint8_t* text, uint8_t* out, uint64_t cap);
 /* One control message parsed: to = 0 a publisher::From, 1 a publisher::To. Offsets index `buf`.
  * value_fixed holds scalar payloads as read (big-endian integers, varints as decoded, zigzag
  * not undone); other values are reported by tag and span. */
@@ -437,6 +443,43 @@ typedef struct NxgCtlMsg {
     uint32_t value_tag, value_aux;
 } NxgCtlMsg;
 bool nxg_msg_parse(const uint8_t* buf, uint64_t len, int to, NxgCtlMsg* m, NetidxError* err);
+
+/* ---- a machine-local anonymous resolver (BASELINE configs[0]) ------------------------------
+ * The control plane the examples need to find each other, host only: the resolver server's
+ * anonymous read and write paths (netidx/src/resolver_server/mod.rs:458-480, 771-860), the write
+ * client's hello and ToWrite::Publish (resolver_client/write_client.rs:194-221), the read client's
+ * hello and ToRead::Resolve -> FromRead::Publisher + FromRead::Resolved (read_client.rs:84-99,
+ * resolver_server/shard_store.rs:160-193, 600-640). Blocking sockets; the server runs a thread per
+ * client. Authentication other than anonymous, referrals and clustering are out of scope. */
+typedef struct NxgResolver NxgResolver;
+typedef struct NxgResolverClient NxgResolverClient;
+NxgResolver* nxg_resolver_start(const char* ipv4, uint16_t port, uint16_t* bound_port,
+                                uint64_t writer_ttl_secs, NetidxError* err);
+void nxg_resolver_stop(NxgResolver* r);
+uint64_t nxg_resolver_n_published(NxgResolver* r);
+/* a publisher's resolver connection: ClientHello::WriteOnly { write_addr, Anonymous, Normal } */
+NxgResolverClient* nxg_resolver_connect_write(const char* ipv4, uint16_t port,
+                                              uint32_t write_ipv4, uint16_t write_port,
+                                              uint64_t* ttl_out, NetidxError* err);
+/* a subscriber's: ClientHello::ReadOnly(Anonymous) */
+NxgResolverClient* nxg_resolver_connect_read(const char* ipv4, uint16_t port, NetidxError* err);
+void nxg_resolver_client_close(NxgResolverClient* c);
+/* ToWrite::Publish(path), true once FromWrite::Published is back */
+bool nxg_resolver_publish(NxgResolverClient* c, const char* path, uint64_t path_len,
+                          NetidxError* err);
+/* ToRead::Resolve(path): the Resolved reply; its first publisher's address from the
+ * FromRead::Publisher that precedes it (n_publishers = 0: nobody publishes the path) */
+typedef struct NxgResolved {
+    uint32_t n_publishers;
+    uint32_t publisher_ipv4; /* host byte order */
+    uint64_t publisher_id;
+    uint16_t publisher_port, resolver_port;
+    uint32_t resolver_ipv4;
+    uint64_t timestamp;
+    uint32_t flags, permissions;
+} NxgResolved;
+bool nxg_resolver_resolve(NxgResolverClient* c, const char* path, uint64_t path_len,
+                          NxgResolved* out, NetidxError* err);
 
 /* ---- host framing (netidx/src/channel.rs) ------------------------------------------------
  * Frame boundaries exactly as WriteChannel::queue_send/try_flush split the buffer. The split

@@ -10,7 +10,8 @@ from .codec import (BUFFER_SHORT, CAPACITY, DEPTH, HINT_MIXED, INVALID_FORMAT, L
                     Columns, Dispatch, FrameReader, PackError, PubTable, PUB_UPDATE, PUB_UPDATE_CHANGED,
                     PUB_UPDATE_CLIENT, SubTable, columns_from_arrays, frame_header,
                     frame_parse_header, frame_split, lib, Comm, NxgRange, range_link, Session,
-                    msg_subscribe, msg_subscribed, msg_heartbeat, msg_parse, TAG_UNSUBSCRIBED)
+                    msg_subscribe, msg_subscribed, msg_heartbeat, msg_parse, msg_update,
+                    TAG_UNSUBSCRIBED, Resolver, ResolverClient)
 
 __all__ = ["Codec", "Columns", "PackError", "CodecError", "columns_from_arrays", "lib",
            "frame_split", "frame_header", "frame_parse_header", "LAYOUT_F64", "LAYOUT_MIXED",
@@ -18,4 +19,5 @@ __all__ = ["Codec", "Columns", "PackError", "CodecError", "columns_from_arrays",
            "CAPACITY", "NOT_F64", "SubTable", "Dispatch", "NO_SLOT",
            "PubTable", "FrameReader", "PUB_UPDATE", "PUB_UPDATE_CHANGED", "PUB_UPDATE_CLIENT",
            "Comm", "NxgRange", "range_link", "Session", "msg_subscribe", "msg_subscribed",
-           "msg_heartbeat", "msg_parse", "TAG_UNSUBSCRIBED"]
+           "msg_heartbeat", "msg_parse", "msg_update", "TAG_UNSUBSCRIBED", "Resolver",
+           "ResolverClient"]

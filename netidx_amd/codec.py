@@ -106,6 +106,13 @@ class NxgCtlMsg(C.Structure):
                 ("value_tag", C.c_uint32), ("value_aux", C.c_uint32)]
 
 
+class NxgResolved(C.Structure):
+    _fields_ = [("n_publishers", C.c_uint32), ("publisher_ipv4", C.c_uint32),
+                ("publisher_id", C.c_uint64), ("publisher_port", C.c_uint16),
+                ("resolver_port", C.c_uint16), ("resolver_ipv4", C.c_uint32),
+                ("timestamp", C.c_uint64), ("flags", C.c_uint32), ("permissions", C.c_uint32)]
+
+
 class NxgStatus(C.Structure):
     _fields_ = [
         ("n_rows", C.c_uint64), ("n_children", C.c_uint64), ("n_ctl", C.c_uint64),
@@ -194,6 +201,20 @@ SIGNATURES = {
     "nxg_msg_subscribed": (C.c_int64, [C.c_char_p, C.c_uint64, C.c_uint64, C.c_uint8, C.c_uint64,
                                        C.c_uint32, C.c_void_p, C.c_void_p, C.c_uint64]),
     "nxg_msg_heartbeat": (C.c_int64, [C.c_void_p, C.c_uint64]),
+    "nxg_msg_update": (C.c_int64, [C.c_uint64, C.c_uint8, C.c_uint64, C.c_uint32, C.c_void_p,
+                                   C.c_void_p, C.c_uint64]),
+    "nxg_resolver_start": (C.c_void_p, [C.c_char_p, C.c_uint16, C.POINTER(C.c_uint16),
+                                        C.c_uint64, C.POINTER(NetidxError)]),
+    "nxg_resolver_stop": (None, [C.c_void_p]),
+    "nxg_resolver_n_published": (C.c_uint64, [C.c_void_p]),
+    "nxg_resolver_connect_write": (C.c_void_p, [C.c_char_p, C.c_uint16, C.c_uint32, C.c_uint16,
+                                                C.POINTER(C.c_uint64), C.POINTER(NetidxError)]),
+    "nxg_resolver_connect_read": (C.c_void_p, [C.c_char_p, C.c_uint16, C.POINTER(NetidxError)]),
+    "nxg_resolver_client_close": (None, [C.c_void_p]),
+    "nxg_resolver_publish": (C.c_bool, [C.c_void_p, C.c_char_p, C.c_uint64,
+                                        C.POINTER(NetidxError)]),
+    "nxg_resolver_resolve": (C.c_bool, [C.c_void_p, C.c_char_p, C.c_uint64,
+                                        C.POINTER(NxgResolved), C.POINTER(NetidxError)]),
     "nxg_msg_parse": (C.c_bool, [C.c_void_p, C.c_uint64, C.c_int, C.POINTER(NxgCtlMsg),
                                  C.POINTER(NetidxError)]),
     "nxg_frame_reader_new": (C.c_void_p, [C.POINTER(NetidxError)]),
@@ -734,6 +755,89 @@ def msg_subscribed(path, id, tag, fixed=0, aux=0, text=b""):
 
 def msg_heartbeat():
     return _msg(lib().nxg_msg_heartbeat)
+
+
+def msg_update(id, tag, fixed=0, aux=0, text=b""):
+    """From::Update(id, scalar value) as one len-wrapped message (nxg_msg_update)."""
+    t = (C.c_uint8 * max(len(text), 1)).from_buffer_copy(text + b"\0")
+    return _msg(lib().nxg_msg_update, id, tag, fixed, aux, t)
+
+
+def _ip4(ip):
+    a = [int(x) for x in ip.split(".")]
+    return (a[0] << 24) | (a[1] << 16) | (a[2] << 8) | a[3]
+
+
+class Resolver:
+    """A machine-local anonymous resolver server (nxg_resolver_start): threads in the library."""
+
+    def __init__(self, ip="127.0.0.1", port=0, writer_ttl=120):
+        err, bp = NetidxError(), C.c_uint16(0)
+        self.h = lib().nxg_resolver_start(ip.encode(), port, C.byref(bp), writer_ttl,
+                                          C.byref(err))
+        _check(bool(self.h), err)
+        self.ip, self.port = ip, bp.value
+
+    def n_published(self):
+        return lib().nxg_resolver_n_published(self.h)
+
+    def stop(self):
+        if self.h:
+            lib().nxg_resolver_stop(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.stop()
+        except Exception:
+            pass
+
+
+class ResolverClient:
+    """A publisher's (write) or subscriber's (read) connection to a resolver."""
+
+    def __init__(self, h, ttl=None):
+        self.h, self.ttl = h, ttl
+
+    @classmethod
+    def write(cls, ip, port, write_addr):
+        err, ttl = NetidxError(), C.c_uint64(0)
+        h = lib().nxg_resolver_connect_write(ip.encode(), port, _ip4(write_addr[0]),
+                                             write_addr[1], C.byref(ttl), C.byref(err))
+        _check(bool(h), err)
+        return cls(h, ttl.value)
+
+    @classmethod
+    def read(cls, ip, port):
+        err = NetidxError()
+        h = lib().nxg_resolver_connect_read(ip.encode(), port, C.byref(err))
+        _check(bool(h), err)
+        return cls(h)
+
+    def publish(self, path):
+        p = path.encode() if isinstance(path, str) else path
+        err = NetidxError()
+        _check(lib().nxg_resolver_publish(self.h, p, len(p), C.byref(err)), err)
+
+    def resolve(self, path):
+        """NxgResolved; publisher address as ("a.b.c.d", port) in .addr"""
+        p = path.encode() if isinstance(path, str) else path
+        r, err = NxgResolved(), NetidxError()
+        _check(lib().nxg_resolver_resolve(self.h, p, len(p), C.byref(r), C.byref(err)), err)
+        ip = r.publisher_ipv4
+        r.addr = (f"{ip >> 24}.{(ip >> 16) & 255}.{(ip >> 8) & 255}.{ip & 255}", r.publisher_port)
+        return r
+
+    def close(self):
+        if self.h:
+            lib().nxg_resolver_client_close(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def msg_parse(buf, to=False):

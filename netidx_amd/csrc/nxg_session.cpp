@@ -33,8 +33,10 @@
 #include <vector>
 
 #include "../../include/nxg_codec.h"
+#include "nxg_wire.h"
 
 namespace {
+using namespace nxgwire;
 
 void serr(NetidxError* err, const char* fmt, ...) {
     if (!err) return;
@@ -51,44 +53,6 @@ constexpr uint32_t kLenMask = 0x7FFFFFFFu;   // channel.rs:35 (bit 31: encrypted
 constexpr uint64_t kMaxBatch = 0x3FFFFFFF;   // channel.rs:34
 constexpr uint64_t kProtocolVersion = 3;     // subscriber/connection.rs:128
 constexpr size_t kRecvChunk = 4u << 20;      // bytes per recv
-
-uint32_t vlen(uint64_t v) {
-    uint32_t n = 1;
-    while (v >= 0x80) {
-        v >>= 7;
-        n++;
-    }
-    return n;
-}
-uint64_t lwlen(uint64_t n) { return n + vlen(n + vlen(n)); }  // pack.rs:522-525
-
-struct Out {
-    std::vector<uint8_t> b;
-    void u8(uint32_t x) { b.push_back((uint8_t)x); }
-    void be(uint64_t v, int n) {
-        for (int i = n - 1; i >= 0; i--) b.push_back((uint8_t)(v >> (8 * i)));
-    }
-    void var(uint64_t v) {
-        while (v >= 0x80) {
-            b.push_back((uint8_t)((v & 0x7f) | 0x80));
-            v >>= 7;
-        }
-        b.push_back((uint8_t)v);
-    }
-    void bytes(const void* p, size_t n) {
-        const uint8_t* q = static_cast<const uint8_t*>(p);
-        b.insert(b.end(), q, q + n);
-    }
-};
-
-// a derived enum message: varint(lw(1 + fields)) variant fields (netidx-derive lib.rs:289-381)
-std::vector<uint8_t> wrap(uint32_t variant, const std::vector<uint8_t>& fields) {
-    Out o;
-    o.var(lwlen(1 + fields.size()));
-    o.u8(variant);
-    o.bytes(fields.data(), fields.size());
-    return o.b;
-}
 
 // a scalar Value (netidx-value lib.rs:361-468): fixed-width and varint tags, text from `text`
 bool put_value(Out& o, uint8_t tag, uint64_t fixed, uint32_t aux, const uint8_t* text,
@@ -475,6 +439,18 @@ int64_t nxg_msg_subscribed(const char* path, uint64_t path_len, uint64_t id, uin
         if (m.size() > cap) return -(int64_t)NXG_CAPACITY;
         memcpy(out, m.data(), m.size());
     }
+    return (int64_t)m.size();
+}
+
+int64_t nxg_msg_update(uint64_t id, uint8_t tag, uint64_t fixed, uint32_t aux,
+                       const uint8_t* text, uint8_t* out, uint64_t cap) {
+    Out f;
+    f.var(id);  // publisher::Id (netidx-core utils.rs:147-164)
+    if (!put_value(f, tag, fixed, aux, text, nullptr)) return -NXG_UNKNOWN_TAG;
+    const std::vector<uint8_t> m = wrap(4, f.b);  // From::Update (netproto publisher.rs:90)
+    if (!out) return (int64_t)m.size();
+    if (cap < m.size()) return -NXG_CAPACITY;
+    memcpy(out, m.data(), m.size());
     return (int64_t)m.size();
 }
 

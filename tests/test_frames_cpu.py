@@ -157,32 +157,44 @@ def test_control_messages():
 
 def test_config1_loopback_one_f64_path():
     """simple_publisher / simple_subscriber (BASELINE configs[0], examples/examples/
-    simple_publisher.rs:21-47) over loopback TCP through the library's sessions: handshake,
-    To::Subscribe, From::Subscribed with the current value, then one From::Update per value and
-    Heartbeats, each in its own frame. No GPU in this config: the update payloads are made by the
-    oracle encoder (test infrastructure) and checked two ways, by the library's message parser
-    and by the oracle's decode."""
+    simple_publisher.rs:21-47, simple_subscriber.rs:21-55) over loopback TCP, every byte on the
+    wire made by the library: a machine-local resolver (nxg_resolver_*), the publisher publishes
+    its path there (ClientHello::WriteOnly, ToWrite::Publish), the subscriber resolves it
+    (ClientHello::ReadOnly, ToRead::Resolve -> FromRead::Publisher + Resolved) and connects to the
+    address it got; then the session handshake, To::Subscribe, From::Subscribed with the current
+    value, one From::Update per value (nxg_msg_update) and Heartbeats, each in its own frame. No
+    GPU in this config. The oracle only checks the received updates."""
     vals = [1.0, -0.0, 2.5, float("inf"), 1e-300, 3.25]
     bits = [struct.unpack("<Q", struct.pack("<d", v))[0] for v in vals]
+    path = "/local/bench/0"
+    res = netidx_amd.Resolver()
     lst = netidx_amd.Session.listen()
+    wc = netidx_amd.ResolverClient.write("127.0.0.1", res.port, ("127.0.0.1", lst.port))
+    wc.publish(path)
+    assert res.n_published() == 1 and wc.ttl == 120
     done = {}
 
     def publisher():
         s = lst.accept()
         sub = netidx_amd.msg_parse(s.recv_frame(), to=True)
         done["path"] = sub.variant, sub.path_len
-        s.send(netidx_amd.msg_subscribed("/local/bench/0", 0, 9, bits[0]))
+        s.send(netidx_amd.msg_subscribed(path, 0, 9, bits[0]))
         for k, b in enumerate(bits[1:]):
             if k % 2:
                 s.send(netidx_amd.msg_heartbeat())
-            s.send(nxo.encode_f64(np.array([0], np.uint64), np.array([b], np.uint64)).tobytes())
+            s.send(netidx_amd.msg_update(0, 9, b))
         done["stats"] = s.stats()
         s.close()
 
     t = threading.Thread(target=publisher)
     t.start()
-    sub = netidx_amd.Session.connect("127.0.0.1", lst.port)
-    sub.send(netidx_amd.msg_subscribe("/local/bench/0"))
+    rc = netidx_amd.ResolverClient.read("127.0.0.1", res.port)
+    r = rc.resolve(path)
+    assert r.n_publishers == 1 and r.addr == ("127.0.0.1", lst.port)
+    assert r.permissions == 0x3F and r.resolver_port == res.port
+    sub = netidx_amd.Session.connect(*r.addr)
+    sub.send(netidx_amd.msg_subscribe(path, timestamp=r.timestamp, permissions=r.permissions,
+                                      resolver=(r.resolver_ipv4, r.resolver_port)))
     first = netidx_amd.msg_parse(sub.recv_frame())
     assert first.variant == 3 and first.id == 0 and first.value_tag == 9
     got, hb = [first.value_fixed], 0
@@ -193,12 +205,29 @@ def test_config1_loopback_one_f64_path():
             hb += 1
             continue
         assert m.variant == 4 and m.id == 0 and m.value_tag == 9 and m.msg_len == len(f)
-        d = nxo.decode(f).trim()
+        d = nxo.decode(f).trim()  # checker
         assert d["err_kind"] == 0 and int(d["fixed"][0]) == m.value_fixed
         got.append(m.value_fixed)
     t.join()
     st = sub.stats()
     sub.close()
     lst.close()
-    assert got == bits and hb == 2 and done["path"] == (0, len("/local/bench/0"))
+    rc.close()
+    wc.close()
+    res.stop()
+    assert got == bits and hb == 2 and done["path"] == (0, len(path))
     assert st["frames_in"] == len(vals) + hb and done["stats"]["frames_out"] == len(vals) + hb
+
+
+def test_msg_update_bytes():
+    """From::Update built by the library: SURVEY.md Appendix B's known answers."""
+    one = struct.unpack("<Q", struct.pack("<d", 1.0))[0]
+    assert netidx_amd.msg_update(0, 9, one).hex() == "0c0400093ff0000000000000"
+    nz = struct.unpack("<Q", struct.pack("<d", -0.0))[0]
+    assert netidx_amd.msg_update(128, 9, nz).hex() == "0d0480010980" + "00" * 7
+    assert netidx_amd.msg_update(0, 16).hex() == "04040010"
+    assert netidx_amd.msg_update(5, 12, 0, 120, b"a" * 120).hex() == "7d04050c78" + "61" * 120
+    for v in (0, 1, 2**21, 2**35 + 3):
+        m = netidx_amd.msg_update(v, 6, 2**64 - 5)
+        d = nxo.decode(m).trim()
+        assert d["err_kind"] == 0 and int(d["id"][0]) == v and int(d["fixed"][0]) == 2**64 - 5

@@ -1,0 +1,127 @@
+"""The machine-local resolver (nxg_resolver.cpp) spoken to byte for byte over raw sockets, with
+every expected byte derived by hand from the reference's rules: raw messages are a u32
+big-endian length + the packed value (netidx/src/channel.rs:63-105); derived structs and enums
+are length-wrapped, enum variants in declaration order (netidx-derive/src/lib.rs); SocketAddr V4
+is 00 + u32 + u16 (netidx-core/src/pack.rs:187-237); the messages are netidx-netproto/src/
+resolver.rs:23-293 and the server's replies resolver_server/mod.rs:300-345, 458-480, 771-860,
+shard_store.rs:160-193 and 600-640.
+"""
+import socket
+import struct
+
+import netidx_amd
+
+VERSION = bytes.fromhex("00000008" "0000000000000003")
+
+
+def recv_exact(s, n):
+    b = b""
+    while len(b) < n:
+        x = s.recv(n - len(b))
+        assert x, "connection closed"
+        b += x
+    return b
+
+
+def recv_frame(s):
+    n = struct.unpack(">I", recv_exact(s, 4))[0]
+    return recv_exact(s, n)
+
+
+def frame(payload):
+    return struct.pack(">I", len(payload)) + payload
+
+
+def addr(ip, port):
+    return b"\x00" + socket.inet_aton(ip) + struct.pack(">H", port)
+
+
+def hello(sock):
+    assert recv_exact(sock, 12) == VERSION
+    sock.sendall(VERSION)
+
+
+def test_write_handshake_publish_heartbeat():
+    res = netidx_amd.Resolver(writer_ttl=77)
+    s = socket.create_connection(("127.0.0.1", res.port))
+    try:
+        hello(s)
+        # ClientHello::WriteOnly(ClientHelloWrite { write_addr 127.0.0.1:5555, Anonymous,
+        # Normal }): fields 7 + 2 + 2 = 11 -> struct lw(11) = 12; enum body 1 + 12 = 13 -> lw 14
+        fields = addr("127.0.0.1", 5555) + b"\x02\x00" + b"\x02\x01"
+        msg = bytes([14, 1, 12]) + fields
+        s.sendall(frame(msg))
+        # ServerHelloWrite { ttl 77, ttl_expired, Anonymous, resolver_id }: 8 + 1 + 2 + 7 = 18
+        # -> lw(18) = 19
+        r = recv_frame(s)
+        assert r == bytes([19]) + struct.pack(">Q", 77) + b"\x01" + b"\x02\x00" + \
+            addr("127.0.0.1", res.port)
+        # a batch of one Heartbeat (02 04) is not answered; Publish("/a") = 05 00 02 2f 61
+        s.sendall(frame(b"\x02\x04"))
+        s.sendall(frame(b"\x05\x00\x02/a" + b"\x05\x00\x02/b"))
+        assert recv_frame(s) == b"\x02\x00\x02\x00"  # FromWrite::Published x2
+        assert res.n_published() == 2
+        # Unpublish("/a") (variant 2) -> Unpublished (02 01); Clear (02 03) -> Unpublished
+        s.sendall(frame(b"\x05\x02\x02/a"))
+        assert recv_frame(s) == b"\x02\x01"
+        assert res.n_published() == 1
+        s.sendall(frame(b"\x02\x03"))
+        assert recv_frame(s) == b"\x02\x01"
+        assert res.n_published() == 0
+    finally:
+        s.close()
+        res.stop()
+
+
+def test_read_handshake_resolve():
+    res = netidx_amd.Resolver()
+    wc = netidx_amd.ResolverClient.write("127.0.0.1", res.port, ("127.0.0.1", 4242))
+    wc.publish("/local/x")
+    s = socket.create_connection(("127.0.0.1", res.port))
+    try:
+        hello(s)
+        # ClientHello::ReadOnly(AuthRead::Anonymous): body 1 + 2 = 3 -> lw(3) = 4
+        s.sendall(frame(b"\x04\x00\x02\x00"))
+        assert recv_frame(s) == b"\x02\x00"  # AuthRead::Anonymous
+        # ToRead::Resolve("/local/x"): body 1 + 1 + 8 = 10 -> lw 11
+        s.sendall(frame(b"\x0b\x00\x08/local/x" + b"\x05\x00\x02/q"))
+        r = recv_frame(s)
+        # FromRead::Publisher(Publisher { resolver, id 0, addr, Sha3_512, Anonymous, None,
+        # Normal }): fields 7 + 1 + 7 + 2 + 2 + 1 + 2 = 22 -> struct 23; enum 24 -> lw 25
+        pub = bytes([25, 0, 23]) + addr("127.0.0.1", res.port) + b"\x00" + \
+            addr("127.0.0.1", 4242) + b"\x02\x00" + b"\x02\x00" + b"\x00" + b"\x02\x01"
+        assert r[:len(pub)] == pub
+        r = r[len(pub):]
+        # FromRead::Resolved(Resolved { resolver, [PublisherRef { 0, b"" }], timestamp, flags 0,
+        # permissions 0x3f }): fields 7 + 1 + 3 + 8 + 4 + 4 = 27 -> struct 28; enum 29 -> lw 30
+        head = bytes([30, 1, 28]) + addr("127.0.0.1", res.port) + b"\x01" + b"\x03\x00\x00"
+        assert r[:len(head)] == head
+        ts, flags, perm = struct.unpack(">QII", r[len(head):len(head) + 16])
+        assert ts > 1_600_000_000 and flags == 0 and perm == 0x3F
+        r = r[len(head) + 16:]
+        # the unpublished path: Resolved with no publishers (fields 7 + 1 + 16 = 24 -> 25; 27)
+        head = bytes([27, 1, 25]) + addr("127.0.0.1", res.port) + b"\x00"
+        assert r[:len(head)] == head and len(r) == len(head) + 16
+    finally:
+        s.close()
+        wc.close()
+        res.stop()
+
+
+def test_clients_against_each_other():
+    res = netidx_amd.Resolver()
+    try:
+        wcs = [netidx_amd.ResolverClient.write("127.0.0.1", res.port, ("127.0.0.1", 7000 + k))
+               for k in range(3)]
+        for k, w in enumerate(wcs):
+            w.publish(f"/p/{k}")
+        rc = netidx_amd.ResolverClient.read("127.0.0.1", res.port)
+        for k in range(3):
+            x = rc.resolve(f"/p/{k}")
+            assert x.n_publishers == 1 and x.addr == ("127.0.0.1", 7000 + k) and x.publisher_id == k
+        assert rc.resolve("/p/9").n_publishers == 0
+        rc.close()
+        for w in wcs:
+            w.close()
+    finally:
+        res.stop()
