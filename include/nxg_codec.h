@@ -374,6 +374,36 @@ bool nxg_decode_archive_batch(NxgCtx* ctx, const uint8_t* buf, uint64_t len, Nxg
 bool nxg_encode_archive_batch(NxgCtx* ctx, const NxgColumns* in, const uint8_t* heap,
                               uint8_t* out, uint64_t cap, uint64_t* len_out, NetidxError* err);
 
+/* ---- compressed archive batches: replaces the compressed branch of ArchiveReader::get_batch_at
+ * (netidx-archive/src/logfile/reader.rs:453-477): a record after its RecordHeader is
+ * u32 BE uncompressed record length | the RecordIndex (indexed files: a varint that is its own
+ * length, then the ids) | one zstd frame of the batch, compressed with the archive's dictionary
+ * (reader.rs:243-244, 737-801; zstd 0.13 = libzstd 1.5, RFC 8878). The frames are decompressed on
+ * the device, many records per call; nxg_decode_archive_batch then decodes each batch.
+ * A dictionary (the archive's, from its header): zstd format (magic EC30A437: entropy tables,
+ * repeat offsets, content) or raw content. */
+typedef struct NxgZstdDict NxgZstdDict;
+NxgZstdDict* nxg_zstd_dict_new(NxgCtx* ctx, const uint8_t* dict, uint64_t len, NetidxError* err);
+void nxg_zstd_dict_free(NxgZstdDict* d);
+/* one record: in, its bytes [off, off + len) of `src` (after the RecordHeader); out, its batch at
+ * [out_off, out_off + out_len) of `dout` (each record has room for its uncompressed length), and
+ * err: 0, or 1 not a zstd frame / trailing bytes, 2 corrupt, 3 the batch is longer than the
+ * record's uncompressed length, 4 dictionary missing or of another id, 5 checksum mismatch, 6
+ * frame content size mismatch, 7 record too short. A record's failure is its own (the
+ * reference fails that get_batch); the others are decompressed. */
+typedef struct NxgArchiveRecord {
+    uint64_t off, len;
+    uint64_t out_off, out_len;
+    uint32_t err, pad;
+} NxgArchiveRecord;
+/* src: host memory (the archive's mmap), src_len bytes; dout: device memory of `cap` bytes (NULL:
+ * *need = the bytes the records need). dict may be NULL (frames without a dictionary). The host
+ * reads the records' lengths and index prefixes; the frames go to the device in one copy.
+ * Synchronous. Returns false on misuse, a HIP failure or cap < *need. */
+bool nxg_archive_decompress(NxgCtx* ctx, const NxgZstdDict* dict, const uint8_t* src,
+                            uint64_t src_len, NxgArchiveRecord* recs, uint32_t n, bool indexed,
+                            uint8_t* dout, uint64_t cap, uint64_t* need, NetidxError* err);
+
 /* ---- the publisher <-> subscriber connection (BASELINE configs[0]) ------------------------
  * Replaces hello_publisher (netidx/src/subscriber/connection.rs:120-140), ClientCtx::hello
  * (publisher/server.rs:367-381), read_task / flush_buf (channel.rs:107-126, 379-443) and the

@@ -113,6 +113,11 @@ class NxgResolved(C.Structure):
                 ("timestamp", C.c_uint64), ("flags", C.c_uint32), ("permissions", C.c_uint32)]
 
 
+class NxgArchiveRecord(C.Structure):
+    _fields_ = [("off", C.c_uint64), ("len", C.c_uint64), ("out_off", C.c_uint64),
+                ("out_len", C.c_uint64), ("err", C.c_uint32), ("pad", C.c_uint32)]
+
+
 class NxgStatus(C.Structure):
     _fields_ = [
         ("n_rows", C.c_uint64), ("n_children", C.c_uint64), ("n_ctl", C.c_uint64),
@@ -175,6 +180,13 @@ SIGNATURES = {
                                       C.POINTER(NetidxError)]),
     "nxg_publish_unsubscribes": (C.c_bool, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64,
                                             C.c_uint32, C.c_void_p, C.POINTER(NetidxError)]),
+    "nxg_zstd_dict_new": (C.c_void_p, [C.c_void_p, C.c_void_p, C.c_uint64,
+                                       C.POINTER(NetidxError)]),
+    "nxg_zstd_dict_free": (None, [C.c_void_p]),
+    "nxg_archive_decompress": (C.c_bool, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64,
+                                          C.POINTER(NxgArchiveRecord), C.c_uint32, C.c_bool,
+                                          C.c_void_p, C.c_uint64, C.POINTER(C.c_uint64),
+                                          C.POINTER(NetidxError)]),
     "nxg_decode_archive_batch": (C.c_bool, [C.c_void_p, C.c_void_p, C.c_uint64,
                                             C.POINTER(NxgColumns), C.POINTER(NxgStatus),
                                             C.POINTER(C.c_uint64), C.POINTER(NetidxError)]),
@@ -241,6 +253,8 @@ def lib():
             raise CodecError(f"{LIB_PATH} missing: build it (python -c 'import __graft_entry__ as g; g.build()')")
         L = C.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
+            if os.environ.get("NXG_LIB") and not hasattr(L, name):
+                continue  # an A/B build of an older source may lack newer entry points
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args
@@ -257,6 +271,24 @@ def _check(ok, err):
 
 def _ptr(t):
     return C.c_void_p(t.data_ptr()) if t is not None else C.c_void_p(0)
+
+
+class ZstdDict:
+    """A device-resident zstd dictionary (nxg_zstd_dict_new / _free)."""
+
+    def __init__(self, h):
+        self.h = h
+
+    def close(self):
+        if self.h:
+            lib().nxg_zstd_dict_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class Columns:
@@ -401,6 +433,37 @@ class Codec:
                                               C.c_void_p(out.data_ptr()), out.numel(), C.byref(n),
                                               C.byref(err)), err)
         return n.value
+
+    def zstd_dict(self, data):
+        """A compressed archive's zstd dictionary on the device (nxg_zstd_dict_new)."""
+        b = bytes(data)
+        a = (C.c_uint8 * max(len(b), 1)).from_buffer_copy(b + b"\0")
+        err = NetidxError()
+        h = lib().nxg_zstd_dict_new(self.ctx, a, len(b), C.byref(err))
+        _check(bool(h), err)
+        return ZstdDict(h)
+
+    def archive_decompress(self, src, records, indexed=False, zdict=None, out=None):
+        """Compressed archive records (host bytes `src`, [(off, len)] after each RecordHeader)
+        decompressed on the device (nxg_archive_decompress). Returns (device uint8 tensor,
+        [(out_off, out_len, err)])."""
+        import torch
+        b = src if isinstance(src, np.ndarray) else np.frombuffer(bytes(src), np.uint8)
+        b = np.ascontiguousarray(b)
+        n = len(records)
+        recs = (NxgArchiveRecord * max(n, 1))()
+        for i, (o, ln) in enumerate(records):
+            recs[i].off, recs[i].len = o, ln
+        need, err = C.c_uint64(0), NetidxError()
+        dh = zdict.h if zdict else None
+        _check(lib().nxg_archive_decompress(self.ctx, dh, C.c_void_p(b.ctypes.data), len(b), recs,
+                                            n, indexed, None, 0, C.byref(need), C.byref(err)), err)
+        if out is None:
+            out = torch.empty(max(need.value, 1), dtype=torch.uint8, device="cuda")
+        _check(lib().nxg_archive_decompress(self.ctx, dh, C.c_void_p(b.ctypes.data), len(b), recs,
+                                            n, indexed, C.c_void_p(out.data_ptr()), out.numel(),
+                                            C.byref(need), C.byref(err)), err)
+        return out, [(recs[i].out_off, recs[i].out_len, recs[i].err) for i in range(n)]
 
     def decode_batch(self, frame, layout=LAYOUT_MIXED, flags=0, device="cuda"):
         """Decode one frame payload; returns (Columns, NxgStatus)."""

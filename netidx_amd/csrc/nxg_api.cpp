@@ -101,6 +101,12 @@ struct NxgCtx {
         uint32_t slot;
     };
     std::vector<Pending> pending;
+    // zstd (compressed archive records): predefined tables, literal buffers, descriptors
+    void* zdefs = nullptr;
+    uint8_t* zlit = nullptr;
+    int zgrid = 0;
+    void* zrecs = nullptr;
+    size_t zrecs_cap = 0;
     DevStatus last{};  // last completed decode's device status (diagnostics)
     uint64_t last_split = 0;  // last completed encode's DevStatus.split_start
 };
@@ -638,6 +644,9 @@ void nxg_ctx_destroy(NxgCtx* c) {
     if (c->dframe) (void)hipFree(c->dframe);
     if (c->escratch) (void)hipFree(c->escratch);
     if (c->rdesc) (void)hipFree(c->rdesc);
+    if (c->zdefs) (void)hipFree(c->zdefs);
+    if (c->zlit) (void)hipFree(c->zlit);
+    if (c->zrecs) (void)hipFree(c->zrecs);
     if (c->dheap) (void)hipFree(c->dheap);
     if (c->dst) (void)hipFree(c->dst);
     if (c->hst) (void)hipHostFree(c->hst);
@@ -1023,6 +1032,164 @@ bool nxg_encode_archive_batch(NxgCtx* c, const NxgColumns* in, const uint8_t* he
     if (!finish_encode(c, in, st, slot, &total, cap, out != nullptr, err)) return false;
     if (in->n_rows == 0) total = hl;
     if (len_out) *len_out = total;
+    return true;
+}
+
+struct NxgZstdDict {
+    int device;
+    void* ddev = nullptr;       // NxzDictDev
+    uint8_t* content = nullptr;  // the dictionary's content (history before every frame)
+};
+
+NxgZstdDict* nxg_zstd_dict_new(NxgCtx* c, const uint8_t* dict, uint64_t len, NetidxError* err) {
+    if (!c || (!dict && len)) {
+        set_err(err, "null argument");
+        return nullptr;
+    }
+    if (!set_device(c, err)) return nullptr;
+    std::vector<uint8_t> host(nxg_zstd_dict_dev_bytes());
+    NxzDictDev* hd = reinterpret_cast<NxzDictDev*>(host.data());
+    uint64_t coff = 0;
+    if (!nxg_zstd_build_dict(dict, len, hd, &coff)) {
+        set_err(err, "not a valid zstd dictionary");
+        return nullptr;
+    }
+    NxgZstdDict* d = new NxgZstdDict();
+    d->device = c->device;
+    const uint64_t clen = len - coff;
+    auto fail = [&](hipError_t e) -> NxgZstdDict* {
+        set_err(err, "zstd dictionary upload: %s", hipGetErrorString(e));
+        nxg_zstd_dict_free(d);
+        return nullptr;
+    };
+    hipError_t e;
+    if ((e = hipMalloc(&d->content, std::max<uint64_t>(clen, 1))) != hipSuccess) return fail(e);
+    if (clen && (e = hipMemcpy(d->content, dict + coff, clen, hipMemcpyHostToDevice)) != hipSuccess)
+        return fail(e);
+    nxg_zstd_set_content(hd, d->content);
+    if ((e = hipMalloc(&d->ddev, host.size())) != hipSuccess) return fail(e);
+    if ((e = hipMemcpy(d->ddev, host.data(), host.size(), hipMemcpyHostToDevice)) != hipSuccess)
+        return fail(e);
+    return d;
+}
+
+void nxg_zstd_dict_free(NxgZstdDict* d) {
+    if (!d) return;
+    (void)hipSetDevice(d->device);
+    if (d->ddev) (void)hipFree(d->ddev);
+    if (d->content) (void)hipFree(d->content);
+    delete d;
+}
+
+bool nxg_archive_decompress(NxgCtx* c, const NxgZstdDict* dict, const uint8_t* src,
+                            uint64_t src_len, NxgArchiveRecord* recs, uint32_t n, bool indexed,
+                            uint8_t* dout, uint64_t cap, uint64_t* need, NetidxError* err) {
+    if (!c || (n && (!recs || !src))) {
+        set_err(err, "null argument");
+        return false;
+    }
+    if (!c->pending.empty()) {
+        set_err(err, "an async operation is pending on this ctx; call nxg_ctx_sync first");
+        return false;
+    }
+    if (is_device_ptr(src)) {
+        set_err(err, "the records must be in host memory (the archive's mmap)");
+        return false;
+    }
+    // the records' headers on the host (reader.rs:453-466): the uncompressed length sizes each
+    // output slot, the index is skipped
+    struct Rec {
+        uint64_t frame_off, frame_len, out_off, out_cap;
+    };
+    std::vector<Rec> rd(n);
+    uint64_t total = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        NxgArchiveRecord& r = recs[i];
+        r.out_len = 0;
+        r.err = 0;
+        r.out_off = total;
+        Rec& x = rd[i];
+        x = Rec{0, 0, total, 0};
+        if (r.off > src_len || r.len > src_len - r.off || r.len < 4) {
+            r.err = 7;
+            continue;
+        }
+        const uint8_t* p = src + r.off;
+        const uint64_t uncomp = ((uint64_t)p[0] << 24) | ((uint64_t)p[1] << 16) |
+                                ((uint64_t)p[2] << 8) | p[3];
+        uint64_t pos = 4;
+        if (indexed) {  // decode_varint (pack.rs:504-520): the index's length, prefix included
+            uint64_t v = 0;
+            uint32_t k = 0;
+            bool ok = false;
+            for (; k < 10 && pos + k < r.len; k++) {
+                v |= (uint64_t)(p[pos + k] & 0x7f) << (7 * k);
+                if (p[pos + k] < 0x80) {
+                    ok = true;
+                    break;
+                }
+            }
+            if (!ok || v > r.len - pos) {
+                r.err = 7;
+                continue;
+            }
+            pos += v;
+        }
+        x.frame_off = r.off + pos;
+        x.frame_len = r.len - pos;
+        x.out_cap = uncomp;
+        total += uncomp;
+    }
+    if (need) *need = total;
+    if (!dout) return true;
+    if (total > cap) {
+        set_err(err, "output buffer too small: the records need %llu bytes, capacity %llu",
+                (unsigned long long)total, (unsigned long long)cap);
+        return false;
+    }
+    if (n == 0) return true;
+    if (!set_device(c, err)) return false;
+    if (!c->zdefs) {
+        std::vector<uint8_t> h(nxg_zstd_defaults_bytes());
+        if (!nxg_zstd_build_defaults(reinterpret_cast<NxzDefaults*>(h.data()))) {
+            set_err(err, "predefined zstd tables");
+            return false;
+        }
+        HIPCHK(hipMalloc(&c->zdefs, h.size()));
+        HIPCHK(hipMemcpy(c->zdefs, h.data(), h.size(), hipMemcpyHostToDevice));
+        c->zgrid = nxg_zstd_grid(c->ncu);
+        HIPCHK(hipMalloc(&c->zlit, (size_t)c->zgrid * nxg_zstd_litbuf_bytes()));
+    }
+    const size_t rb = nxg_zstd_rec_bytes(), sb = nxg_zstd_res_bytes();
+    static_assert(sizeof(Rec) == 32, "NxzRec layout");
+    if (c->zrecs_cap < (size_t)n * (rb + sb)) {
+        HIPCHK(hipStreamSynchronize(c->stream));
+        if (c->zrecs) HIPCHK(hipFree(c->zrecs));
+        c->zrecs = nullptr;
+        c->zrecs_cap = std::max<size_t>((size_t)n * (rb + sb), 1 << 16);
+        HIPCHK(hipMalloc(&c->zrecs, c->zrecs_cap));
+    }
+    uint8_t* drecs = static_cast<uint8_t*>(c->zrecs);
+    uint8_t* dres = drecs + (size_t)n * rb;
+    const uint8_t* dsrc;
+    if (!frame_to_device(c, src, src_len, &dsrc, err)) return false;
+    HIPCHK(hipMemcpyAsync(drecs, rd.data(), (size_t)n * rb, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemsetAsync(dres, 0, (size_t)n * sb, c->stream));
+    HIPCHK(nxg_launch_zstd(dsrc, drecs, n, dict ? dict->ddev : nullptr, c->zdefs, dout, c->zlit,
+                           dres, c->zgrid, c->stream));
+    struct Res {
+        uint64_t out_len;
+        uint32_t err, pad;
+    };
+    std::vector<Res> hr(n);
+    HIPCHK(hipMemcpyAsync(hr.data(), dres, (size_t)n * sb, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    for (uint32_t i = 0; i < n; i++) {
+        if (recs[i].err) continue;  // rejected on the host
+        recs[i].out_len = hr[i].out_len;
+        recs[i].err = hr[i].err;
+        if (recs[i].err) recs[i].out_len = 0;
+    }
     return true;
 }
 

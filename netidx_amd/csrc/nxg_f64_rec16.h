@@ -91,15 +91,37 @@ NXG_DEV uint32_t cand16(uint32_t d0, uint32_t d1, uint32_t d2, uint32_t d3, uint
 }
 
 // 16 bytes at LDS byte offset rel (any alignment)
-NXG_DEV void lds16(const uint8_t* buf, uint32_t rel, uint32_t& e0, uint32_t& e1, uint32_t& e2,
+// LDS images of the wire. LinImg: bytes in order. SwzImg: dword i of the image kept at dword
+// i ^ ((i >> 4) & 15), so that 64 lanes reading at 64-byte strides (one chunk each) hit 32
+// different banks in pairs instead of two banks 16 deep (ds_read_b32 banks: (a / 4) mod 32,
+// MI355X_MICROARCH.md LDS); reads are dword-wise, so any byte offset still works.
+struct LinImg {
+    const uint8_t* b;
+    NXG_DEV uint32_t w(uint32_t i) const { return reinterpret_cast<const uint32_t*>(b)[i]; }
+    NXG_DEV uint32_t byte(uint32_t p) const { return b[p]; }
+};
+struct SwzImg {
+    const uint8_t* b;
+    static NXG_DEV uint32_t sw(uint32_t i) { return i ^ ((i >> 4) & 15u); }
+    NXG_DEV uint32_t w(uint32_t i) const { return reinterpret_cast<const uint32_t*>(b)[sw(i)]; }
+    NXG_DEV uint32_t byte(uint32_t p) const { return b[(sw(p >> 2) << 2) | (p & 3u)]; }
+};
+
+// 16 bytes at image byte offset rel (any alignment)
+template <typename Img>
+NXG_DEV void lds16i(const Img& im, uint32_t rel, uint32_t& e0, uint32_t& e1, uint32_t& e2,
                    uint32_t& e3) {
-    const uint32_t* w = reinterpret_cast<const uint32_t*>(buf + (rel & ~3u));
-    const uint32_t s = rel & 3u;
-    const uint32_t d0 = w[0], d1 = w[1], d2 = w[2], d3 = w[3], d4 = w[4];
+    const uint32_t q = rel >> 2, s = rel & 3u;
+    const uint32_t d0 = im.w(q), d1 = im.w(q + 1), d2 = im.w(q + 2), d3 = im.w(q + 3),
+                   d4 = im.w(q + 4);
     e0 = alignbyte(d1, d0, s);
     e1 = alignbyte(d2, d1, s);
     e2 = alignbyte(d3, d2, s);
     e3 = alignbyte(d4, d3, s);
+}
+NXG_DEV void lds16(const uint8_t* buf, uint32_t rel, uint32_t& e0, uint32_t& e1, uint32_t& e2,
+                   uint32_t& e3) {
+    lds16i(LinImg{buf}, rel, e0, e1, e2, e3);
 }
 
 constexpr uint32_t FAILX = 0xffffffffu;
@@ -108,39 +130,44 @@ constexpr int WIN = 64;  // merge walks must coincide within 64 bytes of the chu
 // Merge point of all record walks starting in [r, r+16) of the LDS image (r 4-aligned), as a
 // position relative to the image; the END position (W - a0) for a chunk at or past the frame's
 // end; FAILX if the walks do not merge.
-NXG_DEV uint32_t merge16(const uint8_t* buf, uint32_t r, uint64_t a0, uint64_t W) {
+template <typename Img>
+NXG_DEV uint32_t merge16i(const Img& buf, uint32_t r, uint64_t a0, uint64_t W) {
     // positions are signed: an exact tile at the start of a byte range images 64 bytes before it
     const int64_t abs_r = (int64_t)a0 + (int64_t)r;
     if (abs_r >= (int64_t)W) return (uint32_t)((int64_t)W - (int64_t)a0);
     const uint64_t remr = (uint64_t)((int64_t)W - abs_r);
-    const uint32_t* w = reinterpret_cast<const uint32_t*>(buf + r);
-    uint32_t cand = cand16(w[0], w[1], w[2], w[3], w[4]);
+    const uint32_t q = r >> 2;
+    uint32_t cand = cand16(buf.w(q), buf.w(q + 1), buf.w(q + 2), buf.w(q + 3), buf.w(q + 4));
     uint64_t S = 0;
     if (remr < 16) S |= 1ull << remr;  // the frame end is a valid (terminal) position
     while (cand) {
         const uint32_t p = __builtin_ctz(cand);
         cand &= cand - 1;
         uint32_t e0, e1, e2, e3;
-        lds16(buf, r + p, e0, e1, e2, e3);
+        lds16i(buf, r + p, e0, e1, e2, e3);
         if (rec_check16(e0, e1, remr - p)) S |= 1ull << p;
     }
     for (int it = 0; it < WIN && __popcll(S) > 1; it++) {
         const uint32_t p = __builtin_ctzll(S);
         S &= S - 1;
         uint32_t e0, e1, e2, e3;
-        lds16(buf, r + p, e0, e1, e2, e3);
+        lds16i(buf, r + p, e0, e1, e2, e3);
         const uint32_t L = rec_check16(e0, e1, remr - p);
         const uint32_t np = p + L;
         if (np >= (uint32_t)WIN) return FAILX;
         bool ok = (np == remr);
         if (!ok) {
-            lds16(buf, r + np, e0, e1, e2, e3);
+            lds16i(buf, r + np, e0, e1, e2, e3);
             ok = rec_check16(e0, e1, remr - np) != 0;
         }
         if (ok) S |= 1ull << np;
     }
     if (__popcll(S) != 1) return FAILX;
     return r + (uint32_t)__builtin_ctzll(S);
+}
+
+NXG_DEV uint32_t merge16(const uint8_t* buf, uint32_t r, uint64_t a0, uint64_t W) {
+    return merge16i(LinImg{buf}, r, a0, W);
 }
 
 // the bytes of the 16 at `pos` (signed, relative to wire) that lie in [-pre, W), zero-filled

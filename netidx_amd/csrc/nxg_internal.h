@@ -196,6 +196,22 @@ struct NxgArchResult {
 uint64_t nxg_arch_scratch_bytes(uint64_t W);
 hipError_t nxg_arch_decode(const uint8_t* buf, uint64_t W, const ColsDesc& cols, uint8_t* scratch,
                            uint32_t* cap_flag, int max_rounds, NxgArchResult* res, hipStream_t s);
+// zstd decompression of compressed archive records (nxg_zstd.hip): host-side table builders and
+// the launch; the device structures are opaque here (their sizes from the *_bytes functions)
+struct NxzDictDev;
+struct NxzDefaults;
+bool nxg_zstd_build_dict(const uint8_t* d, uint64_t n, NxzDictDev* out, uint64_t* content_off);
+bool nxg_zstd_build_defaults(NxzDefaults* o);
+void nxg_zstd_set_content(NxzDictDev* d, const uint8_t* dcontent);
+uint64_t nxg_zstd_dict_dev_bytes();
+uint64_t nxg_zstd_defaults_bytes();
+uint64_t nxg_zstd_rec_bytes();
+uint64_t nxg_zstd_res_bytes();
+uint64_t nxg_zstd_litbuf_bytes();
+int nxg_zstd_grid(int ncu);
+hipError_t nxg_launch_zstd(const uint8_t* dsrc, const void* drecs, uint32_t n, const void* ddict,
+                           const void* ddefs, uint8_t* dout, uint8_t* dlit, void* dres, int grid,
+                           hipStream_t s);
 int nxg_occupancy_enc_f64();
 int nxg_occupancy_enc_general();
 

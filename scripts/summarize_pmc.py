@@ -14,7 +14,7 @@ for d in ("fetch", "write", "sq1", "sq2"):
     acc = collections.defaultdict(lambda: collections.defaultdict(float))
     disp = collections.defaultdict(set)
     for r in csv.DictReader(open(f[0])):
-        k = r["Kernel_Name"].split("(")[0]
+        k = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0]
         if "nxg" not in k:
             continue
         acc[k][r["Counter_Name"]] += float(r["Counter_Value"])
@@ -25,7 +25,7 @@ for d in ("fetch", "write", "sq1", "sq2"):
 st = glob.glob(f"{out}/trace/**/*kernel_stats.csv", recursive=True)
 if st:
     for r in csv.DictReader(open(st[0])):
-        k = r["Name"].split("(")[0]
+        k = r["Name"].replace("(anonymous namespace)::", "").split("(")[0]
         if k in res or "nxg" in k:
             res.setdefault(k, {})["avg_ns"] = float(r["AverageNs"])
             res[k]["calls"] = int(r["Calls"])
