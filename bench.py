@@ -3,7 +3,9 @@
 
 A "step" decodes one batch: a frame payload of From::Update(Id, F64) messages (configs[1],
 10^7 records, 147,886,336 wire bytes), from HBM-resident wire bytes into HBM-resident id/f64
-columns, through the C ABI (nxg_decode_updates_async). With --gpus N each rank decodes its own
+columns, through the C ABI. The K timed frames are a connection's backlog decoded as one stream
+(nxg_decode_frames_async: the record-length probe of frame j+1 runs in the launch that emits
+frame j); the per-call rate (one nxg_decode_updates_async per frame) is reported beside it. With --gpus N each rank decodes its own
 10^7-record shard; the ids are disjoint and there is no data-path collective ("weak" scaling).
 `value` is the whole-job aggregate in M updates/s, over all ranks.
 
@@ -32,10 +34,13 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-# the f64 decode is two launches (nxg_decode_f64_run.hip): the probe (per-tile record counts and
-# prefixes, reads ~1 line per 32 KiB tile) and the emit (reads W, writes 16 N: the dominant one)
-KERNEL_DEC_F64 = "nxg_f64r_emit_kernel"
-KERNELS_DEC_F64 = ["nxg_f64r_probe_kernel", "nxg_f64r_emit_kernel"]
+# the f64 decode (nxg_decode_f64_run.hip) of a stream of frames (nxg_decode_frames_async): one
+# launch per frame, nxg_f64r_fused_kernel = the emit of frame j (reads W, writes 16 N) + the
+# record-length probe of frame j + 1 (reads ~1 line per 32 KiB tile); the first frame's probe and
+# the last frame's emit are launched alone. One call per frame (nxg_decode_updates_async) runs
+# probe + emit as two launches.
+KERNEL_DEC_F64 = "nxg_f64r_fused_kernel"
+KERNELS_DEC_F64 = ["nxg_f64r_probe_kernel", "nxg_f64r_fused_kernel", "nxg_f64r_emit_kernel"]
 
 
 def log(*a):
@@ -136,13 +141,13 @@ def _nxo():
     return nxo
 
 
-def oracle_check_decode(wire, cols, n, n_children=0):
+def oracle_check_decode(wire, cols, n, n_children=0, n_ctl=0):
     """Checker: the product's decoded columns (device) == the oracle's decode of the same wire
     bytes, every row and column. Returns the number of rows checked."""
     import numpy as np
     nxo = _nxo()
     w = wire.cpu().numpy() if hasattr(wire, "cpu") else wire
-    o = nxo.decode(w, cap_rows=n + 1, cap_children=n_children + 1, cap_ctl=1).trim()
+    o = nxo.decode(w, cap_rows=n + 1, cap_children=n_children + 1, cap_ctl=n_ctl + 1).trim()
     assert o["err_kind"] == 0 and len(o["id"]) == n, "oracle rejected the frame"
     g = cols.numpy()
     keys = ["id", "fixed"] if "aux" not in g else ["id", "tag", "fixed", "aux", "ctag", "cfixed",
@@ -264,7 +269,7 @@ def read_traffic(records):
     p = os.path.join(ROOT, "profiles", "pmc_dec_f64.json")
     try:
         j = json.load(open(p))
-        if j.get("records") == records and j.get("kernel") == "+".join(KERNELS_DEC_F64):
+        if j.get("records") == records and j.get("kernel") == KERNEL_DEC_F64:
             return j.get("hbm_bytes_per_launch")
     except Exception:
         pass
@@ -283,18 +288,51 @@ def extras_single_gpu(codec, stream, steps, warmup):
         n = 100_000_000
         cols, wire = make_f64_wire(codec, n, 0)
         out = Columns(n, 0, 0, netidx_amd.LAYOUT_F64, "cuda")
-        wall, kms, st = time_decode(codec, wire, out, n, max(3, steps // 4), 2, 1, stream)
+        k = max(6, steps // 4)
+        wall, kms, st = time_decode(codec, wire, out, n, k, 2, 1, stream, stream_of_frames=True)
         assert st.path == 1 and st.n_rows == n
+        _, kms1, st1 = time_decode(codec, wire, out, n, k, 1, 1, stream)
+        assert st1.path == 1 and st1.n_rows == n
         b = wire.numel() + 16 * n
         ex["decode_f64_1e8"] = {"records": n, "wire_bytes": wire.numel(),
                                 "M_updates_s": round(n / (kms / 1e3) / 1e6, 1),
                                 "kernel_ms": round(kms, 4),
                                 "hbm_frac": round(b / (kms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                                "timed": f"{k} frames as one stream (nxg_decode_frames_async), "
+                                         "HIP events on the codec stream",
+                                "per_call_kernel_ms": round(kms1, 4),
+                                "per_call_hbm_frac": round(b / (kms1 / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
                                 "oracle_rows_checked": oracle_check_decode(wire, out, n)}
         del cols, wire, out
         torch.cuda.empty_cache()
     except Exception as e:  # report, never hide
         ex["decode_f64_1e8"] = {"error": repr(e)}
+    # (a2) the same f64 batches with ids in random order (a batch updating an arbitrary subset of a
+    # publisher's values, publisher/mod.rs:776-845): record lengths vary record to record, so the
+    # length-run decoder hands the frames to the single-pass decoder (nxg_decode_f64_x.hip)
+    for n in (10_000_000, 100_000_000):
+        key = f"decode_f64_random_ids_{'1e7' if n == 10**7 else '1e8'}"
+        try:
+            ids, vals = synth.f64_columns(n, synth.SEED_F64)
+            ids = np.random.default_rng(0x5EED0003).permutation(n).astype(np.uint64)
+            cols = netidx_amd.columns_from_arrays(ids, vals)
+            wire = codec.encode_batch(cols)
+            out = Columns(n, 0, 0, netidx_amd.LAYOUT_F64, "cuda")
+            k = max(6, steps // 4)
+            wall, kms, st = time_decode(codec, wire, out, n, k, 2, 1, stream)
+            assert st.path == 1 and st.n_rows == n
+            b = wire.numel() + 16 * n
+            ex[key] = {"records": n, "wire_bytes": wire.numel(),
+                       "M_updates_s": round(n / (kms / 1e3) / 1e6, 1),
+                       "kernel_ms": round(kms, 4),
+                       "hbm_frac": round(b / (kms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                       "kernel": "nxg_f64x_kernel (after the first frame: the length-run probe "
+                                 "declines it, the next frames go straight to it)",
+                       "oracle_rows_checked": oracle_check_decode(wire, out, n)}
+            del cols, wire, out
+            torch.cuda.empty_cache()
+        except Exception as e:
+            ex[key] = {"error": repr(e)}
     # (b) config 3: mixed-tag decode (general kernel)
     try:
         n = 10_000_000
@@ -347,6 +385,32 @@ def extras_single_gpu(codec, stream, steps, warmup):
         torch.cuda.empty_cache()
     except Exception as e:
         ex["decode_mixed_1e7"] = {"error": repr(e)}
+    # (b0) config 3 as a live subscriber sees it: 1 % Heartbeats between the rows and 1 % of
+    # the rows 200-byte strings (two-byte length prefixes), still on the fast mixed decoder
+    try:
+        n = 10_000_000
+        m, cr, co, cl, cv = synth.mixed_columns_ctl(n)
+        mc = netidx_amd.columns_from_arrays(m.id, m.fixed, m.tag, m.aux, m.ctag, m.cfixed, m.caux,
+                                            cr, co, cl, cv)
+        heap = torch.from_numpy(m.heap.copy()).cuda()
+        wire = codec.encode_batch(mc, heap)
+        out = Columns(n + 1, len(m.ctag) + 1, len(cr) + 1, netidx_amd.LAYOUT_MIXED, "cuda")
+        wall, kms, st = time_decode(codec, wire, out, n, max(3, steps // 4), 1, 1, stream,
+                                    flags=netidx_amd.HINT_MIXED)
+        assert st.path == 4 and st.n_rows == n and st.err_kind == 0, st
+        assert st.n_heartbeat == len(cr)
+        checked = oracle_check_decode(wire, out, n, len(m.ctag), len(cr))
+        b = wire.numel() + n * (8 + 1 + 8 + 4) + 13 * len(m.ctag) + 21 * len(cr)
+        ex["decode_mixed_ctl_1e7"] = {
+            "records": n, "wire_bytes": wire.numel(), "n_heartbeat": len(cr),
+            "n_long_string": int((m.aux[m.tag == 12] >= 100).sum()), "path": st.path,
+            "M_updates_s": round(n / (kms / 1e3) / 1e6, 1), "kernel_ms": round(kms, 4),
+            "hbm_frac": round(b / (kms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+            "oracle_rows_checked": checked, "oracle_columns_checked": "all (ctl included)"}
+        del mc, heap, wire, out
+        torch.cuda.empty_cache()
+    except Exception as e:
+        ex["decode_mixed_ctl_1e7"] = {"error": repr(e)}
     # (b1) archive batches (Vec<BatchItem>): 10^7 items of the config-3 value
     # mix with 5 % Event::Unsubscribed; the product encoder writes the batch, the product decoder
     # reads it back; both checked once against the oracle. Wall clock per synchronous call.
@@ -376,6 +440,8 @@ def extras_single_gpu(codec, stream, steps, warmup):
         checked = oracle_check_archive(buf, out, m)
         b = buf.numel() + n * (8 + 1 + 8 + 4) + 13 * len(m.ctag)
         ex["archive_1e7"] = {"items": n, "batch_bytes": buf.numel(),
+                             "decode_path": {5: "fast (nxg_fa_*)", 3: "exact (nxg_arch_*)"}.get(
+                                 st.path, st.path),
                              "decode_ms": round(t_dec * 1e3, 3),
                              "decode_M_items_s": round(n / t_dec / 1e6, 1),
                              "decode_hbm_frac": round(b / t_dec / 1e9 / HBM_PEAK_GBS, 4),
@@ -386,6 +452,52 @@ def extras_single_gpu(codec, stream, steps, warmup):
         torch.cuda.empty_cache()
     except Exception as e:
         ex["archive_1e7"] = {"error": repr(e)}
+    # (b1z) compressed archive records (reader.rs:453-477): the committed libzstd fixtures'
+    # dictionary records (level 19, the archive's trained dictionary; tests/golden/make_zstd.py),
+    # repeated to ~100 MB of batches, decompressed on the GPU in one call (host records in, H2D
+    # included, wall clock) and every output byte checked against the fixtures' plain bytes
+    try:
+        import json as _json
+        gold = os.path.join(ROOT, "tests", "golden")
+        man = _json.load(open(os.path.join(gold, "zstd_manifest.json")))
+        rec = np.fromfile(os.path.join(gold, "zstd_records.bin"), np.uint8)
+        plain = np.fromfile(os.path.join(gold, "zstd_plain.bin"), np.uint8)
+        zdict = codec.zstd_dict(open(os.path.join(gold, "zstd_dict.bin"), "rb").read())
+        es = [e for e in man["records"] if e["dict"] and not e["indexed"] and e["plain_len"]]
+        per = sum(e["plain_len"] for e in es)
+        R = max(1, (100 << 20) // per)
+        parts, recs, want = [], [], []
+        off = 0
+        for _ in range(R):
+            for e in es:
+                parts.append(rec[e["rec_off"]:e["rec_off"] + e["rec_len"]])
+                recs.append((off, e["rec_len"]))
+                want.append(plain[e["plain_off"]:e["plain_off"] + e["plain_len"]])
+                off += e["rec_len"]
+        src = np.concatenate(parts)
+        out, res = codec.archive_decompress(src, recs, False, zdict)
+        k = max(3, steps // 40)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(k):
+            out, res = codec.archive_decompress(src, recs, False, zdict, out=out)
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / k
+        host = out.cpu().numpy()
+        assert all(r[2] == 0 for r in res), "a record failed to decompress"
+        assert all(np.array_equal(host[r[0]:r[0] + r[1]], w) for r, w in zip(res, want)), \
+            "decompressed bytes differ from the fixtures"
+        tot = sum(r[1] for r in res)
+        ex["archive_zstd_decompress"] = {
+            "records": len(recs), "compressed_bytes": int(len(src)), "plain_bytes": int(tot),
+            "ms": round(dt * 1e3, 3), "plain_GB_s": round(tot / dt / 1e9, 2),
+            "note": "wall clock of nxg_archive_decompress from host records (H2D included); "
+                    "libzstd fixtures (dictionary, level 19) repeated; every byte checked"}
+        zdict.close()
+        del out
+        torch.cuda.empty_cache()
+    except Exception as e:
+        ex["archive_zstd_decompress"] = {"error": repr(e)}
     # (b2) the socket-buffer path: host (pinned) frame -> device decode -> host (pinned) columns,
     # through the same synchronous call (nxg_decode_updates stages H2D and D2H itself); wall
     # clock, so PCIe Gen5 transfers are included. Never the bench `value`.
@@ -772,7 +884,22 @@ def extras_multi_gpu(codec, world, rank, stream):
     wall, kms, st = time_decode(codec, wire, out, nm, 5, 1, world, stream,
                                 flags=netidx_amd.HINT_MIXED)
     assert st.path == 4 and st.n_rows == nm and st.err_kind == 0, st
-    assert torch.equal(out.id[:nm], mc.id[:nm]) and torch.equal(out.tag[:nm], mc.tag[:nm])
+    # every column equals the encode input it was made from (the encoder is the oracle's, checked
+    # byte for byte on rank 0 in the N=1 extras)
+    nc = len(m.ctag)
+    for k in ("id", "tag", "aux"):
+        assert torch.equal(out.t[k][:nm], mc.t[k][:nm]), f"mixed decode differs in column {k}"
+    for k in ("ctag", "cfixed", "caux"):
+        assert torch.equal(out.t[k][:nc], mc.t[k][:nc]), f"mixed decode differs in column {k}"
+    # fixed: the value for scalars; for text the frame offset of the bytes (the input's is a heap
+    # offset), so the text itself is compared
+    txt = out.tag[:nm] == 12
+    assert torch.equal(out.fixed[:nm][~txt], mc.fixed[:nm][~txt]), "mixed decode differs in fixed"
+    lens = out.aux[:nm][txt].long()
+    rep = torch.repeat_interleave(torch.arange(len(lens), device=lens.device), lens)
+    pos = torch.arange(int(lens.sum()), device=lens.device) - (torch.cumsum(lens, 0) - lens)[rep]
+    assert torch.equal(wire[out.fixed[:nm][txt][rep] + pos], heap[mc.fixed[:nm][txt][rep] + pos]), \
+        "mixed decode differs in text bytes"
     kmax = max_over_ranks(kms, world)
     ex["decode_mixed_1e7_per_gpu"] = {
         "records_per_gpu": nm, "world": world, "kernel_ms_slowest_rank": round(kmax, 4),
@@ -805,8 +932,12 @@ def main():
     cols, wire = make_f64_wire(codec, n, rank)
     nbytes = wire.numel()
     out = Columns(n, 0, 0, netidx_amd.LAYOUT_F64, "cuda")
-    wall, kms, st = time_decode(codec, wire, out, n, args.steps, args.warmup, world, stream)
+    wall, kms, st = time_decode(codec, wire, out, n, args.steps, args.warmup, world, stream,
+                                stream_of_frames=True)
     assert st.err_kind == 0 and st.path == 1 and st.n_rows == n, st
+    # the same frames one call each (probe and emit as two launches per frame), for comparison
+    wall1, kms1, st1 = time_decode(codec, wire, out, n, max(20, args.steps // 4), 2, world, stream)
+    assert st1.err_kind == 0 and st1.path == 1 and st1.n_rows == n, st1
     # checker, outside the timed region: every row against the oracle's decode of the same bytes
     checked = oracle_check_decode(wire, out, n) if rank == 0 else 0
 
@@ -836,10 +967,18 @@ def main():
         "gib_per_s": round(world * alg_bytes * args.steps / wall / 2**30, 2),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": read_traffic(n), "kernel": KERNEL_DEC_F64,
+                     "traffic": read_traffic(n),
+                     "traffic_source": "profiles/pmc_dec_f64.json (rocprofv3 FETCH_SIZE x2 + "
+                                       "WRITE_SIZE per decode, committed; not measured in this run)",
+                     "kernel": KERNEL_DEC_F64 + " (emit of frame j + probe of frame j+1)",
                      "kernel_ms": round(kms, 4), "algorithmic_bytes_per_launch": alg_bytes,
-                     "timed": "HIP events around each whole decode: probe + emit launches "
-                              "(" + " + ".join(KERNELS_DEC_F64) + ")"},
+                     "timed": "HIP events on the codec stream around the whole stream of frames "
+                              "(nxg_decode_frames_async: " + " / ".join(KERNELS_DEC_F64) +
+                              "), divided by the frames"},
+        "per_call": {"kernel_ms": round(kms1, 4),
+                     "frac": round(alg_bytes / (kms1 / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                     "timed": "one nxg_decode_updates_async per frame: nxg_f64r_probe_kernel + "
+                              "nxg_f64r_emit_kernel"},
     }
     if rank == 0 and world == 1:
         host = wire.cpu().numpy()

@@ -78,8 +78,9 @@ enum NxgErrKind {
     NXG_CAPACITY = 7, /* output columns too small */
     NXG_NOT_F64 = 8,  /* valid batch, but F64-only columns were supplied for mixed content */
     NXG_TIMEOUT = 9,  /* device-side progress watchdog fired (should never happen) */
-    NXG_UNSUPPORTED = 10, /* publish: UpdateChanged compares a Decimal/Array/Map/Error(Value)/
-                             Abstract value, whose equality the columns do not carry */
+    NXG_UNSUPPORTED = 10, /* publish: an UpdateChanged comparison of values nested deeper than
+                             NXG_MAX_DEPTH levels (every Value variant's equality is implemented,
+                             netidx-value/src/op.rs:133-172) */
 };
 
 #define NXG_MAX_DEPTH 32
@@ -352,18 +353,23 @@ bool nxg_publish_unsubscribes(NxgCtx* ctx, const uint64_t* id, const uint32_t* c
  * (netidx-archive/src/logfile/reader.rs:449/475 over logfile/mod.rs:150-205 BatchItem and
  * netidx/src/subscriber/mod.rs:154-177 Event). `buf` (device memory, `len` bytes) starts with the
  * batch: varint count, then count items of varint Id (as u32) and an Event that is not
- * length-wrapped (0x40 = Unsubscribed, else a bare Value). Bytes after the batch are not read
- * (the uncompressed reader decodes from the record to the end of the mmap).
+ * length-wrapped (0x40 = Unsubscribed, else a bare Value). `len` is what remains of the buffer
+ * (the uncompressed reader decodes from the record to the end of the mmap, reader.rs:449): it
+ * bounds the size guard, while the fast path reads only a window of it that grows geometrically
+ * until the batch fits, so the cost follows the batch. A batch the fast path declines (an error,
+ * Maps, nesting, ...) is decoded by the exact decoder, which walks the whole buffer.
  * Output: MIXED-layout columns (nxg_columns_alloc), one row per item: id = the u32 Id, the
  * Event's Value in tag/fixed/aux (+ children; text offsets index `buf`), Unsubscribed as tag
  * NXG_TAG_UNSUBSCRIBED with fixed 0, aux 0. status: n_rows (= count), n_children, err_kind /
  * err_offset (the failing item's start, 0 for the count and the size guard) with the reference's
- * PackError kinds; path = NXG_PATH_ARCHIVE. *consumed = the batch's length in bytes.
+ * PackError kinds; path = NXG_PATH_ARCHIVE_FAST (the fast path) or NXG_PATH_ARCHIVE (the exact
+ * decoder). *consumed = the batch's length in bytes.
  * Deviation: Event::decode on an empty buffer panics in the reference; here it is
  * NXG_BUFFER_SHORT. Synchronous; false on misuse or a HIP failure. A decode error is reported in
  * `status` (as nxg_decode_updates does), with n_rows = n_children = 0. */
 #define NXG_TAG_UNSUBSCRIBED 0x40
 #define NXG_PATH_ARCHIVE 3
+#define NXG_PATH_ARCHIVE_FAST 5
 bool nxg_decode_archive_batch(NxgCtx* ctx, const uint8_t* buf, uint64_t len, NxgColumns* out,
                               NxgStatus* status, uint64_t* consumed, NetidxError* err);
 /* Replaces <GPooled<Vec<BatchItem>> as Pack>::encode (writer.rs:423-428, pack.rs:941-952):

@@ -62,6 +62,7 @@ struct NxgCtx {
     uint32_t* glws = nullptr;      // general decode: lane words, 256 B per tile
     size_t glws_cap = 0;
     uint64_t* gruns = nullptr;     // general decode: run summaries + bases
+    bool no_fa = false;            // NXG_ARCH_PATH=exact: archive batches on the exact decoder only
     uint8_t* dscratch = nullptr;   // dispatch: counters, offsets, block sums, unmatched count
     size_t dscratch_cap = 0;
     int wgs_dec_gen = 0;
@@ -382,7 +383,8 @@ bool finish_decode(NxgCtx* c, const uint8_t* f, uint64_t len, NxgColumns* out, i
         HIPCHK(hipStreamSynchronize(c->stream));
     }
     DevStatus h = c->hst[slot];
-    if (tried_fast == FAST_RUN && len > 0 && h.fast_fail && h.irregular) {
+    // (irregular bit 1: not an f64 frame at all -- straight on to the mixed decoders)
+    if (tried_fast == FAST_RUN && len > 0 && h.fast_fail && (h.irregular & 3u) == 1u) {
         // record lengths vary record to record: the single-pass decoder of any f64 frame, for
         // this frame and the next kIrregularCalls ones
         c->irregular_left = kIrregularCalls;
@@ -615,7 +617,8 @@ NxgCtx* nxg_ctx_new(int device, NetidxError* err) {
         return fail("hipMalloc(status)", e);
     if ((e = hipMemset(c->dst, 0, sizeof(DevStatus) * kStatusRing)) != hipSuccess)
         return fail("hipMemset(status)", e);
-    if ((e = hipHostMalloc(&c->hst, sizeof(DevStatus) * kStatusRing, hipHostMallocDefault)) !=
+    // (one slot more: the fast archive decoder's FaHead)
+    if ((e = hipHostMalloc(&c->hst, sizeof(DevStatus) * (kStatusRing + 1), hipHostMallocDefault)) !=
         hipSuccess)
         return fail("hipHostMalloc(status)", e);
     // general decode: run summaries + bases (no initialisation needed)
@@ -627,6 +630,8 @@ NxgCtx* nxg_ctx_new(int device, NetidxError* err) {
     c->force_x = fp && strcmp(fp, "x") == 0;
     const char* mp = getenv("NXG_MIXED_PATH");
     c->no_fmx = mp && strcmp(mp, "general") == 0;
+    const char* ap = getenv("NXG_ARCH_PATH");
+    c->no_fa = ap && strcmp(ap, "exact") == 0;
     const char* ff = getenv("NXG_F64R_FLAGS");
     c->f64r_flags = ff ? (uint32_t)strtoul(ff, nullptr, 0) : 0u;
     return c;
@@ -1193,6 +1198,43 @@ bool nxg_archive_decompress(NxgCtx* c, const NxgZstdDict* dict, const uint8_t* s
     return true;
 }
 
+// the fast archive decoder's device results (nxg_archive_fast.hip FaHead)
+struct FaHeadHost {
+    uint32_t fast_fail, arrived;
+    uint64_t end, end_children, items, kids, recounts, pad[2];
+};
+static_assert(sizeof(FaHeadHost) == 64 && sizeof(FaHeadHost) <= sizeof(DevStatus), "FaHead");
+
+// The batch header on the host: the count varint (decode_varint, pack.rs:504-520: at most 10
+// bytes, bits past 64 dropped) and its length; false when it is not a complete varint (the exact
+// decoder reports that) or check_sz! would refuse it (pack.rs:919-925)
+static bool arch_header(NxgCtx* c, const uint8_t* buf, uint64_t len, uint64_t* count, uint32_t* p0,
+                        NetidxError* err) {
+    uint8_t h[10] = {0};
+    const uint64_t n = std::min<uint64_t>(len, 10);
+    if (n == 0) return false;
+    if (is_device_ptr(buf)) {
+        if (hipMemcpyAsync(h, buf, n, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+            hipStreamSynchronize(c->stream) != hipSuccess)
+            return false;
+    } else {
+        memcpy(h, buf, n);
+    }
+    (void)err;
+    uint64_t v = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        const uint64_t b = h[i];
+        v |= i < 9 ? (b & 0x7f) << (7 * i) : (b & 1) << 63;
+        if (b < 0x80) {
+            *count = v;
+            *p0 = i + 1;
+            const uint64_t sz = v > ~0ull / 24 ? ~0ull : v * 24;  // size_of::<BatchItem>()
+            return sz <= kMaxVecBytes && sz <= ((len - (i + 1)) << 8);
+        }
+    }
+    return false;
+}
+
 bool nxg_decode_archive_batch(NxgCtx* c, const uint8_t* buf, uint64_t len, NxgColumns* out,
                               NxgStatus* ust, uint64_t* consumed, NetidxError* err) {
     if (!c || !out || (!buf && len)) {
@@ -1213,6 +1255,47 @@ bool nxg_decode_archive_batch(NxgCtx* c, const uint8_t* buf, uint64_t len, NxgCo
     }
     if (!set_device(c, err)) return false;
     const uint8_t* df;
+    // the fast path (nxg_archive_fast.hip) over a window of the buffer that grows until the batch
+    // fits; anything it declines goes to the exact decoder below over the whole buffer
+    uint64_t count = 0;
+    uint32_t p0 = 0;
+    if (!c->no_fa && arch_header(c, buf, len, &count, &p0, err) && count >= 1 &&
+        count <= out->cap_rows && count < (1ull << 31) && out->tag && out->ctag) {
+        const uint64_t wmax = std::min<uint64_t>(len, 0xfff00000ull);
+        uint64_t W = std::min<uint64_t>(wmax, p0 + count * 24 + 65536);
+        FaHeadHost* hh = reinterpret_cast<FaHeadHost*>(c->hst + kStatusRing);
+#pragma unroll 1
+        for (;;) {
+            if (!frame_to_device(c, buf, W, &df, err)) return false;
+            const size_t need = nxg_fa_scratch_bytes(W);
+            if (need > c->dscratch_cap) {
+                HIPCHK(hipStreamSynchronize(c->stream));
+                if (c->dscratch) HIPCHK(hipFree(c->dscratch));
+                c->dscratch = nullptr;
+                const size_t sz = std::max(need, c->dscratch_cap * 2);
+                HIPCHK(hipMalloc(&c->dscratch, sz));
+                c->dscratch_cap = sz;
+            }
+            HIPCHK(nxg_launch_dec_fa(df, W, p0, count, desc_of(out), c->dscratch, hh, nullptr,
+                                     c->stream));
+            HIPCHK(hipStreamSynchronize(c->stream));
+            if (!hh->fast_fail && hh->end) {
+                NxgStatus s{};
+                s.n_rows = count;
+                s.n_children = hh->end_children;
+                s.path = NXG_PATH_ARCHIVE_FAST;
+                out->n_rows = count;
+                out->n_children = hh->end_children;
+                out->n_ctl = 0;
+                out->layout = NXG_LAYOUT_MIXED;
+                if (ust) *ust = s;
+                if (consumed) *consumed = hh->end - 1;
+                return true;
+            }
+            if (W >= wmax) break;
+            W = std::min(wmax, 2 * W);
+        }
+    }
     if (!frame_to_device(c, buf, len, &df, err)) return false;
     const size_t need = 64 + nxg_arch_scratch_bytes(len);
     if (need > c->dscratch_cap) {

@@ -351,14 +351,16 @@ __global__ __launch_bounds__(TPB) void nxg_arch_emit_kernel(
     const uint64_t s = chunk_start(h, k);
     const uint64_t lim = s + CH < W ? s + CH : W;
     uint64_t q = entry, row = rbase[k], cn = cbase[k];
+    if (h.count == 0 && k == 0) {  // an empty batch ends after its count
+        hp->end = h.p0 + 1;
+        hp->end_children = 0;
+        return;
+    }
 #pragma unroll 1
     for (;;) {
-        if (row == h.count) {  // the batch ends here
-            hp->end = q + 1;
-            hp->end_children = cn;
-            return;
-        }
-        if (q >= lim || row > h.count) return;
+        // (the batch's end is written only by the lane that decodes item count - 1: a chunk after
+        // it may be walked from a wrong entry in trailing bytes and reach row == count too)
+        if (q >= lim || row >= h.count) return;
         if (row >= cols.cap_rows) {
             atomicMax((unsigned long long*)&hp->err_key, err_key(q, NXG_CAPACITY));
             return;
@@ -377,6 +379,11 @@ __global__ __launch_bounds__(TPB) void nxg_arch_emit_kernel(
         cols.id[row] = (uint32_t)id;
         row++;
         q = r;
+        if (row == h.count) {  // the batch ends here
+            hp->end = q + 1;
+            hp->end_children = cn;
+            return;
+        }
     }
 }
 

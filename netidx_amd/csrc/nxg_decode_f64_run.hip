@@ -272,7 +272,8 @@ NXG_DEV bool run_search(const uint8_t* __restrict__ wire, uint64_t W, uint64_t t
 // 2: no unique entry or forced (exact path). `bad`: the frame cannot be decoded from here.
 NXG_DEV void probe_fast(const uint8_t* __restrict__ wire, uint64_t W, uint64_t t, uint32_t lim,
                         bool first, uint32_t flags, int& state, uint32_t& e, uint32_t& L,
-                        uint32_t& L2, uint32_t& ks, uint32_t& count, uint32_t& x, bool& bad) {
+                        uint32_t& L2, uint32_t& ks, uint32_t& count, uint32_t& x, bool& bad,
+                        bool& nof) {
     const uint64_t t0 = t * T;
     const uint64_t rem0 = W - t0;
     uint32_t d[8];
@@ -297,6 +298,9 @@ NXG_DEV void probe_fast(const uint8_t* __restrict__ wire, uint64_t W, uint64_t t
         L1 = e0 & 0xffu;
     }
     const uint32_t p2 = s1 + L1;
+    // every 16 bytes of an f64 frame hold a record start (records are 12..16 bytes): none here,
+    // or no record at the frame's first byte, and the frame is not an f64 frame at all
+    nof = V == 0u || (t == 0 && first && !(V & 1u));
     if (t == 0 && first && !(V & 1u)) {
         bad = true;
     } else if (s1 < 16 && (s1 == rem0 || s1 >= lim)) {
@@ -404,19 +408,21 @@ NXG_DEV void probe_body(const ProbeArgs& a, uint32_t bid, uint8_t (*img)[IMGB],
     const bool first = flags & F_FIRST;
     uint32_t count = 0, e = 0, x = 0, L = 0, L2 = 0, ks = 0;
     int state = 0;  // 0 done, 1 run search, 2 exact
-    bool bad = false;
-    if (has) probe_fast(wire, W, t, lim, first, flags, state, e, L, L2, ks, count, x, bad);
-    // an irregular frame (record lengths that change from record to record: more than 1 tile
-    // in 8 off the runs, here or in any workgroup so far) is left to the persistent decoder, which
-    // the host reruns it on
+    bool bad = false, nof = false;
+    if (has) probe_fast(wire, W, t, lim, first, flags, state, e, L, L2, ks, count, x, bad, nof);
+    // a frame that is not f64 at all (DevStatus.irregular bit 1): the host goes on to the mixed
+    // decoders. An irregular frame (record lengths that change from record to record: more than
+    // 1 tile in 8 off the runs, here or in any workgroup so far; bit 0) is left to the
+    // single-pass decoder, which the host reruns it on.
+    const int nnof = __syncthreads_count(nof);
     const int nirr = __syncthreads_count(state != 0);
     const uint64_t ntg = nt - (uint64_t)bid * TPB < TPB ? nt - (uint64_t)bid * TPB
                                                                : TPB;
     const bool bail = !(flags & F_NO_BAIL) &&
-                      ((uint64_t)nirr * 8 > ntg || (nirr && ld_agent32(&st->irregular)));
+                      (nnof || (uint64_t)nirr * 8 > ntg || (nirr && ld_agent32(&st->irregular)));
     if (bail) {
         if (tid == 0) {
-            atomicOr(&st->irregular, 1u);
+            atomicOr(&st->irregular, nnof ? 2u : 1u);
             atomicOr(&st->fast_fail, 1u);
         }
         state = 0;

@@ -8,21 +8,22 @@
 // A wave takes SPW consecutive 4 KiB sub-tiles, a workgroup four waves (64 KiB), and no wave
 // waits on anything but lower-numbered workgroups (a decoupled look-back), so any number of these
 // decodes can share the GPU:
-//   1. per sub-tile: its bytes and 192 around them into LDS (one coalesced pass; dwords stored
-//      swizzled, SwzImg, so that the lanes' 64-byte-strided reads do not pile onto two banks);
-//      lane j: the merge point of its 64-byte chunk (nxg_f64_rec16.h) and a walk from it to the
-//      next lane's, every record checked completely; lane 0 starts one chunk early, so the walks
-//      cover every record that STARTS in the sub-tile, and each is counted by one lane. The
-//      walks' ends and counts stay in registers;
-//   2. a block scan of the counts, the workgroup's total to the look-back, its first row from it
-//      (one look-back per 64 KiB: the wait on the look-back's front is what bounded a workgroup
-//      per 16 KiB, at 178 us for 10^7 records);
-//   3. per sub-tile: the image again (from L2), the walks again, each record decoded into an LDS
-//      row image, then the wave's rows leave as coalesced 8-byte column stores.
-// The true chain starts at byte 0 (lane 0 of sub-tile 0 walks from there) and every merge point
-// lies on it, so consecutive lanes, waves and workgroups meet by construction: a walk that does
-// not land exactly on the next merge point, a record that fails its check, or walks that do not
-// merge raise fast_fail, and the host reruns the frame on the mixed/general decoders.
+//   1. per sub-tile: its bytes and 64 / 128 around them into LDS (one coalesced pass; dwords
+//      stored swizzled, SwzImg, so that the lanes' 64-byte-strided reads do not pile onto two
+//      banks). Lane j takes the 64 positions of chunk j: S = the positions where a complete record
+//      starts (candidates by SWAR -- a byte in 12..16 then 0x04 -- each checked by rec_check16
+//      with independent loads) and the successors of those records (start + length). No walk:
+//      the starts ARE the frame's records exactly when every start but the frame's first byte is
+//      some start's successor and every successor is a start or the frame end (a start without a
+//      predecessor lies inside a record; following successors from byte 0 then visits every
+//      start and ends at W). Neighbouring chunks' masks come by DPP; lane 0 and lane 63 check the
+//      16 positions before / after the sub-tile themselves. The masks stay in registers;
+//   2. a block scan of the counts (popcounts), the workgroup's total to the look-back, its first
+//      row from it (one look-back per 64 KiB);
+//   3. per sub-tile: the image again (from L2), each start's record decoded (independent loads)
+//      into an LDS row image, then the wave's rows leave as coalesced 8-byte column stores.
+// A check that fails raises fast_fail, and the host reruns the frame on the mixed/general
+// decoders.
 #include "nxg_device.h"
 #include "nxg_f64_rec16.h"
 
@@ -40,32 +41,103 @@ constexpr int WAVES = TPB / 64;
 constexpr int SPW = NXG_F64X_SPW;       // sub-tiles per wave
 constexpr uint64_t WGB = (uint64_t)SUB * SPW * WAVES;  // bytes per workgroup
 constexpr uint32_t MAXR = SUB / 12 + 2;  // rows per sub-tile (records start in it, >= 12 bytes)
+#ifndef NXG_F64X_CB
+#define NXG_F64X_CB 6
+#endif
+constexpr int CB = NXG_F64X_CB;          // candidates checked together (independent loads)
 }  // namespace f64x
 
 namespace {
 using namespace f64x;
 using namespace f64rec16;
 
-// the image of the sub-tile at a0: frame bytes [a0 - 64, a0 + 4096 + 128), dwords swizzled
-NXG_DEV void load_image(uint8_t* buf, const uint8_t* __restrict__ wire, uint64_t a0, uint64_t W,
-                        uint32_t lane) {
+// the image of the sub-tile at a0: frame bytes [a0 - 64, a0 + 4096 + 128), dwords swizzled.
+// fetch issues the loads into registers (the next sub-tile's, while this one is walked); commit
+// stores them into the wave's LDS image.
+struct Prefetch {
+    uint4 v[(IMGB + 1023) / 1024];
+};
+NXG_DEV void fetch_image(Prefetch& pf, const uint8_t* __restrict__ wire, uint64_t a0, uint64_t W,
+                         uint32_t lane) {
+    if (a0 >= W) return;
+#pragma unroll
+    for (uint32_t i = 0; i < (IMGB + 1023) / 1024; i++) {
+        const uint32_t off = i * 1024 + lane * 16;
+        if (off < IMGB) {
+            const int64_t pos = (int64_t)a0 - (int64_t)XLO + (int64_t)off;
+            pf.v[i] = pos >= 0 ? ld16g(wire, (uint64_t)pos, W) : ld16_pre(wire, pos, W, 0);
+        }
+    }
+}
+NXG_DEV void commit_image(uint8_t* buf, const Prefetch& pf, uint32_t lane) {
     uint32_t* bw = reinterpret_cast<uint32_t*>(buf);
     wave_lds_order();  // the previous image's reads are issued
 #pragma unroll
     for (uint32_t i = 0; i < (IMGB + 1023) / 1024; i++) {
         const uint32_t off = i * 1024 + lane * 16;
         if (off < IMGB) {
-            const int64_t pos = (int64_t)a0 - (int64_t)XLO + (int64_t)off;
-            const uint4 v = pos >= 0 ? ld16g(wire, (uint64_t)pos, W) : ld16_pre(wire, pos, W, 0);
             const uint32_t q = off >> 2;
-            bw[SwzImg::sw(q)] = v.x;
-            bw[SwzImg::sw(q + 1)] = v.y;
-            bw[SwzImg::sw(q + 2)] = v.z;
-            bw[SwzImg::sw(q + 3)] = v.w;
+            bw[SwzImg::sw(q)] = pf.v[i].x;
+            bw[SwzImg::sw(q + 1)] = pf.v[i].y;
+            bw[SwzImg::sw(q + 2)] = pf.v[i].z;
+            bw[SwzImg::sw(q + 3)] = pf.v[i].w;
         }
     }
     wave_lds_order();
 }
+
+// Record starts among the 4 * NDW positions from image offset r (4-aligned; frame position of
+// bit 0: fp): S (bit i: a complete record starts at r + i) and the successors of those records
+// (bit i of slo: position r + i, of shi: r + 64 + i). Positions at or past W hold none.
+template <int NDW>
+NXG_DEV void starts_of(const SwzImg& im, uint32_t r, uint64_t fp, uint64_t W, uint64_t& S,
+                       uint64_t& slo, uint64_t& shi) {
+    const uint32_t q0 = r >> 2;
+    uint64_t cm = 0;
+    uint32_t a = im.w(q0);
+#pragma unroll
+    for (int k = 0; k < NDW; k++) {
+        const uint32_t b = im.w(q0 + k + 1);
+        cm |= (uint64_t)nib(len_bytes(a) & zero_bytes(alignbyte(b, a, 1) ^ 0x04040404u)) << (4 * k);
+        a = b;
+    }
+    if (fp >= W) cm = 0;
+    else if (W - fp < 4u * NDW) cm &= (1ull << (W - fp)) - 1ull;
+    S = slo = shi = 0;
+    // up to CB candidates at a time: positions, then their first 8 bytes, then the checks
+#pragma unroll 1
+    while (cm) {
+        uint32_t pp[CB];
+#pragma unroll
+        for (int i = 0; i < CB; i++) {
+            pp[i] = cm ? (uint32_t)__builtin_ctzll(cm) : 64u;
+            cm &= cm - 1;
+        }
+        uint32_t e0[CB], e1[CB];
+#pragma unroll
+        for (int i = 0; i < CB; i++) {
+            const uint32_t rel = r + (pp[i] & 63u);
+            const uint32_t q = rel >> 2, sh = rel & 3u;
+            const uint32_t d0 = im.w(q), d1 = im.w(q + 1), d2 = im.w(q + 2);
+            e0[i] = alignbyte(d1, d0, sh);
+            e1[i] = alignbyte(d2, d1, sh);
+        }
+#pragma unroll
+        for (int i = 0; i < CB; i++) {
+            const uint32_t L = pp[i] < 64u ? rec_check16(e0[i], e1[i], W - (fp + pp[i])) : 0u;
+            if (L) {
+                S |= 1ull << pp[i];
+                const uint32_t nx = pp[i] + L;
+                if (nx < 64u) slo |= 1ull << nx;
+                else shi |= 1ull << (nx - 64u);
+            }
+        }
+    }
+}
+
+// the 64-bit value of the previous / next lane (lane 0 / 63: 0), DPP wave_shr / wave_shl
+NXG_DEV uint64_t prev64(uint64_t v) { return dpp0_64<0x138, 0xf>(v); }
+NXG_DEV uint64_t next64(uint64_t v) { return dpp0_64<0x130, 0xf>(v); }
 
 __global__ __launch_bounds__(TPB) void nxg_f64x_kernel(const uint8_t* __restrict__ wire,
                                                        uint64_t W, uint64_t* __restrict__ oid,
@@ -82,50 +154,41 @@ __global__ __launch_bounds__(TPB) void nxg_f64x_kernel(const uint8_t* __restrict
     const uint64_t w0 = (uint64_t)blockIdx.x * WGB + (uint64_t)w * SUB * SPW;  // the wave's bytes
     uint8_t* buf = img[w];
     const SwzImg im{buf};
-    uint32_t xa[SPW], xb[SPW], n[SPW];
+    uint64_t Sm[SPW];
+    uint32_t n[SPW];
     bool bad = false;
+    Prefetch pf;
+    fetch_image(pf, wire, w0, W, lane);
 #pragma unroll
     for (int s = 0; s < SPW; s++) {
-        xa[s] = xb[s] = n[s] = 0;
+        Sm[s] = 0;
+        n[s] = 0;
         const uint64_t a0 = w0 + (uint64_t)s * SUB;
         if (a0 >= W) continue;
-        load_image(buf, wire, a0, W, lane);
+        commit_image(buf, pf, lane);
+        if (s + 1 < SPW) fetch_image(pf, wire, a0 + SUB, W, lane);  // the next, while checking
         const uint64_t ib = a0 - XLO;  // frame position of image byte 0 (wraps for a0 = 0)
-        // segments: lane 0 from the merge point of the chunk before a0 (the frame start for
-        // a0 = 0), lane j >= 1 from chunk j's; each ends at the next lane's start, lane 63 at
-        // the merge point of the chunk at a0 + 4096
-        const uint32_t xhi = XLO + (W - a0 < SUB ? (uint32_t)(W - a0) : SUB);
-        uint32_t x0 = lane == 0 ? (a0 == 0 ? XLO : merge16i(im, 0, ib, W))
-                                : merge16i(im, XLO + lane * 64, ib, W);
-        uint32_t x1 = wave_next(x0);
-        if (lane == 63) x1 = merge16i(im, XHI, ib, W);
-        bool b = x0 == FAILX || x1 == FAILX || x0 > x1 || (lane == 0 && x0 > XLO);
-        uint32_t c = 0;
-        if (!b) {
-            uint32_t pos = x0;
-            int guard = 0;
-            while (pos < x1 && guard < 24) {
-                uint32_t L;
-                if (pos < xhi) {
-                    uint32_t e0, e1, e2, e3;
-                    lds16i(im, pos, e0, e1, e2, e3);
-                    L = rec_check16(e0, e1, W - (ib + pos));
-                    if (!L) break;
-                    if (pos >= XLO) c++;
-                } else {
-                    // past the sub-tile: step by the length byte (the next sub-tile checks it)
-                    L = im.byte(pos);
-                    if (L - 12u > 4u) break;
-                }
-                pos += L;
-                guard++;
-            }
-            b = pos != x1;
-        }
+        const uint32_t r = XLO + lane * 64;
+        const uint64_t fp = ib + r;  // frame position of the lane's chunk
+        uint64_t S, slo, shi;
+        starts_of<16>(im, r, fp, W, S, slo, shi);
+        // lane 0: the 16 positions before the sub-tile; lane 63: the 16 after it
+        const uint32_t rx = lane == 63 ? XHI : XLO - 16;
+        uint64_t Sx, xlo, xhi;
+        starts_of<4>(im, rx, ib + rx, W, Sx, xlo, xhi);
+        const uint64_t sin = lane == 0 ? xlo >> 16 : prev64(shi);  // successors into the chunk
+        const uint64_t Snx = lane == 63 ? Sx : next64(S);         // the next chunk's starts
+        const uint64_t d = W - fp;  // (fp <= W below: the frame end's bit)
+        const uint64_t wlo = fp <= W && d < 64 ? 1ull << d : 0ull;
+        const uint64_t whi = fp <= W && d >= 64 && d < 128 ? 1ull << (d - 64) : 0ull;
+        const uint64_t first = fp == 0 ? 1ull : 0ull;
+        bool b = (S & ~(slo | sin | first)) != 0 ||  // a start no record leads to
+                 (slo & ~(S | wlo)) != 0 ||          // a successor that is not a start
+                 (shi & ~(Snx | whi)) != 0 ||
+                 (fp == 0 && !(S & 1ull));  // the frame's first byte starts a record
         bad |= b;
-        xa[s] = x0;
-        xb[s] = x1;
-        n[s] = c;
+        Sm[s] = S;
+        n[s] = (uint32_t)__popcll(S);
     }
     const bool wbad = __any(bad);
     if (wbad && lane == 0) atomicOr(&st->fast_fail, 1u);
@@ -134,6 +197,8 @@ __global__ __launch_bounds__(TPB) void nxg_f64x_kernel(const uint8_t* __restrict
     uint32_t ntot = 0;
 #pragma unroll
     for (int s = 0; s < SPW; s++) ntot += n[s];
+    // the first image of the emit pass, loading during the look-back
+    if (SPW > 1) fetch_image(pf, wire, w0, W, lane);
     uint64_t total;
     const uint64_t excl = block_excl_scan<uint64_t, TPB>((uint64_t)ntot, scan_tmp, &total);
     if (w == 0) {
@@ -171,22 +236,31 @@ __global__ __launch_bounds__(TPB) void nxg_f64x_kernel(const uint8_t* __restrict
         if (a0 >= W) break;
         const uint32_t inc = wave_incl_scan<uint32_t>(n[s]);
         const uint32_t nw = wave_last<uint32_t>(inc);
-        if (SPW > 1) load_image(buf, wire, a0, W, lane);
-        const uint32_t xhi = XLO + (W - a0 < SUB ? (uint32_t)(W - a0) : SUB);
+        if (SPW > 1) {
+            commit_image(buf, pf, lane);
+            if (s + 1 < SPW) fetch_image(pf, wire, a0 + SUB, W, lane);
+        }
+        // the lane's records (at most 6 start in 64 bytes), loaded together
         uint32_t k = inc - n[s];
-        uint32_t pos = xa[s];
-        while (pos < xb[s] && pos < xhi) {
-            uint32_t e0, e1, e2, e3;
-            lds16i(im, pos, e0, e1, e2, e3);
-            const uint32_t L = e0 & 0xffu;
-            if (pos >= XLO) {
+        uint64_t m = Sm[s];
+        const uint32_t r = XLO + lane * 64;
+        uint32_t pp[6];
+#pragma unroll
+        for (int i = 0; i < 6; i++) {
+            pp[i] = m ? (uint32_t)__builtin_ctzll(m) : 0u;
+            m &= m - 1;
+        }
+        uint32_t e[6][4];
+#pragma unroll
+        for (int i = 0; i < 6; i++) lds16i(im, r + pp[i], e[i][0], e[i][1], e[i][2], e[i][3]);
+#pragma unroll
+        for (int i = 0; i < 6; i++) {
+            if ((uint32_t)i < n[s]) {
                 uint64_t id, val;
-                rec_decode16(e0, e1, e2, e3, L, id, val);
-                rows[w][k][0] = id;
-                rows[w][k][1] = val;
-                k++;
+                rec_decode16(e[i][0], e[i][1], e[i][2], e[i][3], e[i][0] & 0xffu, id, val);
+                rows[w][k + i][0] = id;
+                rows[w][k + i][1] = val;
             }
-            pos += L;
         }
         wave_lds_order();
         for (uint32_t i = lane; i < nw; i += 64) {

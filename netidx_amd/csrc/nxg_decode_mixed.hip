@@ -1,16 +1,19 @@
 // nxg_decode_mixed.hip -- the fast path of the mixed decode (config 3) for gfx950.
 //
-// Frames whose messages are all From::Update(id, v) with a one-byte length prefix (L < 128) and
-// a value that is a scalar, text, Decimal or an Array of non-container elements -- what a
-// publisher of ordinary values sends -- are decoded in two passes over 4 KiB tiles with no
-// speculation across tiles beyond one checked guess. Anything else (control messages, longer
+// Frames whose messages are From::Update(id, v) with a value that is a scalar, text, Decimal or
+// an Array of non-container elements -- what a publisher of ordinary values sends -- and
+// From::Heartbeat (02 05, kept as a control span, connection.rs:434) are decoded in two passes
+// over 4 KiB tiles with no speculation across tiles beyond one checked guess. Length prefixes of
+// one byte (messages < 128 bytes) and two bytes (< 16384: text values only, the text checked from
+// global memory where it leaves the tile's image) are taken. Anything else (other control
 // messages, Map / Error(Value) / Abstract values, nested containers, any content error) raises
 // fast_fail and the host reruns the frame on the general decoder (nxg_decode_gen.hip), which
 // covers every case and reports errors exactly. The values are decoded by the same restatement
 // as the general path (nxg_msg.h dleaf / dcontainer), so the columns are identical.
 //
-// Message boundaries. With one-byte lengths a message at p ends at p + b[p], and a message start
-// is a byte in [4, 127] followed by the Update variant (4). Per tile, each lane takes a 64-byte
+// Message boundaries. A message at p ends at p + L (L the varint at p; canonical prefixes only),
+// and a message start is a byte in [4, 127] followed by the Update variant (4), 02 05 (a
+// Heartbeat), or a two-byte prefix (a byte >= 0x80, then one in [1, 127]) followed by 4. Per tile, each lane takes a 64-byte
 // chunk: its candidate starts (SWAR over its bytes) and, for its first two candidates, where the
 // chain of messages from them leaves the chunk (an LDS walk of a few steps; every position on the
 // way must be a candidate). One uniform loop over the 64 chunks then follows the true chain from
@@ -34,8 +37,7 @@
 //           confirms the size) and decoded one per lane, the exact walk as the fallback
 #include <algorithm>
 
-#include "nxg_internal.h"
-#include "nxg_msg.h"
+#include "nxg_fmx_common.h"
 
 #ifndef NXG_FMX_SKIP
 #define NXG_FMX_SKIP 0  // timing experiments only: 1 elements, 2 text, 4 row values, 8 row stores
@@ -54,16 +56,7 @@
     } while (0)
 #endif
 
-namespace fmx {
-constexpr uint32_t TILE = 4096;
-constexpr uint32_t CH = 64;
-constexpr uint32_t IMG = TILE + 256;    // image: the tile + 256 B (messages are < 128 bytes)
-constexpr uint32_t MAXM = TILE / 4;     // messages per tile (>= 4 bytes each)
-constexpr uint32_t MAXC = 256;          // array elements per round of 64 messages (lane-parallel)
-constexpr int TPB = 256;
-constexpr uint32_t NONE = 0xffffffffu;
-constexpr uint32_t FAIL = 0xfffffffeu;
-}  // namespace fmx
+
 
 namespace {
 using namespace fmx;
@@ -79,67 +72,34 @@ struct EmitLds {
     uint8_t mark[256];   // utf8_packed
 };
 
-NXG_DEV uint4 ld16(const uint8_t* __restrict__ wire, uint64_t off, uint64_t W) {
-    if (off + 16 <= W) return *reinterpret_cast<const uint4*>(wire + off);
-    uint32_t q[4] = {0, 0, 0, 0};
-    for (int k = 0; k < 16; k++)
-        if (off + k < W) q[k >> 2] |= (uint32_t)wire[off + k] << (8 * (k & 3));
-    return make_uint4(q[0], q[1], q[2], q[3]);
-}
-
-// the tile's image: 4 KiB from 64 lanes x 4, the 256-byte tail from lanes 0..15 (zeros past W),
-// loaded into registers (tile_load, one tile ahead) and then written to LDS (tile_store)
-struct TileRegs {
-    uint4 v[5];
-};
-NXG_DEV void tile_load(TileRegs& g, const uint8_t* __restrict__ wire, uint64_t t0, uint64_t W,
-                       uint32_t lane) {
-    if (t0 + IMG <= W) {
-        const uint4* p = reinterpret_cast<const uint4*>(wire + t0);
-#pragma unroll
-        for (uint32_t i = 0; i < 4; i++) g.v[i] = p[i * 64 + lane];
-        if (lane < 16) g.v[4] = p[256 + lane];
-    } else {
-#pragma unroll
-        for (uint32_t i = 0; i < 4; i++) g.v[i] = ld16(wire, t0 + i * 1024 + lane * 16, W);
-        if (lane < 16) g.v[4] = ld16(wire, t0 + 4096 + lane * 16, W);
-    }
-}
-NXG_DEV void tile_store(uint8_t* img, const TileRegs& g, uint32_t lane) {
-    wave_lds_order();  // the previous tile's reads are issued
-#pragma unroll
-    for (uint32_t i = 0; i < 4; i++) *reinterpret_cast<uint4*>(img + i * 1024 + lane * 16) = g.v[i];
-    if (lane < 16) *reinterpret_cast<uint4*>(img + 4096 + lane * 16) = g.v[4];
-    wave_lds_order();
-}
-
-// contiguous tile ranges per wave: tiles [run_begin(r), run_begin(r + 1)) of R
-NXG_DEV uint64_t run_begin(uint64_t nt, uint32_t R, uint32_t r) { return nt * r / R; }
-
-// image bytes r..r+15 as two little-endian words (reads up to 20 bytes from r & ~3)
-struct Win16 {
-    uint64_t lo, hi;
-};
-NXG_DEV Win16 win16(lds_bytes img, uint32_t r) {
-    lds_words w = (lds_words)(img + (r & ~3u));
-    const uint32_t sh = r & 3u;
-    const uint32_t a0 = w[0], a1 = w[1], a2 = w[2], a3 = w[3], a4 = w[4];
-    return Win16{(uint64_t)alignbyte(a1, a0, sh) | ((uint64_t)alignbyte(a2, a1, sh) << 32),
-                 (uint64_t)alignbyte(a3, a2, sh) | ((uint64_t)alignbyte(a4, a3, sh) << 32)};
-}
-
-// candidate message starts in the lane's chunk: bit i = byte c+i in [4, 127] and byte c+i+1 == 4
+// candidate message starts in the lane's chunk: bit i = byte c+i starts an Update with a one-byte
+// prefix (a byte in [4, 127], then 4), a Heartbeat (02 05), or an Update with a two-byte prefix
+// (a byte >= 0x80, a byte in [1, 127], then 4)
+// The lanes' chunks are 64 bytes (16 banks) apart, so lane j reads its words in the order
+// k + j / 2 (mod 16): at each step the 32 lanes of a half-wave read 32 different banks
+// (ds_read_b32: bank = dword address mod 32), where the plain order put 16 lanes on one bank.
 NXG_DEV uint64_t cand_mask(const uint8_t* img, uint32_t c) {
     const uint32_t* w = reinterpret_cast<const uint32_t*>(img + c);
+    const uint32_t rot = (c >> 7) & 15u;  // (c / 64) / 2
     uint64_t m = 0;
 #pragma unroll
     for (int k = 0; k < 16; k++) {
-        const uint32_t a = w[k], b = w[k + 1];
+        const uint32_t kk = ((uint32_t)k + rot) & 15u;
+        const uint32_t a = w[kk], b = w[kk + 1];
+        const uint32_t a1 = alignbyte(b, a, 1), a2 = alignbyte(b, a, 2);
         const uint32_t len = ((a & 0x7f7f7f7fu) + 0x7c7c7c7cu) & ~a & 0x80808080u;
-        const uint32_t var = zero_bytes(alignbyte(b, a, 1) ^ 0x04040404u);
-        m |= (uint64_t)nib(len & var) << (4 * k);
+        const uint32_t var = zero_bytes(a1 ^ 0x04040404u);
+        const uint32_t hb = zero_bytes(a ^ 0x02020202u) & zero_bytes(a1 ^ 0x05050505u);
+        const uint32_t two = a & ~a1 & ~zero_bytes(a1) & zero_bytes(a2 ^ 0x04040404u) & 0x80808080u;
+        m |= (uint64_t)nib((len & var) | hb | two) << (4 * kk);
     }
     return m;
+}
+
+// the length of the message at tile offset x (its canonical one- or two-byte prefix)
+NXG_DEV uint32_t msg_len(const uint8_t* img, uint32_t x) {
+    const uint32_t b0 = img[x];
+    return b0 < 0x80u ? b0 : (b0 & 0x7fu) | ((uint32_t)img[x + 1] << 7);
 }
 
 // where the chain of messages from tile offset x (a candidate of chunk j) leaves the chunk, or
@@ -150,7 +110,7 @@ NXG_DEV uint32_t chunk_exit(const uint8_t* img, uint32_t x, uint32_t j, uint64_t
 #pragma unroll 1
     for (int g = 0; g < 32 && x < end; g++) {
         if (!((m >> (x - j * CH)) & 1ull)) return FAIL;
-        x += img[x];
+        x += msg_len(img, x);
     }
     return x < end ? FAIL : x;
 }
@@ -291,26 +251,33 @@ NXG_DEV uint32_t tile_chain_scan(uint32_t e, uint32_t lim, uint32_t lane, uint32
     return (uint32_t)__builtin_amdgcn_readlane((int)xl, (int)__builtin_ctzll(lm));
 }
 
-// Header of the message at tile offset p: child slots (Array element count), or FAIL when the
-// message is not for the fast path. The value tag sits after the variant and the id varint.
+// Header of the message at tile offset p: child slots (Array element count), HB for a
+// Heartbeat, or FAIL when the message is not for the fast path. The value tag sits after the
+// variant and the id varint; a message with a two-byte prefix must hold text.
+constexpr uint32_t HB = 0xfffffffdu;
 NXG_DEV uint32_t msg_kids(const uint8_t* img, uint32_t p) {
-    const uint64_t w = win16((lds_bytes)img, p + 2).lo;  // id varint, tag, next byte
+    const uint32_t b0 = img[p];
+    if (b0 == 2u) return img[p + 1] == 5u ? HB : FAIL;  // Heartbeat (02 05)
+    const uint32_t nbp = b0 < 0x80u ? 1u : 2u;
+    const uint64_t w = win16((lds_bytes)img, p + nbp + 1).lo;  // id varint, tag, next byte
     const uint64_t stop = ~w & 0x8080808080808080ull;
     const uint32_t k = stop ? (uint32_t)__builtin_ctzll(stop) >> 3 : 8u;
     if (k >= 5) return FAIL;  // ids wider than 35 bits: the general decoder
     const uint32_t t = (uint32_t)(w >> (8 * k + 8)) & 0xffu;
     const uint32_t c = (uint32_t)(w >> (8 * k + 16)) & 0xffu;
+    if (nbp == 2u) return (t == 12u || t == 13u || t == 18u || (t == 22u && c == 12u)) ? 0u : FAIL;
     if (t == 19) return c < 0x80u ? c : FAIL;
     if (t == 21 || t >= 28u) return FAIL;
     if (t == 22 && c != 12u) return FAIL;  // Error(Value) of a non-String
     return 0;
 }
 
-// the messages of the lane's chunk from its entry: count, child slots, and their starts as bits
-// of the chunk (bit i: chunk byte i)
+// the messages of the lane's chunk from its entry: Updates, Heartbeats, child slots, and their
+// starts as bits of the chunk (bit i: chunk byte i)
 NXG_DEV bool chunk_msgs(const uint8_t* img, uint32_t ce, uint32_t lane, uint32_t lim, uint32_t& n,
-                        uint32_t& kids, uint64_t& bits) {
+                        uint32_t& nhb, uint32_t& kids, uint64_t& bits) {
     n = 0;
+    nhb = 0;
     kids = 0;
     bits = 0;
     if (ce == NONE) return true;
@@ -321,9 +288,13 @@ NXG_DEV bool chunk_msgs(const uint8_t* img, uint32_t ce, uint32_t lane, uint32_t
         const uint32_t k = msg_kids(img, x);
         if (k == FAIL) return false;
         bits |= 1ull << (x - c);
-        n++;
-        kids += k;
-        x += img[x];
+        if (k == HB) {
+            nhb++;
+        } else {
+            n++;
+            kids += k;
+        }
+        x += msg_len(img, x);
     }
     return true;
 }
@@ -331,7 +302,8 @@ NXG_DEV bool chunk_msgs(const uint8_t* img, uint32_t ce, uint32_t lane, uint32_t
 // tile descriptor (count pass -> resolve -> emit)
 struct TileDesc {
     uint32_t entry, exit;  // tile offsets
-    uint32_t rows, kids;
+    uint32_t rows;         // Updates | Heartbeats << 16
+    uint32_t kids;
 };
 
 // The tile's descriptor for the chain from entry e: exit, messages, child slots (FAIL entry and
@@ -343,343 +315,17 @@ NXG_DEV TileDesc count_from(const uint8_t* img, const Cands& cd, uint32_t e, uin
     uint32_t x = tile_chain_scan(e, lim, lane, cd.c0, cd.x0, cd.c1, cd.x1, ce);
     if (x == FAIL) x = tile_chain(img, e, lim, lane, cd.m, cd.c0, cd.x0, cd.c1, cd.x1, ce);
     bool bad = x == FAIL || (last && x != lim);
-    uint32_t n = 0, k = 0;
+    uint32_t n = 0, h = 0, k = 0;
     bits = 0;
-    if (!bad) bad = !chunk_msgs(img, ce, lane, lim, n, k, bits);
+    if (!bad) bad = !chunk_msgs(img, ce, lane, lim, n, h, k, bits);
     bad = __any(bad);
     if (bad) return TileDesc{FAIL, FAIL, 0, 0};
-    return TileDesc{e, x, wave_sum<uint32_t>(n), wave_sum<uint32_t>(k)};
+    const uint32_t nh = wave_sum<uint32_t>(n | (h << 16));
+    // more messages than the emit pass's list holds (Heartbeats are 2 bytes): the general decoder
+    if ((nh & 0xffffu) + (nh >> 16) > MAXM) return TileDesc{FAIL, FAIL, 0, 0};
+    return TileDesc{e, x, nh, wave_sum<uint32_t>(k)};
 }
 
-// ---- the emit pass's value decoder ---------------------------------------------------------------
-// Value::decode (netidx-value/src/lib.rs:470-506) for the values this path takes, restated as
-// nxg_msg.h dleaf / dcontainer do. Every field is computed from the 12 bytes after the tag (three
-// words already in registers) with 32-bit tile offsets, and selected by tag, so that a wave whose
-// lanes hold different tags runs one instruction stream; only a varint longer than 4 bytes and a
-// DateTime outside +-2^42 s or with a leap second branch. Text is checked for UTF-8 by the caller
-// (ascii_ok per lane, utf8_wave for the rest). Any decode error clears ok: the frame then goes to
-// the general decoder, which reports it.
-
-// the 7-bit groups of the (up to) 8 bytes of y, least significant first
-NXG_DEV uint64_t compress7(uint64_t y) {
-    const uint64_t z1 = (y & 0x007f007f007f007full) | ((y >> 1) & 0x3f803f803f803f80ull);
-    const uint64_t z2 = (z1 & 0x00003fff00003fffull) | ((z1 >> 2) & 0x0fffc0000fffc000ull);
-    return (z2 & 0x0fffffffull) | ((z2 >> 4) & 0x00fffffff0000000ull);
-}
-NXG_DEV uint32_t compress7_32(uint32_t y) {
-    return (y & 0x7fu) | ((y >> 1) & 0x3f80u) | ((y >> 2) & 0x1fc000u) | ((y >> 3) & 0xfe00000u);
-}
-
-// LEB128 (pack.rs:504-520) at window byte 0: its length (0: no terminator in 10 bytes); bits
-// past 64 dropped as decode_varint does
-NXG_DEV uint32_t wvar(uint64_t lo, uint64_t hi, uint64_t& v) {
-    const uint64_t stop = ~lo & 0x8080808080808080ull;
-    if (stop) {
-        const uint32_t nb = ((uint32_t)__builtin_ctzll(stop) >> 3) + 1;
-        v = compress7(nb == 8 ? lo : (lo & ((1ull << (8 * nb)) - 1)));
-        return nb;
-    }
-    const uint64_t b8 = hi & 0xffu, b9 = (hi >> 8) & 0xffu;
-    const uint64_t base = compress7(lo);
-    if (b8 < 0x80u) {
-        v = base | (b8 << 56);
-        return 9;
-    }
-    v = base | ((b8 & 0x7fu) << 56) | ((b9 & 1u) << 63);
-    return b9 < 0x80u ? 10u : 0u;
-}
-// the same over the words w0, w1, w2 (bytes 0..11): one to four bytes without a branch
-NXG_DEV uint32_t var3(uint32_t w0, uint32_t w1, uint32_t w2, uint64_t& v) {
-    const uint32_t st = ~w0 & 0x80808080u;
-    if (__builtin_expect(st != 0u, 1)) {
-        const uint32_t nb = ((uint32_t)__builtin_ctz(st) >> 3) + 1;
-        v = compress7_32(w0 & (0xffffffffu >> (32u - 8u * nb)));
-        return nb;
-    }
-    return wvar((uint64_t)w0 | ((uint64_t)w1 << 32), w2, v);
-}
-
-// image bytes r .. r+4n-1 as n little-endian words (reads n+1 aligned words from r & ~3)
-template <int N>
-NXG_DEV void win_words(lds_bytes img, uint32_t r, uint32_t* q) {
-    lds_words w = (lds_words)(img + (r & ~3u));
-    const uint32_t sh = r & 3u;
-    uint32_t a[N + 1];
-#pragma unroll
-    for (int k = 0; k <= N; k++) a[k] = w[k];
-#pragma unroll
-    for (int k = 0; k < N; k++) q[k] = alignbyte(a[k + 1], a[k], sh);
-}
-
-struct FV {
-    uint64_t fixed;
-    uint32_t tag, aux;
-    uint32_t end;         // tile offset after the value
-    uint32_t kids;        // Array: element count
-    uint32_t soff, slen;  // text to check for UTF-8 (slen 0: none)
-    bool ok;
-};
-
-// The value with tag t whose payload starts at tile offset u; P0..P2 = its first 12 bytes; lim =
-// the message end (tile offset, >= u). Arrays only when `arr` (a row).
-// value classes as tag bit sets (bit tests, so that the compiler forms no switch on the tag)
-constexpr uint32_t B(uint32_t t) { return 1u << t; }
-constexpr uint32_t kVarTags = B(1) | B(3) | B(5) | B(7);    // V32 Z32 V64 Z64
-constexpr uint32_t kVar32 = B(1) | B(3), kZig = B(3) | B(7);
-constexpr uint32_t kTxtTags = B(12) | B(13) | B(18) | B(22);  // String Bytes Error(String)
-constexpr uint32_t kSgnTags = B(2) | B(24) | B(26);         // I32 I8 I16
-NXG_DEV FV val_decode(uint32_t t, uint32_t P0, uint32_t P1, uint32_t P2, uint32_t u, uint32_t lim,
-                      bool arr, uint64_t t0) {
-    const uint32_t bit = t < 32u ? 1u << t : 0u;
-    // Error(Value) whose inner value is a String: the String after its tag (12)
-    const bool e22 = bit & B(22);
-    const bool bad = t >= 28u || (bit & B(21)) || ((bit & B(19)) && !arr) ||
-                     (e22 && (P0 & 0xffu) != 12u);
-    P0 = e22 ? alignbyte(P1, P0, 1) : P0;
-    P1 = e22 ? alignbyte(P2, P1, 1) : P1;
-    P2 = e22 ? P2 >> 8 : P2;
-    u += e22 ? 1u : 0u;
-    const uint32_t room = lim > u ? lim - u : 0u;
-    uint64_t v;
-    const uint32_t nb = var3(P0, P1, P2, v);
-    const bool vok = nb != 0 && nb <= room;
-    const uint32_t p = u + nb;  // after a length / count varint
-    const uint32_t rest = lim > p ? lim - p : 0u;
-    const uint32_t v32 = (uint32_t)v;
-    // fixed-size payloads: n big-endian bytes (0: Bool / Null; 12: DateTime, Duration)
-    const uint32_t f1 = fixed_size1(t);
-    const uint32_t n = f1 - 1u;
-    const uint32_t b0 = bswap32(P0), b1 = bswap32(P1);
-    const bool n8 = f1 >= 9u;                       // 8 or 12 bytes
-    const uint32_t sh = (32u - 8u * n) & 31u;       // 1, 2, 4 bytes: b0 >> 24, 16, 0
-    const bool sgn = bit & kSgnTags;
-    const uint32_t lo32 = f1 >= 2u ? (sgn ? (uint32_t)((int32_t)b0 >> sh) : b0 >> sh)
-                                   : ((bit & B(14)) ? 1u : 0u);
-    const uint32_t fhi = n8 ? b0 : (sgn ? (uint32_t)((int32_t)lo32 >> 31) : 0u);
-    const uint32_t flo = n8 ? b1 : lo32;
-    // DateTime::from_timestamp: |secs| < 2^42 with ns < 10^9 is always valid (no branch)
-    uint32_t ns = bswap32(P2);
-    const uint64_t secs = ((uint64_t)b0 << 32) | b1;
-    bool fok = room >= n;
-    const bool easy = ns < 1000000000u && secs + ((1ull << 42) - 1) < (1ull << 43) - 1;
-    if (__builtin_expect((bit & B(10)) && !easy, 0)) fok = fok && datetime_valid((int64_t)secs, ns);
-    // Duration::new normalisation (dleaf case 11); ns < 2^32 < 5 * 10^9
-    const bool dur = bit & B(11);
-    const uint32_t add = dur ? (uint32_t)(ns >= 1000000000u) + (ns >= 2000000000u) +
-                                   (ns >= 3000000000u) + (ns >= 4000000000u)
-                             : 0u;
-    const uint64_t s2 = secs + add;
-    fok = fok && s2 >= secs;
-    ns -= add * 1000000000u;
-    // varint scalars: V32 (truncated), Z32, V64, Z64
-    const uint32_t z32 = (v32 >> 1) ^ (0u - (v32 & 1u));
-    const uint64_t z64 = (v >> 1) ^ (0ull - (v & 1ull));
-    const bool isvar = bit & kVarTags, iszig = bit & kZig, is32 = bit & kVar32;
-    const uint64_t v32x = iszig ? (uint64_t)(int64_t)(int32_t)z32 : (uint64_t)v32;
-    const uint64_t vfix = is32 ? v32x : (iszig ? z64 : v);
-    const bool istxt = bit & kTxtTags, isarr = bit & B(19), isdec = bit & B(20);
-    const bool isfix = f1 != 0u;
-    // Abstract: len-wrapped (dleaf case 27); the wrap may claim past the message
-    const uint64_t take = v >= 1 ? v - vl64(v) : 0ull;
-    const uint32_t l2 = take < (uint64_t)rest ? p + (uint32_t)take : lim;
-    // ValArray header (array.rs:595-612): count guard as dcontainer
-    const bool aok = vok && v <= kMaxVec / 16 && v * 16 <= ((uint64_t)rest << 8);
-    const bool tok = vok && v <= (uint64_t)(room - nb);
-    const bool bok = vok && v >= 1 && l2 >= p + 16u;
-    const bool ok = isfix ? fok : (isvar ? vok : (istxt ? tok : (isarr ? aok : (isdec ? room >= 16u : bok))));
-    FV o;
-    o.tag = (bit & B(17)) ? 16u : (e22 ? 18u : t);
-    o.ok = ok && !bad;
-    const uint32_t endv = isvar || isarr ? p : (istxt ? p + v32 : (isdec ? u + 16u : l2));
-    o.end = isfix ? u + n : endv;
-    const uint64_t off = t0 + (isdec ? u : p);  // text, Decimal, Abstract: where in the frame
-    const uint64_t fval = dur ? s2 : (((uint64_t)fhi << 32) | flo);
-    o.fixed = isfix ? fval : (isvar ? vfix : (isarr ? 0ull : off));
-    const uint32_t avar = istxt || isarr ? v32 : (isdec ? 16u : (isvar ? 0u : l2 - p));
-    o.aux = isfix ? (n == 12u ? ns : 0u) : avar;
-    o.kids = isarr ? v32 : 0u;
-    o.soff = p;
-    o.slen = o.ok && istxt && !(bit & B(13)) ? v32 : 0u;
-    return o;
-}
-
-// index of the first byte >= 0x80 among bytes 0..15 of the words q[0..3] (16: none)
-NXG_DEV uint32_t first_high16(const uint32_t* q) {
-    const uint64_t lo = (((uint64_t)q[1] << 32) | q[0]) & 0x8080808080808080ull;
-    const uint64_t hi = (((uint64_t)q[3] << 32) | q[2]) & 0x8080808080808080ull;
-    return lo ? (uint32_t)__builtin_ctzll(lo) >> 3 : (hi ? 8u + ((uint32_t)__builtin_ctzll(hi) >> 3) : 16u);
-}
-// bytes [s, s + n) of the image are all ASCII: 32 bytes from one batch of LDS reads, longer text
-// (up to 127 bytes) 32 more per step
-NXG_DEV bool ascii_ok(lds_bytes img, uint32_t s, uint32_t n) {
-    bool na = false;
-#pragma unroll 1
-    for (uint32_t k = 0; k < n; k += 32) {
-        uint32_t q[8];
-        win_words<8>(img, s + k, q);
-        const uint32_t f0 = first_high16(q), f1 = first_high16(q + 4);  // 16: none
-        na |= (f0 < 16u ? f0 : (f1 < 16u ? 16u + f1 : 0xffffu)) < n - k;
-    }
-    return !na;
-}
-
-// inclusive max-scan over the wave (DPP, identity 0)
-NXG_DEV uint32_t wave_max_scan(uint32_t x) {
-    x = max(x, dpp0<0x111, 0xf>(x));
-    x = max(x, dpp0<0x112, 0xf>(x));
-    x = max(x, dpp0<0x114, 0xf>(x));
-    x = max(x, dpp0<0x118, 0xf>(x));
-    x = max(x, dpp0<0x142, 0xa>(x));
-    x = max(x, dpp0<0x143, 0xc>(x));
-    return x;
-}
-
-// std::str::from_utf8 (pack.rs:462) of bytes [s, s + n) of the image (s >= 3), checked by the
-// whole wave one byte per lane: a continuation byte exactly where a lead within the three bytes
-// before asks for one, no C0 / C1 / F5..FF, no overlong 3- or 4-byte form, surrogate or code
-// point past U+10FFFF (the byte after E0 / ED / F0 / F4), and every sequence ends inside the text.
-// All 64 lanes must be active.
-NXG_DEV bool utf8_wave(lds_bytes img, uint32_t s, uint32_t n, uint32_t lane) {
-    bool bad = false;
-#pragma unroll 1
-    for (uint32_t i0 = 0; i0 < n; i0 += 64) {
-        const uint32_t i = i0 + lane;
-        if (i < n) {
-            const uint32_t r = s + i - 3;
-            lds_words w = (lds_words)(img + (r & ~3u));
-            const uint32_t x = alignbyte(w[1], w[0], r & 3u);  // bytes i-3 .. i
-            const uint32_t c = x >> 24;
-            const uint32_t c1 = i >= 1 ? (x >> 16) & 0xffu : 0u;
-            const uint32_t c2 = i >= 2 ? (x >> 8) & 0xffu : 0u;
-            const uint32_t c3 = i >= 3 ? x & 0xffu : 0u;
-            const bool cont = (c & 0xc0u) == 0x80u;
-            const bool need = c1 >= 0xc0u || c2 >= 0xe0u || c3 >= 0xf0u;
-            const uint32_t L = c < 0xc0u ? 0u : (c < 0xe0u ? 2u : (c < 0xf0u ? 3u : 4u));
-            bad |= cont != need;
-            bad |= c == 0xc0u || c == 0xc1u || c >= 0xf5u;
-            bad |= (c1 == 0xe0u && c < 0xa0u) || (c1 == 0xedu && c > 0x9fu) ||
-                   (c1 == 0xf0u && c < 0x90u) || (c1 == 0xf4u && c > 0x8fu);
-            bad |= i + L > n;
-        }
-    }
-    return !__any(bad);
-}
-
-// the text of the lanes with `na` (not all ASCII), one after another by the whole wave
-NXG_DEV bool utf8_lanes(lds_bytes img, bool na, uint32_t soff, uint32_t slen, uint32_t lane) {
-    uint64_t m = __ballot(na);
-    bool good = true;
-#pragma unroll 1
-    while (m && good) {
-        const int j = (int)__builtin_ctzll(m);
-        m &= m - 1;
-        good = utf8_wave(img, (uint32_t)__builtin_amdgcn_readlane((int)soff, j),
-                         (uint32_t)__builtin_amdgcn_readlane((int)slen, j), lane);
-    }
-    return good;
-}
-
-// The same, all the texts at once: their bytes laid end to end, one per lane (64 per step), each
-// lane finding its text through `mark` (LDS, 256 bytes: the text starting at each position). More
-// than 256 bytes: utf8_lanes. The checks are utf8_wave's.
-NXG_DEV bool utf8_packed(lds_bytes img, uint8_t* mark, bool na, uint32_t soff, uint32_t slen,
-                         uint32_t lane) {
-    const uint32_t len = na ? slen : 0u;
-    const uint32_t inc = wave_incl_scan<uint32_t>(len);
-    const uint32_t pre = inc - len;
-    const uint32_t T = wave_last<uint32_t>(inc);
-    if (T == 0) return true;
-    if (T > 256u) return utf8_lanes(img, na, soff, slen, lane);
-    reinterpret_cast<uint32_t*>(mark)[lane] = 0u;
-    wave_lds_order();
-    if (len) mark[pre] = (uint8_t)(lane + 1);
-    wave_lds_order();
-    bool bad = false;
-    uint32_t carry = 0;
-#pragma unroll 1
-    for (uint32_t b0 = 0; b0 < T; b0 += 64) {
-        const uint32_t L = b0 + lane;
-        const uint32_t j1 = max(wave_max_scan(L < T ? (uint32_t)mark[L] : 0u), carry);
-        carry = wave_last<uint32_t>(j1);
-        const int j = (int)j1 - 1;  // >= 0: text 0 starts at byte 0
-        const uint32_t s = (uint32_t)__shfl((int)soff, j, 64);
-        const uint32_t n = (uint32_t)__shfl((int)len, j, 64);
-        const uint32_t i = L - (uint32_t)__shfl((int)pre, j, 64);
-        if (L < T) {
-            const uint32_t r = s + i - 3;
-            lds_words w = (lds_words)(img + (r & ~3u));
-            const uint32_t x = alignbyte(w[1], w[0], r & 3u);  // bytes i-3 .. i
-            const uint32_t c = x >> 24;
-            const uint32_t c1 = i >= 1 ? (x >> 16) & 0xffu : 0u;
-            const uint32_t c2 = i >= 2 ? (x >> 8) & 0xffu : 0u;
-            const uint32_t c3 = i >= 3 ? x & 0xffu : 0u;
-            const bool cont = (c & 0xc0u) == 0x80u;
-            const bool need = c1 >= 0xc0u || c2 >= 0xe0u || c3 >= 0xf0u;
-            const uint32_t Lq = c < 0xc0u ? 0u : (c < 0xe0u ? 2u : (c < 0xf0u ? 3u : 4u));
-            bad |= cont != need;
-            bad |= c == 0xc0u || c == 0xc1u || c >= 0xf5u;
-            bad |= (c1 == 0xe0u && c < 0xa0u) || (c1 == 0xedu && c > 0x9fu) ||
-                   (c1 == 0xf0u && c < 0x90u) || (c1 == 0xf4u && c > 0x8fu);
-            bad |= i + Lq > n;
-        }
-    }
-    wave_lds_order();
-    return !__any(bad);
-}
-
-// The deferred text checks of a tile: entries soff | slen << 16 in `list`, 64 per pass (ASCII per
-// lane, the rest by utf8_packed). Uniform; false on invalid UTF-8.
-NXG_DEV bool text_flush(lds_bytes img, const uint32_t* list, uint32_t ntxt, uint8_t* mark,
-                        uint32_t lane, DevStatus* st) {
-    bool good = true;
-#pragma unroll 1
-    for (uint32_t b = 0; b < ntxt && good; b += 64) {
-        const uint32_t i = b + lane;
-        const uint32_t e = i < ntxt ? list[i] : 0u;
-        const uint32_t so = e & 0xffffu, sl = e >> 16;
-        const bool na = sl && !ascii_ok(img, so, sl);
-#if NXG_FMX_PROF
-        {
-            const uint64_t nm = __ballot(na);
-            const uint32_t T = wave_sum<uint32_t>(na ? sl : 0u);
-            if (lane == 0) {
-                atomicAdd(&st->diag[4], 1ull);
-                atomicAdd(&st->diag[5], (unsigned long long)__popcll(nm) | ((unsigned long long)T << 32));
-            }
-        }
-#endif
-        good = utf8_packed(img, mark, na, so, sl, lane);
-    }
-    return good;
-}
-
-// A fixed-size element other than DateTime / Duration (n = 0, 1, 2, 4 or 8 payload bytes): the
-// fixed-size part of val_decode alone. q: 16 bytes from the tag; e0 / elim: tile offsets of the
-// element and of its message end.
-NXG_DEV FV fixed_elem(const uint32_t* q, uint32_t e0, uint32_t elim) {
-    const uint32_t t = q[0] & 0xffu;
-    const uint32_t bit = 1u << (t & 31u);
-    const uint32_t f1 = fixed_size1(t), n = f1 - 1u;
-    const uint32_t b0 = bswap32(alignbyte(q[1], q[0], 1)), b1 = bswap32(alignbyte(q[2], q[1], 1));
-    const bool n8 = f1 == 9u;
-    const uint32_t sh = (32u - 8u * n) & 31u;
-    const bool sgn = bit & kSgnTags;
-    const uint32_t lo32 = f1 >= 2u ? (sgn ? (uint32_t)((int32_t)b0 >> sh) : b0 >> sh)
-                                   : ((bit & B(14)) ? 1u : 0u);
-    FV o;
-    o.tag = (bit & B(17)) ? 16u : t;
-    o.fixed = n8 ? (((uint64_t)b0 << 32) | b1)
-                 : (((uint64_t)(sgn ? (uint32_t)((int32_t)lo32 >> 31) : 0u) << 32) | lo32);
-    o.aux = 0;
-    o.end = e0 + f1;
-    o.kids = 0;
-    o.soff = 0;
-    o.slen = 0;
-    o.ok = elim >= e0 + f1;
-    return o;
-}
-// fixed-size element tags fixed_elem takes (not DateTime 10, Duration 11)
-NXG_DEV bool simple_fixed(uint32_t t) { return fixed_size1(t) != 0u && t != 10u && t != 11u; }
 
 }  // namespace
 
@@ -736,6 +382,28 @@ __global__ __launch_bounds__(TPB) void nxg_fmx_count_kernel(const uint8_t* __res
     if (lane == 0) td[t] = d;
 }
 
+// The exit at which the chain leaves tile t - 1 (t >= 1), from the count pass's descriptors: the
+// last tile before t whose entry is its predecessor's exit keeps its exit; the tiles after it
+// that one long message covers entirely pass it on; FAIL when a tile on the way would need a
+// recount (the emit pass's chain check then fails the frame). Lets a wave's first tile see past
+// the previous wave's recounts.
+NXG_DEV uint32_t exit_before(const TileDesc* td, uint64_t t) {
+    uint64_t k = t - 1;
+#pragma unroll 1
+    for (uint32_t back = 0; k > 0 && back < 64; back++, k--) {
+        const uint32_t bx = td[k - 1].exit;
+        if (bx != FAIL && bx - TILE == td[k].entry) break;
+    }
+    uint32_t x = td[k].exit;
+#pragma unroll 1
+    for (k = k + 1; k < t && x != FAIL; k++) {
+        const uint32_t e = x - TILE;  // tile k's true entry
+        if (e >= TILE) x = e;         // covered: no message starts in tile k
+        else x = e == td[k].entry ? td[k].exit : FAIL;
+    }
+    return x;
+}
+
 // resolve: everything between the count and the emit passes in one launch (no waiting on other
 // workgroups). A lane per tile: a tile whose entry is not its predecessor's exit is recounted
 // from that exit by its wave, tile by tile; then a block scan of (rows | child slots << 32) gives
@@ -747,7 +415,7 @@ __global__ __launch_bounds__(TPB) void nxg_fmx_resolve_kernel(
     const uint8_t* __restrict__ wire, uint64_t W, uint64_t nt, const TileDesc* __restrict__ td,
     TileDesc* __restrict__ td2, uint64_t* __restrict__ starts, uint64_t* __restrict__ tloc,
     uint64_t* __restrict__ bsum, uint64_t* __restrict__ bpre, uint64_t cap_rows,
-    uint64_t cap_children, DevStatus* __restrict__ st) {
+    uint64_t cap_children, uint64_t cap_ctl, bool ctl_ok, DevStatus* __restrict__ st) {
     __shared__ __attribute__((aligned(16))) CountLds lds[TPB / 64];
     __shared__ uint64_t scan_tmp[TPB / 64];
     __shared__ uint32_t is_last;
@@ -755,15 +423,17 @@ __global__ __launch_bounds__(TPB) void nxg_fmx_resolve_kernel(
     const uint64_t tl = (uint64_t)blockIdx.x * TPB + threadIdx.x;
     TileDesc d{FAIL, FAIL, 0, 0};
     bool mis = false;
+    // the exit the chain leaves the wave's previous tile at (lane 0; FAIL: unknown)
+    const uint32_t px0 = lane == 0 && tl > 0 && tl < nt ? exit_before(td, tl) : FAIL;
     if (tl < nt) {
         d = td[tl];
         if (tl > 0) {
             // (a failed predecessor fails the frame in the emit pass's chain check)
-            const uint32_t px = td[tl - 1].exit;
+            const uint32_t px = lane == 0 ? px0 : td[tl - 1].exit;
             mis = px != FAIL && px - TILE != d.entry;
         }
     }
-    uint64_t m = __ballot(mis);
+    const uint64_t m = __ballot(mis);
 #if NXG_FMX_PROF
     if (lane == 0 && m) {
         atomicAdd(&st->diag[5], (unsigned long long)__popcll(m));
@@ -771,57 +441,80 @@ __global__ __launch_bounds__(TPB) void nxg_fmx_resolve_kernel(
     }
 #endif
     uint8_t* img = lds[w].img;
+    if (m) {
+        // in tile order from the first mismatch: a tile is recounted when its entry is not its
+        // predecessor's exit as it stands after the predecessor's own recount (a long message
+        // that covers whole tiles moves the exits of the tiles after it)
+        const uint32_t j0 = (uint32_t)__builtin_ctzll(m);
+        const uint64_t tw = tl - lane;  // the wave's first tile
 #pragma unroll 1
-    while (m) {
-        const uint32_t j = (uint32_t)__builtin_ctzll(m);
-        m &= m - 1;
-        const uint64_t t = tl - lane + j;
-        const uint32_t px = td[t - 1].exit;
-        const uint64_t t0 = t * TILE;
-        const uint32_t lim = (uint32_t)min<uint64_t>(TILE, W - t0);
-        TileRegs g;
-        tile_load(g, wire, t0, W, lane);
-        tile_store(img, g, lane);
-        const Cands cd = lane_cands(img, lane, lim);
-        uint64_t bits;
-        const TileDesc r = count_from(img, cd, px - TILE, lim, t + 1 == nt, lane, bits);
-        starts[t * 64 + lane] = bits;
-        if (lane == j) d = r;
+        for (uint32_t j = j0; j < 64 && tw + j < nt; j++) {
+            const uint64_t t = tw + j;
+            const uint32_t px = j == 0 ? (uint32_t)__builtin_amdgcn_readfirstlane((int)px0)
+                                       : (uint32_t)__builtin_amdgcn_readlane((int)d.exit, (int)(j - 1));
+            const uint32_t ej = (uint32_t)__builtin_amdgcn_readlane((int)d.entry, (int)j);
+            if (px == FAIL || px - TILE == ej) continue;
+            const uint64_t t0 = t * TILE;
+            const uint32_t lim = (uint32_t)min<uint64_t>(TILE, W - t0);
+            TileRegs g;
+            tile_load(g, wire, t0, W, lane);
+            tile_store(img, g, lane);
+            const Cands cd = lane_cands(img, lane, lim);
+            uint64_t bits;
+            const TileDesc r = count_from(img, cd, px - TILE, lim, t + 1 == nt, lane, bits);
+            starts[t * 64 + lane] = bits;
+            if (lane == j) d = r;
+        }
     }
     if (tl < nt) td2[tl] = d;
-    const uint64_t v = tl < nt ? (uint64_t)d.rows | ((uint64_t)d.kids << 32) : 0ull;
-    uint64_t tot;
+    // two scans: (Updates | child slots << 32) and Heartbeats
+    const uint64_t v = tl < nt ? (uint64_t)(d.rows & 0xffffu) | ((uint64_t)d.kids << 32) : 0ull;
+    const uint64_t vh = tl < nt ? (uint64_t)(d.rows >> 16) : 0ull;
+    uint64_t tot, toth;
     const uint64_t ex = block_excl_scan<uint64_t, TPB>(v, scan_tmp, &tot);
-    if (tl < nt) tloc[tl] = ex;
-    // the block sum goes out with an agent-scope store and is drained before the arrival count
+    const uint64_t exh = block_excl_scan<uint64_t, TPB>(vh, scan_tmp, &toth);
+    if (tl < nt) {
+        tloc[2 * tl] = ex;
+        tloc[2 * tl + 1] = exh;
+    }
+    // the block sums go out with agent-scope stores and are drained before the arrival count
     // (an agent-scope fence would write back the XCD's L2, full of the count pass's output);
     // the last block reads the sums with agent-scope loads
     if (threadIdx.x == 0) {
-        st_agent(&bsum[blockIdx.x], tot);
+        st_agent(&bsum[2 * blockIdx.x], tot);
+        st_agent(&bsum[2 * blockIdx.x + 1], toth);
         drain_stores();
         is_last = atomicAdd(&st->diag[7], 1ull) == (unsigned long long)gridDim.x - 1;
     }
     __syncthreads();
     if (!is_last) return;
     const uint32_t nb = gridDim.x;
-    uint64_t run = 0;
+    uint64_t run = 0, runh = 0;
 #pragma unroll 1
     for (uint32_t b0 = 0; b0 < nb; b0 += TPB) {
         const uint32_t b = b0 + threadIdx.x;
-        const uint64_t x = b < nb ? ld_agent(&bsum[b]) : 0ull;
-        uint64_t t2;
+        const uint64_t x = b < nb ? ld_agent(&bsum[2 * b]) : 0ull;
+        const uint64_t xh = b < nb ? ld_agent(&bsum[2 * b + 1]) : 0ull;
+        uint64_t t2, t2h;
         const uint64_t e2 = block_excl_scan<uint64_t, TPB>(x, scan_tmp, &t2);
-        if (b < nb) bpre[b] = run + e2;
+        const uint64_t e2h = block_excl_scan<uint64_t, TPB>(xh, scan_tmp, &t2h);
+        if (b < nb) {
+            bpre[2 * b] = run + e2;
+            bpre[2 * b + 1] = runh + e2h;
+        }
         run += t2;
+        runh += t2h;
     }
     if (threadIdx.x == 0) {
         const uint64_t nr = run & 0xffffffffull, nc = run >> 32;
         // columns too small: the general decoder reports the capacity error
-        if (nr > cap_rows || nc > cap_children) {
+        if (nr > cap_rows || nc > cap_children || runh > cap_ctl || (runh && !ctl_ok)) {
             atomicOr(&st->fast_fail, 1u);
         } else {
             st->n_rows = nr;
             st->n_children = nc;
+            st->n_ctl = runh;
+            st->n_heartbeat = runh;
             st->path = 4;  // the fast mixed decoder (mixed layout)
         }
     }
@@ -836,7 +529,7 @@ __global__ __launch_bounds__(TPB) void nxg_fmx_resolve_kernel(
 __global__ __launch_bounds__(TPB) void nxg_fmx_emit_kernel(
     const uint8_t* __restrict__ wire, uint64_t W, uint64_t nt, const TileDesc* __restrict__ td,
     const uint64_t* __restrict__ tloc, const uint64_t* __restrict__ bpre,
-    const uint64_t* __restrict__ starts, ColsDesc cols, DevStatus* __restrict__ st) {
+    const uint64_t* __restrict__ starts, ColsDesc cols, bool ctl_on, DevStatus* __restrict__ st) {
     __shared__ __attribute__((aligned(16))) EmitLds lds[TPB / 64];
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const uint64_t t = (uint64_t)blockIdx.x * (TPB / 64) + w;
@@ -859,10 +552,14 @@ __global__ __launch_bounds__(TPB) void nxg_fmx_emit_kernel(
     // the chain: this tile is entered at its predecessor's exit (tile 0 at 0); the count pass
     // made the last tile end exactly at W
     const uint32_t px = t ? td[t - 1].exit : TILE;
-    const uint64_t base = bpre[t / TPB] + tloc[t];
-    const uint32_t nm = d.rows;
-    const uint64_t rb = base & 0xffffffffull;
+    const uint64_t base = bpre[2 * (t / TPB)] + tloc[2 * t];
+    uint64_t hnext = bpre[2 * (t / TPB) + 1] + tloc[2 * t + 1];  // next ctl slot (Heartbeats)
+    const uint32_t nm = (d.rows & 0xffffu) + (d.rows >> 16);    // Updates + Heartbeats
+    uint64_t rnext = base & 0xffffffffull;  // next row
     uint64_t cnext = base >> 32;  // first child slot of this round's messages
+    // message ends past this tile offset lie past the frame (long text is checked from global
+    // memory where it leaves the image)
+    const uint32_t fend = (uint32_t)min<uint64_t>(W - t0, 0xffffffffull);
     if (ld_agent32(&st->fast_fail)) return;
     tile_store(img, g, lane);
     // the message list in wire order
@@ -882,12 +579,30 @@ __global__ __launch_bounds__(TPB) void nxg_fmx_emit_kernel(
     for (uint32_t k = 0; k < nm && !bad; k += 64) {
         const uint32_t i = k + lane;
         const bool has = i < nm;
-        const uint32_t p = has ? msg[i] : 0u;
-        // header: length, Update variant (both checked by the count pass), id varint (at most
-        // 5 bytes: the count pass), value tag, then the 12 bytes after the tag
+        const uint32_t p0 = has ? msg[i] : 0u;
+        // a Heartbeat (02 05, checked by the count pass): a control span before the next row
+        const uint32_t c0 = img[p0];
+        const bool ishb = has && c0 == 2u;
+        const bool upd = has && !ishb;
+        const uint64_t hm = __ballot(ishb);
+        const uint32_t hbefore = __builtin_amdgcn_mbcnt_hi((uint32_t)(hm >> 32),
+                                                           __builtin_amdgcn_mbcnt_lo((uint32_t)hm, 0u));
+        const uint64_t row = rnext + (lane - hbefore);  // Updates before this lane in the round
+        if (ishb && ctl_on) {
+            const uint64_t c = hnext + hbefore;
+            cols.ctl_row[c] = row;
+            cols.ctl_off[c] = t0 + p0;
+            cols.ctl_len[c] = 2u;
+            cols.ctl_variant[c] = 5u;
+        }
+        // header: length (one or two bytes), Update variant (both checked by the count pass), id
+        // varint (at most 5 bytes: the count pass), value tag, then the 12 bytes after the tag;
+        // read from p, the last length byte
+        const uint32_t nbp = c0 < 0x80u ? 1u : 2u;
+        const uint32_t p = p0 + nbp - 1u;
         uint32_t h[5];
         win_words<5>(limg, p, h);
-        const uint32_t lim = p + (h[0] & 0xffu);
+        const uint32_t lim = p0 + (nbp == 1u ? c0 : (c0 & 0x7fu) | ((h[0] & 0xffu) << 7));
         const uint32_t a = alignbyte(h[1], h[0], 2), b = alignbyte(h[2], h[1], 2);  // bytes 2..9
         const uint32_t sa = ~a & 0x80808080u;
         const uint32_t nb = sa ? ((uint32_t)__builtin_ctz(sa) >> 3) + 1 : 5u;
@@ -899,16 +614,18 @@ __global__ __launch_bounds__(TPB) void nxg_fmx_emit_kernel(
         const uint32_t g0 = up ? h[2] : h[1], g1 = up ? h[3] : h[2], g2 = up ? h[4] : h[3],
                        g3 = up ? 0u : h[4];
         const uint32_t su = u & 3u;
-        FV o = val_decode(tg, alignbyte(g1, g0, su), alignbyte(g2, g1, su),
-                          alignbyte(g3, g2, su), p + u, lim, true, t0);
+        FV o = val_decode(upd ? tg : 1u, alignbyte(g1, g0, su), alignbyte(g2, g1, su),
+                          alignbyte(g3, g2, su), p + u, upd ? lim : p + u + 12u, true, t0);
         if (NXG_FMX_SKIP & 4) o = FV{g0, tg, g1, lim, 0, 0, 0, true};
-        bool ok = !has || ((sa != 0u || !(b & 0x80u)) && u <= (lim - p) && lim <= wend && o.ok);
+        // past the image: text only (the count pass), checked here from global memory
+        const bool far = upd && lim > wend;
+        bool ok = !upd || ((sa != 0u || !(b & 0x80u)) && u <= (lim - p) && lim <= fend && o.ok);
+        if (far && ok && o.slen) ok = utf8_ok(GlbSrc{(gbl_bytes)wire}, t0 + o.soff, o.slen);
         PMARK(1);
-        // text: the lanes with non-ASCII bytes are checked by the whole wave
         // text: checked once per tile (text_flush) from a list in `el`
         bad = __any(!ok);
         if (!bad && !(NXG_FMX_SKIP & 2)) {
-            const bool tx = has && o.slen;
+            const bool tx = upd && !far && o.slen;
             const uint64_t tm = __ballot(tx);
             const uint32_t tn = (uint32_t)__popcll(tm);
             if (ntxt + tn > MAXC) {
@@ -921,12 +638,16 @@ __global__ __launch_bounds__(TPB) void nxg_fmx_emit_kernel(
         }
         PMARK(2);
         if (bad) break;
-        const uint32_t kd = has ? o.kids : 0u;
+        const uint32_t kd = upd ? o.kids : 0u;
         const uint32_t kinc = wave_incl_scan<uint32_t>(kd);
         const uint32_t kpre = kinc - kd;
         const uint32_t rk = wave_last<uint32_t>(kinc);
-        if (has && !(NXG_FMX_SKIP & 8)) {
-            const uint64_t row = rb + i;
+        {
+            const uint32_t nh = (uint32_t)__popcll(hm);
+            rnext += min(nm - k, 64u) - nh;
+            hnext += nh;
+        }
+        if (upd && !(NXG_FMX_SKIP & 8)) {
             cols.id[row] = id;
             cols.tag[row] = (uint8_t)o.tag;
             cols.fixed[row] = o.tag == 19u ? cnext + kpre : o.fixed;
@@ -937,170 +658,9 @@ __global__ __launch_bounds__(TPB) void nxg_fmx_emit_kernel(
             cnext += rk;
             continue;
         }
-        // array elements (non-containers)
-        // Array elements (non-containers). Stride path: an array whose first element has a fixed
-        // size is taken to be all elements of that size; element j of the round is found from
-        // its array (a max-scan over `mark`) and checked by its own tag. Any array that does not
-        // fit (a variable-size element) sends the round to the exact walk below.
-        bool strided = false;
-        if (rk <= MAXC) {
-            const uint32_t ep = o.end;
-            const uint32_t f1a = kd && ep < lim ? fixed_size1(img[ep]) : 0u;
-#if NXG_FMX_PROF
-#endif
-            if (!__any(kd && f1a == 0u)) {
-                uint8_t* mark = lds[w].mark;
-                reinterpret_cast<uint32_t*>(mark)[lane] = 0u;
-                wave_lds_order();
-                if (kd) mark[kpre] = (uint8_t)(lane + 1);
-                wave_lds_order();
-                strided = true;
-                uint32_t carry = 0;
-#pragma unroll 1
-                for (uint32_t j0 = 0; j0 < rk; j0 += 64) {
-                    const uint32_t j = j0 + lane;
-                    const bool he = j < rk;
-                    const uint32_t a1 = max(wave_max_scan(he ? (uint32_t)mark[j] : 0u), carry);
-                    carry = wave_last<uint32_t>(a1);
-                    const int ai = (int)a1 - 1;  // mark[0] is set: the first array's kpre is 0
-                    // (ds_bpermute reads 0 from inactive lanes: all 64 take part)
-                    const uint32_t fa = (uint32_t)__shfl((int)f1a, ai, 64);
-                    const uint32_t epa = (uint32_t)__shfl((int)ep, ai, 64);
-                    const uint32_t kpa = (uint32_t)__shfl((int)kpre, ai, 64);
-                    const uint32_t lma = (uint32_t)__shfl((int)lim, ai, 64);
-                    const uint32_t e0 = he ? epa + (j - kpa) * fa : 8u;
-                    const uint32_t elim = he ? lma : 16u;
-                    uint32_t q[4];
-                    win_words<4>(limg, e0, q);
-                    const uint32_t et = q[0] & 0xffu;
-                    if (!__all(!he || (e0 < elim && fixed_size1(et) == fa))) {
-                        strided = false;
-                        break;
-                    }
-                    FV e;
-                    if (__all(!he || simple_fixed(et))) {  // scalars only: no text, no branches
-                        e = fixed_elem(q, e0, elim);
-                        bad = __any(he && !e.ok);
-                    } else {  // DateTime / Duration elements
-                        e = val_decode(et, alignbyte(q[1], q[0], 1), alignbyte(q[2], q[1], 1),
-                                       alignbyte(q[3], q[2], 1), e0 + 1, elim, false, t0);
-                        bad = __any(he && !e.ok);
-                    }
-                    if (bad) break;
-                    const uint64_t slot = cnext + j;
-                    if (he && slot < cols.cap_children) {
-                        cols.ctag[slot] = (uint8_t)e.tag;
-                        cols.cfixed[slot] = e.fixed;
-                        cols.caux[slot] = e.aux;
-                    }
-                }
-                wave_lds_order();
-                if (bad) break;
-            }
-        }
-        PMARK(4);
-#if NXG_FMX_PROF
-        _acc[7] += strided;
-#endif
-        if (!strided && ntxt) {  // the exact walk below uses el
-            bad = !text_flush(limg, el, ntxt, lds[w].mark, lane, st);
-            ntxt = 0;
-            wave_lds_order();
-            if (bad) break;
-        }
-        if (strided) {
-        } else if (rk <= MAXC) {
-            // element starts: a run of elements of the first one's fixed size is confirmed 8 at
-            // a time from tags loaded together; other elements are sized by val_decode
-            uint32_t ep = o.end;
-#pragma unroll 1
-            for (uint32_t c = 0; c < kd;) {
-                if (ep >= lim) {
-                    ok = false;
-                    break;
-                }
-                const uint32_t et = img[ep];
-                const uint32_t f1 = fixed_size1(et);  // 1 + payload bytes (0: variable size)
-                if (f1) {
-                    uint32_t tg[8];
-#pragma unroll
-                    for (uint32_t r = 1; r < 8; r++) {
-                        const uint32_t x = ep + r * f1;
-                        tg[r] = c + r < kd && x < lim ? img[x] : 0xffu;
-                    }
-                    uint32_t r = 1;
-#pragma unroll
-                    for (uint32_t k = 1; k < 8; k++) r += (r == k && fixed_size1(tg[k]) == f1) ? 1u : 0u;
-#pragma unroll 1
-                    for (uint32_t k = 0; k < r; k++) {
-                        const uint32_t x = ep + k * f1;
-                        el[kpre + c + k] = x | ((lim - x) << 13);
-                    }
-                    ep += r * f1;
-                    c += r;
-                } else {
-                    el[kpre + c] = ep | ((lim - ep) << 13);
-                    uint32_t q[3];
-                    win_words<3>(limg, ep + 1, q);
-                    const FV e = val_decode(et, q[0], q[1], q[2], ep + 1, lim, false, t0);
-                    ok = e.ok;
-                    ep = e.end;
-                    c++;
-                    if (!ok) break;
-                }
-            }
-            bad = __any(!ok);
-            if (bad) break;
-            wave_lds_order();
-#pragma unroll 1
-            for (uint32_t j0 = 0; j0 < rk; j0 += 64) {
-                const uint32_t j = j0 + lane;
-                const bool he = j < rk;
-                const uint32_t ev = he ? el[j] : (8u << 13) | 8u;
-                const uint32_t e0 = ev & 0x1fffu, elim = e0 + (ev >> 13);
-                uint32_t q[4];
-                win_words<4>(limg, e0, q);
-                FV e;
-                if (__all(!he || simple_fixed(q[0] & 0xffu))) {  // scalars only: no text, no branches
-                    e = fixed_elem(q, e0, elim);
-                    bad = __any(he && !e.ok);
-                } else {
-                    e = val_decode(q[0] & 0xffu, alignbyte(q[1], q[0], 1), alignbyte(q[2], q[1], 1),
-                                   alignbyte(q[3], q[2], 1), e0 + 1, elim, false, t0);
-                    const bool eok = !he || e.ok;
-                    const bool ena = he && eok && e.slen && !ascii_ok(limg, e.soff, e.slen);
-                    bad = __any(!eok) || !utf8_packed(limg, lds[w].mark, ena, e.soff, e.slen, lane);
-                }
-                if (bad) break;
-                const uint64_t slot = cnext + j;
-                if (he && slot < cols.cap_children) {
-                    cols.ctag[slot] = (uint8_t)e.tag;
-                    cols.cfixed[slot] = e.fixed;
-                    cols.caux[slot] = e.aux;
-                }
-            }
-            wave_lds_order();
-        } else {  // more elements than the list holds: each lane decodes its own
-            uint32_t ep = o.end;
-#pragma unroll 1
-            for (uint32_t c = 0; ok && c < kd; c++) {
-                ok = ep < lim;
-                if (!ok) break;
-                const uint32_t et = img[ep];
-                uint32_t q[3];
-                win_words<3>(limg, ep + 1, q);
-                const FV e = val_decode(et, q[0], q[1], q[2], ep + 1, lim, false, t0);
-                ok = e.ok && (!e.slen || utf8_ok(LdsSrc{limg, t0}, t0 + e.soff, e.slen));
-                const uint64_t slot = cnext + kpre + c;
-                if (ok && slot < cols.cap_children) {
-                    cols.ctag[slot] = (uint8_t)e.tag;
-                    cols.cfixed[slot] = e.fixed;
-                    cols.caux[slot] = e.aux;
-                }
-                ep = e.end;
-            }
-            bad = __any(!ok);
-        }
+        bad = round_elements(img, lds[w].mark, el, kd, kpre, rk, o.end, lim, cnext, cols, t0, lane,
+                             ntxt, st);
+        if (bad) break;
         PMARK(5);
         cnext += rk;
     }
@@ -1123,9 +683,9 @@ uint64_t nxg_fmx_tiles(uint64_t W) { return (W + TILE - 1) / TILE; }
 
 uint64_t nxg_fmx_scratch_bytes(uint64_t W) {
     const uint64_t nt = nxg_fmx_tiles(W);
-    // 2 descs 32 B, message starts 512 B, tloc 8 B per tile; bsum + bpre 16 B per 256 tiles;
+    // 2 descs 32 B, message starts 512 B, tloc 16 B per tile; bsum + bpre 32 B per 256 tiles;
     // alignment
-    return nt * 552 + 16 * (nt / TPB + 1) + 6 * 16;
+    return nt * 560 + 32 * (nt / TPB + 1) + 6 * 16;
 }
 
 // persistent grids: every workgroup co-resident (count: [0], emit: [1])
@@ -1153,10 +713,10 @@ hipError_t nxg_launch_dec_fmx(const uint8_t* wire, uint64_t W, const ColsDesc& c
     TileDesc* td = reinterpret_cast<TileDesc*>(take(16 * nt));
     TileDesc* td2 = reinterpret_cast<TileDesc*>(take(16 * nt));
     uint64_t* starts = reinterpret_cast<uint64_t*>(take(512 * nt));
-    uint64_t* tloc = reinterpret_cast<uint64_t*>(take(8 * nt));
+    uint64_t* tloc = reinterpret_cast<uint64_t*>(take(16 * nt));
     const uint64_t nb = (nt + TPB - 1) / TPB;
-    uint64_t* bsum = reinterpret_cast<uint64_t*>(take(8 * nb));
-    uint64_t* bpre = reinterpret_cast<uint64_t*>(take(8 * nb));
+    uint64_t* bsum = reinterpret_cast<uint64_t*>(take(16 * nb));
+    uint64_t* bpre = reinterpret_cast<uint64_t*>(take(16 * nb));
     constexpr uint64_t WV = TPB / 64;  // waves per workgroup
     // one tile per wave measured faster than persistent waves with the next tile prefetched
     // (count 184 vs 237 us, emit 534 vs 653 us at 10^7 records): the passes are bound by the
@@ -1165,9 +725,11 @@ hipError_t nxg_launch_dec_fmx(const uint8_t* wire, uint64_t W, const ColsDesc& c
     const uint32_t gc = (uint32_t)((nt + WV - 1) / WV);
     hipLaunchKernelGGL(nxg_fmx_count_kernel, dim3(gc), dim3(TPB), 0, s, wire, W, nt, td, starts,
                        nxg_take_zero_slot());
+    const bool ctl_on = cols.ctl_row && cols.ctl_off && cols.ctl_len && cols.ctl_variant;
     hipLaunchKernelGGL(nxg_fmx_resolve_kernel, dim3((uint32_t)nb), dim3(TPB), 0, s, wire, W, nt,
-                       td, td2, starts, tloc, bsum, bpre, cols.cap_rows, cols.cap_children, st);
+                       td, td2, starts, tloc, bsum, bpre, cols.cap_rows, cols.cap_children,
+                       cols.cap_ctl, ctl_on, st);
     hipLaunchKernelGGL(nxg_fmx_emit_kernel, dim3(gc), dim3(TPB), 0, s, wire, W, nt, td2, tloc,
-                       bpre, starts, cols, st);
+                       bpre, starts, cols, ctl_on, st);
     return hipGetLastError();
 }

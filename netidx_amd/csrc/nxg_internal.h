@@ -17,7 +17,9 @@ struct DevStatus {
     uint32_t runs_valid;   // general decode: runs on the true chain, 0 = all (resolve -> emit)
     uint64_t total_bytes;  // encode: bytes written
     uint32_t nonf64;       // general path ran into content that F64-only columns cannot hold
-    uint32_t irregular;    // f64 run decode: record lengths vary too often (=> persistent kernel)
+    // f64 run decode: bit 0 record lengths vary too often (=> the single-pass decoder), bit 1
+    // not an f64 frame (=> the mixed decoders)
+    uint32_t irregular;
     // general decode: first error as ~(offset << 8 | kind), combined with atomicMax (0 = none)
     uint64_t err_key;
     // encode: 1 + the start offset of the message that holds byte MAX_BATCH, i.e. where
@@ -194,6 +196,11 @@ struct NxgArchResult {
     int rounds;  // chain rounds run (-1: the serial fallback)
 };
 uint64_t nxg_arch_scratch_bytes(uint64_t W);
+// the fast path of archive batch decode (nxg_archive_fast.hip)
+uint64_t nxg_fa_scratch_bytes(uint64_t W);
+hipError_t nxg_launch_dec_fa(const uint8_t* buf, uint64_t W, uint32_t p0, uint64_t count,
+                             const ColsDesc& cols, uint8_t* scratch, void* hhead, DevStatus* st,
+                             hipStream_t s);
 hipError_t nxg_arch_decode(const uint8_t* buf, uint64_t W, const ColsDesc& cols, uint8_t* scratch,
                            uint32_t* cap_flag, int max_rounds, NxgArchResult* res, hipStream_t s);
 // zstd decompression of compressed archive records (nxg_zstd.hip): host-side table builders and

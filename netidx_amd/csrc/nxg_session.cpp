@@ -18,6 +18,7 @@
 // with nxg_encode_frames (MAX_BATCH cuts), copies the payload into pinned memory and writes each
 // frame behind its header. Control messages (the handshake, Subscribe, Subscribed, Heartbeat)
 // are built and parsed here on the host: they are a few bytes each.
+#include <algorithm>
 #include <arpa/inet.h>
 #include <hip/hip_runtime.h>
 #include <netinet/in.h>
@@ -161,12 +162,17 @@ bool reserve(NxgSession* s, size_t need, NetidxError* err) {
     return true;
 }
 
-// read until `n` bytes are buffered from head; false on EOF or error
+// read until `n` bytes are buffered from head; false on EOF or error. The buffer grows only as
+// bytes arrive (room for at most twice what is buffered, or one receive chunk more), so a peer's
+// length field alone never allocates (pins) a large buffer -- as read_task's buffer grows with
+// what it has read (channel.rs:426-437).
 bool fill(NxgSession* s, size_t n, NetidxError* err) {
-    if (!reserve(s, n, err)) return false;
     while (s->tail - s->head < n) {
+        const size_t have = s->tail - s->head;
+        const size_t want = std::min(n, std::max(2 * have, have + kRecvChunk));
+        if (!reserve(s, want, err)) return false;
         size_t room = s->cap - s->tail;
-        if (room > kRecvChunk && s->tail - s->head + kRecvChunk >= n) room = kRecvChunk;
+        if (room > kRecvChunk && have + kRecvChunk >= n) room = kRecvChunk;
         const ssize_t k = ::recv(s->fd, s->buf + s->tail, room, 0);
         if (k < 0) {
             if (errno == EINTR) continue;

@@ -113,6 +113,32 @@ def mixed_columns(n, seed=SEED_MIXED):
     return MixedColumns(ids, tag, fixed, aux, ctag, cfixed.astype(np.uint64), caux, heap)
 
 
+def mixed_columns_ctl(n, seed=SEED_MIXED, p_hb=0.01, p_long=0.01, long_len=200):
+    """Config 3 as a live subscriber sees it: the mixed_columns rows with about p_long of the
+    scalar rows turned into long_len-byte strings (two-byte length prefixes; every eighth holds
+    multibyte code points) and about p_hb * n Heartbeats (From::Heartbeat, 02 05) between rows.
+    Returns (MixedColumns, ctl_row, ctl_off, ctl_len, ctl_variant): the control spans point at
+    one 02 05 appended to the heap."""
+    m = mixed_columns(n, seed)
+    rng = np.random.default_rng(seed + 7)
+    long_rows = np.flatnonzero((rng.random(n) < p_long) & (m.tag != 19))
+    k = len(long_rows)
+    body = rng.integers(0x61, 0x7B, (k, long_len), dtype=np.uint8)
+    body[::8, 100:103] = (0xE2, 0x82, 0xAC)  # '€'
+    base = len(m.heap)
+    m.tag[long_rows] = 12
+    m.fixed[long_rows] = (base + long_len * np.arange(k)).astype(np.uint64)
+    m.aux[long_rows] = long_len
+    hb_off = base + k * long_len
+    m.heap = np.concatenate([m.heap, body.reshape(-1), np.array([2, 5], np.uint8)])
+    nh = int(round(n * p_hb))
+    ctl_row = np.sort(rng.integers(0, n + 1, nh)).astype(np.uint64)
+    ctl_off = np.full(nh, hb_off, np.uint64)
+    ctl_len = np.full(nh, 2, np.uint32)
+    ctl_variant = np.full(nh, 5, np.uint8)
+    return m, ctl_row, ctl_off, ctl_len, ctl_variant
+
+
 SEED_ARCHIVE = 0x5EED0006
 
 

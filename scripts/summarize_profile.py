@@ -21,7 +21,12 @@ import sys
 from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-DEC = ("nxg_f64r_probe_kernel", "nxg_f64r_emit_kernel")  # one decode = both launches
+# a stream of frames (bench.py's timed region): one nxg_f64r_fused_kernel launch per decode (the
+# emit of frame j + the probe of frame j + 1); one call per frame: probe + emit (the comparison
+# leg)
+FUSED = "nxg_f64r_fused_kernel"
+DEC = (FUSED,)
+ALL = ("nxg_f64r_probe_kernel", "nxg_f64r_emit_kernel", FUSED)
 
 
 def rows(pattern):
@@ -59,7 +64,7 @@ def main():
             (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
     summary = {"records": records, "wire_bytes": bench["config"]["wire_bytes_per_gpu"],
                "bench_kernel_ms": bench["roofline"]["kernel_ms"], "kernels": {}}
-    for k in DEC:
+    for k in ALL:
         v = dur.get(k, [])
         summary["kernels"][k] = {"dispatches": len(v),
                                  "mean_us": round(sum(v) / len(v), 2) if v else None}
@@ -67,7 +72,7 @@ def main():
         d, names = per_dispatch(rows(os.path.join(out, sub, "**", "*counter_collection.csv")))
         acc = defaultdict(lambda: defaultdict(list))
         for k, cs in d.items():
-            if names[k] in DEC:
+            if names[k] in ALL:
                 for c, v in cs.items():
                     acc[names[k]][c].append(v)
         for kn, cs in acc.items():
@@ -81,7 +86,7 @@ def main():
     summary["emit_store_bytes_per_decode"] = 16 * records
     summary["decode_us_from_trace"] = round(sum(per[k]["mean_us"] or 0 for k in DEC), 2)
     json.dump(summary, open(os.path.join(prof, f"{tag}_dec_f64_profile.json"), "w"), indent=1)
-    pmc = {"records": records, "kernel": "+".join(DEC),
+    pmc = {"records": records, "kernel": FUSED,
            "hbm_bytes_per_launch": int(fetch + write),
            "read_bytes": int(fetch), "write_bytes_raw": int(write),
            "source": f"profiles/{tag}_dec_f64_profile.json (FETCH_SIZE x2 per gfx950 note)"}

@@ -136,6 +136,36 @@ def test_handshake_bytes_publisher_side():
     lst.close()
 
 
+def test_bogus_frame_length_allocates_nothing_up_front():
+    """A peer that sends a frame header claiming 1 GiB and then a few bytes before closing: the
+    receive fails with the connection closed, quickly, and the receive buffer grew only with the
+    bytes that came (read_task grows its buffer as bytes arrive, channel.rs:426-437)."""
+    import time
+    srv = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+    srv.bind(("127.0.0.1", 0))
+    srv.listen(1)
+    port = srv.getsockname()[1]
+
+    def publisher():
+        c, _ = srv.accept()
+        c.sendall(VERSION_RAW)
+        recv_exact(c, 18)
+        c.sendall(HELLO_ANON_RAW)
+        c.sendall(struct.pack(">I", 1 << 30) + b"x" * 10)
+        c.close()
+
+    t = threading.Thread(target=publisher)
+    t.start()
+    s = netidx_amd.Session.connect("127.0.0.1", port)
+    t0 = time.perf_counter()
+    with pytest.raises(netidx_amd.CodecError, match="closed"):
+        s.recv_frame()
+    assert time.perf_counter() - t0 < 5
+    t.join()
+    s.close()
+    srv.close()
+
+
 def test_control_messages():
     """From::Subscribed / Heartbeat built and parsed by the library; every byte derived from the
     derive rules (lib.rs:289-381) and Value::encode (value lib.rs:361-468)."""

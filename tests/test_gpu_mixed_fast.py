@@ -166,14 +166,14 @@ def _with(mg, n, seed, extra_at, extra):
     return mg.batch(msgs)[0]
 
 
-@pytest.mark.parametrize("case", ["heartbeat", "unsubscribed", "long_string", "map", "nested",
-                                  "error_value", "wide_id", "abstract_long"])
+@pytest.mark.parametrize("case", ["unsubscribed", "long_array", "map", "nested",
+                                  "error_value", "wide_id", "abstract_long", "huge_string"])
 def test_rejected_frames_fall_back_exactly(codec, case):
     mg = _mg()
     extra = {
-        "heartbeat": ("hb",),
         "unsubscribed": ("raw", 2, mg.enc_varint(99)),
-        "long_string": ("u", 1, (12, b"L" * 300)),
+        "long_array": ("u", 1, (19, [(9, 1)] * 20)),  # 128 bytes or more: not text
+        "huge_string": ("u", 1, (12, b"L" * 17000)),  # a three-byte length prefix
         "map": ("u", 1, (21, [((9, 1), (12, b"k"))])),
         "nested": ("u", 1, (19, [(19, [(9, 5)])])),
         "error_value": ("u", 1, (22, (9, 7))),
@@ -271,8 +271,8 @@ def _string_frame(mg, s, as_element, tag=12, n=300, seed=0):
     msgs = [("u", rng.getrandbits(20), flat_value(rng, mg)) for _ in range(n)]
     v = (19, [(9, 7), (tag, s), (6, -1)]) if as_element else (tag, s)
     msgs.insert(n // 2, ("u", 99, v))
-    # messages of 128 bytes or more are the general decoder's
-    return mg.batch(msgs)[0], len(mg.update(99, v)) < 128
+    # messages of 128 bytes or more are the general decoder's unless they hold text
+    return mg.batch(msgs)[0], len(mg.update(99, v)) < 128 or not as_element
 
 
 @pytest.mark.parametrize("as_element", [False, True])
@@ -313,3 +313,107 @@ def test_fast_utf8_invalid_sequences(as_element):
         cols, st = _decode_fresh(wire)
         assert st.err_kind == 0 and st.path == (4 if fast else 2), s
         assert_same_as_oracle(cols, st, wire)
+
+
+# ---- Heartbeats and two-byte length prefixes ---------------------------------------------------
+@pytest.mark.parametrize("case", ["first", "middle", "last", "runs", "every_other", "only"])
+def test_fast_heartbeats(codec, case):
+    """From::Heartbeat (02 05) anywhere in the frame stays on the fast path: a control span
+    (ctl_row = the next row, ctl_off, ctl_len 2, variant 5) as the oracle's."""
+    mg = _mg()
+    rng = random.Random(hash(case) & 0xffff)
+    msgs = [("u", rng.getrandbits(20), flat_value(rng, mg)) for _ in range(6000)]
+    if case == "first":
+        msgs.insert(0, ("hb",))
+    elif case == "middle":
+        msgs.insert(3000, ("hb",))
+    elif case == "last":
+        msgs.append(("hb",))
+    elif case == "runs":  # runs of up to 300 (more than a tile's worth at some tile edges)
+        for at in (10, 2000, 4000, 5999):
+            msgs[at:at] = [("hb",)] * rng.choice([1, 2, 63, 64, 65, 300])
+    elif case == "every_other":
+        msgs = [m for x in msgs[:3000] for m in (x, ("hb",))]
+    else:
+        msgs = [("hb",)] * 900  # 1800 bytes: one tile
+    wire, _ = mg.batch(msgs)
+    cols, st = gpu_decode(codec, wire, flags=hint())
+    assert st.err_kind == 0 and st.path == 4, (st.path, st.err_kind)
+    assert_same_as_oracle(cols, st, wire)
+    assert reencode(codec, cols, wire) == wire
+
+
+def test_heartbeats_past_the_tile_list_fall_back(codec):
+    """A tile of more Heartbeats than the emit pass's list holds: the general decoder."""
+    mg = _mg()
+    wire, _ = mg.batch([("u", 1, (9, 5))] + [("hb",)] * 5000 + [("u", 2, (9, 6))])
+    cols, st = gpu_decode(codec, wire, flags=hint())
+    assert st.err_kind == 0
+    assert_same_as_oracle(cols, st, wire)
+
+
+@pytest.mark.parametrize("tag", [12, 13, 18, 22])
+def test_fast_two_byte_prefix_text(codec, tag):
+    """Text values of 120 .. 16000 bytes (two-byte length prefixes), among short messages and
+    across tile edges: the fast path where a message fits the tile's image or leaves it (the
+    text then checked from global memory); longer than a tile may fall back. Columns as the
+    oracle's either way."""
+    mg = _mg()
+    rng = random.Random(tag)
+    for lens in ([120, 121, 122, 123, 124, 125, 126, 127, 128, 129, 130, 200, 255, 256, 257],
+                 [1000, 3000, 4000, 4090], [4100, 9000, 16000]):
+        msgs = []
+        for i in range(3000):
+            if rng.random() < 0.02:
+                ln = rng.choice(lens)
+                body = bytes(rng.randrange(0x61, 0x7b) for _ in range(ln))
+                if i % 3 == 0 and tag != 13:
+                    body = body[:ln // 2 - 1] + "é".encode() + body[ln // 2 + 1:]
+                v = (22, (12, body)) if tag == 22 else (tag, body)
+                msgs.append(("u", rng.getrandbits(30), v))
+            else:
+                msgs.append(("u", rng.getrandbits(14), flat_value(rng, mg)))
+        wire, _ = mg.batch(msgs)
+        cols, st = gpu_decode(codec, wire, flags=hint())
+        assert st.err_kind == 0, st.err_kind
+        if max(lens) < 4096:
+            assert st.path == 4, (lens, st.path)
+        assert_same_as_oracle(cols, st, wire)
+        if tag != 22:  # (Error(String) re-encodes in its one-tag spelling, 18)
+            assert reencode(codec, cols, wire) == wire
+
+
+@pytest.mark.parametrize("where", [5, 150, 1000, 3000, 5999])
+def test_long_text_bad_utf8_first_error(where):
+    """Invalid UTF-8 inside a long string, in the tile's image or past it: the oracle's first
+    error (the general decoder reports it)."""
+    mg = _mg()
+    rng = random.Random(where)
+    body = bytearray(b"t" * 6000)
+    body[where] = 0xC3  # a lead without its continuation
+    msgs = [("u", rng.getrandbits(14), flat_value(rng, mg)) for _ in range(400)]
+    msgs.insert(200, ("u", 77, (12, bytes(body[:max(where + 10, 130)]))))
+    wire, _ = mg.batch(msgs)
+    cols, st = _decode_fresh(wire)
+    assert st.err_kind != 0
+    assert_same_as_oracle(cols, st, wire)
+
+
+@pytest.mark.parametrize("n", [1000, 200_000])
+def test_fast_config3_with_heartbeats_and_long_strings(codec, n):
+    """Config 3 as a live subscriber sees it (synth.mixed_columns_ctl: 1 % Heartbeats, 1 % of
+    the rows 200-byte strings): on the fast path, every column as the oracle's, and the encode
+    of the same columns gives the frame back."""
+    import netidx_amd
+    import torch
+    from netidx_amd import synth
+    m, cr, co, cl, cv = synth.mixed_columns_ctl(n, 400 + n)
+    mc = netidx_amd.columns_from_arrays(m.id, m.fixed, m.tag, m.aux, m.ctag, m.cfixed, m.caux,
+                                        cr, co, cl, cv)
+    heap = torch.from_numpy(m.heap.copy()).cuda()
+    wire = codec.encode_batch(mc, heap).cpu().numpy().tobytes()
+    cols, st = gpu_decode(codec, wire, flags=hint())
+    assert st.err_kind == 0 and st.path == 4, (st.path, st.err_kind)
+    assert st.n_heartbeat == len(cr) and st.n_ctl == len(cr)
+    assert_same_as_oracle(cols, st, wire)
+    assert reencode(codec, cols, wire) == wire
