@@ -109,6 +109,7 @@ struct NxgCtx {
     void* zrecs = nullptr;
     size_t zrecs_cap = 0;
     DevStatus last{};  // last completed decode's device status (diagnostics)
+    uint64_t fa_last[8] = {};  // the last fast archive attempt's FaHead (diagnostics)
     uint64_t last_split = 0;  // last completed encode's DevStatus.split_start
 };
 
@@ -573,6 +574,12 @@ const char* nxg_version(void) { return "nxg 0.1.0 gfx950"; }
 // Not part of the ABI: the last decode's kernel diagnostics (DevStatus::diag), for profiling.
 void nxg_debug_diag(NxgCtx* c, unsigned long long out[8]) {
     for (int i = 0; i < 8; i++) out[i] = c ? c->last.diag[i] : 0;
+}
+
+// Not part of the ABI: the last fast archive attempt's FaHead (fast_fail | arrived << 32, end,
+// end_children, items, kids, recounts, decline reasons, 1 + the last declining tile).
+void nxg_debug_fa(NxgCtx* c, unsigned long long out[8]) {
+    for (int i = 0; i < 8; i++) out[i] = c ? c->fa_last[i] : 0;
 }
 
 void nxg_error_free(NetidxError* err) {
@@ -1201,7 +1208,7 @@ bool nxg_archive_decompress(NxgCtx* c, const NxgZstdDict* dict, const uint8_t* s
 // the fast archive decoder's device results (nxg_archive_fast.hip FaHead)
 struct FaHeadHost {
     uint32_t fast_fail, arrived;
-    uint64_t end, end_children, items, kids, recounts, pad[2];
+    uint64_t end, end_children, items, kids, recounts, why, why_tile;
 };
 static_assert(sizeof(FaHeadHost) == 64 && sizeof(FaHeadHost) <= sizeof(DevStatus), "FaHead");
 
@@ -1279,6 +1286,7 @@ bool nxg_decode_archive_batch(NxgCtx* c, const uint8_t* buf, uint64_t len, NxgCo
             HIPCHK(nxg_launch_dec_fa(df, W, p0, count, desc_of(out), c->dscratch, hh, nullptr,
                                      c->stream));
             HIPCHK(hipStreamSynchronize(c->stream));
+            memcpy(c->fa_last, hh, sizeof c->fa_last);
             if (!hh->fast_fail && hh->end) {
                 NxgStatus s{};
                 s.n_rows = count;

@@ -53,7 +53,8 @@ struct FaHead {
     uint64_t end_children;   // child slots of items 0 .. count - 1
     uint64_t items, kids;    // totals on the chains (diagnostics)
     uint64_t recounts;       // tiles recounted by the resolve pass (diagnostics)
-    uint64_t pad[2];
+    uint64_t why;            // emit: reasons of a decline, bits (diagnostics, nxg_debug_fa)
+    uint64_t why_tile;       // emit: 1 + the last tile that declined (diagnostics)
 };
 static_assert(sizeof(FaHead) == 64, "FaHead layout");
 
@@ -284,12 +285,15 @@ NXG_DEV FaDesc count_tile(lds_bytes img, uint64_t t, uint64_t W, uint32_t E, uin
 
 }  // namespace
 
-// The exit at which the chain leaves tile t - 1 (t >= 1), from the count pass's descriptors: the
-// last tile before t whose entry is its predecessor's exit keeps its exit; the tiles after it
-// that one long item covers entirely (their true entry past their end) pass it on; FAIL when a
-// tile on the way would need a recount (the emit pass's chain check then fails the frame).
+// The exit at which the chain leaves tile t - 1 (t >= 1), by the whole wave (uniform), from the
+// count pass's descriptors: the last tile before t whose entry is its predecessor's exit keeps
+// its exit; each tile after it passes the chain on -- a tile one long item covers entirely (its
+// true entry past its end) unchanged, a tile entered at its counted entry by its counted exit,
+// and a tile entered elsewhere (the end of a long item that covered the tiles before it) by a
+// recount from its true entry, as the wave that owns it does. FAIL: the chain breaks on the way.
 // Lets a wave's first tile see past the previous wave's recounts (long text across waves).
-NXG_DEV uint32_t exit_before(const FaDesc* td, uint64_t t) {
+NXG_DEV uint32_t exit_before(const uint8_t* __restrict__ buf, uint64_t W, const FaDesc* td,
+                             uint64_t t, uint8_t* img, uint32_t lane) {
     uint64_t k = t - 1;
 #pragma unroll 1
     for (uint32_t back = 0; k > 0 && back < 64; back++, k--) {
@@ -303,10 +307,19 @@ NXG_DEV uint32_t exit_before(const FaDesc* td, uint64_t t) {
         const uint32_t e = x - TILE;  // tile k's true entry
         if (e >= TILE) {
             x = e;  // covered: no item starts in tile k
-        } else {
-            const FaDesc a = td[k];
-            x = e == a.entry && !(a.items & BROKEN) ? a.exit : FAIL;
+            continue;
         }
+        const FaDesc a = td[k];
+        if (e == a.entry && !(a.items & BROKEN)) {
+            x = a.exit;
+            continue;
+        }
+        CountRegs g;
+        count_load(g, buf, k * TILE, W, lane);
+        count_store(img, g, lane);
+        uint64_t bits;
+        const FaDesc r = count_tile((lds_bytes)img, k, W, e, lane, bits);
+        x = (r.items & BROKEN) ? FAIL : r.exit;
     }
     return x;
 }
@@ -345,8 +358,10 @@ __global__ __launch_bounds__(TPB) void nxg_fa_resolve_kernel(
     const uint64_t tl = (uint64_t)blockIdx.x * TPB + threadIdx.x;
     FaDesc d{FAIL, FAIL, BROKEN, 0};
     bool mis = false;
-    // the exit the chain leaves the wave's previous tile at (lane 0; FAIL: unknown)
-    const uint32_t px0 = lane == 0 && tl > 0 && tl < nt ? exit_before(td, tl) : FAIL;
+    uint8_t* img = lds[w].img;
+    // the exit the chain leaves the wave's previous tile at (FAIL: unknown), by the whole wave
+    const uint64_t tw = tl - lane;  // the wave's first tile
+    const uint32_t px0 = tw > 0 && tw < nt ? exit_before(buf, W, td, tw, img, lane) : FAIL;
     if (tl < nt) {
         d = td[tl];
         if (lane == 0) {
@@ -357,20 +372,18 @@ __global__ __launch_bounds__(TPB) void nxg_fa_resolve_kernel(
         }
     }
     const uint64_t m = __ballot(mis);
-    uint8_t* img = lds[w].img;
     if (m) {
         // in tile order from the first mismatch: a tile is recounted when its entry is not its
         // predecessor's exit as it stands after the predecessor's own recount (a long item that
         // covers whole tiles moves the exits of the tiles after it)
         const uint32_t j0 = (uint32_t)__builtin_ctzll(m);
-        const uint64_t tw = tl - lane;  // the wave's first tile
         uint32_t nrc = 0;
 #pragma unroll 1
         for (uint32_t j = j0; j < 64 && tw + j < nt; j++) {
             const uint64_t t = tw + j;
             uint32_t px, pi;
             if (j == 0) {  // t >= 1: lane 0 of wave 0 never mismatches
-                px = (uint32_t)__builtin_amdgcn_readfirstlane((int)px0);
+                px = px0;
                 pi = 0;
             } else {
                 px = (uint32_t)__builtin_amdgcn_readlane((int)d.exit, (int)(j - 1));
@@ -452,14 +465,15 @@ __global__ __launch_bounds__(TPB) void nxg_fa_emit_kernel(
         const FaDesc pd = td[t - 1];
         bad |= pd.exit == FAIL || (pd.items & BROKEN) || pd.exit - TILE != d.entry;
     }
-    if (rb + items < count && ((d.items & BROKEN) || t + 1 == nt)) bad = true;
+    uint32_t why = bad ? 1u : 0u;
+    if (rb + items < count && ((d.items & BROKEN) || t + 1 == nt)) bad = true, why |= 2u;
     const uint32_t nm = (uint32_t)min<uint64_t>(items, count - rb);  // the batch's items here
     uint64_t cnext = base >> 32;
     if (ld_agent32(&hp->fast_fail)) return;
     tile_store(img, g, lane);
     const uint32_t n0 = (uint32_t)__popcll(bits);
     uint32_t at = wave_incl_scan<uint32_t>(n0) - n0;
-    bad |= wave_last<uint32_t>(at + n0) != items;
+    if (wave_last<uint32_t>(at + n0) != items) bad = true, why |= 4u;
 #pragma unroll 1
     while (bits) {
         msg[at++] = (uint16_t)(lane * CH + (uint32_t)__builtin_ctzll(bits));
@@ -497,12 +511,14 @@ __global__ __launch_bounds__(TPB) void nxg_fa_emit_kernel(
                            (!arr || o.end <= elim));
         if (far && ok && o.slen) ok = utf8_ok(GlbSrc{(gbl_bytes)buf}, t0 + o.soff, o.slen);
         bad = __any(!ok);
+        if (bad) why |= 8u | (__any(has && !o.ok) ? 16u : 0u) | (__any(far && arr) ? 32u : 0u);
         if (!bad) {
             const bool tx = has && !far && o.slen;
             const uint64_t tm = __ballot(tx);
             const uint32_t tn = (uint32_t)__popcll(tm);
             if (ntxt + tn > MAXC) {
                 bad = !text_flush(limg, el, ntxt, lds[w].mark, lane, st);
+                if (bad) why |= 64u;
                 ntxt = 0;
                 wave_lds_order();
             }
@@ -519,6 +535,7 @@ __global__ __launch_bounds__(TPB) void nxg_fa_emit_kernel(
         const uint32_t rk = wave_last<uint32_t>(kinc);
         if (cnext + rk > cols.cap_children) {  // the exact decoder reports the capacity error
             bad = true;
+            why |= 128u;
             break;
         }
         const uint64_t row = rb + i;
@@ -536,12 +553,22 @@ __global__ __launch_bounds__(TPB) void nxg_fa_emit_kernel(
         if (rk) {
             bad = round_elements(img, lds[w].mark, el, kd, kpre, rk, o.end, elim, cnext, cols, t0,
                                  lane, ntxt, st);
-            if (bad) break;
+            if (bad) {
+                why |= 256u;
+                break;
+            }
         }
         cnext += rk;
     }
-    if (!bad && ntxt) bad = !text_flush(limg, el, ntxt, lds[w].mark, lane, st);
-    if (bad && lane == 0) atomicOr(&hp->fast_fail, 1u);
+    if (!bad && ntxt) {
+        bad = !text_flush(limg, el, ntxt, lds[w].mark, lane, st);
+        if (bad) why |= 512u;
+    }
+    if (bad && lane == 0) {
+        atomicOr(&hp->fast_fail, 1u);
+        atomicOr((unsigned long long*)&hp->why, (unsigned long long)why);
+        atomicMax((unsigned long long*)&hp->why_tile, (unsigned long long)t + 1);
+    }
 }
 
 // ---- launch (host) --------------------------------------------------------------------------------

@@ -159,6 +159,9 @@ __global__ __launch_bounds__(TPB) void nxg_f64x_kernel(const uint8_t* __restrict
     bool bad = false;
     Prefetch pf;
     fetch_image(pf, wire, w0, W, lane);
+    // q: the frame position of the chain's first record start at or past the sub-tile, carried
+    // from sub-tile to sub-tile of the wave (~0: not known -- the wave's first sub-tile)
+    uint64_t q = ~0ull;
 #pragma unroll
     for (int s = 0; s < SPW; s++) {
         Sm[s] = 0;
@@ -170,25 +173,78 @@ __global__ __launch_bounds__(TPB) void nxg_f64x_kernel(const uint8_t* __restrict
         const uint64_t ib = a0 - XLO;  // frame position of image byte 0 (wraps for a0 = 0)
         const uint32_t r = XLO + lane * 64;
         const uint64_t fp = ib + r;  // frame position of the lane's chunk
+        // The chain's entry into the sub-tile: the frame start, the previous sub-tile's exit, or
+        // (the wave's first sub-tile) a walk from the merge point of the 16 bytes at a0 - 64,
+        // where the walks from every valid-looking start meet (so on the true chain, records
+        // being at most 16 bytes long), to the first start at or past a0. Lane 0 alone.
+        if (a0 == 0) {
+            q = 0;
+        } else if (q == ~0ull) {
+            uint32_t x = FAILX;
+            if (lane == 0) {
+                x = merge16i(im, 0, ib, W);
+                while (x < XLO) {
+                    uint32_t e0, e1, e2, e3;
+                    lds16i(im, x, e0, e1, e2, e3);
+                    const uint32_t L = rec_check16(e0, e1, W - (ib + x));
+                    x = L ? x + L : FAILX;
+                }
+            }
+            x = (uint32_t)__builtin_amdgcn_readfirstlane((int)x);
+            if (x == FAILX) bad = true;
+            else q = ib + x;
+        }
+        const uint64_t inc = lane == 0 && q != ~0ull && q - a0 < 64 ? 1ull << (q - a0) : 0ull;
         uint64_t S, slo, shi;
         starts_of<16>(im, r, fp, W, S, slo, shi);
-        // lane 0: the 16 positions before the sub-tile; lane 63: the 16 after it
-        const uint32_t rx = lane == 63 ? XHI : XLO - 16;
+        // lane 63: the starts among the 16 positions after the sub-tile
         uint64_t Sx, xlo, xhi;
-        starts_of<4>(im, rx, ib + rx, W, Sx, xlo, xhi);
-        const uint64_t sin = lane == 0 ? xlo >> 16 : prev64(shi);  // successors into the chunk
-        const uint64_t Snx = lane == 63 ? Sx : next64(S);         // the next chunk's starts
+        starts_of<4>(im, XHI, ib + XHI, W, Sx, xlo, xhi);
+        // False starts -- bytes inside a record that read as one (an f64's bytes may) -- are
+        // those no start leads to, or whose only predecessors are false: dropped until every
+        // start has a predecessor (in its chunk, the previous chunk, or the entry). What remains
+        // is exactly the chain through the sub-tile: each start leads back to the entry.
+        // The DPP moves run in every lane, the edge lanes' own terms OR-ed in: a DPP move in a
+        // branch reads 0 from a lane that is switched off.
+        uint64_t sin = prev64(shi) | inc;
+        for (int it = 0;; it++) {
+            const uint64_t roots = S & ~(slo | sin);
+            if (!__any(roots != 0)) break;
+            if (it == 64) {  // a long chain of false starts: the frame is rerun
+                bad = true;
+                break;
+            }
+            S &= ~roots;
+            slo = shi = 0;
+            for (uint64_t m = S; m; m &= m - 1) {
+                const uint32_t p = (uint32_t)__builtin_ctzll(m);
+                const uint32_t nx = p + im.byte(r + p);
+                if (nx < 64u) slo |= 1ull << nx;
+                else shi |= 1ull << (nx - 64u);
+            }
+            sin = prev64(shi) | inc;
+        }
+        const uint64_t Snx = next64(S) | (lane == 63 ? Sx : 0ull);  // the next chunk's starts
         const uint64_t d = W - fp;  // (fp <= W below: the frame end's bit)
         const uint64_t wlo = fp <= W && d < 64 ? 1ull << d : 0ull;
         const uint64_t whi = fp <= W && d >= 64 && d < 128 ? 1ull << (d - 64) : 0ull;
-        const uint64_t first = fp == 0 ? 1ull : 0ull;
-        bool b = (S & ~(slo | sin | first)) != 0 ||  // a start no record leads to
-                 (slo & ~(S | wlo)) != 0 ||          // a successor that is not a start
+        bool b = (slo & ~(S | wlo)) != 0 ||  // a successor that is not a start
                  (shi & ~(Snx | whi)) != 0 ||
-                 (fp == 0 && !(S & 1ull));  // the frame's first byte starts a record
+                 (inc & ~(S | wlo)) != 0;    // the entry is not a start
+#ifdef NXG_F64X_DIAG
+        if (b) nxg_f64x_diag(fp, S, slo, sin, shi, Snx, wlo, whi);
+#endif
         bad |= b;
         Sm[s] = S;
         n[s] = (uint32_t)__popcll(S);
+        // the next sub-tile's entry: lane 63's last start + its length
+        uint64_t qn = ~0ull;
+        if (lane == 63 && S) {
+            const uint32_t pl = 63u - (uint32_t)__builtin_clzll(S);
+            qn = fp + pl + im.byte(r + pl);
+        }
+        q = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)qn, 63) |
+            ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(qn >> 32), 63) << 32);
     }
     const bool wbad = __any(bad);
     if (wbad && lane == 0) atomicOr(&st->fast_fail, 1u);

@@ -382,12 +382,15 @@ __global__ __launch_bounds__(TPB) void nxg_fmx_count_kernel(const uint8_t* __res
     if (lane == 0) td[t] = d;
 }
 
-// The exit at which the chain leaves tile t - 1 (t >= 1), from the count pass's descriptors: the
-// last tile before t whose entry is its predecessor's exit keeps its exit; the tiles after it
-// that one long message covers entirely pass it on; FAIL when a tile on the way would need a
-// recount (the emit pass's chain check then fails the frame). Lets a wave's first tile see past
+// The exit at which the chain leaves tile t - 1 (t >= 1), by the whole wave (uniform), from the
+// count pass's descriptors: the last tile before t whose entry is its predecessor's exit keeps
+// its exit; each tile after it passes the chain on -- a tile one long message covers entirely
+// unchanged, a tile entered at its counted entry by its counted exit, and a tile entered
+// elsewhere (a false guess, or the end of a long message) by a recount from its true entry, as
+// the wave that owns it does. FAIL: the chain breaks on the way. Lets a wave's first tile see past
 // the previous wave's recounts.
-NXG_DEV uint32_t exit_before(const TileDesc* td, uint64_t t) {
+NXG_DEV uint32_t exit_before(const uint8_t* __restrict__ wire, uint64_t W, uint64_t nt,
+                             const TileDesc* td, uint64_t t, uint8_t* img, uint32_t lane) {
     uint64_t k = t - 1;
 #pragma unroll 1
     for (uint32_t back = 0; k > 0 && back < 64; back++, k--) {
@@ -398,8 +401,23 @@ NXG_DEV uint32_t exit_before(const TileDesc* td, uint64_t t) {
 #pragma unroll 1
     for (k = k + 1; k < t && x != FAIL; k++) {
         const uint32_t e = x - TILE;  // tile k's true entry
-        if (e >= TILE) x = e;         // covered: no message starts in tile k
-        else x = e == td[k].entry ? td[k].exit : FAIL;
+        if (e >= TILE) {
+            x = e;  // covered: no message starts in tile k
+            continue;
+        }
+        const TileDesc a = td[k];
+        if (e == a.entry) {
+            x = a.exit;
+            continue;
+        }
+        const uint64_t t0 = k * TILE;
+        const uint32_t lim = (uint32_t)min<uint64_t>(TILE, W - t0);
+        TileRegs g;
+        tile_load(g, wire, t0, W, lane);
+        tile_store(img, g, lane);
+        const Cands cd = lane_cands(img, lane, lim);
+        uint64_t bits;
+        x = count_from(img, cd, e, lim, k + 1 == nt, lane, bits).exit;
     }
     return x;
 }
@@ -423,8 +441,10 @@ __global__ __launch_bounds__(TPB) void nxg_fmx_resolve_kernel(
     const uint64_t tl = (uint64_t)blockIdx.x * TPB + threadIdx.x;
     TileDesc d{FAIL, FAIL, 0, 0};
     bool mis = false;
-    // the exit the chain leaves the wave's previous tile at (lane 0; FAIL: unknown)
-    const uint32_t px0 = lane == 0 && tl > 0 && tl < nt ? exit_before(td, tl) : FAIL;
+    uint8_t* img = lds[w].img;
+    // the exit the chain leaves the wave's previous tile at (FAIL: unknown), by the whole wave
+    const uint64_t tw = tl - lane;  // the wave's first tile
+    const uint32_t px0 = tw > 0 && tw < nt ? exit_before(wire, W, nt, td, tw, img, lane) : FAIL;
     if (tl < nt) {
         d = td[tl];
         if (tl > 0) {
@@ -440,17 +460,15 @@ __global__ __launch_bounds__(TPB) void nxg_fmx_resolve_kernel(
         atomicMax(&st->diag[4], (unsigned long long)__popcll(m));
     }
 #endif
-    uint8_t* img = lds[w].img;
     if (m) {
         // in tile order from the first mismatch: a tile is recounted when its entry is not its
         // predecessor's exit as it stands after the predecessor's own recount (a long message
         // that covers whole tiles moves the exits of the tiles after it)
         const uint32_t j0 = (uint32_t)__builtin_ctzll(m);
-        const uint64_t tw = tl - lane;  // the wave's first tile
 #pragma unroll 1
         for (uint32_t j = j0; j < 64 && tw + j < nt; j++) {
             const uint64_t t = tw + j;
-            const uint32_t px = j == 0 ? (uint32_t)__builtin_amdgcn_readfirstlane((int)px0)
+            const uint32_t px = j == 0 ? px0
                                        : (uint32_t)__builtin_amdgcn_readlane((int)d.exit, (int)(j - 1));
             const uint32_t ej = (uint32_t)__builtin_amdgcn_readlane((int)d.entry, (int)j);
             if (px == FAIL || px - TILE == ej) continue;

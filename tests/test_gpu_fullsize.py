@@ -294,6 +294,83 @@ def test_f64_single_pass_decoder_everywhere():
         c.close()
 
 
+def _false_record(L, rng):
+    """8 value bytes whose bytes 1.. read as a record of length L: `L 04 varint(L - 11 bytes) 09`
+    (L <= 14: the varint and the tag fit in the value)."""
+    nb = L - 11
+    b = [0x41, L, 0x04] + [0x80 | int(rng.integers(0, 128)) for _ in range(nb - 1)] + \
+        [int(rng.integers(1, 128)), 0x09]
+    b += [int(x) for x in rng.integers(0, 256, 8 - len(b))]
+    return np.frombuffer(bytes(b), ">u8")[0]
+
+
+def _record_lengths(ids):
+    return 11 + np.where(ids < 128, 1, np.where(ids < 1 << 14, 2, np.where(ids < 1 << 21, 3, 4)))
+
+
+def _plant_false_starts(ids, vals, frac, rng):
+    """f64 values whose bytes read as a record (`L 04 id 09 ...`, L the value's own record
+    length), so that the frame holds positions that pass every record check but are not starts.
+    Returns the planted values and the row indices."""
+    rows = np.nonzero(rng.random(len(ids)) < frac)[0]
+    lens = _record_lengths(ids)
+    vals = vals.copy()
+    for k in rows:
+        if lens[k] <= 14:
+            vals[k] = _false_record(int(lens[k]), rng)
+    return vals, rows
+
+
+@pytest.mark.parametrize("path", ["x", "auto"])
+def test_f64_false_record_starts(path):
+    """Values whose bytes look like records (a false start passes every per-record check): the
+    single-pass decoder drops the starts no record leads to and stays on path 1, bit-exact, for
+    sparse false starts (random rows, and rows at the 4 KiB sub-tile edges); a frame where every
+    value hides a false start (a false chain beside the true one through the whole frame) is still
+    decoded exactly (on whichever path the decoders settle)."""
+    import netidx_amd
+    import nxo
+    from netidx_amd import synth
+    from netidx_amd.codec import Columns
+    c = _codec_env("NXG_F64_PATH", "x") if path == "x" else netidx_amd.Codec(0)
+    rng = np.random.default_rng(97)
+    try:
+        n = 400_000
+        ids, vals = synth.f64_columns(n, 98)
+        ids = rng.permutation(ids)
+        for frac in (0.001, 0.02):
+            v2, rows = _plant_false_starts(ids, vals, frac, rng)
+            assert len(rows) > 100
+            wire = nxo.encode_f64(ids, v2)
+            cols = Columns(n, 0, 0, netidx_amd.LAYOUT_F64, "cuda")
+            for _ in range(2):  # (auto: the second frame goes straight to the single-pass decoder)
+                _assert_f64(cols, _decode_dev(c, wire, cols), wire, n)
+        # false starts in the records that straddle each 4 KiB sub-tile edge, and their neighbours
+        lens = _record_lengths(ids)
+        starts = np.concatenate([[0], np.cumsum(lens)[:-1]])
+        edge = np.nonzero((starts // 4096) != ((starts + lens - 1) // 4096))[0]
+        near = np.unique(np.concatenate([edge, edge - 1, edge + 1]).clip(0, n - 1))
+        v3 = vals.copy()
+        for k in near:
+            if lens[k] <= 14:
+                v3[k] = _false_record(int(lens[k]), rng)
+        wire = nxo.encode_f64(ids, v3)
+        assert wire[starts[-1]] == lens[-1]
+        cols = Columns(n, 0, 0, netidx_amd.LAYOUT_F64, "cuda")
+        _assert_f64(cols, _decode_dev(c, wire, cols), wire, n)
+        # every value hides a false start: exact on any path
+        v4, _ = _plant_false_starts(ids, vals, 1.0, rng)
+        wire = nxo.encode_f64(ids, v4)
+        cols = Columns(n, 0, 0, netidx_amd.LAYOUT_F64, "cuda")
+        st = _decode_dev(c, wire, cols)
+        o = nxo.decode(wire, cap_rows=n + 1, cap_children=1, cap_ctl=1).trim()
+        g = cols.numpy()
+        assert st.err_kind == 0 and st.n_rows == n
+        assert np.array_equal(g["id"], o["id"]) and np.array_equal(g["fixed"], o["fixed"])
+    finally:
+        c.close()
+
+
 def test_f64_random_order_decodes_on_two_streams_at_once():
     """The two-stream co-residency test on a frame with ids in random order (the single-pass
     decoder: its workgroups wait only on lower-numbered ones)."""
