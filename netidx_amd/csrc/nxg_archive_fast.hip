@@ -54,7 +54,7 @@ struct FaHead {
     uint64_t items, kids;    // totals on the chains (diagnostics)
     uint64_t recounts;       // tiles recounted by the resolve pass (diagnostics)
     uint64_t why;            // emit: reasons of a decline, bits (diagnostics, nxg_debug_fa)
-    uint64_t why_tile;       // emit: 1 + the last tile that declined (diagnostics)
+    uint64_t why_tile;       // emit: the first tile that declined (diagnostics, see below)
 };
 static_assert(sizeof(FaHead) == 64, "FaHead layout");
 
@@ -350,7 +350,8 @@ __global__ __launch_bounds__(TPB) void nxg_fa_count_kernel(const uint8_t* __rest
 __global__ __launch_bounds__(TPB) void nxg_fa_resolve_kernel(
     const uint8_t* __restrict__ buf, uint64_t W, uint64_t nt, const FaDesc* __restrict__ td,
     FaDesc* __restrict__ td2, uint64_t* __restrict__ starts, uint64_t* __restrict__ tloc,
-    uint64_t* __restrict__ bsum, uint64_t* __restrict__ bpre, FaHead* __restrict__ hp) {
+    uint64_t* __restrict__ bsum, uint64_t* __restrict__ bpre, uint64_t* __restrict__ wexit,
+    FaHead* __restrict__ hp) {
     __shared__ __attribute__((aligned(16))) FaCountLds lds[TPB / 64];
     __shared__ uint64_t scan_tmp[TPB / 64];
     __shared__ uint32_t is_last;
@@ -361,7 +362,21 @@ __global__ __launch_bounds__(TPB) void nxg_fa_resolve_kernel(
     uint8_t* img = lds[w].img;
     // the exit the chain leaves the wave's previous tile at (FAIL: unknown), by the whole wave
     const uint64_t tw = tl - lane;  // the wave's first tile
-    const uint32_t px0 = tw > 0 && tw < nt ? exit_before(buf, W, td, tw, img, lane) : FAIL;
+    uint32_t px0 = tw > 0 && tw < nt ? exit_before(buf, W, td, tw, img, lane) : FAIL;
+    if (tw > 0 && tw < nt && px0 == FAIL) {
+        // no tile of the count pass to start from within 64 (a batch of long text: nearly every
+        // tile starts inside one): the previous wave's exit after its recounts, which it
+        // publishes below. Only lower-numbered waves are waited on (dispatched earlier, so
+        // resident or done); on the watchdog the emit pass's chain check fails the batch.
+        const uint64_t t_start = rt_now();
+        uint64_t v = ld_agent(&wexit[tw / 64 - 1]);
+#pragma unroll 1
+        while (!(v >> 63) && rt_now() - t_start <= kSpinTicks) {
+            __builtin_amdgcn_s_sleep(2);
+            v = ld_agent(&wexit[tw / 64 - 1]);
+        }
+        px0 = (v >> 63) && !((v >> 62) & 1ull) ? (uint32_t)v : FAIL;
+    }
     if (tl < nt) {
         d = td[tl];
         if (lane == 0) {
@@ -403,6 +418,13 @@ __global__ __launch_bounds__(TPB) void nxg_fa_resolve_kernel(
         if (lane == 0) atomicAdd((unsigned long long*)&hp->recounts, (unsigned long long)nrc);
     }
     if (tl < nt) td2[tl] = d;
+    {  // the exit the chain leaves the wave's last tile at, for the next wave (bit 62: broken)
+        const uint32_t lx = (uint32_t)__builtin_amdgcn_readlane((int)d.exit, 63);
+        const uint32_t li = (uint32_t)__builtin_amdgcn_readlane((int)d.items, 63);
+        if (lane == 0 && tw < nt)
+            st_agent(&wexit[tw / 64],
+                     (1ull << 63) | ((li & BROKEN) || lx == FAIL ? 1ull << 62 : 0ull) | lx);
+    }
     const uint64_t v = tl < nt ? (uint64_t)(d.items & ~BROKEN) | ((uint64_t)d.kids << 32) : 0ull;
     uint64_t tot;
     const uint64_t ex = block_excl_scan<uint64_t, TPB>(v, scan_tmp, &tot);
@@ -567,15 +589,18 @@ __global__ __launch_bounds__(TPB) void nxg_fa_emit_kernel(
     if (bad && lane == 0) {
         atomicOr(&hp->fast_fail, 1u);
         atomicOr((unsigned long long*)&hp->why, (unsigned long long)why);
-        atomicMax((unsigned long long*)&hp->why_tile, (unsigned long long)t + 1);
+        // the first declining tile and its reasons: ~t << 16 | why, kept by the maximum
+        atomicMax((unsigned long long*)&hp->why_tile,
+                  ((unsigned long long)(~t & 0xffffffffffffull) << 16) | (why & 0xffffu));
     }
 }
 
 // ---- launch (host) --------------------------------------------------------------------------------
 uint64_t nxg_fa_scratch_bytes(uint64_t W) {
     const uint64_t nt = (W + TILE - 1) / TILE;
-    // head 64 B; 2 descs 32 B, starts 512 B, tloc 8 B per tile; bsum + bpre 16 B per 256 tiles
-    return 64 + nt * 552 + 16 * (nt / TPB + 1) + 6 * 16;
+    // head 64 B; 2 descs 32 B, starts 512 B, tloc 8 B per tile; bsum + bpre 16 B per 256 tiles;
+    // one exit word per 64 tiles
+    return 64 + nt * 552 + 16 * (nt / TPB + 1) + 8 * (nt / 64 + 1) + 7 * 16;
 }
 
 // One pass of the fast path over buf[0, W) (W < 2^32; the batch's count and its varint's length
@@ -600,13 +625,16 @@ hipError_t nxg_launch_dec_fa(const uint8_t* buf, uint64_t W, uint32_t p0, uint64
     const uint64_t nb = (nt + TPB - 1) / TPB;
     uint64_t* bsum = reinterpret_cast<uint64_t*>(take(8 * nb));
     uint64_t* bpre = reinterpret_cast<uint64_t*>(take(8 * nb));
+    const uint64_t nwv = (nt + 63) / 64;
+    uint64_t* wexit = reinterpret_cast<uint64_t*>(take(8 * nwv));
     hipError_t e;
     if ((e = hipMemsetAsync(hp, 0, sizeof(FaHead), s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(wexit, 0, 8 * nwv, s)) != hipSuccess) return e;
     constexpr uint64_t WV = TPB / 64;
     const uint32_t gc = (uint32_t)((nt + WV - 1) / WV);
     hipLaunchKernelGGL(nxg_fa_count_kernel, dim3(gc), dim3(TPB), 0, s, buf, W, nt, p0, td, starts);
     hipLaunchKernelGGL(nxg_fa_resolve_kernel, dim3((uint32_t)nb), dim3(TPB), 0, s, buf, W, nt, td,
-                       td2, starts, tloc, bsum, bpre, hp);
+                       td2, starts, tloc, bsum, bpre, wexit, hp);
     hipLaunchKernelGGL(nxg_fa_emit_kernel, dim3(gc), dim3(TPB), 0, s, buf, W, nt, p0, count, td2,
                        tloc, bpre, starts, cols, hp, st);
     if ((e = hipGetLastError()) != hipSuccess) return e;

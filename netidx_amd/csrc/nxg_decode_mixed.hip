@@ -432,7 +432,8 @@ NXG_DEV uint32_t exit_before(const uint8_t* __restrict__ wire, uint64_t W, uint6
 __global__ __launch_bounds__(TPB) void nxg_fmx_resolve_kernel(
     const uint8_t* __restrict__ wire, uint64_t W, uint64_t nt, const TileDesc* __restrict__ td,
     TileDesc* __restrict__ td2, uint64_t* __restrict__ starts, uint64_t* __restrict__ tloc,
-    uint64_t* __restrict__ bsum, uint64_t* __restrict__ bpre, uint64_t cap_rows,
+    uint64_t* __restrict__ bsum, uint64_t* __restrict__ bpre, uint64_t* __restrict__ wexit,
+    uint64_t cap_rows,
     uint64_t cap_children, uint64_t cap_ctl, bool ctl_ok, DevStatus* __restrict__ st) {
     __shared__ __attribute__((aligned(16))) CountLds lds[TPB / 64];
     __shared__ uint64_t scan_tmp[TPB / 64];
@@ -444,7 +445,21 @@ __global__ __launch_bounds__(TPB) void nxg_fmx_resolve_kernel(
     uint8_t* img = lds[w].img;
     // the exit the chain leaves the wave's previous tile at (FAIL: unknown), by the whole wave
     const uint64_t tw = tl - lane;  // the wave's first tile
-    const uint32_t px0 = tw > 0 && tw < nt ? exit_before(wire, W, nt, td, tw, img, lane) : FAIL;
+    uint32_t px0 = tw > 0 && tw < nt ? exit_before(wire, W, nt, td, tw, img, lane) : FAIL;
+    if (tw > 0 && tw < nt && px0 == FAIL) {
+        // no tile of the count pass to start from within 64 (frames of long messages): the
+        // previous wave's exit after its recounts, which it publishes below. Only lower-numbered
+        // waves are waited on (dispatched earlier, so resident or done); on the watchdog the
+        // emit pass's chain check fails the frame.
+        const uint64_t t_start = rt_now();
+        uint64_t v = ld_agent(&wexit[tw / 64 - 1]);
+#pragma unroll 1
+        while (!(v >> 63) && rt_now() - t_start <= kSpinTicks) {
+            __builtin_amdgcn_s_sleep(2);
+            v = ld_agent(&wexit[tw / 64 - 1]);
+        }
+        px0 = (v >> 63) ? (uint32_t)v : FAIL;
+    }
     if (tl < nt) {
         d = td[tl];
         if (tl > 0) {
@@ -485,6 +500,10 @@ __global__ __launch_bounds__(TPB) void nxg_fmx_resolve_kernel(
         }
     }
     if (tl < nt) td2[tl] = d;
+    {  // the exit the chain leaves the wave's last tile at (FAIL: broken), for the next wave
+        const uint32_t lx = (uint32_t)__builtin_amdgcn_readlane((int)d.exit, 63);
+        if (lane == 0 && tw < nt) st_agent(&wexit[tw / 64], (1ull << 63) | lx);
+    }
     // two scans: (Updates | child slots << 32) and Heartbeats
     const uint64_t v = tl < nt ? (uint64_t)(d.rows & 0xffffu) | ((uint64_t)d.kids << 32) : 0ull;
     const uint64_t vh = tl < nt ? (uint64_t)(d.rows >> 16) : 0ull;
@@ -702,8 +721,8 @@ uint64_t nxg_fmx_tiles(uint64_t W) { return (W + TILE - 1) / TILE; }
 uint64_t nxg_fmx_scratch_bytes(uint64_t W) {
     const uint64_t nt = nxg_fmx_tiles(W);
     // 2 descs 32 B, message starts 512 B, tloc 16 B per tile; bsum + bpre 32 B per 256 tiles;
-    // alignment
-    return nt * 560 + 32 * (nt / TPB + 1) + 6 * 16;
+    // one exit word per 64 tiles; alignment
+    return nt * 560 + 32 * (nt / TPB + 1) + 8 * (nt / 64 + 1) + 7 * 16;
 }
 
 // persistent grids: every workgroup co-resident (count: [0], emit: [1])
@@ -735,6 +754,10 @@ hipError_t nxg_launch_dec_fmx(const uint8_t* wire, uint64_t W, const ColsDesc& c
     const uint64_t nb = (nt + TPB - 1) / TPB;
     uint64_t* bsum = reinterpret_cast<uint64_t*>(take(16 * nb));
     uint64_t* bpre = reinterpret_cast<uint64_t*>(take(16 * nb));
+    const uint64_t nwv = (nt + 63) / 64;
+    uint64_t* wexit = reinterpret_cast<uint64_t*>(take(8 * nwv));
+    hipError_t e = hipMemsetAsync(wexit, 0, 8 * nwv, s);
+    if (e != hipSuccess) return e;
     constexpr uint64_t WV = TPB / 64;  // waves per workgroup
     // one tile per wave measured faster than persistent waves with the next tile prefetched
     // (count 184 vs 237 us, emit 534 vs 653 us at 10^7 records): the passes are bound by the
@@ -745,7 +768,7 @@ hipError_t nxg_launch_dec_fmx(const uint8_t* wire, uint64_t W, const ColsDesc& c
                        nxg_take_zero_slot());
     const bool ctl_on = cols.ctl_row && cols.ctl_off && cols.ctl_len && cols.ctl_variant;
     hipLaunchKernelGGL(nxg_fmx_resolve_kernel, dim3((uint32_t)nb), dim3(TPB), 0, s, wire, W, nt,
-                       td, td2, starts, tloc, bsum, bpre, cols.cap_rows, cols.cap_children,
+                       td, td2, starts, tloc, bsum, bpre, wexit, cols.cap_rows, cols.cap_children,
                        cols.cap_ctl, ctl_on, st);
     hipLaunchKernelGGL(nxg_fmx_emit_kernel, dim3(gc), dim3(TPB), 0, s, wire, W, nt, td2, tloc,
                        bpre, starts, cols, ctl_on, st);

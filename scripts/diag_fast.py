@@ -89,10 +89,19 @@ def long_text():
         out = Columns(len(items) + 1, len(buf) + 1, 1, netidx_amd.LAYOUT_MIXED, "cuda")
         st, used = c.decode_archive(d, d.numel(), out, check=False)
         fa = (C.c_ulonglong * 8)()
-        cm.lib().nxg_debug_fa(c.ctx, fa)
+        cm.lib().nxg_debug_fa(C.c_void_p(c.ctx if isinstance(c.ctx, int) else c.ctx.value), fa)
         print(f"long_text sizes {sizes}: {len(buf)} bytes, path {st.path} err {st.err_kind}; "
               f"FaHead fast_fail {fa[0] & 0xffffffff} end {fa[1]} items {fa[3]} recounts {fa[5]} "
-              f"why {fa[6]:#x} tile {fa[7] - 1} of {(len(buf) + 4095) // 4096}", flush=True)
+              f"why {fa[6]:#x}; first declining tile {(~(fa[7] >> 16)) & 0xffffffffffff} "
+              f"(why {fa[7] & 0xffff:#x}) of {(len(buf) + 4095) // 4096}", flush=True)
+        # the items around that tile: where each item starts (host walk of the batch)
+        ft = (~(fa[7] >> 16)) & 0xffffffffffff
+        pos, lens = len(varint(len(items))), []
+        for it in items:
+            lens.append((pos, len(it)))
+            pos += len(it)
+        near = [(p, l) for p, l in lens if p + l > (ft - 1) * 4096 and p < (ft + 1) * 4096]
+        print("  items near it (start, len):", [(p - ft * 4096, l) for p, l in near][:40])
         c.close()
 
 

@@ -384,6 +384,28 @@ def test_fast_two_byte_prefix_text(codec, tag):
             assert reencode(codec, cols, wire) == wire
 
 
+@pytest.mark.parametrize("share", [0.3, 1.0])
+def test_fast_text_heavy_frames(codec, share):
+    """Frames whose bytes are nearly all long text (a third, or every message, 1000 .. 16000
+    bytes): almost every 4 KiB tile starts inside a message, so no tile of the count pass can
+    anchor a wave's first tile; each wave takes the chain's exit from the wave before it. Still
+    the fast path, every column as the oracle's."""
+    mg = _mg()
+    rng = random.Random(int(share * 10))
+    msgs = []
+    for i in range(6000 if share < 1 else 3000):
+        if rng.random() < share:
+            body = bytes(rng.randrange(0x61, 0x7b) for _ in range(rng.randrange(1000, 16000)))
+            msgs.append(("u", rng.getrandbits(30), (12, body)))
+        else:
+            msgs.append(("u", rng.getrandbits(14), flat_value(rng, mg)))
+    wire, _ = mg.batch(msgs)
+    assert len(wire) > 200 * 64 * 1024 // 16  # many waves of 64 tiles
+    cols, st = gpu_decode(codec, wire, flags=hint())
+    assert st.err_kind == 0 and st.path == 4, (st.path, st.err_kind)
+    assert_same_as_oracle(cols, st, wire)
+
+
 @pytest.mark.parametrize("where", [5, 150, 1000, 3000, 5999])
 def test_long_text_bad_utf8_first_error(where):
     """Invalid UTF-8 inside a long string, in the tile's image or past it: the oracle's first
