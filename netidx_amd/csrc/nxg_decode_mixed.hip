@@ -39,6 +39,9 @@
 
 #include "nxg_fmx_common.h"
 
+#ifndef NXG_FMX_CAND
+#define NXG_FMX_CAND 7  // candidate rules (A/B timing only): 1 one-byte prefix, 2 Heartbeat, 4 two-byte
+#endif
 #ifndef NXG_FMX_SKIP
 #define NXG_FMX_SKIP 0  // timing experiments only: 1 elements, 2 text, 4 row values, 8 row stores
 #endif
@@ -73,15 +76,19 @@ struct EmitLds {
 };
 
 // candidate message starts in the lane's chunk: bit i = byte c+i starts an Update with a one-byte
-// prefix (a byte in [4, 127], then 4), a Heartbeat (02 05), or an Update with a two-byte prefix
-// (a byte >= 0x80, a byte in [1, 127], then 4)
+// prefix (a byte in [4, 127], then 4) or a Heartbeat (02 05): the return value; or an Update with
+// a two-byte prefix (a byte >= 0x80, a byte in [1, 127], then 4): `two`. The two-byte pattern is
+// common inside ordinary messages (a two-byte id followed by value tag 4), so those candidates
+// only ever continue a chain (chunk walks); the chunk's first two candidates, the tile's entry
+// guesses and the chain scan use the one-byte ones (a chain through a long message is walked).
 // The lanes' chunks are 64 bytes (16 banks) apart, so lane j reads its words in the order
 // k + j / 2 (mod 16): at each step the 32 lanes of a half-wave read 32 different banks
 // (ds_read_b32: bank = dword address mod 32), where the plain order put 16 lanes on one bank.
-NXG_DEV uint64_t cand_mask(const uint8_t* img, uint32_t c) {
+NXG_DEV uint64_t cand_mask(const uint8_t* img, uint32_t c, uint64_t& two) {
     const uint32_t* w = reinterpret_cast<const uint32_t*>(img + c);
     const uint32_t rot = (c >> 7) & 15u;  // (c / 64) / 2
     uint64_t m = 0;
+    two = 0;
 #pragma unroll
     for (int k = 0; k < 16; k++) {
         const uint32_t kk = ((uint32_t)k + rot) & 15u;
@@ -90,8 +97,10 @@ NXG_DEV uint64_t cand_mask(const uint8_t* img, uint32_t c) {
         const uint32_t len = ((a & 0x7f7f7f7fu) + 0x7c7c7c7cu) & ~a & 0x80808080u;
         const uint32_t var = zero_bytes(a1 ^ 0x04040404u);
         const uint32_t hb = zero_bytes(a ^ 0x02020202u) & zero_bytes(a1 ^ 0x05050505u);
-        const uint32_t two = a & ~a1 & ~zero_bytes(a1) & zero_bytes(a2 ^ 0x04040404u) & 0x80808080u;
-        m |= (uint64_t)nib((len & var) | hb | two) << (4 * kk);
+        const uint32_t tw = a & ~a1 & ~zero_bytes(a1) & zero_bytes(a2 ^ 0x04040404u) & 0x80808080u;
+        m |= (uint64_t)nib(((NXG_FMX_CAND & 1) ? (len & var) : 0u) | ((NXG_FMX_CAND & 2) ? hb : 0u))
+             << (4 * kk);
+        two |= (uint64_t)nib((NXG_FMX_CAND & 4) ? tw : 0u) << (4 * kk);
     }
     return m;
 }
@@ -142,16 +151,18 @@ NXG_DEV uint32_t tile_chain(const uint8_t* img, uint32_t e, uint32_t lim, uint32
     return x;
 }
 
-// per lane: the chunk's candidates and the first two's chunk exits
+// per lane: the chunk's candidates (every kind), and the first two one-byte / Heartbeat
+// candidates with their chunk exits
 struct Cands {
     uint64_t m;
     uint32_t c0, x0, c1, x1;
 };
 NXG_DEV Cands lane_cands(const uint8_t* img, uint32_t lane, uint32_t lim) {
     Cands r;
-    r.m = cand_mask(img, lane * CH);
+    uint64_t two;
+    uint64_t m = cand_mask(img, lane * CH, two);
+    r.m = m | two;
     r.c0 = r.c1 = r.x0 = r.x1 = FAIL;
-    uint64_t m = r.m;
     if (m) {
         r.c0 = lane * CH + (uint32_t)__builtin_ctzll(m);
         m &= m - 1;
@@ -342,10 +353,13 @@ NXG_DEV TileDesc count_tile(const uint8_t* img, uint64_t t, uint64_t nt, uint64_
     TileDesc d{FAIL, FAIL, 0, 0};
     bits = 0;
     if (t == 0) return count_from(img, cd, 0, lim, last, lane, bits);
-    uint64_t mm = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)cd.m, 0) |
-                  ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(cd.m >> 32), 0) << 32);
-    uint64_t m1 = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)cd.m, 1) |
-                  ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(cd.m >> 32), 1) << 32);
+    // the guesses: the first one-byte / Heartbeat candidates of chunks 0 and 1 (c0, c1)
+    const uint32_t g00 = (uint32_t)__builtin_amdgcn_readlane((int)cd.c0, 0);
+    const uint32_t g01 = (uint32_t)__builtin_amdgcn_readlane((int)cd.c1, 0);
+    const uint32_t g10 = (uint32_t)__builtin_amdgcn_readlane((int)cd.c0, 1);
+    const uint32_t g11 = (uint32_t)__builtin_amdgcn_readlane((int)cd.c1, 1);
+    uint64_t mm = (g00 != FAIL ? 1ull << g00 : 0ull) | (g01 != FAIL ? 1ull << g01 : 0ull);
+    uint64_t m1 = (g10 != FAIL ? 1ull << (g10 - CH) : 0ull) | (g11 != FAIL ? 1ull << (g11 - CH) : 0ull);
 #pragma unroll 1
     for (int tries = 0; tries < 4 && d.entry == FAIL && (mm | m1); tries++) {
         uint32_t g;
@@ -459,6 +473,7 @@ __global__ __launch_bounds__(TPB) void nxg_fmx_resolve_kernel(
             v = ld_agent(&wexit[tw / 64 - 1]);
         }
         px0 = (v >> 63) ? (uint32_t)v : FAIL;
+        if (lane == 0) atomicAdd(&st->diag[4], 1ull);  // waves that waited (diagnostics)
     }
     if (tl < nt) {
         d = td[tl];
@@ -497,6 +512,7 @@ __global__ __launch_bounds__(TPB) void nxg_fmx_resolve_kernel(
             const TileDesc r = count_from(img, cd, px - TILE, lim, t + 1 == nt, lane, bits);
             starts[t * 64 + lane] = bits;
             if (lane == j) d = r;
+            if (lane == 0) atomicAdd(&st->diag[5], 1ull);  // recounted tiles (diagnostics)
         }
     }
     if (tl < nt) td2[tl] = d;
