@@ -44,6 +44,15 @@ constexpr uint32_t MAXR = SUB / 12 + 2;  // rows per sub-tile (records start in 
 #ifndef NXG_F64X_CB
 #define NXG_F64X_CB 6
 #endif
+#ifndef NXG_F64X_OCC
+#define NXG_F64X_OCC 0  // >0: waves per SIMD asked of the register allocator (A/B)
+#endif
+#ifndef NXG_F64X_CHEAP
+#define NXG_F64X_CHEAP 1  // 0: every candidate checked as a record before it counts as a start
+#endif                    // (10^7 random-order ids: 128.6 us, against 105.6 us for 1)
+#ifndef NXG_F64X_LASTX
+#define NXG_F64X_LASTX 0  // 1: the 16 positions after a sub-tile are read only after the wave's last (A/B)
+#endif
 constexpr int CB = NXG_F64X_CB;          // candidates checked together (independent loads)
 }  // namespace f64x
 
@@ -104,6 +113,19 @@ NXG_DEV void starts_of(const SwzImg& im, uint32_t r, uint64_t fp, uint64_t W, ui
     if (fp >= W) cm = 0;
     else if (W - fp < 4u * NDW) cm &= (1ull << (W - fp)) - 1ull;
     S = slo = shi = 0;
+    if (NXG_F64X_CHEAP) {
+        // every candidate (a byte in 12..16 then 04) taken as a start, its successor from its
+        // length byte; the records are checked completely where they are decoded
+        S = cm;
+#pragma unroll 1
+        for (uint64_t m = cm; m; m &= m - 1) {
+            const uint32_t p = (uint32_t)__builtin_ctzll(m);
+            const uint32_t nx = p + im.byte(r + p);
+            if (nx < 64u) slo |= 1ull << nx;
+            else shi |= 1ull << (nx - 64u);
+        }
+        return;
+    }
     // up to CB candidates at a time: positions, then their first 8 bytes, then the checks
 #pragma unroll 1
     while (cm) {
@@ -139,7 +161,7 @@ NXG_DEV void starts_of(const SwzImg& im, uint32_t r, uint64_t fp, uint64_t W, ui
 NXG_DEV uint64_t prev64(uint64_t v) { return dpp0_64<0x138, 0xf>(v); }
 NXG_DEV uint64_t next64(uint64_t v) { return dpp0_64<0x130, 0xf>(v); }
 
-__global__ __launch_bounds__(TPB) void nxg_f64x_kernel(const uint8_t* __restrict__ wire,
+__global__ __launch_bounds__(TPB, NXG_F64X_OCC) void nxg_f64x_kernel(const uint8_t* __restrict__ wire,
                                                        uint64_t W, uint64_t* __restrict__ oid,
                                                        uint64_t* __restrict__ oval, uint64_t cap,
                                                        uint64_t* tstat, uint32_t epoch,
@@ -197,9 +219,11 @@ __global__ __launch_bounds__(TPB) void nxg_f64x_kernel(const uint8_t* __restrict
         const uint64_t inc = lane == 0 && q != ~0ull && q - a0 < 64 ? 1ull << (q - a0) : 0ull;
         uint64_t S, slo, shi;
         starts_of<16>(im, r, fp, W, S, slo, shi);
-        // lane 63: the starts among the 16 positions after the sub-tile
-        uint64_t Sx, xlo, xhi;
-        starts_of<4>(im, XHI, ib + XHI, W, Sx, xlo, xhi);
+        // lane 63: the starts among the 16 positions after the sub-tile. Inside the wave the next
+        // sub-tile's entry check covers them (LASTX), so only the wave's last sub-tile reads them.
+        const bool need_x = !NXG_F64X_LASTX || s == SPW - 1 || a0 + SUB >= W;
+        uint64_t Sx = 0, xlo, xhi;
+        if (need_x) starts_of<4>(im, XHI, ib + XHI, W, Sx, xlo, xhi);
         // False starts -- bytes inside a record that read as one (an f64's bytes may) -- are
         // those no start leads to, or whose only predecessors are false: dropped until every
         // start has a predecessor (in its chunk, the previous chunk, or the entry). What remains
@@ -228,8 +252,9 @@ __global__ __launch_bounds__(TPB) void nxg_f64x_kernel(const uint8_t* __restrict
         const uint64_t d = W - fp;  // (fp <= W below: the frame end's bit)
         const uint64_t wlo = fp <= W && d < 64 ? 1ull << d : 0ull;
         const uint64_t whi = fp <= W && d >= 64 && d < 128 ? 1ull << (d - 64) : 0ull;
+        const uint64_t shic = need_x || lane != 63 ? shi : 0ull;
         bool b = (slo & ~(S | wlo)) != 0 ||  // a successor that is not a start
-                 (shi & ~(Snx | whi)) != 0 ||
+                 (shic & ~(Snx | whi)) != 0 ||
                  (inc & ~(S | wlo)) != 0;    // the entry is not a start
 #ifdef NXG_F64X_DIAG
         if (b) nxg_f64x_diag(fp, S, slo, sin, shi, Snx, wlo, whi);
@@ -285,7 +310,7 @@ __global__ __launch_bounds__(TPB) void nxg_f64x_kernel(const uint8_t* __restrict
     // the wave's first row: the block prefix of its lane 0
     uint64_t row0 = sh_base + ((uint64_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)excl) |
                                ((uint64_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(excl >> 32)) << 32));
-    bool over = false;
+    bool over = false, vbad = false;
 #pragma unroll
     for (int s = 0; s < SPW; s++) {
         const uint64_t a0 = w0 + (uint64_t)s * SUB;
@@ -313,6 +338,9 @@ __global__ __launch_bounds__(TPB) void nxg_f64x_kernel(const uint8_t* __restrict
         for (int i = 0; i < 6; i++) {
             if ((uint32_t)i < n[s]) {
                 uint64_t id, val;
+                if (NXG_F64X_CHEAP)
+                    vbad |= rec_check16(e[i][0], e[i][1], W - (a0 + lane * 64 + pp[i])) !=
+                            (e[i][0] & 0xffu);
                 rec_decode16(e[i][0], e[i][1], e[i][2], e[i][3], e[i][0] & 0xffu, id, val);
                 rows[w][k + i][0] = id;
                 rows[w][k + i][1] = val;
@@ -332,6 +360,7 @@ __global__ __launch_bounds__(TPB) void nxg_f64x_kernel(const uint8_t* __restrict
         row0 += nw;
     }
     if (__any(over) && lane == 0) atomicOr(&st->capacity, 1u);
+    if (__any(vbad) && lane == 0) atomicOr(&st->fast_fail, 1u);  // (CHEAP: a start not a record)
 }
 
 }  // namespace
