@@ -118,7 +118,9 @@ def time_decode(codec, wire, out, n, steps, warmup, world, stream, flags=0, stre
                 codec.sync()
 
     for _ in range(warmup):
-        enqueue(1)
+        # (a stream warms up with two frames: one frame takes the one-call path, and the stream's
+        # second descriptor array is allocated on its first use)
+        enqueue(2 if stream_of_frames else 1)
         codec.sync()
     barrier(world)
     torch.cuda.synchronize()
