@@ -370,8 +370,9 @@ __global__ __launch_bounds__(TPB) void nxg_fa_resolve_kernel(
         // resident or done); on the watchdog the emit pass's chain check fails the batch.
         const uint64_t t_start = rt_now();
         uint64_t v = ld_agent(&wexit[tw / 64 - 1]);
+        uint32_t polls = 0;
 #pragma unroll 1
-        while (!(v >> 63) && rt_now() - t_start <= kSpinTicks) {
+        while (!(v >> 63) && !spin_expired(t_start, ++polls)) {
             __builtin_amdgcn_s_sleep(2);
             v = ld_agent(&wexit[tw / 64 - 1]);
         }

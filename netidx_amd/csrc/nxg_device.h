@@ -32,6 +32,13 @@ NXG_DEV void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 // watchdog: 100 MHz s_memrealtime, bound every spin (deadlock => NXG_TIMEOUT, never a hang)
 NXG_DEV uint64_t rt_now() { return __builtin_amdgcn_s_memrealtime(); }
 constexpr uint64_t kSpinTicks = 200ull * 1000 * 1000;  // 2 s at 100 MHz
+constexpr uint32_t kSpinPolls = 1u << 20;               // ~1 s of polls at ~1 us each
+// A bounded spin ends when BOTH 2 s have passed and about 1 s of polls were made: the clock
+// alone would also count time the queue spent switched out (GPUs shared by several processes,
+// compute wave save/restore), during which the waited-for workgroup cannot make progress either.
+NXG_DEV bool spin_expired(uint64_t t_start, uint32_t polls) {
+    return polls > kSpinPolls && rt_now() - t_start > kSpinTicks;
+}
 
 NXG_DEV uint32_t vl64(uint64_t v) {
     uint32_t hb = 63u - (uint32_t)__clzll((long long)(v | 1ull));
@@ -150,6 +157,7 @@ NXG_DEV uint64_t lookback_prefix(const uint64_t* tstat, uint32_t tile, uint32_t 
     uint64_t base = 0;
     int64_t pred = (int64_t)tile - 1;
     const uint64_t t_start = rt_now();
+    uint32_t polls = 0;
     give_up = false;
     int nu = 1;  // rows of 64 words polled in this step
     while (pred >= 0) {
@@ -185,7 +193,7 @@ NXG_DEV uint64_t lookback_prefix(const uint64_t* tstat, uint32_t tile, uint32_t 
                 const int64_t idx = pred - 64 * u - (int64_t)lane;
                 if (u < nu && lb_flag(s[u], epoch) == 0) s[u] = ld_agent(&tstat[idx]);
             }
-            if ((abort && ld_agent32(abort)) || rt_now() - t_start > kSpinTicks) {
+            if ((abort && ld_agent32(abort)) || spin_expired(t_start, ++polls)) {
                 give_up = true;
                 return 0;
             }
