@@ -1208,7 +1208,7 @@ bool nxg_archive_decompress(NxgCtx* c, const NxgZstdDict* dict, const uint8_t* s
 // the fast archive decoder's device results (nxg_archive_fast.hip FaHead)
 struct FaHeadHost {
     uint32_t fast_fail, arrived;
-    uint64_t end, end_children, items, kids, recounts, why, why_tile;
+    uint64_t end, end_children, items, ticket, recounts, why, why_tile;
 };
 static_assert(sizeof(FaHeadHost) == 64 && sizeof(FaHeadHost) <= sizeof(DevStatus), "FaHead");
 

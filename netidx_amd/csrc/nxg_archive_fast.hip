@@ -51,7 +51,8 @@ struct FaHead {
     uint32_t arrived;        // resolve: blocks done
     uint64_t end;            // 1 + the end of item count - 1 (0: not seen)
     uint64_t end_children;   // child slots of items 0 .. count - 1
-    uint64_t items, kids;    // totals on the chains (diagnostics)
+    uint64_t items;          // total on the chains (diagnostics)
+    uint64_t ticket;         // resolve: blocks by ticket (next_tile)
     uint64_t recounts;       // tiles recounted by the resolve pass (diagnostics)
     uint64_t why;            // emit: reasons of a decline, bits (diagnostics, nxg_debug_fa)
     uint64_t why_tile;       // emit: the first tile that declined (diagnostics, see below)
@@ -355,8 +356,11 @@ __global__ __launch_bounds__(TPB) void nxg_fa_resolve_kernel(
     __shared__ __attribute__((aligned(16))) FaCountLds lds[TPB / 64];
     __shared__ uint64_t scan_tmp[TPB / 64];
     __shared__ uint32_t is_last;
+    __shared__ uint32_t sh_tile;
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const uint64_t tl = (uint64_t)blockIdx.x * TPB + threadIdx.x;
+    // blocks by ticket: a wave waits only on waves that are running
+    const uint32_t bid = next_tile((unsigned long long*)&hp->ticket, &sh_tile);
+    const uint64_t tl = (uint64_t)bid * TPB + threadIdx.x;
     FaDesc d{FAIL, FAIL, BROKEN, 0};
     bool mis = false;
     uint8_t* img = lds[w].img;
@@ -431,7 +435,7 @@ __global__ __launch_bounds__(TPB) void nxg_fa_resolve_kernel(
     const uint64_t ex = block_excl_scan<uint64_t, TPB>(v, scan_tmp, &tot);
     if (tl < nt) tloc[tl] = ex;
     if (threadIdx.x == 0) {
-        st_agent(&bsum[blockIdx.x], tot);
+        st_agent(&bsum[bid], tot);
         drain_stores();
         is_last = atomicAdd(&hp->arrived, 1u) == gridDim.x - 1;
     }
@@ -450,7 +454,6 @@ __global__ __launch_bounds__(TPB) void nxg_fa_resolve_kernel(
     }
     if (threadIdx.x == 0) {
         hp->items = run & 0xffffffffull;
-        hp->kids = run >> 32;
     }
 }
 

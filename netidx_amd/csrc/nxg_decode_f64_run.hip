@@ -503,11 +503,14 @@ NXG_DEV void probe_body(const ProbeArgs& a, uint32_t bid, uint8_t (*img)[IMGB],
     }
 }
 
+// The probe's workgroups take their tile groups by ticket (DevStatus.diag[6], zeroed with the
+// slot): its look-back then waits only on workgroups that are running (next_tile).
 __global__ __launch_bounds__(TPB) void nxg_f64r_probe_kernel(ProbeArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t img[TPB / 64][IMGB];
     __shared__ uint64_t scan_tmp[TPB / 64];
     __shared__ uint64_t sh_base;
-    probe_body(a, blockIdx.x, img, scan_tmp, sh_base);
+    __shared__ uint32_t sh_tile;
+    probe_body(a, next_tile(&a.st->diag[6], &sh_tile), img, scan_tmp, sh_base);
 }
 
 // ---- emit: one wave per tile ---------------------------------------------------------------------
@@ -859,8 +862,10 @@ __global__ __launch_bounds__(TPB) void nxg_f64r_fused_kernel(EmitArgs ea, ProbeA
     __shared__ __attribute__((aligned(16))) uint8_t img[TPB / 64][IMGB];
     __shared__ uint64_t scan_tmp[TPB / 64];
     __shared__ uint64_t sh_base;
+    __shared__ uint32_t sh_tile;
     if (blockIdx.x < npg) {
-        if ((uint64_t)blockIdx.x * TPB < pa.nt) probe_body(pa, blockIdx.x, img, scan_tmp, sh_base);
+        const uint32_t bid = next_tile(&pa.st->diag[6], &sh_tile);
+        if ((uint64_t)bid * TPB < pa.nt) probe_body(pa, bid, img, scan_tmp, sh_base);
         return;
     }
     emit_body(ea, blockIdx.x - npg, img);

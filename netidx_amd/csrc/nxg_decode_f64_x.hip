@@ -172,8 +172,11 @@ __global__ __launch_bounds__(TPB, NXG_F64X_OCC) void nxg_f64x_kernel(const uint8
     __shared__ __attribute__((aligned(16))) uint64_t rows[WAVES][MAXR][2];
     __shared__ uint64_t scan_tmp[WAVES];
     __shared__ uint64_t sh_base;
+    __shared__ uint32_t sh_tile;
     const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const uint64_t w0 = (uint64_t)blockIdx.x * WGB + (uint64_t)w * SUB * SPW;  // the wave's bytes
+    // this workgroup's 64 KiB, by ticket (the look-back waits only on running workgroups)
+    const uint32_t bid = next_tile(&st->diag[6], &sh_tile);
+    const uint64_t w0 = (uint64_t)bid * WGB + (uint64_t)w * SUB * SPW;  // the wave's bytes
     uint8_t* buf = img[w];
     const SwzImg im{buf};
     uint64_t Sm[SPW];
@@ -284,23 +287,23 @@ __global__ __launch_bounds__(TPB, NXG_F64X_OCC) void nxg_f64x_kernel(const uint8
     const uint64_t excl = block_excl_scan<uint64_t, TPB>((uint64_t)ntot, scan_tmp, &total);
     if (w == 0) {
         uint64_t base = 0;
-        if (blockIdx.x == 0) {
+        if (bid == 0) {
             if (lane == 0) st_agent(&tstat[0], lb_word(kFlagInc, epoch, total));
         } else {
-            if (lane == 0) st_agent(&tstat[blockIdx.x], lb_word(kFlagAgg, epoch, total));
+            if (lane == 0) st_agent(&tstat[bid], lb_word(kFlagAgg, epoch, total));
             bool give_up;
-            base = lookback_prefix<4>(tstat, blockIdx.x, epoch, nullptr, give_up);
+            base = lookback_prefix<4>(tstat, bid, epoch, nullptr, give_up);
             if (give_up) {
                 if (lane == 0) {
                     atomicOr(&st->timeout, 1u);
                     atomicOr(&st->fast_fail, 1u);
                 }
             } else if (lane == 0) {
-                st_agent(&tstat[blockIdx.x], lb_word(kFlagInc, epoch, base + total));
+                st_agent(&tstat[bid], lb_word(kFlagInc, epoch, base + total));
             }
         }
         if (lane == 0) sh_base = base;
-        if (blockIdx.x == gridDim.x - 1 && lane == 0) {
+        if (bid == gridDim.x - 1 && lane == 0) {
             st->n_rows = base + total;
             st->path = 1;
         }

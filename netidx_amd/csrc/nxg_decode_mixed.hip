@@ -452,8 +452,11 @@ __global__ __launch_bounds__(TPB) void nxg_fmx_resolve_kernel(
     __shared__ __attribute__((aligned(16))) CountLds lds[TPB / 64];
     __shared__ uint64_t scan_tmp[TPB / 64];
     __shared__ uint32_t is_last;
+    __shared__ uint32_t sh_tile;
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const uint64_t tl = (uint64_t)blockIdx.x * TPB + threadIdx.x;
+    // blocks by ticket (DevStatus.diag[6]): a wave waits only on waves that are running
+    const uint32_t bid = next_tile(&st->diag[6], &sh_tile);
+    const uint64_t tl = (uint64_t)bid * TPB + threadIdx.x;
     TileDesc d{FAIL, FAIL, 0, 0};
     bool mis = false;
     uint8_t* img = lds[w].img;
@@ -535,8 +538,8 @@ __global__ __launch_bounds__(TPB) void nxg_fmx_resolve_kernel(
     // (an agent-scope fence would write back the XCD's L2, full of the count pass's output);
     // the last block reads the sums with agent-scope loads
     if (threadIdx.x == 0) {
-        st_agent(&bsum[2 * blockIdx.x], tot);
-        st_agent(&bsum[2 * blockIdx.x + 1], toth);
+        st_agent(&bsum[2 * bid], tot);
+        st_agent(&bsum[2 * bid + 1], toth);
         drain_stores();
         is_last = atomicAdd(&st->diag[7], 1ull) == (unsigned long long)gridDim.x - 1;
     }

@@ -144,6 +144,19 @@ NXG_DEV T wave_sum(T v) {
 }
 
 // ---- decoupled look-back with a wide window ---------------------------------------------------
+// The next tile of a look-back kernel for this workgroup, handed out by an atomic ticket in the
+// order workgroups actually start. The hardware dispatches in order only per XCD: on a GPU that
+// several processes share, one XCD can fall behind, and a workgroup whose look-back waits on a
+// lower blockIdx not yet dispatched there would spin until the watchdog (seen with 2-3 processes
+// on one device). With tickets every tile waited on was taken by a running workgroup.
+// Block-wide (contains __syncthreads); `sh` is a __shared__ word.
+NXG_DEV uint32_t next_tile(unsigned long long* ticket, uint32_t* sh) {
+    __syncthreads();  // every thread has read the previous ticket
+    if (threadIdx.x == 0) *sh = (uint32_t)atomicAdd(ticket, 1ull);
+    __syncthreads();
+    return *sh;
+}
+
 // Exclusive prefix of `tile` over the epoch-tagged tile words tstat[0..tile). Called by one full
 // wave. The first poll covers the 64 nearest predecessors (lane l owns tile-1-l); when none of
 // them is inclusive yet, later polls cover 64*U predecessors at once (word tile-1-64u-l for

@@ -80,9 +80,11 @@ __global__ __launch_bounds__(TPB) void nxg_enc_f64_kernel(
     __shared__ __attribute__((aligned(16))) uint8_t stg[MAXB_ALL];
     __shared__ uint32_t scan_tmp[4];
     __shared__ uint64_t sh_base;
+    __shared__ uint32_t sh_tile;
 
     const uint32_t tid = threadIdx.x, lane = tid & 63;
-    for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    unsigned long long* tk = &st->diag[6];  // tile tickets (zeroed with the status slot)
+    for (uint32_t tile = next_tile(tk, &sh_tile); tile < ntiles; tile = next_tile(tk, &sh_tile)) {
         const uint64_t r0 = (uint64_t)tile * ETILE + (uint64_t)tid * ERPT;
         uint64_t ids[ERPT], vals[ERPT];
         if (r0 + ERPT <= n) {
