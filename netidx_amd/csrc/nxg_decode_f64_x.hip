@@ -172,10 +172,9 @@ __global__ __launch_bounds__(TPB, NXG_F64X_OCC) void nxg_f64x_kernel(const uint8
     __shared__ __attribute__((aligned(16))) uint64_t rows[WAVES][MAXR][2];
     __shared__ uint64_t scan_tmp[WAVES];
     __shared__ uint64_t sh_base;
-    __shared__ uint32_t sh_tile;
     const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    // this workgroup's 64 KiB, by ticket (the look-back waits only on running workgroups)
-    const uint32_t bid = next_tile(&st->diag[6], &sh_tile);
+    // (blockIdx order: a ticket counter measured 0.104 -> 0.120 ms at 10^7 records)
+    const uint32_t bid = blockIdx.x;
     const uint64_t w0 = (uint64_t)bid * WGB + (uint64_t)w * SUB * SPW;  // the wave's bytes
     uint8_t* buf = img[w];
     const SwzImg im{buf};

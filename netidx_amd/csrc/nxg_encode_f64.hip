@@ -70,6 +70,55 @@ NXG_DEV void put_rec_global(uint8_t* out, uint64_t o, uint64_t id, uint64_t val)
 #pragma unroll
     for (int i = 7; i >= 0; i--) out[o++] = (uint8_t)(val >> (8 * i));
 }
+// The exclusive byte prefix of `tile`, by wave 0 of its workgroup: a decoupled look-back over
+// the tiles' published byte counts (lane l polls tile pred - l) that never depends on another
+// workgroup being scheduled. A predecessor that has published nothing after kPatience polls has
+// its byte count computed here from its ids (16 KiB of reads), so the look-back always
+// progresses: dispatch is in order only per XCD, and on a GPU shared by several processes an XCD
+// can fall behind with the awaited workgroup not yet dispatched (seen with 2-3 processes on one
+// device); a ticket counter instead cost 66 us at 10^7 records (one contended atomic per tile).
+#ifndef NXG_ENC_PATIENCE
+#define NXG_ENC_PATIENCE 128  // (0 in a test build: every unpublished predecessor counted here)
+#endif
+constexpr uint32_t kPatience = NXG_ENC_PATIENCE;
+NXG_DEV uint64_t lookback_selfhelp(const uint64_t* tstat, uint32_t tile, uint32_t epoch,
+                                   const uint64_t* __restrict__ id, uint64_t n, uint32_t lane) {
+    uint64_t base = 0;
+    int64_t pred = (int64_t)tile - 1;
+#pragma unroll 1
+    while (pred >= 0) {
+        const int64_t idx = pred - (int64_t)lane;
+        uint64_t s = idx >= 0 ? ld_agent(&tstat[idx]) : lb_word(kFlagInc, epoch, 0);
+        uint32_t polls = 0;
+#pragma unroll 1
+        for (;;) {
+            const uint64_t f = lb_flag(s, epoch);
+            const uint64_t im = __ballot(f == kFlagInc);
+            const uint32_t lf = im ? (uint32_t)__builtin_ctzll(im) : 64u;
+            const uint64_t holes = __ballot(f == 0 && lane < lf);
+            if (!holes) break;  // every tile up to the nearest inclusive one has its count
+            if (++polls > kPatience) {
+                // the nearest hole's byte count, from its ids
+                const uint32_t h = (uint32_t)__builtin_ctzll(holes);
+                const uint64_t r0 = (uint64_t)(pred - (int64_t)h) * ETILE;
+                uint64_t b = 0;
+                for (uint64_t r = r0 + lane; r < r0 + ETILE && r < n; r += 64) b += rec_len(id[r]);
+                const uint64_t agg = wave_sum<uint64_t>(b);
+                if (lane == h) s = lb_word(kFlagAgg, epoch, agg);
+                polls = 0;
+                continue;
+            }
+            __builtin_amdgcn_s_sleep(1);
+            if (f == 0 && idx >= 0) s = ld_agent(&tstat[idx]);
+        }
+        const uint64_t im = __ballot(lb_flag(s, epoch) == kFlagInc);
+        const uint32_t lf = im ? (uint32_t)__builtin_ctzll(im) : 64u;
+        base += wave_sum<uint64_t>(lane <= lf ? (s & kValMask) : 0ull);
+        if (im) break;
+        pred -= 64;
+    }
+    return base;
+}
 }  // namespace
 
 __global__ __launch_bounds__(TPB) void nxg_enc_f64_kernel(
@@ -80,11 +129,9 @@ __global__ __launch_bounds__(TPB) void nxg_enc_f64_kernel(
     __shared__ __attribute__((aligned(16))) uint8_t stg[MAXB_ALL];
     __shared__ uint32_t scan_tmp[4];
     __shared__ uint64_t sh_base;
-    __shared__ uint32_t sh_tile;
 
     const uint32_t tid = threadIdx.x, lane = tid & 63;
-    unsigned long long* tk = &st->diag[6];  // tile tickets (zeroed with the status slot)
-    for (uint32_t tile = next_tile(tk, &sh_tile); tile < ntiles; tile = next_tile(tk, &sh_tile)) {
+    for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const uint64_t r0 = (uint64_t)tile * ETILE + (uint64_t)tid * ERPT;
         uint64_t ids[ERPT], vals[ERPT];
         if (r0 + ERPT <= n) {
@@ -123,9 +170,7 @@ __global__ __launch_bounds__(TPB) void nxg_enc_f64_kernel(
         if (tid < 64) {
             uint64_t base = 0;
             if (tile != 0) {
-                bool give_up;
-                base = lookback_prefix<LB_U>(tstat, tile, epoch, nullptr, give_up);
-                if (give_up && lane == 0) atomicOr(&st->timeout, 1u);
+                base = lookback_selfhelp(tstat, tile, epoch, id, n, lane);
                 if (lane == 0) st_agent(&tstat[tile], lb_word(kFlagInc, epoch, base + tbytes));
             }
             if (lane == 0) sh_base = base;

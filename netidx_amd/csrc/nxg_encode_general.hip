@@ -329,11 +329,9 @@ __global__ __launch_bounds__(TPB) void nxg_enc_rows_kernel(
     __shared__ uint32_t len_lds[GTILE];  // message length per row (0: absent or erroring)
     __shared__ uint8_t cls_lds[GTILE];   // value class per row (CLS_GEN: the general walk)
     static_assert(GSTG < 65536, "staging offsets fit 16 bits");
-    __shared__ uint32_t sh_tile;
     const uint32_t tid = threadIdx.x, lane = tid & 63;
     const uint64_t n = c.n_rows;
-    unsigned long long* tk = &st->diag[6];  // tile tickets (zeroed with the status slot)
-    for (uint32_t tile = next_tile(tk, &sh_tile); tile < ntiles; tile = next_tile(tk, &sh_tile)) {
+    for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const uint64_t rt = (uint64_t)tile * GTILE;
         const uint64_t r0 = rt + (uint64_t)tid * GRPT;
         // 1. classify by tag and bucket the rows (wave-ballot counting sort in LDS); a wave then
