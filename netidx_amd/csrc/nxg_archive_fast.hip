@@ -166,19 +166,69 @@ NXG_DEV uint32_t chunk_walk(lds_bytes img, uint32_t x, uint32_t c, uint32_t end,
     return x;
 }
 
-// The guessed exit of [c, end): the walk from c, one byte on after a failed parse. first: where
-// its last unbroken run of items starts (every item from there to the exit parsed in a row)
-NXG_DEV uint32_t spec_walk(lds_bytes img, uint32_t c, uint32_t end, uint32_t wl, uint32_t& first) {
-    uint32_t x = c;
-    first = c;
+// Where an item can start among the 64 positions from image offset c (4-aligned; the image holds
+// c + 72 bytes): bit i when bytes c+i.. read as an Id varint of 1..5 bytes followed by a byte that
+// can begin an Event (0x40, or a Value tag < 28), the first checks item_end makes. A superset of
+// the item starts, from SWAR over 18 words, so a spec walk skips the positions between candidates
+// instead of trying a parse at every byte (text and f64 bytes mostly fail the tag test).
+NXG_DEV uint64_t item_cands(lds_bytes img, uint32_t c) {
+    uint64_t T = 0, G = 0;  // T: bytes < 0x80 (varint end), G: possible Event first bytes
+    uint32_t th = 0, gh = 0;  // positions 64..71
+#pragma unroll
+    for (int k = 0; k < 18; k++) {
+        const uint32_t a = *reinterpret_cast<const __attribute__((address_space(3))) uint32_t*>(
+            img + c + 4 * k);
+        const uint32_t t = ~a & 0x80808080u;
+        const uint32_t lt28 = ~(((a & 0x7f7f7f7fu) + 0x64646464u) | a) & 0x80808080u;
+        const uint32_t g = lt28 | zero_bytes(a ^ 0x40404040u);
+        if (k < 16) {
+            T |= (uint64_t)nib(t) << (4 * k);
+            G |= (uint64_t)nib(g) << (4 * k);
+        } else {
+            th |= nib(t) << (4 * (k - 16));
+            gh |= nib(g) << (4 * (k - 16));
+        }
+    }
+    // x >> s over the 72 positions (s in 1..5)
+    auto sh = [](uint64_t lo, uint32_t hi, uint32_t s) { return (lo >> s) | ((uint64_t)hi << (64 - s)); };
+    const uint64_t C = ~T;
+    const uint64_t T1 = sh(T, th, 1), T2 = sh(T, th, 2), T3 = sh(T, th, 3), T4 = sh(T, th, 4);
+    const uint64_t C1 = ~T1, C2 = ~T2, C3 = ~T3;
+    const uint64_t G1 = sh(G, gh, 1), G2 = sh(G, gh, 2), G3 = sh(G, gh, 3), G4 = sh(G, gh, 4),
+                   G5 = sh(G, gh, 5);
+    return (T & G1) | (C & T1 & G2) | (C & C1 & T2 & G3) | (C & C1 & C2 & T3 & G4) |
+           (C & C1 & C2 & C3 & T4 & G5);
+}
+
+// The guessed exit of [x0, end): the walk from x0, on to the next candidate position
+// (item_cands: bit i = position cb + i, which skips only positions where the parse would fail)
+// after a failed parse. first: where its last unbroken run of items starts (every item from
+// there to the exit parsed in a row); rbits / rkids: that run's item starts (bit i = cb + i) and
+// child slots.
+NXG_DEV uint32_t spec_walk(lds_bytes img, uint32_t x0, uint32_t cb, uint32_t end, uint32_t wl,
+                           uint32_t& first, uint64_t cm, uint64_t& rbits, uint32_t& rkids) {
+    auto next = [&](uint32_t p) -> uint32_t {  // the first candidate at or after p
+        const uint32_t d = p - cb;
+        const uint64_t rest = d < 64 ? cm & (~0ull << d) : 0ull;
+        return rest ? cb + (uint32_t)__builtin_ctzll(rest) : end;
+    };
+    uint32_t x = next(x0);
+    first = x;
+    rbits = 0;
+    rkids = 0;
 #pragma unroll 1
     while (x < end) {
         uint32_t k;
         const uint32_t e = item_end(img, x, wl, CIMGL, k);
         if (e == FAIL) {
-            first = ++x;
+            x = next(x + 1);
+            first = x;
+            rbits = 0;
+            rkids = 0;
             continue;
         }
+        if (x - cb < 64) rbits |= 1ull << (x - cb);
+        rkids += k;
         x = e;
     }
     return x;
@@ -264,12 +314,20 @@ NXG_DEV FaDesc count_tile(lds_bytes img, uint64_t t, uint64_t W, uint32_t E, uin
     const uint32_t lim = PRE + (uint32_t)min<uint64_t>(TILE, W - t0);
     const uint32_t wl = PRE + (uint32_t)min<uint64_t>(W - t0, 0xffffffffull - PRE);
     const uint32_t c = PRE + lane * CH, end = min(c + CH, lim);
-    uint32_t first;
-    const uint32_t g = c < lim ? spec_walk(img, c, end, wl, first) : c;
+    uint32_t first, rkids = 0;
+    uint64_t rbits = 0;
+    const uint32_t g = c < lim ? spec_walk(img, c, c, end, wl, first, item_cands((lds_bytes)img, c),
+                                           rbits, rkids)
+                               : c;
     uint32_t ge = 0;
-    if (E == NONE) {  // lane 0 also walks the bytes before the tile
-        uint32_t f2;
-        ge = lane == 0 ? spec_walk(img, 0, PRE, wl, f2) : 0u;
+    if (E == NONE) {  // lane 0 also walks the bytes before the tile (two 64-byte halves)
+        uint32_t f2, k2;
+        uint64_t b2;
+        if (lane == 0) {
+            ge = spec_walk(img, 0, 0, CH, wl, f2, item_cands((lds_bytes)img, 0), b2, k2);
+            if (ge < PRE)
+                ge = spec_walk(img, ge, CH, PRE, wl, f2, item_cands((lds_bytes)img, CH), b2, k2);
+        }
         E = (uint32_t)__builtin_amdgcn_readlane((int)ge, 0);
     } else {
         E += PRE;
@@ -280,7 +338,19 @@ NXG_DEV FaDesc count_tile(lds_bytes img, uint64_t t, uint64_t W, uint32_t E, uin
     uint32_t n = 0, kids = 0, brk = FAIL;
     uint64_t bits = 0;
     uint32_t X = A;
-    if (A < end) X = chunk_walk(img, A, c, end, wl, n, kids, bits, brk);
+    if (A < end) {
+        // entered at an item of the spec walk's last unbroken run: the exact walk from there is
+        // that run (the same parses), so its counts are the run's
+        const uint32_t d = A - c;
+        if (d < 64 && ((rbits >> d) & 1ull) && (A == first || rkids == 0)) {
+            bits = rbits & (~0ull << d);
+            n = (uint32_t)__popcll(bits);
+            kids = rkids;
+            X = g;
+        } else {
+            X = chunk_walk(img, A, c, end, wl, n, kids, bits, brk);
+        }
+    }
     return chain_from(img, E, lim, wl, lane, A, X, n, kids, bits, brk, obits);
 }
 
