@@ -414,6 +414,38 @@ __global__ __launch_bounds__(TPB) void nxg_fa_count_kernel(const uint8_t* __rest
     if (lane == 0) td[t] = d;
 }
 
+#ifndef NXG_FA_FIX_PASSES
+#define NXG_FA_FIX_PASSES 2
+#endif
+// fix: one wave per tile, all tiles at once. A tile whose guessed entry is not its predecessor's
+// counted exit is recounted from that exit. A false guess almost always merges into the true
+// chain inside its tile, so the counted exits are right and these recounts are independent: done
+// here in parallel instead of one after another in the resolve pass's waves (942 of 46,598 tiles
+// at 10^7 items). A predecessor being recounted at the same moment may be read before or after
+// its rewrite: every descriptor written is a complete count from some entry, and the resolve
+// pass checks the chain and recounts in order whatever still disagrees.
+__global__ __launch_bounds__(TPB) void nxg_fa_fix_kernel(const uint8_t* __restrict__ buf,
+                                                         uint64_t W, uint64_t nt,
+                                                         FaDesc* __restrict__ td,
+                                                         uint64_t* __restrict__ starts) {
+    __shared__ __attribute__((aligned(16))) FaCountLds lds[TPB / 64];
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint64_t t = (uint64_t)blockIdx.x * (TPB / 64) + w;
+    if (t == 0 || t >= nt) return;
+    const uint32_t px = __builtin_amdgcn_readfirstlane(td[t - 1].exit);
+    const uint32_t pi = __builtin_amdgcn_readfirstlane(td[t - 1].items);
+    const uint32_t e = __builtin_amdgcn_readfirstlane(td[t].entry);
+    if (px == FAIL || (pi & BROKEN) || px - TILE == e || px - TILE >= TILE) return;
+    uint8_t* img = lds[w].img;
+    CountRegs g;
+    count_load(g, buf, t * TILE, W, lane);
+    count_store(img, g, lane);
+    uint64_t bits;
+    const FaDesc d = count_tile((lds_bytes)img, t, W, px - TILE, lane, bits);
+    starts[t * 64 + lane] = bits;
+    if (lane == 0) td[t] = d;
+}
+
 // resolve: a lane per tile. A tile whose entry is not its (unbroken) predecessor's exit is
 // recounted from that exit by its wave; then block scans of (items | child slots << 32) give each
 // tile its offset in the block (tloc), and the last block to arrive (FaHead.arrived) scans the
@@ -707,6 +739,9 @@ hipError_t nxg_launch_dec_fa(const uint8_t* buf, uint64_t W, uint32_t p0, uint64
     constexpr uint64_t WV = TPB / 64;
     const uint32_t gc = (uint32_t)((nt + WV - 1) / WV);
     hipLaunchKernelGGL(nxg_fa_count_kernel, dim3(gc), dim3(TPB), 0, s, buf, W, nt, p0, td, starts);
+    // twice: the second pass catches the tiles whose predecessor the first one recounted
+    for (int k = 0; k < NXG_FA_FIX_PASSES; k++)
+        hipLaunchKernelGGL(nxg_fa_fix_kernel, dim3(gc), dim3(TPB), 0, s, buf, W, nt, td, starts);
     hipLaunchKernelGGL(nxg_fa_resolve_kernel, dim3((uint32_t)nb), dim3(TPB), 0, s, buf, W, nt, td,
                        td2, starts, tloc, bsum, bpre, wexit, hp);
     hipLaunchKernelGGL(nxg_fa_emit_kernel, dim3(gc), dim3(TPB), 0, s, buf, W, nt, p0, count, td2,

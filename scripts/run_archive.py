@@ -22,4 +22,10 @@ out = Columns(n + 1, len(m.ctag) + 1, 1, netidx_amd.LAYOUT_MIXED, "cuda")
 for _ in range(reps):
     st, used = c.decode_archive(buf, buf.numel(), out)
 ok = torch.equal(out.id[:n].cpu(), mc.id[:n].cpu()) and torch.equal(out.tag[:n].cpu(), mc.tag[:n].cpu())
-print(f"n={n} path {st.path} rows {st.n_rows} used {used} ok {ok}", flush=True)
+import ctypes as C  # noqa: E402
+from netidx_amd import codec as cm  # noqa: E402
+fa = (C.c_ulonglong * 8)()
+cm.lib().nxg_debug_fa(C.c_void_p(c.ctx), fa)
+tiles = (buf.numel() + 4095) // 4096
+print(f"n={n} path {st.path} rows {st.n_rows} used {used} ok {ok}; tiles {tiles}, recounted by "
+      f"the resolve pass {fa[5]}", flush=True)
