@@ -1300,7 +1300,10 @@ bool nxg_decode_archive_batch(NxgCtx* c, const uint8_t* buf, uint64_t len, NxgCo
                 if (consumed) *consumed = hh->end - 1;
                 return true;
             }
-            if (W >= wmax) break;
+            // a larger window helps only a chain that ran out of window (decline reasons 1 and
+            // 2: a broken or mismatched chain); a decode error or a declined value goes straight
+            // to the exact decoder
+            if (W >= wmax || (hh->why & ~3ull)) break;
             W = std::min(wmax, 2 * W);
         }
     }
