@@ -415,7 +415,7 @@ __global__ __launch_bounds__(TPB) void nxg_fa_count_kernel(const uint8_t* __rest
 }
 
 #ifndef NXG_FA_FIX_PASSES
-#define NXG_FA_FIX_PASSES 2
+#define NXG_FA_FIX_PASSES 1  // (2: a second pass for tiles whose predecessor the first recounted)
 #endif
 // fix: one wave per tile, all tiles at once. A tile whose guessed entry is not its predecessor's
 // counted exit is recounted from that exit. A false guess almost always merges into the true
@@ -739,7 +739,7 @@ hipError_t nxg_launch_dec_fa(const uint8_t* buf, uint64_t W, uint32_t p0, uint64
     constexpr uint64_t WV = TPB / 64;
     const uint32_t gc = (uint32_t)((nt + WV - 1) / WV);
     hipLaunchKernelGGL(nxg_fa_count_kernel, dim3(gc), dim3(TPB), 0, s, buf, W, nt, p0, td, starts);
-    // twice: the second pass catches the tiles whose predecessor the first one recounted
+    // (a second pass would catch the tiles whose predecessor the first one recounted)
     for (int k = 0; k < NXG_FA_FIX_PASSES; k++)
         hipLaunchKernelGGL(nxg_fa_fix_kernel, dim3(gc), dim3(TPB), 0, s, buf, W, nt, td, starts);
     hipLaunchKernelGGL(nxg_fa_resolve_kernel, dim3((uint32_t)nb), dim3(TPB), 0, s, buf, W, nt, td,
