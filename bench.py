@@ -780,14 +780,16 @@ def extras_single_gpu(codec, stream, steps, warmup):
     return ex
 
 
-def make_comm(codec, world, rank):
-    """The library's RCCL communicator (nxg_comm_init; its id broadcast over torch.distributed),
-    or None where RCCL cannot serve (gloo rehearsals with ranks sharing one GPU): then the
-    torch.distributed mirrors of netidx_amd/shard.py run the same protocols."""
+def make_comm(codec, world, rank, buffers):
+    """The library's communicator for the multi-rank protocols (nxg_multi.cpp): RCCL
+    (nxg_comm_init; its id broadcast over torch.distributed), or -- where RCCL cannot serve, gloo
+    rehearsals with ranks sharing one GPU -- the same protocols over a torch.distributed transport
+    (nxg_comm_init_ops, netidx_amd/shard.py gloo_comm; `buffers` are staged through the host)."""
     import netidx_amd
     import torch.distributed as dist
+    from netidx_amd import shard
     if BACKEND == "gloo":
-        return None
+        return shard.gloo_comm(codec, world, rank, buffers)
     obj = [netidx_amd.Comm.unique_id() if rank == 0 else None]
     dist.broadcast_object_list(obj, src=0)
     return netidx_amd.Comm(codec, world, rank, obj[0])
@@ -813,22 +815,12 @@ def extras_multi_gpu(codec, world, rank, stream):
     cols = netidx_amd.columns_from_arrays(ids, vals)
     cap = 15 * total + 64
     dout = torch.empty(cap, dtype=torch.uint8, device="cuda")
-    comm = make_comm(codec, world, rank)
-    via = "rccl (nxg_encode_allgather)" if comm else "torch.distributed mirror (shard.py)"
+    comm = make_comm(codec, world, rank, [dout])
+    via = ("rccl (nxg_encode_allgather)" if BACKEND != "gloo" else
+           "gloo transport via nxg_comm_init_ops (nxg_encode_allgather)")
 
     def encode_gather():
-        if comm:
-            return comm.encode_allgather(cols, None, dout.data_ptr(), cap)
-        ln = codec.encoded_len(cols)
-        off = shard.shard_offsets(ln, world, coll_device())
-        codec.encode_into(cols, None, dout.data_ptr() + int(off[rank]), cap - int(off[rank]))
-        if coll_device() == "cuda":
-            shard.allgather_at_offsets(dout, off, rank, world)
-        else:
-            host = dout[: int(off[-1])].cpu()
-            shard.allgather_at_offsets(host, off, rank, world)
-            dout[: int(off[-1])].copy_(host)
-        return int(off[-1]), [int(x) for x in off[:-1]]
+        return comm.encode_allgather(cols, None, dout.data_ptr(), cap)
 
     times = []
     for it in range(3):
@@ -849,10 +841,7 @@ def extras_multi_gpu(codec, world, rank, stream):
     out = Columns(n + 2 * total // world // 100 + 1024, 0, 0, netidx_amd.LAYOUT_F64, "cuda")
 
     def decode_ranges():
-        if comm:
-            return comm.decode_sharded(dout, W, out)
-        return shard.decode_sharded(
-            lambda bb, ee: codec.decode_range(dout, W, bb, ee, out), W, rank, world)
+        return comm.decode_sharded(dout, W, out)
 
     decode_ranges()
     times = []
@@ -864,7 +853,7 @@ def extras_multi_gpu(codec, world, rank, stream):
         torch.cuda.synchronize()
         times.append(time.perf_counter() - t0)
     t = max_over_ranks(min(times), world)
-    nr = int(rng[4] if isinstance(rng, tuple) else rng.n_rows)
+    nr = int(rng.n_rows)
     # checker: rows [row_off, row_off + nr) of the batch (ids are the global row numbers)
     got_id = out.id[:nr].cpu().numpy().view(np.uint64)
     got_val = out.fixed[:nr].cpu().numpy().view(np.uint64)
@@ -907,8 +896,7 @@ def extras_multi_gpu(codec, world, rank, stream):
     ex["decode_mixed_1e7_per_gpu"] = {
         "records_per_gpu": nm, "world": world, "kernel_ms_slowest_rank": round(kmax, 4),
         "M_updates_s": round(world * nm / (kmax / 1e3) / 1e6, 1)}
-    if comm:
-        comm.close()
+    comm.close()
     return ex
 
 

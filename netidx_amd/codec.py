@@ -472,6 +472,13 @@ class Codec:
         st = self.decode_into(frame, n, cols, flags)
         return cols, st
 
+    def last_diag(self):
+        """DevStatus.diag of the last completed decode (diagnostics, not ABI): for an f64 frame,
+        diag[1] == 1 when the sequential-id decoder (nxg_decode_f64_seq.hip) produced it."""
+        a = (C.c_ulonglong * 8)()
+        lib().nxg_debug_diag(C.c_void_p(self.ctx), a)
+        return list(a)
+
     def decode_async(self, dframe_ptr, nbytes, cols, flags=0):
         err = NetidxError()
         _check(lib().nxg_decode_updates_async(self.ctx, C.c_void_p(dframe_ptr), nbytes,

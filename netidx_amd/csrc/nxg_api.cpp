@@ -74,6 +74,11 @@ struct NxgCtx {
     size_t rdesc_cap = 0;
     uint32_t irregular_left = 0;
     bool force_x = false;
+    // before both: the one-launch decoder of frames whose ids count up by one
+    // (nxg_decode_f64_seq.hip), unless it rejected a recent frame of this connection: then it is
+    // skipped for the next kSeqSkipCalls calls (NXG_F64_PATH=run skips it always)
+    uint32_t seq_left = 0;
+    bool no_seq = false;
     // mixed decode: the fast decoder (nxg_decode_mixed.hip) unless it rejected a recent frame of
     // this connection; then the general decoder for the next kMixFailCalls calls
     // (NXG_MIXED_PATH=general: always the general decoder)
@@ -289,9 +294,14 @@ NxgColumns staged_view(NxgCtx* c, const NxgColumns* like) {
 
 constexpr uint32_t kIrregularCalls = 64;
 constexpr uint32_t kMixFailCalls = 16;
+constexpr uint32_t kSeqSkipCalls = 64;
 
-// path codes of a fast attempt (Pending::fast): homogeneous f64 (RUN, 1P) or mixed (MIX)
-enum { FAST_NONE = 0, FAST_RUN = 1, FAST_X = 2, FAST_MIX = 3 };
+// path codes of a fast attempt (Pending::fast): homogeneous f64 (SEQ, RUN, X) or mixed (MIX)
+enum { FAST_NONE = 0, FAST_RUN = 1, FAST_X = 2, FAST_MIX = 3, FAST_SEQ = 4 };
+
+bool seq_active(const NxgCtx* c) {
+    return !c->no_seq && !c->force_x && c->seq_left == 0 && c->irregular_left == 0;
+}
 
 bool ensure_rdesc(NxgCtx* c, size_t bytes, NetidxError* err) {
     if (bytes <= c->rdesc_cap) return true;
@@ -315,8 +325,16 @@ bool enqueue_dec_x(NxgCtx* c, const uint8_t* f, uint64_t len, NxgColumns* out, D
 }
 
 // Homogeneous-f64 attempt; *path receives the FAST_* code of the decoder that was enqueued.
+// try_seq: the sequential-id decoder may be tried first (not on a rerun after it declined).
 bool enqueue_dec_fast(NxgCtx* c, const uint8_t* f, uint64_t len, NxgColumns* out, DevStatus* st,
-                      int* path, NetidxError* err) {
+                      int* path, NetidxError* err, bool try_seq = true) {
+    if (try_seq && len > 0 && seq_active(c)) {
+        *path = FAST_SEQ;
+        HIPCHK(nxg_launch_dec_f64s(f, len, out->id, out->fixed, out->cap_rows, st,
+                                   nxg_take_zero_slot(), c->stream));
+        return true;
+    }
+    if (c->seq_left) c->seq_left--;
     if (!c->force_x && c->irregular_left == 0) {
         *path = FAST_RUN;
         if (!ensure_tstat(c, nxg_dec_f64r_groups(len), err)) return false;
@@ -384,6 +402,25 @@ bool finish_decode(NxgCtx* c, const uint8_t* f, uint64_t len, NxgColumns* out, i
         HIPCHK(hipStreamSynchronize(c->stream));
     }
     DevStatus h = c->hst[slot];
+    if (tried_fast == FAST_SEQ && len > 0 && h.fast_fail) {
+        if (h.irregular & 2u) {
+            // not an f64 frame at all: on to the mixed decoders (as after the length-run probe)
+            tried_fast = FAST_RUN;
+        } else {
+            // an f64 frame whose ids do not count up by one: the length-run (or single-pass)
+            // decoder, and this one skipped for the next kSeqSkipCalls calls
+            c->seq_left = kSeqSkipCalls;
+            DevStatus* st2;
+            uint32_t slot2;
+            if (!begin_call(c, &st2, &slot2, err)) return false;
+            const bool ok = enqueue_dec_fast(c, f, len, out, st2, &tried_fast, err, false);
+            if (!end_call(c, err) || !ok) return false;
+            HIPCHK(hipMemcpyAsync(c->hst + slot2, st2, sizeof(DevStatus), hipMemcpyDeviceToHost,
+                                  c->stream));
+            HIPCHK(hipStreamSynchronize(c->stream));
+            h = c->hst[slot2];
+        }
+    }
     // (irregular bit 1: not an f64 frame at all -- straight on to the mixed decoders)
     if (tried_fast == FAST_RUN && len > 0 && h.fast_fail && (h.irregular & 3u) == 1u) {
         // record lengths vary record to record: the single-pass decoder of any f64 frame, for
@@ -635,6 +672,7 @@ NxgCtx* nxg_ctx_new(int device, NetidxError* err) {
     nxg_fmx_wgs(c->ncu, c->wgs_fmx);
     const char* fp = getenv("NXG_F64_PATH");
     c->force_x = fp && strcmp(fp, "x") == 0;
+    c->no_seq = fp && (strcmp(fp, "run") == 0 || strcmp(fp, "x") == 0);
     const char* mp = getenv("NXG_MIXED_PATH");
     c->no_fmx = mp && strcmp(mp, "general") == 0;
     const char* ap = getenv("NXG_ARCH_PATH");
@@ -812,7 +850,7 @@ bool nxg_decode_frames_async(NxgCtx* c, uint32_t n, const uint8_t* const* dframe
         max_len = std::max(max_len, lens[j]);
     }
     const bool run_path = !(flags & NXG_DECODE_HINT_MIXED) && !c->force_x &&
-                          c->irregular_left == 0 && n > 1;
+                          c->irregular_left == 0 && n > 1 && !seq_active(c);
     if (!run_path) {
         for (uint32_t j = 0; j < n; j++)
             if (!nxg_decode_updates_async(c, dframes[j], lens[j], douts[j], flags, err))
@@ -825,6 +863,8 @@ bool nxg_decode_frames_async(NxgCtx* c, uint32_t n, const uint8_t* const* dframe
     if (!ensure_tstat(c, nxg_dec_f64r_groups(max_len), err)) return false;
     if (!ensure_rdesc(c, 2 * half, err)) return false;
     std::vector<NxgF64rFrame> fr(n);
+    std::vector<NxgCtx::Pending> pend;
+    pend.reserve(n);
     uint32_t nonempty = 0;  // descriptor arrays alternate over the frames that launch
     for (uint32_t j = 0; j < n; j++) {
         DevStatus* st;
@@ -843,9 +883,12 @@ bool nxg_decode_frames_async(NxgCtx* c, uint32_t n, const uint8_t* const* dframe
         f.zst = nxg_take_zero_slot();
         // an empty frame launches nothing: its zero-ahead slot is cleared here
         if (lens[j] == 0) HIPCHK(hipMemsetAsync(f.zst, 0, sizeof(DevStatus), c->stream));
-        c->pending.push_back({1, FAST_RUN, dframes[j], lens[j], douts[j], nullptr, 0, st, slot});
+        pend.push_back({1, FAST_RUN, dframes[j], lens[j], douts[j], nullptr, 0, st, slot});
     }
+    // (the frames become pending only once their launches are enqueued: a failed launch leaves
+    // no call behind whose status slot no kernel wrote)
     HIPCHK(nxg_launch_dec_f64r_stream(fr.data(), n, c->tstat, c->f64r_flags, c->stream));
+    c->pending.insert(c->pending.end(), pend.begin(), pend.end());
     return true;
 }
 

@@ -18,7 +18,8 @@ struct DevStatus {
     uint64_t total_bytes;  // encode: bytes written
     uint32_t nonf64;       // general path ran into content that F64-only columns cannot hold
     // f64 run decode: bit 0 record lengths vary too often (=> the single-pass decoder), bit 1
-    // not an f64 frame (=> the mixed decoders)
+    // not an f64 frame (=> the mixed decoders); sequential-id decode: bit 2 the ids do not count
+    // up by one (=> the length-run decoder)
     uint32_t irregular;
     // general decode: first error as ~(offset << 8 | kind), combined with atomicMax (0 = none)
     uint64_t err_key;
@@ -98,6 +99,11 @@ uint64_t nxg_dec_f64x_groups(uint64_t W);
 hipError_t nxg_launch_dec_f64x(const uint8_t* wire, uint64_t W, uint64_t* oid, uint64_t* oval,
                                uint64_t cap, uint64_t* tstat, uint32_t epoch, DevStatus* st,
                                hipStream_t s);
+// f64 decode of a frame whose ids count up by one (nxg_decode_f64_seq.hip): one launch, no scratch.
+// Declines with fast_fail + DevStatus.irregular bit 1 (not f64) or bit 2 (another f64 frame).
+uint64_t nxg_dec_f64s_groups(uint64_t W);
+hipError_t nxg_launch_dec_f64s(const uint8_t* wire, uint64_t W, uint64_t* oid, uint64_t* oval,
+                               uint64_t cap, DevStatus* st, DevStatus* zst, hipStream_t s);
 // f64 decode by length runs (nxg_decode_f64_run.hip): probe + emit launches. `desc` holds 16 bytes
 // per tile (nxg_dec_f64r_tiles(W)), `tstat` nxg_dec_f64r_groups(W) epoch-tagged words. Sets
 // DevStatus.irregular (and fast_fail) for frames whose record lengths vary record to record.

@@ -38,6 +38,7 @@
 #include <map>
 #include <mutex>
 #include <string>
+#include <list>
 #include <thread>
 #include <vector>
 
@@ -209,12 +210,19 @@ struct NxgResolver {
     std::atomic<bool> stop{false};
     std::thread acceptor;
     std::mutex mu;
-    std::vector<std::thread> clients;
-    std::vector<int> client_fds;
+    // one thread per connection; a finished connection closes its socket at once (the peer sees
+    // EOF) and its thread is joined by the acceptor at the next accept, or by nxg_resolver_stop
+    struct Conn {
+        std::thread t;
+        int fd;
+        bool done = false;
+    };
+    std::list<Conn> conns;
     struct Pub {
         uint64_t id;
         Addr4 addr;
         uint32_t priority;
+        uint64_t last_seen;  // seconds: the last message on its write connection (writer TTL)
     };
     std::vector<Pub> pubs;                                  // by connection, PublisherId order
     std::map<std::string, std::pair<uint64_t, uint32_t>> published;  // path -> (id, flags)
@@ -223,6 +231,37 @@ struct NxgResolver {
     void serve(int fd);
     void serve_read(int fd);
     void serve_write(int fd, const Addr4& write_addr, uint32_t priority);
+    // (under mu) forget a publisher: its paths and its entry
+    void drop_publisher(uint64_t id) {
+        for (auto it = published.begin(); it != published.end();)
+            it = it->second.first == id ? published.erase(it) : std::next(it);
+        for (auto it = pubs.begin(); it != pubs.end();)
+            it = it->id == id ? pubs.erase(it) : std::next(it);
+    }
+    // (under mu) publishers silent for longer than the writer TTL are expired (the reference's
+    // resolver drops a writer's data when its TTL runs out without heartbeats)
+    void expire(uint64_t now) {
+        if (!ttl) return;
+        std::vector<uint64_t> dead;
+        for (const Pub& p : pubs)
+            if (now > p.last_seen + ttl) dead.push_back(p.id);
+        for (uint64_t id : dead) drop_publisher(id);
+    }
+    void touch(uint64_t id, uint64_t now) {
+        for (Pub& p : pubs)
+            if (p.id == id) p.last_seen = now;
+    }
+    // (under mu) join the threads of finished connections
+    void reap() {
+        for (auto it = conns.begin(); it != conns.end();) {
+            if (it->done) {
+                if (it->t.joinable()) it->t.join();
+                it = conns.erase(it);
+            } else {
+                ++it;
+            }
+        }
+    }
 };
 
 void NxgResolver::serve(int fd) {
@@ -274,6 +313,7 @@ void NxgResolver::serve_read(int fd) {
                 uint32_t flags = 0;
                 {
                     std::lock_guard<std::mutex> g(mu);
+                    expire(now);
                     auto it = published.find(path);
                     if (it != published.end()) {
                         ids.push_back(it->second.first);
@@ -310,8 +350,17 @@ void NxgResolver::serve_write(int fd, const Addr4& write_addr, uint32_t priority
     {
         std::lock_guard<std::mutex> g(mu);
         id = next_id++;
-        pubs.push_back(Pub{id, write_addr, priority});
+        pubs.push_back(Pub{id, write_addr, priority, (uint64_t)time(nullptr)});
     }
+    // a write connection that ends (peer gone, or dropped on a PackError) takes its paths with it
+    struct Drop {
+        NxgResolver* r;
+        uint64_t id;
+        ~Drop() {
+            std::lock_guard<std::mutex> g(r->mu);
+            r->drop_publisher(id);
+        }
+    } drop{this, id};
     {  // ServerHelloWrite { ttl, ttl_expired, auth: Anonymous, resolver_id }
         Out f;
         f.be(ttl, 8);
@@ -325,6 +374,10 @@ void NxgResolver::serve_write(int fd, const Addr4& write_addr, uint32_t priority
         Out reply;
         In in(m.data(), m.size());
         size_t n_msgs = 0, n_heartbeat = 0;
+        {
+            std::lock_guard<std::mutex> g(mu);
+            touch(id, (uint64_t)time(nullptr));
+        }
         while (in.left()) {
             size_t end;
             uint32_t variant;
@@ -455,8 +508,18 @@ NxgResolver* nxg_resolver_start(const char* ipv4, uint16_t port, uint16_t* bound
             const int one = 1;
             setsockopt(c, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
             std::lock_guard<std::mutex> g(r->mu);
-            r->client_fds.push_back(c);
-            r->clients.emplace_back([r, c] { r->serve(c); });
+            r->reap();
+            r->conns.emplace_back();
+            NxgResolver::Conn* cn = &r->conns.back();
+            cn->fd = c;
+            cn->t = std::thread([r, cn, c] {
+                r->serve(c);
+                std::lock_guard<std::mutex> g2(r->mu);
+                shutdown(c, SHUT_RDWR);
+                close(c);
+                cn->fd = -1;
+                cn->done = true;
+            });
         }
     });
     return r;
@@ -468,14 +531,15 @@ void nxg_resolver_stop(NxgResolver* r) {
     shutdown(r->lfd, SHUT_RDWR);
     close(r->lfd);
     if (r->acceptor.joinable()) r->acceptor.join();
-    std::vector<std::thread> ts;
+    std::list<NxgResolver::Conn> cs;
     {
         std::lock_guard<std::mutex> g(r->mu);
-        for (int c : r->client_fds) shutdown(c, SHUT_RDWR);
-        ts.swap(r->clients);
+        for (auto& c : r->conns)
+            if (c.fd >= 0) shutdown(c.fd, SHUT_RDWR);  // each thread closes its own socket
+        cs.splice(cs.end(), r->conns);
     }
-    for (auto& t : ts) t.join();
-    for (int c : r->client_fds) close(c);
+    for (auto& c : cs)
+        if (c.t.joinable()) c.t.join();
     delete r;
 }
 

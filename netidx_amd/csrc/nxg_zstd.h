@@ -244,15 +244,17 @@ NXZ_HD uint32_t read_huf_weights(const uint8_t* p, uint32_t n, uint8_t* w, uint3
             return (uint32_t)v;
         };
         uint32_t s1 = rd(al), s2 = rd(al);
+        // FSE_decompress into 255 weights: libzstd fails a write past index 253 (`op > omax - 2`,
+        // each write may be followed by the other state's final one), so at most 255 are decoded
         for (;;) {
-            if (nw >= 255) return 0;
+            if (nw > 253) return 0;
             w[nw++] = fse[s1].sym;
             s1 = fse[s1].base + rd(fse[s1].nbits);
             if (bp < 0) {
                 w[nw++] = fse[s2].sym;
                 break;
             }
-            if (nw >= 255) return 0;
+            if (nw > 253) return 0;
             w[nw++] = fse[s2].sym;
             s2 = fse[s2].base + rd(fse[s2].nbits);
             if (bp < 0) {
@@ -272,7 +274,12 @@ NXZ_HD uint32_t read_huf_weights(const uint8_t* p, uint32_t n, uint8_t* w, uint3
     if (mb > kHufMaxBits) return 0;
     const uint32_t rest = (1u << mb) - total;
     if (rest & (rest - 1)) return 0;  // not a power of two
+    if (nw >= 256) return 0;          // no room for the implied weight (w holds 256)
     w[nw++] = (uint8_t)(highbit(rest) + 1);
+    // HUF_readStats' tree check: at least two weight-1 symbols, an even number of them
+    uint32_t r1 = 0;
+    for (uint32_t i = 0; i < nw; i++) r1 += w[i] == 1;
+    if (r1 < 2 || (r1 & 1)) return 0;
     *n_sym = nw;
     *max_bits = mb;
     return used;

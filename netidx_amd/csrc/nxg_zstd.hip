@@ -419,7 +419,8 @@ NXG_DEV uint32_t block_compressed(ZLds& L, Frame& f, const uint8_t* ip, uint32_t
         if (sf == 0) {  // one stream
             if (lane == 0) ok = huf_stream(L, d, dn, litbuf, rs, f.huf_bits);
         } else {  // four streams behind a jump table
-            if (dn < 10) return Z_CORRUPT;
+            // libzstd: fewer than MIN_LITERALS_FOR_4_STREAMS (6) literals cannot be 4 streams
+            if (dn < 10 || rs < 6) return Z_CORRUPT;
             const uint32_t s1 = (uint32_t)rd_le(d, 2), s2 = (uint32_t)rd_le(d + 2, 2),
                            s3 = (uint32_t)rd_le(d + 4, 2);
             if (6u + s1 + s2 + s3 >= dn) return Z_CORRUPT;

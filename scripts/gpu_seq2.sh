@@ -1,0 +1,9 @@
+#!/bin/bash
+# round 4: the sequential-id decoder, scalar setup: its tests, then the A/B
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd $R
+mkdir -p gpurun_out/seq2
+timeout -k 10 400 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_f64_seq.py > gpurun_out/seq2/tests.log 2>&1 || { tail -30 gpurun_out/seq2/tests.log; exit 1; }
+tail -3 gpurun_out/seq2/tests.log
+scripts/gpu_ab_f64s.sh "10000000 100000000" base nt1 r8 2>&1 | grep -v amdgpu.ids | tee gpurun_out/seq2/ab.log

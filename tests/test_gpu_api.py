@@ -26,6 +26,22 @@ def codec():
     c.close()
 
 
+@pytest.fixture(scope="module", params=["seq", "run"])
+def dcodec(request):
+    """Decode tests run on both f64 front ends: the sequential-id kernel first (the default), and
+    the length-run decoder (NXG_F64_PATH=run), whose stream of frames fuses frame j + 1's probe
+    into frame j's emit."""
+    import os
+    import netidx_amd
+    os.environ["NXG_F64_PATH"] = "" if request.param == "seq" else "run"
+    try:
+        c = netidx_amd.Codec(0)
+    finally:
+        del os.environ["NXG_F64_PATH"]
+    yield c
+    c.close()
+
+
 def _vl(ids):
     ids = np.asarray(ids, np.uint64)
     n = np.ones(len(ids), np.int64)
@@ -141,7 +157,7 @@ def test_sync_finishes_every_pending_call(codec):
 
 
 @pytest.mark.parametrize("seed", [11, 12])
-def test_decode_frames_stream(codec, seed):
+def test_decode_frames_stream(dcodec, seed):
     """nxg_decode_frames_async: a backlog of frames of varied shape, each into its own columns --
     f64 frames of odd and even record counts (the 16-byte pair stores at both row parities),
     ids across the varint widths, an empty frame, a frame with a Heartbeat (the fast path rejects
@@ -166,8 +182,8 @@ def test_decode_frames_stream(codec, seed):
     dev = [torch.from_numpy(np.frombuffer(w, np.uint8).copy()).cuda() if w else
            torch.empty(16, dtype=torch.uint8, device="cuda") for w in frames]
     outs = [Columns.for_frame(max(len(w), 16), netidx_amd.LAYOUT_MIXED, "cuda") for w in frames]
-    codec.decode_frames_async([d.data_ptr() for d in dev], [len(w) for w in frames], outs)
-    codec.sync()
+    dcodec.decode_frames_async([d.data_ptr() for d in dev], [len(w) for w in frames], outs)
+    dcodec.sync()
     for w, o in zip(frames, outs):
         ref = nxo.decode(w).trim()
         g = o.numpy()
@@ -176,7 +192,7 @@ def test_decode_frames_stream(codec, seed):
     assert outs[9].s.n_heartbeat == 1
 
 
-def test_decode_frames_stream_shared_columns_1e7(codec):
+def test_decode_frames_stream_shared_columns_1e7(dcodec):
     """The bench's shape: one 10^7-record f64 frame decoded 6 times as a stream into one set of
     columns (the probe of frame j + 1 runs beside the emit of frame j), bit-exact."""
     import netidx_amd
@@ -186,12 +202,12 @@ def test_decode_frames_stream_shared_columns_1e7(codec):
     n = 10_000_000
     ids, vals = synth.f64_columns(n, synth.SEED_F64)
     cols = netidx_amd.columns_from_arrays(ids, vals)
-    wire = codec.encode_batch(cols)
+    wire = dcodec.encode_batch(cols)
     out = Columns(n, 0, 0, netidx_amd.LAYOUT_F64, "cuda")
     for rep in range(2):
         out.id.zero_()
         out.fixed.zero_()
-        codec.decode_frames_async([wire.data_ptr()] * 6, [wire.numel()] * 6, [out] * 6)
-        st = codec.sync()
+        dcodec.decode_frames_async([wire.data_ptr()] * 6, [wire.numel()] * 6, [out] * 6)
+        st = dcodec.sync()
         assert st.path == 1 and st.n_rows == n
         assert torch.equal(out.id[:n], cols.id[:n]) and torch.equal(out.fixed[:n], cols.fixed[:n])

@@ -31,6 +31,21 @@ def codec():
     c.close()
 
 
+@pytest.fixture(scope="module", params=["seq", "run"])
+def f64codec(request):
+    """The f64 front ends: the sequential-id kernel (default) and the length-run decoder
+    (NXG_F64_PATH=run)."""
+    import netidx_amd
+    os.environ["NXG_F64_PATH"] = "" if request.param == "seq" else "run"
+    try:
+        c = netidx_amd.Codec(0)
+    finally:
+        del os.environ["NXG_F64_PATH"]
+    c.front = request.param
+    yield c
+    c.close()
+
+
 def _decode_dev(codec, wire, cols, flags=0):
     import torch
     dw = torch.from_numpy(np.ascontiguousarray(wire)).cuda()
@@ -48,7 +63,7 @@ def _assert_f64(cols, st, wire, n):
     assert np.array_equal(g["fixed"], o["fixed"])
 
 
-def test_config2_f64_decode_10m_every_row(codec):
+def test_config2_f64_decode_10m_every_row(f64codec):
     import netidx_amd
     import nxo
     from netidx_amd import synth
@@ -58,13 +73,14 @@ def test_config2_f64_decode_10m_every_row(codec):
     wire = nxo.encode_f64(ids, vals)
     assert len(wire) == 147_886_336
     cols = Columns(n, 0, 0, netidx_amd.LAYOUT_F64, "cuda")
-    st = _decode_dev(codec, wire, cols)
+    st = _decode_dev(f64codec, wire, cols)
     _assert_f64(cols, st, wire, n)
+    assert (f64codec.last_diag()[1] == 1) == (f64codec.front == "seq")
 
 
-def test_f64_decode_past_the_infinity_cache_every_row(codec):
-    """A 2 * 10^7-record frame (296 MB, past the 256 MiB Infinity Cache): the length-run emit
-    takes its XCD-contiguous workgroup order there; every row against the oracle."""
+def test_f64_decode_past_the_infinity_cache_every_row(f64codec):
+    """A 2 * 10^7-record frame (296 MB, past the 256 MiB Infinity Cache): both f64 front ends
+    take their XCD-contiguous workgroup order there; every row against the oracle."""
     import netidx_amd
     from netidx_amd import synth
     from netidx_amd.codec import Columns
@@ -74,7 +90,7 @@ def test_f64_decode_past_the_infinity_cache_every_row(codec):
     wire = nxo.encode_f64(ids, vals)
     assert len(wire) > 256 << 20
     cols = Columns(n, 0, 0, netidx_amd.LAYOUT_F64, "cuda")
-    st = _decode_dev(codec, wire, cols)
+    st = _decode_dev(f64codec, wire, cols)
     _assert_f64(cols, st, wire, n)
 
 
@@ -136,7 +152,7 @@ def test_config4_mixed_encode_10m_every_byte(codec):
     assert np.array_equal(out, wire)
 
 
-def test_f64_ids_across_2_28_on_the_fast_path(codec):
+def test_f64_ids_across_2_28_on_the_fast_path(f64codec):
     """Ids grow from a per-process counter (netidx-core/src/utils.rs:130-134): a long-lived
     publisher crosses 2^28, where ids take 5 varint bytes. 10^6 records straddling it."""
     import netidx_amd
@@ -147,12 +163,12 @@ def test_f64_ids_across_2_28_on_the_fast_path(codec):
     ids, vals = synth.f64_columns(n, 71, id_offset=2**28 - n // 2)
     wire = nxo.encode_f64(ids, vals)
     cols = Columns(n, 0, 0, netidx_amd.LAYOUT_F64, "cuda")
-    _assert_f64(cols, _decode_dev(codec, wire, cols), wire, n)
+    _assert_f64(cols, _decode_dev(f64codec, wire, cols), wire, n)
     # 5-byte ids everywhere (random order within [2^28, 2^35))
     rng = np.random.default_rng(72)
     ids = rng.integers(2**28, 2**35, n, dtype=np.uint64)
     wire = nxo.encode_f64(ids, vals)
-    _assert_f64(cols, _decode_dev(codec, wire, cols), wire, n)
+    _assert_f64(cols, _decode_dev(f64codec, wire, cols), wire, n)
 
 
 def test_f64_ids_in_random_order(codec):
@@ -179,10 +195,12 @@ def test_f64_run_decoder_exact_path_everywhere():
     from netidx_amd import synth
     from netidx_amd.codec import Columns
     os.environ["NXG_F64R_FLAGS"] = "3"
+    os.environ["NXG_F64_PATH"] = "run"
     try:
         c = netidx_amd.Codec(0)
     finally:
         del os.environ["NXG_F64R_FLAGS"]
+        del os.environ["NXG_F64_PATH"]
     try:
         n = 300_000
         cols = Columns(n, 0, 0, netidx_amd.LAYOUT_F64, "cuda")

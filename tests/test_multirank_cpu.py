@@ -1,17 +1,13 @@
-"""Multi-rank protocols on the CPU: gloo, world size 2 and 3, one process per rank.
+"""The torch.distributed transport of the multi-rank calls on the CPU: gloo, world size 2 and 3,
+one process per rank.
 
-bench.py --gpus N runs one process per GPU; the library's RCCL calls (nxg_encode_allgather,
-nxg_decode_sharded) and their torch.distributed mirrors in netidx_amd/shard.py follow the same
-protocols, checked here over gloo with the oracle standing in for the per-rank GPU kernels:
-
-- config 5's encode: shards encoded in rank order, one all-gather of their sizes, every shard
-  delivered at its final byte offset by grouped send/recv; every rank ends with exactly the whole
-  batch's frame (the oracle decodes it: every id and value in order);
-- one frame decoded in byte ranges: each rank takes the messages that start in its range,
-  nxg_range_link (the product's host code) links the ranges' summaries and numbers their rows,
-  including cuts inside records and a rank whose first guess at its entry is off the chain (it
-  decodes again from its predecessor's exit);
-- the timing reduction takes the slowest rank.
+The protocols (nxg_encode_allgather, nxg_decode_sharded) live only in the library and are tested
+in test_multirank_lib_cpu.py (CPU) and test_gpu_multirank.py (GPU). Here: the transport that
+netidx_amd/shard.py hands them through nxg_comm_init_ops where RCCL cannot serve --
+- the grouped send/recv of shards at their byte offsets (config 5's all-gather): shards encoded
+  in rank order end up as exactly the whole batch's frame on every rank (the oracle decodes it:
+  every id and value in order);
+- the timing reduction takes the slowest rank; the record / byte split.
 """
 import os
 import socket
@@ -44,7 +40,9 @@ def _rank_encode(rank, world, port, total, outdir):
         b, e = shard.shard_range(total, world, rank)
         ids, vals = synth.f64_columns(e - b, synth.SEED_8GPU, id_offset=b)
         wire = nxo.encode_f64(ids, vals)
-        off = shard.shard_offsets(len(wire), world)
+        lens = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+        dist.all_gather(lens, torch.tensor([len(wire)], dtype=torch.int64))
+        off = np.concatenate([[0], np.cumsum([int(x) for x in lens])])
         out = torch.zeros(int(off[-1]), dtype=torch.uint8)
         out[int(off[rank]):int(off[rank + 1])] = torch.from_numpy(wire)  # the shard in place
         shard.allgather_at_offsets(out, off, rank, world)
@@ -76,69 +74,6 @@ def test_encode_allgather_at_offsets_rebuilds_the_whole_batch(tmp_path, world, t
     assert d.s.err_kind == 0 and d.s.n_rows == total
     t = d.trim()
     assert np.array_equal(t["id"], ids) and np.array_equal(t["fixed"], vals)
-
-
-def _starts(wire):
-    """Message start offsets of a frame (the oracle's chain: each length prefix is the message
-    length, netidx-core/src/pack.rs:537-555; f64 records are < 128 bytes: one-byte prefixes)."""
-    st, p = [], 0
-    while p < len(wire):
-        st.append(p)
-        p += int(wire[p])
-    return np.array(st, np.int64)
-
-
-def _rank_decode(rank, world, port, total, seed, liar, outdir):
-    _init(rank, world, port)
-    try:
-        ids, vals = synth.f64_columns(total, seed)
-        wire = nxo.encode_f64(ids, vals)
-        W = len(wire)
-        starts = _starts(wire)
-        calls = []
-
-        def decode_range(b, e):
-            """The GPU range decode's contract, restated from the oracle's chain: messages that
-            start in [b, e); entry = first start >= b, exit = first start >= e (or W). Rank
-            `liar` first guesses an entry inside a record (as a false record header would)."""
-            i0 = int(np.searchsorted(starts, b))
-            i1 = int(np.searchsorted(starts, e))
-            entry = int(starts[i0]) if i0 < len(starts) else W
-            exit_ = int(starts[i1]) if i1 < len(starts) else W
-            rows = i1 - i0
-            if rank == liar and not calls:
-                entry, exit_, rows = entry + 3, exit_ + 5, rows - 1
-            calls.append((b, e))
-            o = nxo.decode(wire[entry:exit_] if rank != liar or len(calls) > 1 else wire[:0],
-                           cap_children=1, cap_ctl=1).trim()
-            np.save(os.path.join(outdir, f"rows{rank}.npy"), o["fixed"])
-            return (b, e, entry, exit_, rows, 1, 0)
-
-        off, mine = shard.decode_sharded(decode_range, W, rank, world)
-        np.save(os.path.join(outdir, f"dec{rank}.npy"),
-                np.array([off, len(calls)] + list(mine), dtype=np.int64))
-        dist.barrier()
-    finally:
-        dist.destroy_process_group()
-
-
-@pytest.mark.parametrize("world,total,liar", [(2, 30_001, -1), (3, 20_000, 1), (2, 5000, 1)])
-def test_decode_byte_ranges_link_and_number_rows(tmp_path, world, total, liar):
-    mp.spawn(_rank_decode, args=(world, _free_port(), total, 91, liar, str(tmp_path)),
-             nprocs=world, join=True)
-    ids, vals = synth.f64_columns(total, 91)
-    W = len(nxo.encode_f64(ids, vals))
-    got = []
-    for r in range(world):
-        d = np.load(tmp_path / f"dec{r}.npy")
-        off, ncalls, rng = int(d[0]), int(d[1]), d[2:]
-        b, e = shard.shard_range(W, world, r)
-        assert (int(rng[0]), int(rng[1])) == (b, e)
-        assert ncalls == (2 if r == liar else 1)  # the liar decoded again, from the true chain
-        rows = np.load(tmp_path / f"rows{r}.npy")
-        assert off == len(got) and len(rows) == int(rng[4])
-        got.extend(rows.tolist())
-    assert np.array_equal(np.array(got, np.uint64), vals)  # every record once, in order
 
 
 def test_shard_range_partitions():

@@ -125,3 +125,60 @@ def test_clients_against_each_other():
             w.close()
     finally:
         res.stop()
+
+
+def test_closed_publisher_is_forgotten_and_dropped_peer_sees_eof():
+    """a write connection that ends takes its paths with it (the resolver no longer
+    returns a dead publisher's address), and a peer the server drops (here: an unknown ToWrite
+    tag) sees EOF at once instead of blocking."""
+    import time
+    res = netidx_amd.Resolver()
+    try:
+        w = netidx_amd.ResolverClient.write("127.0.0.1", res.port, ("127.0.0.1", 7100))
+        w.publish("/gone")
+        rc = netidx_amd.ResolverClient.read("127.0.0.1", res.port)
+        assert rc.resolve("/gone").n_publishers == 1
+        w.close()
+        for _ in range(100):  # the server thread notices the close
+            if rc.resolve("/gone").n_publishers == 0:
+                break
+            time.sleep(0.01)
+        assert rc.resolve("/gone").n_publishers == 0 and res.n_published() == 0
+        rc.close()
+        # a raw write client that sends an unknown ToWrite variant is dropped: EOF, not a hang
+        s = socket.create_connection(("127.0.0.1", res.port))
+        s.settimeout(5)
+        hello(s)
+        # ClientHello::WriteOnly { write_addr, Anonymous, priority } as test_write_handshake does
+        fields = addr("127.0.0.1", 7101) + b"\x02\x00" + b"\x02\x01"
+        s.sendall(frame(bytes([14, 1, 12]) + fields))
+        recv_frame(s)  # ServerHelloWrite
+        s.sendall(frame(bytes([2, 99])))  # ToWrite variant 99: UnknownTag -> the server drops us
+        assert s.recv(1) == b""  # EOF
+        s.close()
+        # many connections come and go: the server keeps serving
+        for k in range(50):
+            x = netidx_amd.ResolverClient.read("127.0.0.1", res.port)
+            x.close()
+        rc = netidx_amd.ResolverClient.read("127.0.0.1", res.port)
+        assert rc.resolve("/nothing").n_publishers == 0
+        rc.close()
+    finally:
+        res.stop()
+
+
+def test_writer_ttl_expires_a_silent_publisher():
+    """A publisher that stops talking (no heartbeats) is forgotten after the writer TTL."""
+    import time
+    res = netidx_amd.Resolver(writer_ttl=1)
+    try:
+        w = netidx_amd.ResolverClient.write("127.0.0.1", res.port, ("127.0.0.1", 7200))
+        w.publish("/quiet")
+        rc = netidx_amd.ResolverClient.read("127.0.0.1", res.port)
+        assert rc.resolve("/quiet").n_publishers == 1
+        time.sleep(2.2)
+        assert rc.resolve("/quiet").n_publishers == 0
+        rc.close()
+        w.close()
+    finally:
+        res.stop()
