@@ -3,11 +3,14 @@
 
 A "step" decodes one batch: a frame payload of From::Update(Id, F64) messages (configs[1],
 10^7 records, 147,886,336 wire bytes), from HBM-resident wire bytes into HBM-resident id/f64
-columns, through the C ABI. The K timed frames are a connection's backlog decoded as one stream
-(nxg_decode_frames_async: the record-length probe of frame j+1 runs in the launch that emits
-frame j); the per-call rate (one nxg_decode_updates_async per frame) is reported beside it. With --gpus N each rank decodes its own
-10^7-record shard; the ids are disjoint and there is no data-path collective ("weak" scaling).
-`value` is the whole-job aggregate in M updates/s, over all ranks.
+columns, through the C ABI. The K timed frames are a connection's backlog (nxg_decode_frames_async)
+of 3 distinct frames decoded in rotation into 3 column sets, so that every decode streams from HBM
+(3 x 308 MB is past three times the 256 MiB Infinity Cache). The frames' ids count up by one, so
+the sequential-id decoder (nxg_decode_f64_seq.hip, one launch per frame) takes them; the
+length-run decoder of any f64 frame (NXG_F64_PATH=run) and the same-frame rate of earlier rounds
+are reported beside it. With --gpus N each rank decodes its own 10^7-record shard; the ids are
+disjoint and there is no data-path collective ("weak" scaling). `value` is the whole-job
+aggregate in M updates/s, over all ranks.
 
 The inputs come from the product encoder (config 4). Outside the timed regions every leg is
 checked once against the CPU oracle (oracle/nx_oracle.c, as the checker): decoded columns vs the
@@ -16,7 +19,7 @@ encode of the same columns. The oracle is also the cpu_baseline leg.
 
 Also reported on the same JSON line:
   roofline       the decode's algorithmic bytes (W + 16 N) / mean time of one decode (HIP
-                 events on the codec stream) vs the 8 TB/s HBM3E peak;
+                 events on the codec stream around the backlog) vs the 8 TB/s HBM3E peak;
   cpu_baseline   the C restatement of the reference decoder (oracle/, 1 core) on this host;
   extras         10^8-record decode (north-star size), mixed-tag decode (config 3), the
                  host-memory (PCIe-inclusive) decode path, f64 encode (config 4), subscriber
@@ -41,6 +44,9 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # probe + emit as two launches.
 KERNEL_DEC_F64 = "nxg_f64r_fused_kernel"
 KERNELS_DEC_F64 = ["nxg_f64r_probe_kernel", "nxg_f64r_fused_kernel", "nxg_f64r_emit_kernel"]
+# the sequential-id decoder (nxg_decode_f64_seq.hip): one launch per frame, the first choice for
+# frames whose ids count up by one (a publisher updating all of its values)
+KERNEL_SEQ = "nxg_f64s_kernel"
 
 
 def log(*a):
@@ -96,31 +102,38 @@ def make_f64_wire(codec, n, rank):
 
 
 def time_decode(codec, wire, out, n, steps, warmup, world, stream, flags=0, stream_of_frames=False):
-    """Returns (wall seconds max over ranks, mean kernel ms, last status). stream_of_frames: the
-    frames go through nxg_decode_frames_async (a connection's backlog: frame j+1's probe runs in
-    frame j's emit launch), up to 500 per call; else one nxg_decode_updates_async per frame."""
+    """Returns (wall seconds max over ranks, mean ms per frame from HIP events, last status).
+    `wire` / `out` may be lists: frame j is wire[j % len] decoded into out[j % len] (distinct
+    frames and column sets: with 3 of them at 10^7 records the working set, 924 MB, is past three
+    times the 256 MiB Infinity Cache, so every decode streams from HBM). stream_of_frames: the
+    frames go through nxg_decode_frames_async (a connection's backlog), up to 500 per call; else
+    one nxg_decode_updates_async per frame."""
     import torch
-    nbytes = wire.numel()
+    wires = wire if isinstance(wire, (list, tuple)) else [wire]
+    outs = out if isinstance(out, (list, tuple)) else [out]
+    m_ = len(wires)
 
     def enqueue(k):
         if stream_of_frames:
             i = 0
             while i < k:
                 m = min(500, k - i)
-                codec.decode_frames_async([wire.data_ptr()] * m, [nbytes] * m, [out] * m, flags)
+                sel = [(i + j) % m_ for j in range(m)]
+                codec.decode_frames_async([wires[j].data_ptr() for j in sel],
+                                          [wires[j].numel() for j in sel], [outs[j] for j in sel],
+                                          flags)
                 i += m
                 if i < k:
                     codec.sync()
             return
         for i in range(k):
-            codec.decode_async(wire.data_ptr(), nbytes, out, flags)
+            j = i % m_
+            codec.decode_async(wires[j].data_ptr(), wires[j].numel(), outs[j], flags)
             if (i + 1) % 500 == 0 and i + 1 < k:  # at most 512 async calls in flight
                 codec.sync()
 
     for _ in range(warmup):
-        # (a stream warms up with two frames: one frame takes the one-call path, and the stream's
-        # second descriptor array is allocated on its first use)
-        enqueue(2 if stream_of_frames else 1)
+        enqueue(max(2, m_))
         codec.sync()
     barrier(world)
     torch.cuda.synchronize()
@@ -135,6 +148,22 @@ def time_decode(codec, wire, out, n, steps, warmup, world, stream, flags=0, stre
     barrier(world)
     wall = max_over_ranks(time.perf_counter() - t0, world)
     return wall, e0.elapsed_time(e1) / steps, st
+
+
+def f64_kernel_name(codec):
+    """The f64 decoder that produced the last decode: the sequential-id kernel or the
+    length-run probe + emit (DevStatus.diag[1])."""
+    return KERNEL_SEQ if codec.last_diag()[1] == 1 else " + ".join(KERNELS_DEC_F64)
+
+
+def codec_run_path(device):
+    """A second context whose f64 frames take the length-run decoder (NXG_F64_PATH=run)."""
+    import netidx_amd
+    os.environ["NXG_F64_PATH"] = "run"
+    try:
+        return netidx_amd.Codec(device)
+    finally:
+        del os.environ["NXG_F64_PATH"]
 
 
 def _nxo():
@@ -266,16 +295,72 @@ def cpu_baseline_threads(wire_host, ids, seconds, threads=16):
     return n * reps / t_total, reps, t_total
 
 
-def read_traffic(records):
+def read_traffic(records, kernel):
     """HBM bytes per launch from the committed rocprofv3 PMC summary, if it matches."""
     p = os.path.join(ROOT, "profiles", "pmc_dec_f64.json")
     try:
         j = json.load(open(p))
-        if j.get("records") == records and j.get("kernel") == KERNEL_DEC_F64:
+        if j.get("records") == records and j.get("kernel") == kernel:
             return j.get("hbm_bytes_per_launch")
     except Exception:
         pass
     return None
+
+
+def read_split(records):
+    """Per-kernel average durations of the f64 decoders at this size, from the committed rocprofv3
+    kernel trace (profiles/f64_kernel_split.json), if present."""
+    p = os.path.join(ROOT, "profiles", "f64_kernel_split.json")
+    try:
+        j = json.load(open(p))
+        return j.get(str(records))
+    except Exception:
+        return None
+
+
+def zstd_cpu_baseline(src, recs, want, dict_bytes, seconds=3.0):
+    """The reference's CPU path for compressed archive records: one host core decompressing each
+    record's zstd frame with the archive's dictionary (zstd::bulk::Decompressor::with_dictionary +
+    decompress_to_buffer, netidx-archive/src/logfile/reader.rs:243-244, 453-477), here the
+    system libzstd through ctypes (the zstd 0.13 crate wraps libzstd 1.5; this image has 1.4.8).
+    Each record is a u32 BE plain length, then the frame. Returns the cpu_baseline object, or the
+    reason it could not run."""
+    import ctypes as C
+    import numpy as np
+    try:
+        Z = C.CDLL("libzstd.so.1")
+    except OSError as e:
+        return {"error": f"libzstd not loadable: {e}"}
+    Z.ZSTD_createDCtx.restype = C.c_void_p
+    Z.ZSTD_createDDict.restype = C.c_void_p
+    Z.ZSTD_createDDict.argtypes = [C.c_void_p, C.c_size_t]
+    Z.ZSTD_decompress_usingDDict.restype = C.c_size_t
+    Z.ZSTD_decompress_usingDDict.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p,
+                                             C.c_size_t, C.c_void_p]
+    Z.ZSTD_isError.argtypes = [C.c_size_t]
+    dctx = Z.ZSTD_createDCtx()
+    db = C.create_string_buffer(bytes(dict_bytes), len(dict_bytes))
+    ddict = Z.ZSTD_createDDict(db, len(dict_bytes))
+    src = np.ascontiguousarray(src)
+    cap = max(len(w) for w in want) + 64
+    dst = np.empty(cap, np.uint8)
+    base = src.ctypes.data
+    reps, t, nbytes = 0, 0.0, 0
+    ok = True
+    while t < seconds or reps == 0:
+        t0 = time.perf_counter()
+        for (off, ln), w in zip(recs, want):
+            r = Z.ZSTD_decompress_usingDDict(dctx, dst.ctypes.data, cap, base + off + 4, ln - 4,
+                                             ddict)
+            ok &= not Z.ZSTD_isError(r) and r == len(w)
+            nbytes += len(w)
+        t += time.perf_counter() - t0
+        reps += 1
+    ok &= bool(np.array_equal(dst[:len(want[-1])], want[-1]))
+    return {"value": round(nbytes / t / 1e9, 3), "unit": "plain GB/s", "cores": 1,
+            "kind": "dependency (libzstd, the library the reference calls)", "ok": bool(ok),
+            "sample": f"the {len(recs)} records decompressed {reps}x ({t:.1f} s) by the system "
+                      "libzstd (ZSTD_decompress_usingDDict, one core)"}
 
 
 def extras_single_gpu(codec, stream, steps, warmup):
@@ -285,28 +370,50 @@ def extras_single_gpu(codec, stream, steps, warmup):
     from netidx_amd import synth
     from netidx_amd.codec import Columns
     ex = {}
-    # (a) north-star size: 10^8 f64 records on one GPU
+    # (a) north-star size: 10^8 f64 records on one GPU. Two frames and column sets in rotation
+    # (3.1 GB each: far past the Infinity Cache either way), as one backlog; then the length-run
+    # decoder on the same frames, and one call per frame.
     try:
         n = 100_000_000
         cols, wire = make_f64_wire(codec, n, 0)
-        out = Columns(n, 0, 0, netidx_amd.LAYOUT_F64, "cuda")
-        k = max(6, steps // 4)
-        # (the one-call-per-frame leg first: it also warms the GPU up for the stream)
-        _, kms1, st1 = time_decode(codec, wire, out, n, k, 2, 1, stream)
-        assert st1.path == 1 and st1.n_rows == n
-        wall, kms, st = time_decode(codec, wire, out, n, k, 2, 1, stream, stream_of_frames=True)
+        wires = [wire, wire.clone()]
+        outs = [Columns(n, 0, 0, netidx_amd.LAYOUT_F64, "cuda") for _ in range(2)]
+        k = max(12, steps // 2)
+        _, kms, st = time_decode(codec, wires, outs, n, k, 2, 1, stream, stream_of_frames=True)
         assert st.path == 1 and st.n_rows == n
+        kname = f64_kernel_name(codec)
+        _, kms1, st1 = time_decode(codec, wires, outs, n, k, 1, 1, stream)
+        assert st1.path == 1 and st1.n_rows == n
+        crun = codec_run_path(0)
+        crun.set_stream(stream.cuda_stream)
+        _, kms_run, st2 = time_decode(crun, wires, outs, n, k, 2, 1, stream, stream_of_frames=True)
+        assert st2.path == 1 and st2.n_rows == n
+        _, kms_run1, st3 = time_decode(crun, wires, outs, n, k, 1, 1, stream)
+        assert st3.path == 1 and st3.n_rows == n
+        crun.close()
         b = wire.numel() + 16 * n
+
+        def fr(ms):
+            return round(b / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4)
+
         ex["decode_f64_1e8"] = {"records": n, "wire_bytes": wire.numel(),
                                 "M_updates_s": round(n / (kms / 1e3) / 1e6, 1),
-                                "kernel_ms": round(kms, 4),
-                                "hbm_frac": round(b / (kms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
-                                "timed": f"{k} frames as one stream (nxg_decode_frames_async), "
-                                         "HIP events on the codec stream",
-                                "per_call_kernel_ms": round(kms1, 4),
-                                "per_call_hbm_frac": round(b / (kms1 / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
-                                "oracle_rows_checked": oracle_check_decode(wire, out, n)}
-        del cols, wire, out
+                                "kernel_ms": round(kms, 4), "hbm_frac": fr(kms),
+                                "kernel": kname,
+                                "timed": f"{k} frames as one backlog (nxg_decode_frames_async), 2 "
+                                         "frames and column sets in rotation, HIP events on the "
+                                         "codec stream",
+                                "per_call_kernel_ms": round(kms1, 4), "per_call_hbm_frac": fr(kms1),
+                                "length_run_decoder": {
+                                    "kernels": " / ".join(KERNELS_DEC_F64),
+                                    "backlog_kernel_ms": round(kms_run, 4),
+                                    "backlog_hbm_frac": fr(kms_run),
+                                    "per_call_kernel_ms": round(kms_run1, 4),
+                                    "per_call_hbm_frac": fr(kms_run1)},
+                                "kernel_split": read_split(n),
+                                "oracle_rows_checked": sum(oracle_check_decode(wire, o, n)
+                                                           for o in outs)}
+        del cols, wire, wires, outs
         torch.cuda.empty_cache()
     except Exception as e:  # report, never hide
         ex["decode_f64_1e8"] = {"error": repr(e)}
@@ -442,6 +549,19 @@ def extras_single_gpu(codec, stream, steps, warmup):
         assert st.n_rows == n and used == buf.numel()
         checked = oracle_check_archive(buf, out, m)
         b = buf.numel() + n * (8 + 1 + 8 + 4) + 13 * len(m.ctag)
+        # cpu_baseline: the reference reads an archive batch on one host core (reader.rs:449-477,
+        # Pack decode of the Vec<BatchItem>): the oracle's decode_archive, 1 core, a bounded
+        # sample (the whole batch, repeated for about 3 s)
+        host_buf = buf.cpu().numpy()
+        nxo = _nxo()
+        reps, t_cpu = 0, 0.0
+        while t_cpu < 3.0 or reps == 0:
+            t0 = time.perf_counter()
+            o, used_o = nxo.decode_archive(host_buf, cap_rows=n + 1, cap_children=len(m.ctag) + 1)
+            t_cpu += time.perf_counter() - t0
+            reps += 1
+            assert used_o == len(host_buf)
+        del o
         ex["archive_1e7"] = {"items": n, "batch_bytes": buf.numel(),
                              "decode_path": {5: "fast (nxg_fa_*)", 3: "exact (nxg_arch_*)"}.get(
                                  st.path, st.path),
@@ -450,7 +570,12 @@ def extras_single_gpu(codec, stream, steps, warmup):
                              "decode_hbm_frac": round(b / t_dec / 1e9 / HBM_PEAK_GBS, 4),
                              "encode_ms": round(t_enc * 1e3, 3),
                              "encode_M_items_s": round(n / t_enc / 1e6, 1),
-                             "oracle_items_checked": checked}
+                             "oracle_items_checked": checked,
+                             "cpu_baseline": {"value": round(n * reps / t_cpu / 1e6, 3),
+                                              "unit": "M items/s", "cores": 1, "kind": "port",
+                                              "sample": f"the whole {n}-item batch decoded "
+                                                        f"{reps}x ({t_cpu:.1f} s) by "
+                                                        "oracle/nx_oracle.c decode_archive"}}
         del mc, heap, buf, out
         torch.cuda.empty_cache()
     except Exception as e:
@@ -495,7 +620,9 @@ def extras_single_gpu(codec, stream, steps, warmup):
             "records": len(recs), "compressed_bytes": int(len(src)), "plain_bytes": int(tot),
             "ms": round(dt * 1e3, 3), "plain_GB_s": round(tot / dt / 1e9, 2),
             "note": "wall clock of nxg_archive_decompress from host records (H2D included); "
-                    "libzstd fixtures (dictionary, level 19) repeated; every byte checked"}
+                    "libzstd fixtures (dictionary, level 19) repeated; every byte checked",
+            "cpu_baseline": zstd_cpu_baseline(src, recs, want,
+                                              open(os.path.join(gold, "zstd_dict.bin"), "rb").read())}
         zdict.close()
         del out
         torch.cuda.empty_cache()
@@ -922,19 +1049,36 @@ def main():
 
     cols, wire = make_f64_wire(codec, n, rank)
     nbytes = wire.numel()
-    out = Columns(n, 0, 0, netidx_amd.LAYOUT_F64, "cuda")
-    wall, kms, st = time_decode(codec, wire, out, n, args.steps, args.warmup, world, stream,
+    # three distinct frames and column sets, decoded in rotation: each decode streams from HBM
+    # (working set 3 x (W + 16 N) = 924 MB at 10^7 records, past 3 x the 256 MiB Infinity Cache)
+    wires = [wire, wire.clone(), wire.clone()]
+    outs = [Columns(n, 0, 0, netidx_amd.LAYOUT_F64, "cuda") for _ in range(3)]
+    wall, kms, st = time_decode(codec, wires, outs, n, args.steps, args.warmup, world, stream,
                                 stream_of_frames=True)
     assert st.err_kind == 0 and st.path == 1 and st.n_rows == n, st
-    # the same frames one call each (probe and emit as two launches per frame), for comparison
-    wall1, kms1, st1 = time_decode(codec, wire, out, n, max(20, args.steps // 4), 2, world, stream)
+    kname = f64_kernel_name(codec)
+    # the same frame into the same columns every time (cache-assisted; earlier rounds' method)
+    _, kms_same, st1 = time_decode(codec, wire, outs[0], n, max(20, args.steps // 4), 2, world,
+                                   stream, stream_of_frames=True)
     assert st1.err_kind == 0 and st1.path == 1 and st1.n_rows == n, st1
-    # checker, outside the timed region: every row against the oracle's decode of the same bytes
-    checked = oracle_check_decode(wire, out, n) if rank == 0 else 0
+    # the length-run decoder (any f64 frame; probe of frame j + 1 fused into the emit of frame j)
+    crun = codec_run_path(local)
+    crun.set_stream(stream.cuda_stream)
+    _, kms_run, st2 = time_decode(crun, wires, outs, n, max(20, args.steps // 4), 2, world,
+                                  stream, stream_of_frames=True)
+    assert st2.err_kind == 0 and st2.path == 1 and st2.n_rows == n, st2
+    crun.close()
+    # checker, outside the timed regions: every row of every column set against the oracle's
+    # decode of the same bytes
+    checked = sum(oracle_check_decode(wire, o, n) for o in outs) if rank == 0 else 0
 
     value = world * n * args.steps / wall / 1e6
     alg_bytes = nbytes + 16 * n
     achieved = alg_bytes / (kms / 1e3) / 1e9
+
+    def frac(ms):
+        return round(alg_bytes / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4)
+
     line = {
         "metric": "Value-batch decode: M updates/s/GPU + GiB/s (device-resident) vs HBM roofline",
         "value": round(value, 2),
@@ -948,7 +1092,7 @@ def main():
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic (SplitMix64 f64 values, sequential ids; wire made by the product "
-                "encoder)",
+                "encoder); 3 distinct frames decoded in rotation into 3 column sets",
         "config": {"workload": "decode 10^7-record all-f64 From::Update batch per GPU "
                                "(BASELINE configs[1])",
                    "records_per_gpu": n, "wire_bytes_per_gpu": nbytes,
@@ -958,18 +1102,21 @@ def main():
         "gib_per_s": round(world * alg_bytes * args.steps / wall / 2**30, 2),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": read_traffic(n),
+                     "traffic": read_traffic(n, kname),
                      "traffic_source": "profiles/pmc_dec_f64.json (rocprofv3 FETCH_SIZE x2 + "
                                        "WRITE_SIZE per decode, committed; not measured in this run)",
-                     "kernel": KERNEL_DEC_F64 + " (emit of frame j + probe of frame j+1)",
+                     "kernel": kname,
                      "kernel_ms": round(kms, 4), "algorithmic_bytes_per_launch": alg_bytes,
-                     "timed": "HIP events on the codec stream around the whole stream of frames "
-                              "(nxg_decode_frames_async: " + " / ".join(KERNELS_DEC_F64) +
-                              "), divided by the frames"},
-        "per_call": {"kernel_ms": round(kms1, 4),
-                     "frac": round(alg_bytes / (kms1 / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
-                     "timed": "one nxg_decode_updates_async per frame: nxg_f64r_probe_kernel + "
-                              "nxg_f64r_emit_kernel"},
+                     "timed": "HIP events on the codec stream around the whole backlog of frames "
+                              "(nxg_decode_frames_async), divided by the frames; 3 distinct "
+                              "frames and column sets in rotation (every decode from HBM)"},
+        "same_frame": {"kernel_ms": round(kms_same, 4), "frac": frac(kms_same),
+                       "timed": "one frame into one column set every time (rounds 1-3's method: "
+                                "partly served by the Infinity Cache)"},
+        "length_run_decoder": {"kernel_ms": round(kms_run, 4), "frac": frac(kms_run),
+                               "kernels": " / ".join(KERNELS_DEC_F64),
+                               "timed": "NXG_F64_PATH=run: the decoder of any f64 frame, the 3 "
+                                        "frames in rotation as one backlog"},
     }
     if rank == 0 and world == 1:
         host = wire.cpu().numpy()

@@ -43,6 +43,7 @@ constexpr int kStatusRing = 1024;  // at most kStatusRing/2 async calls in fligh
 
 }  // namespace
 
+uint32_t nxg_patience = 128;
 thread_local DevStatus* nxg_zero_slot = nullptr;
 thread_local bool nxg_zero_used = false;
 
@@ -677,6 +678,9 @@ NxgCtx* nxg_ctx_new(int device, NetidxError* err) {
     c->no_fmx = mp && strcmp(mp, "general") == 0;
     const char* ap = getenv("NXG_ARCH_PATH");
     c->no_fa = ap && strcmp(ap, "exact") == 0;
+    // (process-wide, set by every context created: tests make one with 0 and then a default one)
+    const char* lp = getenv("NXG_LOOKBACK_PATIENCE");
+    nxg_patience = lp ? (uint32_t)strtoul(lp, nullptr, 0) : 128u;
     const char* ff = getenv("NXG_F64R_FLAGS");
     c->f64r_flags = ff ? (uint32_t)strtoul(ff, nullptr, 0) : 0u;
     return c;

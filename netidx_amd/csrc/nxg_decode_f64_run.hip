@@ -45,8 +45,7 @@ constexpr uint32_t T = NXG_F64R_T;  // tile bytes (the probe's unit)
 constexpr uint32_t EREC = NXG_F64R_EREC;  // records per emit wave (a tile's records, in order)
 constexpr uint32_t ESUB = (T / 12 + EREC) / EREC;  // emit waves per tile (records >= 12 B)
 static_assert(T + 16 <= 65535, "Desc.x is 16 bits");
-constexpr uint32_t SUB = 4096;    // exact path: LDS image of 64 chunks of 64 bytes
-constexpr uint32_t HALO = 128;    // look-ahead bytes past the image (merge walks, records)
+constexpr uint32_t IMGB = f64rec16::kXImg;  // exact path (nxg_f64_rec16.h): LDS image per wave
 constexpr int TPB = 256;
 constexpr uint32_t MODE_EXACT = 0;  // Desc.mode: 12..16 = uniform record length
 
@@ -74,134 +73,6 @@ static_assert(sizeof(Desc) == 16, "Desc is one 16-byte load");
 namespace {
 using namespace f64r;
 using namespace f64rec16;
-
-// Exact path for tile t, by the whole wave, in 4 KiB sub-tiles. A sub-tile at a0 owns the
-// records that START in [a0, a0 + 4096), like a uniform tile. Its LDS image holds the bytes
-// [a0 - 64, a0 + 4096 + HALO) (image offset = position - a0 + 64). Lane j walks the chain from
-// the merge point of chunk j to that of chunk j + 1; lane 0 starts one chunk earlier (the chunk
-// before a0, whose merge point precedes a0: the frame start for a0 = 0), so the walks cover
-// every record from before a0 to past a0 + 4096, and each record is counted by exactly one lane.
-// Returns (wave-uniform) the record count, the entry (first start - t0), the exit x (first start
-// at or past t0 + T, or the frame end, minus t0) and `bad`. With EMIT the records go to rows
-// base + index (a rare path: plain stores).
-constexpr uint32_t XLO = 64;            // image offset of a0
-constexpr uint32_t XHI = XLO + SUB;     // image offset of a0 + 4096
-constexpr uint32_t IMGB = XHI + HALO;   // image bytes
-// `pre`: bytes readable before wire[0] (a byte range that does not start the frame)
-template <bool EMIT>
-NXG_DEV void exact_tile(const uint8_t* __restrict__ wire, uint64_t W, uint64_t R, bool first,
-                        uint64_t pre, uint64_t t, uint8_t* buf, uint32_t lane, uint64_t base,
-                        uint64_t* __restrict__ oid, uint64_t* __restrict__ oval, uint64_t cap,
-                        uint32_t& count, uint32_t& entry, uint32_t& x, bool& bad, bool& over) {
-    const uint64_t t0 = t * T;
-    count = 0;
-    entry = 0;
-    x = 0;
-    uint32_t prev_exit = 0;
-    for (uint32_t s = 0; s < T / SUB; s++) {
-        const uint64_t a0 = t0 + (uint64_t)s * SUB;
-        if (a0 >= R) break;
-        // records that START before the range end are this range's (a range decode: R < W)
-        const uint32_t xhi = XLO + (R - a0 < SUB ? (uint32_t)(R - a0) : SUB);
-        const uint64_t ib = a0 - XLO;  // frame position of image byte 0 (wraps for a0 = 0)
-        wave_lds_order();
-#pragma unroll
-        for (uint32_t i = 0; i < (IMGB + 1023) / 1024; i++) {
-            const uint32_t off = i * 1024 + lane * 16;
-            if (off < IMGB) {
-                const int64_t pos = (int64_t)a0 - (int64_t)XLO + (int64_t)off;
-                const uint4 v = pos >= 0 ? ld16g(wire, (uint64_t)pos, W) : ld16_pre(wire, pos, W, pre);
-                *reinterpret_cast<uint4*>(buf + off) = v;
-            }
-        }
-        wave_lds_order();
-        // segment starts: lane 0 the chunk before a0, lane j >= 1 chunk j; ends: the next lane's
-        // start, lane 63 the merge point of the chunk at a0 + 4096
-        uint32_t xa;
-        if (lane == 0) xa = (a0 == 0 && first) ? XLO : merge16(buf, 0, ib, W);
-        else xa = merge16(buf, XLO + lane * 64, ib, W);
-        uint32_t xb = wave_next(xa);
-        if (lane == 63) xb = merge16(buf, XHI, ib, W);
-        bool b = xa == FAILX || xb == FAILX || xa > xb || (lane == 0 && xa > XLO);
-        // walk: count the records that start in [XLO, xhi); note the first start >= XLO (lane 0)
-        // and the first position >= xhi (the exit)
-        uint32_t n = 0, fst = FAILX, ex = FAILX;
-        if (!b) {
-            uint32_t pos = xa;
-            int guard = 0;
-            while (pos < xb && guard < 24) {
-                if (pos >= XLO && fst == FAILX) fst = pos;
-                if (pos >= xhi) {
-                    if (ex == FAILX) ex = pos;
-                } else {
-                    uint32_t e0, e1, e2, e3;
-                    lds16(buf, pos, e0, e1, e2, e3);
-                    const uint32_t L = rec_check16(e0, e1, W - (ib + pos));
-                    if (!L) break;
-                    if (pos >= XLO) n++;
-                    pos += L;
-                    guard++;
-                    continue;
-                }
-                // past the sub-tile: step by the length byte only (the next sub-tile checks it)
-                const uint32_t L = buf[pos];
-                if (L - 12u > 4u) break;
-                pos += L;
-                guard++;
-            }
-            b = pos != xb;
-            if (pos >= XLO && fst == FAILX) fst = pos;  // segment end (e.g. the frame end)
-            if (pos >= xhi && ex == FAILX) ex = pos;
-        }
-        if (__any(b)) {
-            bad = true;
-            return;
-        }
-        const uint32_t f0 = (uint32_t)__builtin_amdgcn_readlane((int)fst, 0);
-        const uint32_t exw = wave_min_u32(ex);
-        if (s == 0) entry = f0 - XLO;
-        else if (f0 != prev_exit) {  // the sub-tiles' chains must meet
-            bad = true;
-            return;
-        }
-        const uint32_t inc = wave_incl_scan(n);
-        if (EMIT) {
-            uint64_t row = base + count + (inc - n);
-            uint32_t pos = xa;
-            while (pos < xb && pos < xhi) {
-                uint32_t e0, e1, e2, e3;
-                lds16(buf, pos, e0, e1, e2, e3);
-                const uint32_t L = e0 & 0xffu;
-                if (pos >= XLO) {
-                    uint64_t id, val;
-                    rec_decode16(e0, e1, e2, e3, L, id, val);
-                    if (row < cap) {
-                        oid[row] = id;
-                        oval[row] = val;
-                    } else {
-                        over = true;
-                    }
-                    row++;
-                }
-                pos += L;
-            }
-        }
-        count += wave_last(inc);
-        // the chain leaves the sub-tile at exw (image offset); the frame end if it ends inside
-        const uint32_t endw = W - ib < (uint64_t)IMGB ? (uint32_t)(W - ib) : FAILX;
-        const uint32_t xo = exw != FAILX ? exw : endw;
-        if (xo == FAILX) {
-            bad = true;
-            return;
-        }
-        prev_exit = xo - SUB;  // the next sub-tile's entry, as an image offset
-        if (xhi < XHI && exw != FAILX) {  // the range ends inside this sub-tile
-            x = s * SUB + (xo - XLO);
-            break;
-        }
-        x = s * SUB + (xo - XLO);
-    }
-}
 
 }  // namespace
 
@@ -457,7 +328,7 @@ NXG_DEV void probe_body(const ProbeArgs& a, uint32_t bid, uint8_t (*img)[IMGB],
         em &= em - 1;
         uint32_t c, en, xx;
         bool b = false, ov = false;
-        exact_tile<false>(wire, W, R, first, pre, (uint64_t)bid * TPB + w * 64 + j,
+        exact_tile<false, T>(wire, W, R, first, pre, (uint64_t)bid * TPB + w * 64 + j,
                           img[w], lane, 0, nullptr, nullptr, 0, c, en, xx, b, ov);
         if (lane == j) {
             count = c;
@@ -837,7 +708,7 @@ NXG_DEV void emit_body(const EmitArgs& a, uint32_t blk, uint8_t (*img)[IMGB]) {
     } else {
         uint32_t c, en, xx;
         bool b = false;
-        exact_tile<true>(wire, W, R, flags & F_FIRST, pre, t, img[w], lane, D.base, a.oid, a.oval,
+        exact_tile<true, T>(wire, W, R, flags & F_FIRST, pre, t, img[w], lane, D.base, a.oid, a.oval,
                          a.cap, c, en, xx, b, over);
         bad |= b || c != D.count || en != D.entry || xx != D.x;
     }

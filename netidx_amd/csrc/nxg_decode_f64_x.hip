@@ -6,8 +6,9 @@
 // 1..5 varint bytes (< 2^35), records of 12..16 bytes.
 //
 // A wave takes SPW consecutive 4 KiB sub-tiles, a workgroup four waves (64 KiB), and no wave
-// waits on anything but lower-numbered workgroups (a decoupled look-back), so any number of these
-// decodes can share the GPU:
+// waits on a workgroup that may not be running (a decoupled look-back whose unpublished
+// predecessors are counted by the waiting workgroup itself), so any number of these decodes can
+// share the GPU:
 //   1. per sub-tile: its bytes and 64 / 128 around them into LDS (one coalesced pass; dwords
 //      stored swizzled, SwzImg, so that the lanes' 64-byte-strided reads do not pile onto two
 //      banks). Lane j takes the 64 positions of chunk j: S = the positions where a complete record
@@ -45,8 +46,8 @@ constexpr uint32_t MAXR = SUB / 12 + 2;  // rows per sub-tile (records start in 
 #define NXG_F64X_CB 6
 #endif
 #ifndef NXG_F64X_OCC
-#define NXG_F64X_OCC 0  // >0: waves per SIMD asked of the register allocator (A/B)
-#endif
+#define NXG_F64X_OCC 4  // waves per SIMD asked of the register allocator (the self-help path
+#endif                  // alone would push the kernel to 134 VGPRs, 3 waves)
 #ifndef NXG_F64X_CHEAP
 #define NXG_F64X_CHEAP 1  // 0: every candidate checked as a record before it counts as a start
 #endif                    // (10^7 random-order ids: 128.6 us, against 105.6 us for 1)
@@ -161,19 +162,123 @@ NXG_DEV void starts_of(const SwzImg& im, uint32_t r, uint64_t fp, uint64_t W, ui
 NXG_DEV uint64_t prev64(uint64_t v) { return dpp0_64<0x138, 0xf>(v); }
 NXG_DEV uint64_t next64(uint64_t v) { return dpp0_64<0x130, 0xf>(v); }
 
+// Phase 1 of one sub-tile whose image (at a0) is in `buf`: S (the chain's record starts in the
+// lane's chunk), n = |S|, the chain's entry into the next sub-tile in q (carried in; ~0 for a
+// wave's first sub-tile: found from the merge point before a0). `bad` when the starts are not a
+// chain. Wave-collective.
+NXG_DEV void subtile_starts(const uint8_t* __restrict__ wire, uint64_t W, uint8_t* buf, uint64_t a0,
+                            bool last_sub, uint32_t lane, uint64_t& q, uint64_t& Sm, uint32_t& n,
+                            bool& bad) {
+    const SwzImg im{buf};
+    const uint64_t ib = a0 - XLO;  // frame position of image byte 0 (wraps for a0 = 0)
+    const uint32_t r = XLO + lane * 64;
+    const uint64_t fp = ib + r;  // frame position of the lane's chunk
+    // The chain's entry into the sub-tile: the frame start, the previous sub-tile's exit, or
+    // (the wave's first sub-tile) a walk from the merge point of the 16 bytes at a0 - 64,
+    // where the walks from every valid-looking start meet (so on the true chain, records
+    // being at most 16 bytes long), to the first start at or past a0. Lane 0 alone.
+    if (a0 == 0) {
+        q = 0;
+    } else if (q == ~0ull) {
+        uint32_t x = FAILX;
+        if (lane == 0) {
+            x = merge16i(im, 0, ib, W);
+            while (x < XLO) {
+                uint32_t e0, e1, e2, e3;
+                lds16i(im, x, e0, e1, e2, e3);
+                const uint32_t L = rec_check16(e0, e1, W - (ib + x));
+                x = L ? x + L : FAILX;
+            }
+        }
+        x = (uint32_t)__builtin_amdgcn_readfirstlane((int)x);
+        if (x == FAILX) bad = true;
+        else q = ib + x;
+    }
+    const uint64_t inc = lane == 0 && q != ~0ull && q - a0 < 64 ? 1ull << (q - a0) : 0ull;
+    uint64_t S, slo, shi;
+    starts_of<16>(im, r, fp, W, S, slo, shi);
+    // lane 63: the starts among the 16 positions after the sub-tile. Inside the wave the next
+    // sub-tile's entry check covers them (LASTX), so only the wave's last sub-tile reads them.
+    const bool need_x = !NXG_F64X_LASTX || last_sub || a0 + SUB >= W;
+    uint64_t Sx = 0, xlo, xhi;
+    if (need_x) starts_of<4>(im, XHI, ib + XHI, W, Sx, xlo, xhi);
+    // False starts -- bytes inside a record that read as one (an f64's bytes may) -- are
+    // those no start leads to, or whose only predecessors are false: dropped until every
+    // start has a predecessor (in its chunk, the previous chunk, or the entry). What remains
+    // is exactly the chain through the sub-tile: each start leads back to the entry.
+    // The DPP moves run in every lane, the edge lanes' own terms OR-ed in: a DPP move in a
+    // branch reads 0 from a lane that is switched off.
+    uint64_t sin = prev64(shi) | inc;
+    for (int it = 0;; it++) {
+        const uint64_t roots = S & ~(slo | sin);
+        if (!__any(roots != 0)) break;
+        if (it == 64) {  // a long chain of false starts: the frame is rerun
+            bad = true;
+            break;
+        }
+        S &= ~roots;
+        slo = shi = 0;
+        for (uint64_t m = S; m; m &= m - 1) {
+            const uint32_t p = (uint32_t)__builtin_ctzll(m);
+            const uint32_t nx = p + im.byte(r + p);
+            if (nx < 64u) slo |= 1ull << nx;
+            else shi |= 1ull << (nx - 64u);
+        }
+        sin = prev64(shi) | inc;
+    }
+    const uint64_t Snx = next64(S) | (lane == 63 ? Sx : 0ull);  // the next chunk's starts
+    const uint64_t d = W - fp;  // (fp <= W below: the frame end's bit)
+    const uint64_t wlo = fp <= W && d < 64 ? 1ull << d : 0ull;
+    const uint64_t whi = fp <= W && d >= 64 && d < 128 ? 1ull << (d - 64) : 0ull;
+    const uint64_t shic = need_x || lane != 63 ? shi : 0ull;
+    bool b = (slo & ~(S | wlo)) != 0 ||  // a successor that is not a start
+             (shic & ~(Snx | whi)) != 0 ||
+             (inc & ~(S | wlo)) != 0;    // the entry is not a start
+#ifdef NXG_F64X_DIAG
+    if (b) nxg_f64x_diag(fp, S, slo, sin, shi, Snx, wlo, whi);
+#endif
+    bad |= b;
+    Sm = S;
+    n = (uint32_t)__popcll(S);
+    // the next sub-tile's entry: lane 63's last start + its length
+    uint64_t qn = ~0ull;
+    if (lane == 63 && S) {
+        const uint32_t pl = 63u - (uint32_t)__builtin_clzll(S);
+        qn = fp + pl + im.byte(r + pl);
+    }
+    q = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)qn, 63) |
+        ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(qn >> 32), 63) << 32);
+}
+
+// The record count of workgroup g's bytes, by one wave with its own LDS image `buf` (self-help:
+// the look-back's predecessor g has not published it): the f64 decoders' exact path
+// (nxg_f64_rec16.h exact_tile: merge points and lane walks), which counts the records that start
+// in the range. On a valid frame that is g's own count (both are the true chain's starts in g's
+// bytes); if the walks find no chain the frame is rerun (fast_fail), as g itself would.
+NXG_DEV uint64_t wg_count(const uint8_t* __restrict__ wire, uint64_t W, uint8_t* buf, uint64_t g,
+                          uint32_t lane, DevStatus* st) {
+    static_assert(IMGB == kXImg && SUB == kXSub && XLO == kXLo, "the exact path's image");
+    uint32_t c, en, xx;
+    bool b = false, ov = false;
+    exact_tile<false, (uint32_t)WGB>(wire, W, W, true, 0, g, buf, lane, 0, nullptr, nullptr, 0, c,
+                                     en, xx, b, ov);
+    if (b && lane == 0) atomicOr(&st->fast_fail, 1u);
+    return c;
+}
+
 __global__ __launch_bounds__(TPB, NXG_F64X_OCC) void nxg_f64x_kernel(const uint8_t* __restrict__ wire,
                                                        uint64_t W, uint64_t* __restrict__ oid,
                                                        uint64_t* __restrict__ oval, uint64_t cap,
                                                        uint64_t* tstat, uint32_t epoch,
                                                        DevStatus* __restrict__ st,
-                                                       DevStatus* zst) {
+                                                       DevStatus* zst, uint32_t patience) {
     zero_status(zst);
     __shared__ __attribute__((aligned(16))) uint8_t img[WAVES][IMGB];
     __shared__ __attribute__((aligned(16))) uint64_t rows[WAVES][MAXR][2];
     __shared__ uint64_t scan_tmp[WAVES];
     __shared__ uint64_t sh_base;
     const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    // (blockIdx order: a ticket counter measured 0.104 -> 0.120 ms at 10^7 records)
+    // (blockIdx order with self-help; a ticket counter measured 0.104 -> 0.120 ms at 10^7)
     const uint32_t bid = blockIdx.x;
     const uint64_t w0 = (uint64_t)bid * WGB + (uint64_t)w * SUB * SPW;  // the wave's bytes
     uint8_t* buf = img[w];
@@ -194,84 +299,7 @@ __global__ __launch_bounds__(TPB, NXG_F64X_OCC) void nxg_f64x_kernel(const uint8
         if (a0 >= W) continue;
         commit_image(buf, pf, lane);
         if (s + 1 < SPW) fetch_image(pf, wire, a0 + SUB, W, lane);  // the next, while checking
-        const uint64_t ib = a0 - XLO;  // frame position of image byte 0 (wraps for a0 = 0)
-        const uint32_t r = XLO + lane * 64;
-        const uint64_t fp = ib + r;  // frame position of the lane's chunk
-        // The chain's entry into the sub-tile: the frame start, the previous sub-tile's exit, or
-        // (the wave's first sub-tile) a walk from the merge point of the 16 bytes at a0 - 64,
-        // where the walks from every valid-looking start meet (so on the true chain, records
-        // being at most 16 bytes long), to the first start at or past a0. Lane 0 alone.
-        if (a0 == 0) {
-            q = 0;
-        } else if (q == ~0ull) {
-            uint32_t x = FAILX;
-            if (lane == 0) {
-                x = merge16i(im, 0, ib, W);
-                while (x < XLO) {
-                    uint32_t e0, e1, e2, e3;
-                    lds16i(im, x, e0, e1, e2, e3);
-                    const uint32_t L = rec_check16(e0, e1, W - (ib + x));
-                    x = L ? x + L : FAILX;
-                }
-            }
-            x = (uint32_t)__builtin_amdgcn_readfirstlane((int)x);
-            if (x == FAILX) bad = true;
-            else q = ib + x;
-        }
-        const uint64_t inc = lane == 0 && q != ~0ull && q - a0 < 64 ? 1ull << (q - a0) : 0ull;
-        uint64_t S, slo, shi;
-        starts_of<16>(im, r, fp, W, S, slo, shi);
-        // lane 63: the starts among the 16 positions after the sub-tile. Inside the wave the next
-        // sub-tile's entry check covers them (LASTX), so only the wave's last sub-tile reads them.
-        const bool need_x = !NXG_F64X_LASTX || s == SPW - 1 || a0 + SUB >= W;
-        uint64_t Sx = 0, xlo, xhi;
-        if (need_x) starts_of<4>(im, XHI, ib + XHI, W, Sx, xlo, xhi);
-        // False starts -- bytes inside a record that read as one (an f64's bytes may) -- are
-        // those no start leads to, or whose only predecessors are false: dropped until every
-        // start has a predecessor (in its chunk, the previous chunk, or the entry). What remains
-        // is exactly the chain through the sub-tile: each start leads back to the entry.
-        // The DPP moves run in every lane, the edge lanes' own terms OR-ed in: a DPP move in a
-        // branch reads 0 from a lane that is switched off.
-        uint64_t sin = prev64(shi) | inc;
-        for (int it = 0;; it++) {
-            const uint64_t roots = S & ~(slo | sin);
-            if (!__any(roots != 0)) break;
-            if (it == 64) {  // a long chain of false starts: the frame is rerun
-                bad = true;
-                break;
-            }
-            S &= ~roots;
-            slo = shi = 0;
-            for (uint64_t m = S; m; m &= m - 1) {
-                const uint32_t p = (uint32_t)__builtin_ctzll(m);
-                const uint32_t nx = p + im.byte(r + p);
-                if (nx < 64u) slo |= 1ull << nx;
-                else shi |= 1ull << (nx - 64u);
-            }
-            sin = prev64(shi) | inc;
-        }
-        const uint64_t Snx = next64(S) | (lane == 63 ? Sx : 0ull);  // the next chunk's starts
-        const uint64_t d = W - fp;  // (fp <= W below: the frame end's bit)
-        const uint64_t wlo = fp <= W && d < 64 ? 1ull << d : 0ull;
-        const uint64_t whi = fp <= W && d >= 64 && d < 128 ? 1ull << (d - 64) : 0ull;
-        const uint64_t shic = need_x || lane != 63 ? shi : 0ull;
-        bool b = (slo & ~(S | wlo)) != 0 ||  // a successor that is not a start
-                 (shic & ~(Snx | whi)) != 0 ||
-                 (inc & ~(S | wlo)) != 0;    // the entry is not a start
-#ifdef NXG_F64X_DIAG
-        if (b) nxg_f64x_diag(fp, S, slo, sin, shi, Snx, wlo, whi);
-#endif
-        bad |= b;
-        Sm[s] = S;
-        n[s] = (uint32_t)__popcll(S);
-        // the next sub-tile's entry: lane 63's last start + its length
-        uint64_t qn = ~0ull;
-        if (lane == 63 && S) {
-            const uint32_t pl = 63u - (uint32_t)__builtin_clzll(S);
-            qn = fp + pl + im.byte(r + pl);
-        }
-        q = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)qn, 63) |
-            ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(qn >> 32), 63) << 32);
+        subtile_starts(wire, W, buf, a0, s == SPW - 1, lane, q, Sm[s], n[s], bad);
     }
     const bool wbad = __any(bad);
     if (wbad && lane == 0) atomicOr(&st->fast_fail, 1u);
@@ -280,8 +308,18 @@ __global__ __launch_bounds__(TPB, NXG_F64X_OCC) void nxg_f64x_kernel(const uint8
     uint32_t ntot = 0;
 #pragma unroll
     for (int s = 0; s < SPW; s++) ntot += n[s];
-    // the first image of the emit pass, loading during the look-back
-    if (SPW > 1) fetch_image(pf, wire, w0, W, lane);
+    // the first image of the emit pass, loading during the look-back (waves 1..3; wave 0 runs the
+    // look-back, whose self-help path needs the registers)
+    if (SPW > 1 && w != 0) fetch_image(pf, wire, w0, W, lane);
+    // the start masks wait in the wave's (still unused) row buffer across the look-back, so that
+    // they hold no registers there
+    uint32_t* stash = reinterpret_cast<uint32_t*>(rows[w]);
+#pragma unroll
+    for (int s = 0; s < SPW; s++) {
+        stash[(3 * s) * 64 + lane] = (uint32_t)Sm[s];
+        stash[(3 * s + 1) * 64 + lane] = (uint32_t)(Sm[s] >> 32);
+        stash[(3 * s + 2) * 64 + lane] = n[s];
+    }
     uint64_t total;
     const uint64_t excl = block_excl_scan<uint64_t, TPB>((uint64_t)ntot, scan_tmp, &total);
     if (w == 0) {
@@ -290,16 +328,12 @@ __global__ __launch_bounds__(TPB, NXG_F64X_OCC) void nxg_f64x_kernel(const uint8
             if (lane == 0) st_agent(&tstat[0], lb_word(kFlagInc, epoch, total));
         } else {
             if (lane == 0) st_agent(&tstat[bid], lb_word(kFlagAgg, epoch, total));
-            bool give_up;
-            base = lookback_prefix<4>(tstat, bid, epoch, nullptr, give_up);
-            if (give_up) {
-                if (lane == 0) {
-                    atomicOr(&st->timeout, 1u);
-                    atomicOr(&st->fast_fail, 1u);
-                }
-            } else if (lane == 0) {
-                st_agent(&tstat[bid], lb_word(kFlagInc, epoch, base + total));
-            }
+            // no wait on a workgroup that may not be running: an unpublished predecessor's count
+            // is computed here from its bytes (self-help), in this wave's LDS image
+            base = lookback_selfhelp_fn(tstat, bid, epoch, patience, [&](uint64_t g) -> uint64_t {
+                return wg_count(wire, W, buf, g, lane, st);
+            });
+            if (lane == 0) st_agent(&tstat[bid], lb_word(kFlagInc, epoch, base + total));
         }
         if (lane == 0) sh_base = base;
         if (bid == gridDim.x - 1 && lane == 0) {
@@ -309,6 +343,13 @@ __global__ __launch_bounds__(TPB, NXG_F64X_OCC) void nxg_f64x_kernel(const uint8
     }
     __syncthreads();
     if (wbad) return;  // (a bad sub-tile has raised fast_fail: the frame is rerun)
+    if (SPW > 1 && w == 0) fetch_image(pf, wire, w0, W, lane);
+#pragma unroll
+    for (int s = 0; s < SPW; s++) {
+        Sm[s] = (uint64_t)stash[(3 * s) * 64 + lane] | ((uint64_t)stash[(3 * s + 1) * 64 + lane] << 32);
+        n[s] = stash[(3 * s + 2) * 64 + lane];
+    }
+    wave_lds_order();  // (the row buffer is written below)
     // the wave's first row: the block prefix of its lane 0
     uint64_t row0 = sh_base + ((uint64_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)excl) |
                                ((uint64_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(excl >> 32)) << 32));
@@ -378,6 +419,6 @@ hipError_t nxg_launch_dec_f64x(const uint8_t* wire, uint64_t W, uint64_t* oid, u
     if (ng == 0) return hipSuccess;
     if (ng > 0x7fffffffull) return hipErrorInvalidValue;
     hipLaunchKernelGGL(nxg_f64x_kernel, dim3((uint32_t)ng), dim3(TPB), 0, s, wire, W, oid, oval,
-                       cap, tstat, epoch, st, nxg_take_zero_slot());
+                       cap, tstat, epoch, st, nxg_take_zero_slot(), nxg_patience);
     return hipGetLastError();
 }

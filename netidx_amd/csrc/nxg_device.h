@@ -223,6 +223,50 @@ NXG_DEV uint64_t lookback_prefix(const uint64_t* tstat, uint32_t tile, uint32_t 
     return base;
 }
 
+// Exclusive prefix of `tile` over the epoch-tagged words tstat[0..tile), by one full wave, that
+// never depends on another workgroup being scheduled: a predecessor that has published nothing
+// after `patience` polls has its aggregate computed here by `count(t)` (wave-collective, returns
+// the wave-uniform aggregate of tile t, exactly what tile t itself publishes). Dispatch is in order
+// only per XCD: on a GPU shared by several processes an XCD can fall behind with the awaited
+// workgroup not yet dispatched, and a plain look-back would wait on it until the watchdog.
+template <typename F>
+NXG_DEV uint64_t lookback_selfhelp_fn(const uint64_t* tstat, uint32_t tile, uint32_t epoch,
+                                      uint32_t patience, F&& count) {
+    const uint32_t lane = lane_id();
+    uint64_t base = 0;
+    int64_t pred = (int64_t)tile - 1;
+#pragma unroll 1
+    while (pred >= 0) {
+        const int64_t idx = pred - (int64_t)lane;
+        uint64_t s = idx >= 0 ? ld_agent(&tstat[idx]) : lb_word(kFlagInc, epoch, 0);
+        uint32_t polls = 0;
+#pragma unroll 1
+        for (;;) {
+            const uint64_t f = lb_flag(s, epoch);
+            const uint64_t im = __ballot(f == kFlagInc);
+            const uint32_t lf = im ? (uint32_t)__builtin_ctzll(im) : 64u;
+            const uint64_t holes = __ballot(f == 0 && lane < lf);
+            if (!holes) break;  // every tile up to the nearest inclusive one has its count
+            if (++polls > patience) {
+                // the nearest hole's aggregate, computed here
+                const uint32_t h = (uint32_t)__builtin_ctzll(holes);
+                const uint64_t agg = count((uint64_t)(pred - (int64_t)h));
+                if (lane == h) s = lb_word(kFlagAgg, epoch, agg);
+                polls = 0;
+                continue;
+            }
+            __builtin_amdgcn_s_sleep(1);
+            if (f == 0 && idx >= 0) s = ld_agent(&tstat[idx]);
+        }
+        const uint64_t im = __ballot(lb_flag(s, epoch) == kFlagInc);
+        const uint32_t lf = im ? (uint32_t)__builtin_ctzll(im) : 64u;
+        base += wave_sum<uint64_t>(lane <= lf ? (s & kValMask) : 0ull);
+        if (im) break;
+        pred -= 64;
+    }
+    return base;
+}
+
 // exclusive scan over a 256-thread block; `tmp` = 4 (or more) T in LDS. Returns the exclusive
 // prefix, sets *total. Contains __syncthreads().
 template <typename T, int NT>

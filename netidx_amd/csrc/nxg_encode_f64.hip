@@ -77,54 +77,23 @@ NXG_DEV void put_rec_global(uint8_t* out, uint64_t o, uint64_t id, uint64_t val)
 // progresses: dispatch is in order only per XCD, and on a GPU shared by several processes an XCD
 // can fall behind with the awaited workgroup not yet dispatched (seen with 2-3 processes on one
 // device); a ticket counter instead cost 66 us at 10^7 records (one contended atomic per tile).
-#ifndef NXG_ENC_PATIENCE
-#define NXG_ENC_PATIENCE 128  // (0 in a test build: every unpublished predecessor counted here)
-#endif
-constexpr uint32_t kPatience = NXG_ENC_PATIENCE;
 NXG_DEV uint64_t lookback_selfhelp(const uint64_t* tstat, uint32_t tile, uint32_t epoch,
-                                   const uint64_t* __restrict__ id, uint64_t n, uint32_t lane) {
-    uint64_t base = 0;
-    int64_t pred = (int64_t)tile - 1;
-#pragma unroll 1
-    while (pred >= 0) {
-        const int64_t idx = pred - (int64_t)lane;
-        uint64_t s = idx >= 0 ? ld_agent(&tstat[idx]) : lb_word(kFlagInc, epoch, 0);
-        uint32_t polls = 0;
-#pragma unroll 1
-        for (;;) {
-            const uint64_t f = lb_flag(s, epoch);
-            const uint64_t im = __ballot(f == kFlagInc);
-            const uint32_t lf = im ? (uint32_t)__builtin_ctzll(im) : 64u;
-            const uint64_t holes = __ballot(f == 0 && lane < lf);
-            if (!holes) break;  // every tile up to the nearest inclusive one has its count
-            if (++polls > kPatience) {
-                // the nearest hole's byte count, from its ids
-                const uint32_t h = (uint32_t)__builtin_ctzll(holes);
-                const uint64_t r0 = (uint64_t)(pred - (int64_t)h) * ETILE;
-                uint64_t b = 0;
-                for (uint64_t r = r0 + lane; r < r0 + ETILE && r < n; r += 64) b += rec_len(id[r]);
-                const uint64_t agg = wave_sum<uint64_t>(b);
-                if (lane == h) s = lb_word(kFlagAgg, epoch, agg);
-                polls = 0;
-                continue;
-            }
-            __builtin_amdgcn_s_sleep(1);
-            if (f == 0 && idx >= 0) s = ld_agent(&tstat[idx]);
-        }
-        const uint64_t im = __ballot(lb_flag(s, epoch) == kFlagInc);
-        const uint32_t lf = im ? (uint32_t)__builtin_ctzll(im) : 64u;
-        base += wave_sum<uint64_t>(lane <= lf ? (s & kValMask) : 0ull);
-        if (im) break;
-        pred -= 64;
-    }
-    return base;
+                                   const uint64_t* __restrict__ id, uint64_t n, uint32_t lane,
+                                   uint32_t patience) {
+    // a hole's byte count from its ids
+    return lookback_selfhelp_fn(tstat, tile, epoch, patience, [&](uint64_t t) -> uint64_t {
+        const uint64_t r0 = t * ETILE;
+        uint64_t b = 0;
+        for (uint64_t r = r0 + lane; r < r0 + ETILE && r < n; r += 64) b += rec_len(id[r]);
+        return wave_sum<uint64_t>(b);
+    });
 }
 }  // namespace
 
 __global__ __launch_bounds__(TPB) void nxg_enc_f64_kernel(
     const uint64_t* __restrict__ id, const uint64_t* __restrict__ val, uint64_t n,
     uint8_t* __restrict__ out, uint64_t cap, uint64_t* __restrict__ tstat, uint32_t ntiles,
-    uint32_t epoch, DevStatus* __restrict__ st, DevStatus* zst) {
+    uint32_t epoch, DevStatus* __restrict__ st, DevStatus* zst, uint32_t patience) {
     zero_status(zst);
     __shared__ __attribute__((aligned(16))) uint8_t stg[MAXB_ALL];
     __shared__ uint32_t scan_tmp[4];
@@ -170,7 +139,7 @@ __global__ __launch_bounds__(TPB) void nxg_enc_f64_kernel(
         if (tid < 64) {
             uint64_t base = 0;
             if (tile != 0) {
-                base = lookback_selfhelp(tstat, tile, epoch, id, n, lane);
+                base = lookback_selfhelp(tstat, tile, epoch, id, n, lane, patience);
                 if (lane == 0) st_agent(&tstat[tile], lb_word(kFlagInc, epoch, base + tbytes));
             }
             if (lane == 0) sh_base = base;
@@ -243,7 +212,7 @@ hipError_t nxg_launch_enc_f64(const uint64_t* id, const uint64_t* val, uint64_t 
     if (nt == 0) return hipSuccess;
     const uint64_t g = grid <= 0 ? nt : (nt < (uint64_t)grid ? nt : (uint64_t)grid);
     hipLaunchKernelGGL(nxg_enc_f64_kernel, dim3(g), dim3(TPB), 0, s, id, val, n, out, cap, tstat,
-                       (uint32_t)nt, epoch, st, nxg_take_zero_slot());
+                       (uint32_t)nt, epoch, st, nxg_take_zero_slot(), nxg_patience);
     return hipGetLastError();
 }
 

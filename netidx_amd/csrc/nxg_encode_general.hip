@@ -296,6 +296,34 @@ NXG_DEV uint64_t ctl_upto(const uint64_t* ctl_row, uint64_t n_ctl, uint64_t r) {
     return lo;
 }
 
+// Row r's message length exactly as the rows kernel sizes it (0 for a row whose value errs:
+// that tile reports the error itself).
+NXG_DEV uint64_t row_msg_len(const ColsDesc& c, uint64_t r, bool arch) {
+    const Slot v = get_slot(c, true, r);
+    uint64_t vlen = 0;
+    uint32_t err = 0;
+    const uint32_t cl = arch && v.tag == 0x40u ? (uint32_t)CLS_SCAL : value_class(v.tag);
+    switch (cl) {
+    case CLS_FIX8: vlen = 9; break;
+    case CLS_TEXT: vlen = 1 + vl64(v.aux) + v.aux; break;
+    case CLS_TIME: vlen = 13; break;
+    case CLS_SCAL:
+        vlen = arch && v.tag == 0x40u ? 1 : scalar_len(v);
+        if (!vlen) vlen = value_len(c, true, r, &err);
+        break;
+    case CLS_ARR: {
+        bool flat;
+        vlen = row_len_flat(c, r, flat);
+        if (!flat) vlen = value_len(c, true, r, &err);
+        break;
+    }
+    default: vlen = value_len(c, true, r, &err); break;
+    }
+    const uint64_t ml = err ? 0ull : arch ? vl64((uint32_t)c.id[r]) + vlen : lwlen(1 + vl64(c.id[r]) + vlen);
+    if (!err && ml > (arch ? 0xFFFFFFFFull : 0x3FFFFFFFull)) return 0;
+    return ml;
+}
+
 }  // namespace
 
 // exclusive prefix of ctl_len into ctl_pre[0..n_ctl] (one workgroup)
@@ -317,7 +345,7 @@ __global__ __launch_bounds__(TPB) void nxg_enc_rows_kernel(
     ColsDesc c, const uint8_t* __restrict__ heap, uint8_t* __restrict__ out, uint64_t cap,
     const uint64_t* __restrict__ ctl_pre, uint64_t* __restrict__ row_off,
     uint64_t* __restrict__ tstat, uint32_t ntiles, uint32_t epoch, DevStatus* __restrict__ st,
-    DevStatus* zst, uint64_t arch_base) {
+    DevStatus* zst, uint64_t arch_base, uint32_t patience) {
     const bool arch = arch_base != 0;
     zero_status(zst);
     __shared__ uint64_t tmp[4];
@@ -432,7 +460,17 @@ __global__ __launch_bounds__(TPB) void nxg_enc_rows_kernel(
 #if NXG_ENC_SKIP & 1
                 give_up = false;  // timing experiments only: no look-back (wrong offsets)
 #else
-                base = lookback_prefix<NXG_ENC_LBU>(tstat, tile, epoch, nullptr, give_up);
+                // no wait on a workgroup that may not be running: an unpublished predecessor's
+                // byte count is computed here from its rows (self-help)
+                give_up = false;
+                base = lookback_selfhelp_fn(
+                    tstat, tile, epoch, patience, [&](uint64_t t) -> uint64_t {
+                        const uint64_t q0 = t * GTILE;
+                        uint64_t b = 0;
+                        for (uint64_t r = q0 + lane; r < q0 + GTILE && r < n; r += 64)
+                            b += row_msg_len(c, r, arch);
+                        return wave_sum<uint64_t>(b);
+                    });
 #endif
                 if (give_up && lane == 0) atomicOr(&st->timeout, 1u);
                 if (lane == 0) st_agent(&tstat[tile], lb_word(kFlagInc, epoch, base + tot));
@@ -589,7 +627,7 @@ hipError_t nxg_launch_enc_general(const ColsDesc& cd, const uint8_t* heap, uint8
         const uint64_t g = grid <= 0 ? nt : (nt < (uint64_t)grid ? nt : (uint64_t)grid);
         hipLaunchKernelGGL(nxg_enc_rows_kernel, dim3(g), dim3(TPB), 0, s, cd, heap, out, cap,
                            cd.n_ctl ? ctl_pre : nullptr, row_off, tstat, (uint32_t)nt, epoch, st, nxg_take_zero_slot(),
-                           arch_base);
+                           arch_base, nxg_patience);
     }
     if (cd.n_ctl && out) {
         const uint64_t nb = (cd.n_ctl + TPB - 1) / TPB;

@@ -183,4 +183,138 @@ __device__ __attribute__((noinline)) uint4 ld16_pre(const uint8_t* __restrict__ 
     return make_uint4(v[0], v[1], v[2], v[3]);
 }
 
+// The exact path of the f64 decoders: records counted (and, with EMIT, decoded) by the whole wave
+// over 4 KiB sub-tiles whose LDS image holds kXImg bytes: [a0 - 64, a0 + 4096 + 128).
+constexpr uint32_t kXSub = 4096;              // bytes per sub-tile
+constexpr uint32_t kXHalo = 128;              // look-ahead past the sub-tile
+constexpr uint32_t kXLo = 64;                 // image offset of a0
+constexpr uint32_t kXHi = kXLo + kXSub;       // image offset of a0 + 4096
+constexpr uint32_t kXImg = kXHi + kXHalo;     // image bytes
+
+// Exact path for tile t (T bytes), by the whole wave, in 4 KiB sub-tiles. A sub-tile at a0 owns the
+// records that START in [a0, a0 + 4096), like a uniform tile. Its LDS image holds the bytes
+// [a0 - 64, a0 + 4096 + kXHalo) (image offset = position - a0 + 64). Lane j walks the chain from
+// the merge point of chunk j to that of chunk j + 1; lane 0 starts one chunk earlier (the chunk
+// before a0, whose merge point precedes a0: the frame start for a0 = 0), so the walks cover
+// every record from before a0 to past a0 + 4096, and each record is counted by exactly one lane.
+// Returns (wave-uniform) the record count, the entry (first start - t0), the exit x (first start
+// at or past t0 + T, or the frame end, minus t0) and `bad`. With EMIT the records go to rows
+// base + index (a rare path: plain stores).
+// `pre`: bytes readable before wire[0] (a byte range that does not start the frame)
+template <bool EMIT, uint32_t T>
+NXG_DEV void exact_tile(const uint8_t* __restrict__ wire, uint64_t W, uint64_t R, bool first,
+                        uint64_t pre, uint64_t t, uint8_t* buf, uint32_t lane, uint64_t base,
+                        uint64_t* __restrict__ oid, uint64_t* __restrict__ oval, uint64_t cap,
+                        uint32_t& count, uint32_t& entry, uint32_t& x, bool& bad, bool& over) {
+    const uint64_t t0 = t * T;
+    count = 0;
+    entry = 0;
+    x = 0;
+    uint32_t prev_exit = 0;
+    for (uint32_t s = 0; s < T / kXSub; s++) {
+        const uint64_t a0 = t0 + (uint64_t)s * kXSub;
+        if (a0 >= R) break;
+        // records that START before the range end are this range's (a range decode: R < W)
+        const uint32_t xhi = kXLo + (R - a0 < kXSub ? (uint32_t)(R - a0) : kXSub);
+        const uint64_t ib = a0 - kXLo;  // frame position of image byte 0 (wraps for a0 = 0)
+        wave_lds_order();
+#pragma unroll
+        for (uint32_t i = 0; i < (kXImg + 1023) / 1024; i++) {
+            const uint32_t off = i * 1024 + lane * 16;
+            if (off < kXImg) {
+                const int64_t pos = (int64_t)a0 - (int64_t)kXLo + (int64_t)off;
+                const uint4 v = pos >= 0 ? ld16g(wire, (uint64_t)pos, W) : ld16_pre(wire, pos, W, pre);
+                *reinterpret_cast<uint4*>(buf + off) = v;
+            }
+        }
+        wave_lds_order();
+        // segment starts: lane 0 the chunk before a0, lane j >= 1 chunk j; ends: the next lane's
+        // start, lane 63 the merge point of the chunk at a0 + 4096
+        uint32_t xa;
+        if (lane == 0) xa = (a0 == 0 && first) ? kXLo : merge16(buf, 0, ib, W);
+        else xa = merge16(buf, kXLo + lane * 64, ib, W);
+        uint32_t xb = wave_next(xa);
+        if (lane == 63) xb = merge16(buf, kXHi, ib, W);
+        bool b = xa == FAILX || xb == FAILX || xa > xb || (lane == 0 && xa > kXLo);
+        // walk: count the records that start in [kXLo, xhi); note the first start >= kXLo (lane 0)
+        // and the first position >= xhi (the exit)
+        uint32_t n = 0, fst = FAILX, ex = FAILX;
+        if (!b) {
+            uint32_t pos = xa;
+            int guard = 0;
+            while (pos < xb && guard < 24) {
+                if (pos >= kXLo && fst == FAILX) fst = pos;
+                if (pos >= xhi) {
+                    if (ex == FAILX) ex = pos;
+                } else {
+                    uint32_t e0, e1, e2, e3;
+                    lds16(buf, pos, e0, e1, e2, e3);
+                    const uint32_t L = rec_check16(e0, e1, W - (ib + pos));
+                    if (!L) break;
+                    if (pos >= kXLo) n++;
+                    pos += L;
+                    guard++;
+                    continue;
+                }
+                // past the sub-tile: step by the length byte only (the next sub-tile checks it)
+                const uint32_t L = buf[pos];
+                if (L - 12u > 4u) break;
+                pos += L;
+                guard++;
+            }
+            b = pos != xb;
+            if (pos >= kXLo && fst == FAILX) fst = pos;  // segment end (e.g. the frame end)
+            if (pos >= xhi && ex == FAILX) ex = pos;
+        }
+        if (__any(b)) {
+            bad = true;
+            return;
+        }
+        const uint32_t f0 = (uint32_t)__builtin_amdgcn_readlane((int)fst, 0);
+        const uint32_t exw = wave_min_u32(ex);
+        if (s == 0) entry = f0 - kXLo;
+        else if (f0 != prev_exit) {  // the sub-tiles' chains must meet
+            bad = true;
+            return;
+        }
+        const uint32_t inc = wave_incl_scan(n);
+        if (EMIT) {
+            uint64_t row = base + count + (inc - n);
+            uint32_t pos = xa;
+            while (pos < xb && pos < xhi) {
+                uint32_t e0, e1, e2, e3;
+                lds16(buf, pos, e0, e1, e2, e3);
+                const uint32_t L = e0 & 0xffu;
+                if (pos >= kXLo) {
+                    uint64_t id, val;
+                    rec_decode16(e0, e1, e2, e3, L, id, val);
+                    if (row < cap) {
+                        oid[row] = id;
+                        oval[row] = val;
+                    } else {
+                        over = true;
+                    }
+                    row++;
+                }
+                pos += L;
+            }
+        }
+        count += wave_last(inc);
+        // the chain leaves the sub-tile at exw (image offset); the frame end if it ends inside
+        const uint32_t endw = W - ib < (uint64_t)kXImg ? (uint32_t)(W - ib) : FAILX;
+        const uint32_t xo = exw != FAILX ? exw : endw;
+        if (xo == FAILX) {
+            bad = true;
+            return;
+        }
+        prev_exit = xo - kXSub;  // the next sub-tile's entry, as an image offset
+        if (xhi < kXHi && exw != FAILX) {  // the range ends inside this sub-tile
+            x = s * kXSub + (xo - kXLo);
+            break;
+        }
+        x = s * kXSub + (xo - kXLo);
+    }
+}
+
+
 }  // namespace f64rec16

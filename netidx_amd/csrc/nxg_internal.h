@@ -78,6 +78,11 @@ constexpr int TILE = TPB * RPT;        // records per tile
 constexpr int MAXB = TILE * 15 + 32;   // staging bytes (f64 records <= 15 B for ids < 2^28)
 }  // namespace f64enc
 
+// Polls of an unpublished look-back predecessor before its aggregate is computed by the waiting
+// workgroup itself (self-help look-backs); NXG_LOOKBACK_PATIENCE at context creation (tests: 0,
+// every unpublished predecessor computed).
+extern uint32_t nxg_patience;
+
 // launchers (each defined next to its kernel)
 struct ColsDesc;
 // Every launcher takes the call's status slot `st` and `zst`, the slot that the call 512 calls
