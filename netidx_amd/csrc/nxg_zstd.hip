@@ -709,6 +709,27 @@ bool nxg_zstd_build_defaults(NxzDefaults* o) {
 }
 
 void nxg_zstd_set_content(NxzDictDev* d, const uint8_t* dcontent) { d->content = dcontent; }
+
+// Not part of the ABI (tests, host only, no GPU): the Huffman tree description reader and the
+// dictionary parser on arbitrary bytes. Returns the bytes the tree used (0: rejected) / whether
+// the dictionary parses.
+extern "C" uint32_t nxg_debug_huf_weights(const uint8_t* p, uint32_t n, uint32_t* n_sym) {
+    uint8_t w[256];
+    FseCell fse[64];
+    int16_t norm[64];
+    uint16_t next[64];
+    uint32_t ns = 0, mb = 0;
+    const uint32_t u = read_huf_weights(p, n, w, &ns, &mb, fse, norm, next);
+    if (n_sym) *n_sym = ns;
+    return u;
+}
+extern "C" bool nxg_debug_zstd_dict_ok(const uint8_t* d, uint64_t n) {
+    NxzDictDev* o = new NxzDictDev();
+    uint64_t coff = 0;
+    const bool ok = nxg_zstd_build_dict(d, n, o, &coff);
+    delete o;
+    return ok;
+}
 uint64_t nxg_zstd_dict_dev_bytes() { return sizeof(NxzDictDev); }
 uint64_t nxg_zstd_defaults_bytes() { return sizeof(NxzDefaults); }
 uint64_t nxg_zstd_rec_bytes() { return sizeof(NxzRec); }

@@ -107,3 +107,33 @@ def test_errors_are_per_record(codec, fx):
     out, res = _run(codec, None, rec, es[:2], False)
     assert all(r[2] == 4 for r in res)
     zd.close()
+
+
+def test_crafted_frames_rejected_on_the_device(codec):
+    """crafted frames libzstd rejects (tests/golden/make_zstd_crafted.py) -- a Huffman
+    tree description of 256 weights, one without two weight-1 symbols, four-stream literals of
+    fewer than 6 bytes -- fail their record on the GPU too (a per-record error, never output), and
+    a good fixture record decompressed in the same call is unaffected."""
+    m = json.load(open(os.path.join(G, "zstd_crafted.json")))["cases"]
+    ents = json.load(open(os.path.join(G, "zstd_manifest.json")))["records"]
+    rec = open(os.path.join(G, "zstd_records.bin"), "rb").read()
+    plain = open(os.path.join(G, "zstd_plain.bin"), "rb").read()
+    good = [e for e in ents if not e["dict"] and not e["indexed"] and e["plain_len"]][0]
+    parts, recs = [], []
+    off = 0
+    for c in m:
+        f = bytes.fromhex(c["frame"])
+        r = (len(f) + 64).to_bytes(4, "big") + f  # generous plain length: the frame must fail
+        parts.append(r)
+        recs.append((off, len(r)))
+        off += len(r)
+    g = rec[good["rec_off"]:good["rec_off"] + good["rec_len"]]
+    parts.append(g)
+    recs.append((off, len(g)))
+    src = np.frombuffer(b"".join(parts), np.uint8)
+    out, res = codec.archive_decompress(src, recs, False, None)
+    for c, (oo, ol, er) in zip(m, res):
+        assert er != 0, c["name"]
+    oo, ol, er = res[-1]
+    assert er == 0 and out.cpu().numpy()[oo:oo + ol].tobytes() == \
+        plain[good["plain_off"]:good["plain_off"] + good["plain_len"]]

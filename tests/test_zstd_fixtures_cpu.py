@@ -66,3 +66,53 @@ def test_batch_payloads_decode_with_the_oracle():
         assert o.s.err_kind == 0 and used == len(p)
         n += 1
     assert n >= 40
+
+
+def _crafted():
+    return json.load(open(os.path.join(G, "zstd_crafted.json")))["cases"]
+
+
+def test_crafted_tree_descriptions_rejected_on_the_host():
+    """the Huffman tree reader shared by the host dictionary parser and the device
+    (nxg_zstd.h read_huf_weights) rejects what libzstd rejects -- a weight description that decodes
+    to 256 weights (libzstd stops at 255) and one without two weight-1 symbols -- and a dictionary
+    built on either fails to load. The fixture's own libzstd verdicts are asserted too; the real
+    archive dictionary's tree is the positive control."""
+    import ctypes as C
+    from netidx_amd.codec import lib
+    L = lib()
+    L.nxg_debug_huf_weights.restype = C.c_uint32
+    L.nxg_debug_huf_weights.argtypes = [C.c_char_p, C.c_uint32, C.POINTER(C.c_uint32)]
+    L.nxg_debug_zstd_dict_ok.restype = C.c_bool
+    L.nxg_debug_zstd_dict_ok.argtypes = [C.c_char_p, C.c_uint64]
+    ns = C.c_uint32(0)
+    d = load()[3]
+    assert L.nxg_debug_huf_weights(d[8:], len(d) - 8, C.byref(ns)) > 0 and ns.value > 1
+    assert L.nxg_debug_zstd_dict_ok(d, len(d))
+    seen = 0
+    for c in _crafted():
+        if c["dict"] is None:
+            continue
+        db = bytes.fromhex(c["dict"])
+        tree = db[8:]
+        assert L.nxg_debug_huf_weights(tree, len(tree), C.byref(ns)) == 0, c["name"]
+        assert not L.nxg_debug_zstd_dict_ok(db, len(db)), c["name"]
+        assert c["libzstd_dict"] in ("rejected", None) and c["libzstd_frame"] in ("rejected", None)
+        seen += 1
+    assert seen == 2
+
+
+def test_crafted_256_weight_description_is_what_it_says():
+    """The crafted FSE description really decodes to 256 weights whose sum rule holds (the case
+    the old bound let through), by the generator's independent restatement."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("mzc", os.path.join(G, "make_zstd_crafted.py"))
+    mzc = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mzc)
+    c = [x for x in _crafted() if x["name"] == "huf_256_weights"][0]
+    tree = bytes.fromhex(c["dict"])[8:]
+    hb = tree[0]
+    norm, log, used = mzc.read_ncount(tree[1:1 + hb], 15)
+    cells = mzc.build_fse(norm, log)
+    w = mzc.fse_weights(tree[1 + used:1 + hb], cells, log, 10**6)
+    assert len(w) == 256 and mzc.weights_ok(w)
