@@ -251,6 +251,14 @@ def lib():
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise CodecError(f"{LIB_PATH} missing: build it (python -c 'import __graft_entry__ as g; g.build()')")
+        # One HIP runtime per process: torch carries its own libamdhip64 and must load it before
+        # this library's NEEDED libamdhip64.so.7 is resolved (the loader then reuses torch's); if
+        # /opt/rocm's were loaded first, torch would find no GPU ("No HIP GPUs are available").
+        try:
+            import torch
+            torch.cuda.is_available()
+        except ImportError:
+            pass
         L = C.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
             if os.environ.get("NXG_LIB") and not hasattr(L, name):

@@ -610,6 +610,16 @@ extern "C" {
 const char* nxg_version(void) { return "nxg 0.1.0 gfx950"; }
 
 // Not part of the ABI: the last decode's kernel diagnostics (DevStatus::diag), for profiling.
+void nxg_debug_status(NxgCtx* c, unsigned long long out[6]) {
+    const DevStatus z{};
+    const DevStatus& h = c ? c->last : z;
+    out[0] = h.fast_fail;
+    out[1] = h.irregular;
+    out[2] = h.path;
+    out[3] = h.n_rows;
+    out[4] = h.err_kind;
+    out[5] = h.timeout;
+}
 void nxg_debug_diag(NxgCtx* c, unsigned long long out[8]) {
     for (int i = 0; i < 8; i++) out[i] = c ? c->last.diag[i] : 0;
 }
@@ -1701,7 +1711,79 @@ bool nxg_decode_range(NxgCtx* c, const uint8_t* dframe, uint64_t W, uint64_t beg
         set_err(err, "device look-back watchdog expired");
         return false;
     }
-    if (h.fast_fail) return true;  // ok = 0: not a homogeneous-f64 range
+    // (a copy: later attempts take other ring slots)
+    const DevStatus h0 = h;
+    c->last = h0;
+    bool declined = h0.fast_fail != 0;
+    if (declined && (h0.irregular & 3u) == 1u) {
+        // record lengths that vary record to record (ids in any order: a batch updating an
+        // arbitrary subset of a publisher's values): the single-pass decoder in range mode
+        DevStatus* st2;
+        uint32_t slot2;
+        if (!begin_call(c, &st2, &slot2, err)) return false;
+        bool ok2 = ensure_tstat(c, nxg_dec_f64x_groups(R), err);
+        if (ok2) {
+            const hipError_t e = nxg_launch_dec_f64x_range(dframe, W, begin, end, out->id,
+                                                           out->fixed, out->cap_rows, c->tstat,
+                                                           c->epoch, st2, c->stream);
+            if (e != hipSuccess) {
+                set_err(err, "range decode launch: %s", hipGetErrorString(e));
+                ok2 = false;
+            }
+        }
+        if (!end_call(c, err) || !ok2) return false;
+        HIPCHK(hipMemcpyAsync(c->hst + slot2, st2, sizeof(DevStatus), hipMemcpyDeviceToHost,
+                              c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        const DevStatus& h2 = c->hst[slot2];
+        c->last = h2;
+        if (!h2.fast_fail && h2.diag[2] && h2.diag[3]) {
+            rng->entry = begin + h2.diag[2] - 1;
+            rng->exit = begin + h2.diag[3] - 1;
+            rng->n_rows = h2.n_rows;
+            rng->ok = 1;
+            rng->err_kind = h2.capacity ? NXG_CAPACITY : 0;
+            out->n_rows = h2.n_rows;
+            out->layout = NXG_LAYOUT_F64;
+            return true;
+        }
+    }
+    if (declined && mixed_capable(out) && R < (1ull << 32)) {
+        // not an f64 frame: the fast mixed decoder in range mode (frames of short Updates and
+        // Heartbeats; anything it declines is ok = 0, for the caller to decode whole)
+        DevStatus* st2;
+        uint32_t slot2;
+        if (!begin_call(c, &st2, &slot2, err)) return false;
+        const ColsDesc d = desc_of(out);
+        bool ok2 = ensure_glws(c, nxg_fmx_scratch_bytes(R), err);
+        if (ok2) {
+            const hipError_t e = nxg_launch_dec_fmx_range(dframe, W, begin, end, d,
+                                                          reinterpret_cast<uint8_t*>(c->glws),
+                                                          c->wgs_fmx, st2, c->stream);
+            if (e != hipSuccess) {
+                set_err(err, "range decode launch: %s", hipGetErrorString(e));
+                ok2 = false;
+            }
+        }
+        if (!end_call(c, err) || !ok2) return false;
+        HIPCHK(hipMemcpyAsync(c->hst + slot2, st2, sizeof(DevStatus), hipMemcpyDeviceToHost,
+                              c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        const DevStatus& h2 = c->hst[slot2];
+        c->last = h2;
+        if (h2.fast_fail || h2.path != 4 || !h2.diag[2] || !h2.diag[3]) return true;  // ok = 0
+        rng->entry = begin + h2.diag[2] - 1;
+        rng->exit = begin + h2.diag[3] - 1;
+        rng->n_rows = h2.n_rows;
+        rng->ok = 1;
+        out->n_rows = h2.n_rows;
+        out->n_children = h2.n_children;
+        out->n_ctl = h2.n_ctl;
+        out->n_heartbeat = h2.n_heartbeat;
+        out->layout = NXG_LAYOUT_MIXED;
+        return true;
+    }
+    if (declined) return true;  // ok = 0: not a range these decoders take
     // Desc: base u64 | count u16 | ks u16 | x u16 | entry u8 | mode u8 (nxg_decode_f64_run.hip)
     uint16_t xl;
     memcpy(&xl, dl + 12, 2);

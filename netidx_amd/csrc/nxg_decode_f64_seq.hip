@@ -45,6 +45,10 @@ constexpr uint64_t kXcdMin = 256ull << 20;  // frames past the Infinity Cache (2
 #define NXG_F64S_LDS 0  // dynamic LDS per workgroup (A/B: caps the waves per CU)
 #endif
 constexpr uint32_t F_XCD = 1;
+#ifndef NXG_F64S_XRUN
+#define NXG_F64S_XRUN 64  // workgroups per XCD run (frames past the Infinity Cache)
+#endif
+constexpr uint64_t XRUN = NXG_F64S_XRUN;
 
 // pos(k), the byte where record k starts: record j is 12 + #{t in 1..4 : i0 + j >= 2^(7t)} bytes
 // long (ids < 2^35), so pos(k) = 12 k + sum_t clamp(i0 + k - 2^(7t), 0, k). Wave-uniform callers
@@ -58,24 +62,6 @@ NXG_DEV uint64_t pos_of(uint64_t i0, uint64_t k) {
         p += x < k ? x : k;
     }
     return p;
-}
-
-// Records in a frame of W bytes (approximately: the XCD remap needs only a balanced split). The
-// segment holding W by its start position, then the float quotient.
-NXG_DEV uint64_t records_est(uint64_t i0, uint64_t W) {
-    uint64_t k = 0, P = 0;
-    uint32_t L = 11u + vl64(i0);
-#pragma unroll
-    for (uint32_t t = 1; t <= 4; t++) {
-        const uint64_t B = 1ull << (7 * t);
-        if (B <= i0) continue;
-        const uint64_t kb = B - i0, pb = pos_of(i0, kb);
-        if (pb > W) break;
-        k = kb;
-        P = pb;
-        L = 12u + t;
-    }
-    return k + (uint64_t)((float)(W - P) * (1.0f / (float)L)) + 1;
 }
 
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
@@ -327,15 +313,16 @@ __global__ __launch_bounds__(f64s::TPB) void nxg_f64s_kernel(const uint8_t* __re
     uint64_t i0, v0;
     rec_decode16(h0.x, h0.y, h0.z, h0.w, hl, i0, v0);
     // Workgroups go to the 8 XCDs round-robin; a frame larger than the Infinity Cache streams from
-    // HBM, and there each XCD takes a contiguous eighth of the records (the remap is a bijection on
-    // the first nb workgroups, nb from an estimate of the record count; the rest keep their index).
+    // HBM, and there each XCD takes runs of XRUN consecutive workgroups' records (XRUN x 1024
+    // records, ~1 MB of wire): XCD x's k-th workgroup decodes run (k / XRUN) * 8 + x, at position
+    // k % XRUN. A bijection on the whole groups of 8 runs; the grid's last partial group keeps its
+    // indices. (No record count is needed: the waves past the frame's end exit.)
     uint64_t blk = blockIdx.x;
     if (flags & F_XCD) {
-        const uint64_t nb =
-            min((records_est(i0, W) + WREC * (TPB / 64) - 1) / (WREC * (TPB / 64)), (uint64_t)gridDim.x);
-        if (blk < nb) {
-            const uint64_t q = nb / 8, rr = nb % 8, x = blk % 8;
-            blk = x * q + min(x, rr) + blk / 8;
+        const uint64_t full = (uint64_t)gridDim.x / (8 * XRUN) * (8 * XRUN);
+        if (blk < full) {
+            const uint64_t x = blk % 8, k = blk / 8;
+            blk = ((k / XRUN) * 8 + x) * XRUN + k % XRUN;
         }
     }
     const uint64_t k0 = (blk * (TPB / 64) + w) * WREC;

@@ -61,6 +61,14 @@ namespace {
 using namespace f64x;
 using namespace f64rec16;
 
+// The decoded range: `wire` is its first byte, W the bytes from there to the frame's end, R <= W
+// the range's length (records that START before R are the range's; the bytes after are read as
+// look-ahead), `pre` bytes readable before wire[0], `first`: the range starts the frame.
+struct XRange {
+    uint64_t W, R, pre;
+    bool first;
+};
+
 // the image of the sub-tile at a0: frame bytes [a0 - 64, a0 + 4096 + 128), dwords swizzled.
 // fetch issues the loads into registers (the next sub-tile's, while this one is walked); commit
 // stores them into the wave's LDS image.
@@ -68,14 +76,14 @@ struct Prefetch {
     uint4 v[(IMGB + 1023) / 1024];
 };
 NXG_DEV void fetch_image(Prefetch& pf, const uint8_t* __restrict__ wire, uint64_t a0, uint64_t W,
-                         uint32_t lane) {
+                         uint32_t lane, uint64_t pre = 0) {
     if (a0 >= W) return;
 #pragma unroll
     for (uint32_t i = 0; i < (IMGB + 1023) / 1024; i++) {
         const uint32_t off = i * 1024 + lane * 16;
         if (off < IMGB) {
             const int64_t pos = (int64_t)a0 - (int64_t)XLO + (int64_t)off;
-            pf.v[i] = pos >= 0 ? ld16g(wire, (uint64_t)pos, W) : ld16_pre(wire, pos, W, 0);
+            pf.v[i] = pos >= 0 ? ld16g(wire, (uint64_t)pos, W) : ld16_pre(wire, pos, W, pre);
         }
     }
 }
@@ -166,9 +174,10 @@ NXG_DEV uint64_t next64(uint64_t v) { return dpp0_64<0x130, 0xf>(v); }
 // lane's chunk), n = |S|, the chain's entry into the next sub-tile in q (carried in; ~0 for a
 // wave's first sub-tile: found from the merge point before a0). `bad` when the starts are not a
 // chain. Wave-collective.
-NXG_DEV void subtile_starts(const uint8_t* __restrict__ wire, uint64_t W, uint8_t* buf, uint64_t a0,
-                            bool last_sub, uint32_t lane, uint64_t& q, uint64_t& Sm, uint32_t& n,
-                            bool& bad) {
+NXG_DEV void subtile_starts(const uint8_t* __restrict__ wire, const XRange& rg, uint8_t* buf,
+                            uint64_t a0, bool last_sub, uint32_t lane, uint64_t& q, uint64_t& Sm,
+                            uint32_t& n, bool& bad, DevStatus* st) {
+    const uint64_t W = rg.W, R = rg.R;
     const SwzImg im{buf};
     const uint64_t ib = a0 - XLO;  // frame position of image byte 0 (wraps for a0 = 0)
     const uint32_t r = XLO + lane * 64;
@@ -177,7 +186,7 @@ NXG_DEV void subtile_starts(const uint8_t* __restrict__ wire, uint64_t W, uint8_
     // (the wave's first sub-tile) a walk from the merge point of the 16 bytes at a0 - 64,
     // where the walks from every valid-looking start meet (so on the true chain, records
     // being at most 16 bytes long), to the first start at or past a0. Lane 0 alone.
-    if (a0 == 0) {
+    if (a0 == 0 && rg.first) {
         q = 0;
     } else if (q == ~0ull) {
         uint32_t x = FAILX;
@@ -238,8 +247,11 @@ NXG_DEV void subtile_starts(const uint8_t* __restrict__ wire, uint64_t W, uint8_
     if (b) nxg_f64x_diag(fp, S, slo, sin, shi, Snx, wlo, whi);
 #endif
     bad |= b;
-    Sm = S;
-    n = (uint32_t)__popcll(S);
+    // the range's records: the starts before R (the chain checks above used them all)
+    const uint64_t keep = fp >= R ? 0ull : (R - fp >= 64 ? ~0ull : (1ull << (R - fp)) - 1ull);
+    Sm = S & keep;
+    n = (uint32_t)__popcll(Sm);
+    if (a0 == 0 && lane == 0) st->diag[2] = q + 1;  // the range's entry (+1; 0: unknown)
     // the next sub-tile's entry: lane 63's last start + its length
     uint64_t qn = ~0ull;
     if (lane == 63 && S) {
@@ -248,6 +260,27 @@ NXG_DEV void subtile_starts(const uint8_t* __restrict__ wire, uint64_t W, uint8_
     }
     q = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)qn, 63) |
         ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(qn >> 32), 63) << 32);
+    if (R <= a0 + SUB) {
+        // the range ends in this sub-tile: its exit is the first start at or past R, else the
+        // chain's entry into the next sub-tile
+        const uint64_t past = S & ~keep;
+        const uint64_t fx = past ? fp + (uint64_t)__builtin_ctzll(past) : ~0ull;
+        const uint32_t lo = wave_min_u32((uint32_t)(fx == ~0ull ? 0xffffffffu : (uint32_t)(fx - a0)));
+        // (no start at or past R here: the end of the sub-tile's last record -- lane 63 may hold
+        // none, where the frame ends inside the sub-tile)
+        uint64_t qe = ~0ull;
+        if (S) {
+            const uint32_t pl = 63u - (uint32_t)__builtin_clzll(S);
+            qe = fp + pl + im.byte(r + pl);
+        }
+        const uint64_t hm = __ballot(S != 0);
+        const int hl = hm ? 63 - __builtin_clzll(hm) : 0;
+        const uint64_t qlast =
+            (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)qe, hl) |
+            ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(qe >> 32), hl) << 32);
+        const uint64_t ex = lo != 0xffffffffu ? a0 + lo : (hm ? qlast : q);
+        if (lane == 0) st->diag[3] = ex + 1;  // (+1; 0: unknown)
+    }
 }
 
 // The record count of workgroup g's bytes, by one wave with its own LDS image `buf` (self-help:
@@ -255,24 +288,25 @@ NXG_DEV void subtile_starts(const uint8_t* __restrict__ wire, uint64_t W, uint8_
 // (nxg_f64_rec16.h exact_tile: merge points and lane walks), which counts the records that start
 // in the range. On a valid frame that is g's own count (both are the true chain's starts in g's
 // bytes); if the walks find no chain the frame is rerun (fast_fail), as g itself would.
-NXG_DEV uint64_t wg_count(const uint8_t* __restrict__ wire, uint64_t W, uint8_t* buf, uint64_t g,
-                          uint32_t lane, DevStatus* st) {
+NXG_DEV uint64_t wg_count(const uint8_t* __restrict__ wire, const XRange& rg, uint8_t* buf,
+                          uint64_t g, uint32_t lane, DevStatus* st) {
     static_assert(IMGB == kXImg && SUB == kXSub && XLO == kXLo, "the exact path's image");
     uint32_t c, en, xx;
     bool b = false, ov = false;
-    exact_tile<false, (uint32_t)WGB>(wire, W, W, true, 0, g, buf, lane, 0, nullptr, nullptr, 0, c,
-                                     en, xx, b, ov);
+    exact_tile<false, (uint32_t)WGB>(wire, rg.W, rg.R, rg.first, rg.pre, g, buf, lane, 0, nullptr,
+                                     nullptr, 0, c, en, xx, b, ov);
     if (b && lane == 0) atomicOr(&st->fast_fail, 1u);
     return c;
 }
 
 __global__ __launch_bounds__(TPB, NXG_F64X_OCC) void nxg_f64x_kernel(const uint8_t* __restrict__ wire,
-                                                       uint64_t W, uint64_t* __restrict__ oid,
+                                                       XRange rg, uint64_t* __restrict__ oid,
                                                        uint64_t* __restrict__ oval, uint64_t cap,
                                                        uint64_t* tstat, uint32_t epoch,
                                                        DevStatus* __restrict__ st,
                                                        DevStatus* zst, uint32_t patience) {
     zero_status(zst);
+    const uint64_t W = rg.W, R = rg.R;
     __shared__ __attribute__((aligned(16))) uint8_t img[WAVES][IMGB];
     __shared__ __attribute__((aligned(16))) uint64_t rows[WAVES][MAXR][2];
     __shared__ uint64_t scan_tmp[WAVES];
@@ -287,7 +321,7 @@ __global__ __launch_bounds__(TPB, NXG_F64X_OCC) void nxg_f64x_kernel(const uint8
     uint32_t n[SPW];
     bool bad = false;
     Prefetch pf;
-    fetch_image(pf, wire, w0, W, lane);
+    fetch_image(pf, wire, w0, W, lane, rg.pre);
     // q: the frame position of the chain's first record start at or past the sub-tile, carried
     // from sub-tile to sub-tile of the wave (~0: not known -- the wave's first sub-tile)
     uint64_t q = ~0ull;
@@ -296,10 +330,11 @@ __global__ __launch_bounds__(TPB, NXG_F64X_OCC) void nxg_f64x_kernel(const uint8
         Sm[s] = 0;
         n[s] = 0;
         const uint64_t a0 = w0 + (uint64_t)s * SUB;
-        if (a0 >= W) continue;
+        if (a0 >= R) continue;
         commit_image(buf, pf, lane);
-        if (s + 1 < SPW) fetch_image(pf, wire, a0 + SUB, W, lane);  // the next, while checking
-        subtile_starts(wire, W, buf, a0, s == SPW - 1, lane, q, Sm[s], n[s], bad);
+        if (s + 1 < SPW && a0 + SUB < R)
+            fetch_image(pf, wire, a0 + SUB, W, lane, rg.pre);  // the next, while checking
+        subtile_starts(wire, rg, buf, a0, s == SPW - 1, lane, q, Sm[s], n[s], bad, st);
     }
     const bool wbad = __any(bad);
     if (wbad && lane == 0) atomicOr(&st->fast_fail, 1u);
@@ -310,7 +345,7 @@ __global__ __launch_bounds__(TPB, NXG_F64X_OCC) void nxg_f64x_kernel(const uint8
     for (int s = 0; s < SPW; s++) ntot += n[s];
     // the first image of the emit pass, loading during the look-back (waves 1..3; wave 0 runs the
     // look-back, whose self-help path needs the registers)
-    if (SPW > 1 && w != 0) fetch_image(pf, wire, w0, W, lane);
+    if (SPW > 1 && w != 0) fetch_image(pf, wire, w0, W, lane, rg.pre);
     // the start masks wait in the wave's (still unused) row buffer across the look-back, so that
     // they hold no registers there
     uint32_t* stash = reinterpret_cast<uint32_t*>(rows[w]);
@@ -331,7 +366,7 @@ __global__ __launch_bounds__(TPB, NXG_F64X_OCC) void nxg_f64x_kernel(const uint8
             // no wait on a workgroup that may not be running: an unpublished predecessor's count
             // is computed here from its bytes (self-help), in this wave's LDS image
             base = lookback_selfhelp_fn(tstat, bid, epoch, patience, [&](uint64_t g) -> uint64_t {
-                return wg_count(wire, W, buf, g, lane, st);
+                return wg_count(wire, rg, buf, g, lane, st);
             });
             if (lane == 0) st_agent(&tstat[bid], lb_word(kFlagInc, epoch, base + total));
         }
@@ -343,7 +378,7 @@ __global__ __launch_bounds__(TPB, NXG_F64X_OCC) void nxg_f64x_kernel(const uint8
     }
     __syncthreads();
     if (wbad) return;  // (a bad sub-tile has raised fast_fail: the frame is rerun)
-    if (SPW > 1 && w == 0) fetch_image(pf, wire, w0, W, lane);
+    if (SPW > 1 && w == 0) fetch_image(pf, wire, w0, W, lane, rg.pre);
 #pragma unroll
     for (int s = 0; s < SPW; s++) {
         Sm[s] = (uint64_t)stash[(3 * s) * 64 + lane] | ((uint64_t)stash[(3 * s + 1) * 64 + lane] << 32);
@@ -357,12 +392,12 @@ __global__ __launch_bounds__(TPB, NXG_F64X_OCC) void nxg_f64x_kernel(const uint8
 #pragma unroll
     for (int s = 0; s < SPW; s++) {
         const uint64_t a0 = w0 + (uint64_t)s * SUB;
-        if (a0 >= W) break;
+        if (a0 >= R) break;
         const uint32_t inc = wave_incl_scan<uint32_t>(n[s]);
         const uint32_t nw = wave_last<uint32_t>(inc);
         if (SPW > 1) {
             commit_image(buf, pf, lane);
-            if (s + 1 < SPW) fetch_image(pf, wire, a0 + SUB, W, lane);
+            if (s + 1 < SPW && a0 + SUB < R) fetch_image(pf, wire, a0 + SUB, W, lane, rg.pre);
         }
         // the lane's records (at most 6 start in 64 bytes), loaded together
         uint32_t k = inc - n[s];
@@ -410,15 +445,26 @@ __global__ __launch_bounds__(TPB, NXG_F64X_OCC) void nxg_f64x_kernel(const uint8
 
 uint64_t nxg_dec_f64x_groups(uint64_t W) { return (W + WGB - 1) / WGB; }
 
-// Decodes a whole frame of W bytes. `tstat` holds nxg_dec_f64x_groups(W) epoch-tagged words (no
-// initialisation needed).
+// Decodes the records that start in [begin, end) of a frame of W bytes (a whole frame: 0, W).
+// `tstat` holds nxg_dec_f64x_groups(end - begin) epoch-tagged words (no initialisation needed).
+// The range's entry (first record start at or past begin) and exit (at or past end), relative to
+// begin and + 1, go to DevStatus.diag[2] / diag[3].
+hipError_t nxg_launch_dec_f64x_range(const uint8_t* wire, uint64_t W, uint64_t begin,
+                                     uint64_t end, uint64_t* oid, uint64_t* oval, uint64_t cap,
+                                     uint64_t* tstat, uint32_t epoch, DevStatus* st,
+                                     hipStream_t s) {
+    if (begin > end || end > W) return hipErrorInvalidValue;
+    const uint64_t ng = nxg_dec_f64x_groups(end - begin);
+    if (ng == 0) return hipSuccess;
+    if (ng > 0x7fffffffull) return hipErrorInvalidValue;
+    const XRange rg{W - begin, end - begin, begin < 64 ? begin : 64, begin == 0};
+    hipLaunchKernelGGL(nxg_f64x_kernel, dim3((uint32_t)ng), dim3(TPB), 0, s, wire + begin, rg, oid,
+                       oval, cap, tstat, epoch, st, nxg_take_zero_slot(), nxg_patience);
+    return hipGetLastError();
+}
+
 hipError_t nxg_launch_dec_f64x(const uint8_t* wire, uint64_t W, uint64_t* oid, uint64_t* oval,
                                uint64_t cap, uint64_t* tstat, uint32_t epoch, DevStatus* st,
                                hipStream_t s) {
-    const uint64_t ng = nxg_dec_f64x_groups(W);
-    if (ng == 0) return hipSuccess;
-    if (ng > 0x7fffffffull) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(nxg_f64x_kernel, dim3((uint32_t)ng), dim3(TPB), 0, s, wire, W, oid, oval,
-                       cap, tstat, epoch, st, nxg_take_zero_slot(), nxg_patience);
-    return hipGetLastError();
+    return nxg_launch_dec_f64x_range(wire, W, 0, W, oid, oval, cap, tstat, epoch, st, s);
 }

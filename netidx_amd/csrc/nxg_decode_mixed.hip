@@ -310,6 +310,22 @@ NXG_DEV bool chunk_msgs(const uint8_t* img, uint32_t ce, uint32_t lane, uint32_t
     return true;
 }
 
+// The decoded range: `wire` is its first byte, W the bytes from there to the frame's end, R <= W
+// the range's length (messages that START before R are the range's; the rest is read as
+// look-ahead), base = the range's offset in the frame (text / control offsets are frame
+// offsets), first = the range starts the frame (tile 0 is entered at 0; else its entry is
+// guessed like any tile's). A whole frame: {W, W, 0, true}.
+struct FRange {
+    uint64_t W, R, base;
+    bool first;
+    // the end of tile t's messages (tile offset): the tile end, or the range's
+    NXG_DEV uint32_t lim(uint64_t t) const {
+        return (uint32_t)min<uint64_t>(TILE, R - t * TILE);
+    }
+    // the range's last tile, when the range ends the frame: its chain must end exactly there
+    NXG_DEV bool last(uint64_t t, uint64_t nt) const { return t + 1 == nt && R == W; }
+};
+
 // tile descriptor (count pass -> resolve -> emit)
 struct TileDesc {
     uint32_t entry, exit;  // tile offsets
@@ -344,15 +360,14 @@ NXG_DEV TileDesc count_from(const uint8_t* img, const Cands& cd, uint32_t e, uin
 // its entry: the first candidates of its first two chunks, in order, until one gives a complete
 // chain. A false guess whose chain merges into the true one gives the true exit but wrong counts:
 // the fix pass recounts such tiles from their predecessor's exit.
-NXG_DEV TileDesc count_tile(const uint8_t* img, uint64_t t, uint64_t nt, uint64_t W,
+NXG_DEV TileDesc count_tile(const uint8_t* img, uint64_t t, uint64_t nt, const FRange& rg,
                             uint32_t lane, uint64_t& bits) {
-    const uint64_t t0 = t * TILE;
-    const uint32_t lim = (uint32_t)min<uint64_t>(TILE, W - t0);
-    const bool last = t + 1 == nt;
+    const uint32_t lim = rg.lim(t);
+    const bool last = rg.last(t, nt);
     const Cands cd = lane_cands(img, lane, lim);
     TileDesc d{FAIL, FAIL, 0, 0};
     bits = 0;
-    if (t == 0) return count_from(img, cd, 0, lim, last, lane, bits);
+    if (t == 0 && rg.first) return count_from(img, cd, 0, lim, last, lane, bits);
     // the guesses: the first one-byte / Heartbeat candidates of chunks 0 and 1 (c0, c1)
     const uint32_t g00 = (uint32_t)__builtin_amdgcn_readlane((int)cd.c0, 0);
     const uint32_t g01 = (uint32_t)__builtin_amdgcn_readlane((int)cd.c1, 0);
@@ -377,7 +392,7 @@ NXG_DEV TileDesc count_tile(const uint8_t* img, uint64_t t, uint64_t nt, uint64_
 
 // count pass: one wave per tile
 __global__ __launch_bounds__(TPB) void nxg_fmx_count_kernel(const uint8_t* __restrict__ wire,
-                                                            uint64_t W, uint64_t nt,
+                                                            FRange rg, uint64_t nt,
                                                             TileDesc* __restrict__ td,
                                                             uint64_t* __restrict__ starts,
                                                             DevStatus* zst) {
@@ -388,10 +403,10 @@ __global__ __launch_bounds__(TPB) void nxg_fmx_count_kernel(const uint8_t* __res
     if (t >= nt) return;
     uint8_t* img = lds[w].img;
     TileRegs g;
-    tile_load(g, wire, t * TILE, W, lane);
+    tile_load(g, wire, t * TILE, rg.W, lane);
     tile_store(img, g, lane);
     uint64_t bits;
-    const TileDesc d = count_tile(img, t, nt, W, lane, bits);
+    const TileDesc d = count_tile(img, t, nt, rg, lane, bits);
     starts[t * 64 + lane] = bits;
     if (lane == 0) td[t] = d;
 }
@@ -403,8 +418,9 @@ __global__ __launch_bounds__(TPB) void nxg_fmx_count_kernel(const uint8_t* __res
 // elsewhere (a false guess, or the end of a long message) by a recount from its true entry, as
 // the wave that owns it does. FAIL: the chain breaks on the way. Lets a wave's first tile see past
 // the previous wave's recounts.
-NXG_DEV uint32_t exit_before(const uint8_t* __restrict__ wire, uint64_t W, uint64_t nt,
+NXG_DEV uint32_t exit_before(const uint8_t* __restrict__ wire, const FRange& rg, uint64_t nt,
                              const TileDesc* td, uint64_t t, uint8_t* img, uint32_t lane) {
+    const uint64_t W = rg.W;
     uint64_t k = t - 1;
 #pragma unroll 1
     for (uint32_t back = 0; k > 0 && back < 64; back++, k--) {
@@ -425,13 +441,13 @@ NXG_DEV uint32_t exit_before(const uint8_t* __restrict__ wire, uint64_t W, uint6
             continue;
         }
         const uint64_t t0 = k * TILE;
-        const uint32_t lim = (uint32_t)min<uint64_t>(TILE, W - t0);
+        const uint32_t lim = rg.lim(k);
         TileRegs g;
         tile_load(g, wire, t0, W, lane);
         tile_store(img, g, lane);
         const Cands cd = lane_cands(img, lane, lim);
         uint64_t bits;
-        x = count_from(img, cd, e, lim, k + 1 == nt, lane, bits).exit;
+        x = count_from(img, cd, e, lim, rg.last(k, nt), lane, bits).exit;
     }
     return x;
 }
@@ -444,7 +460,7 @@ NXG_DEV uint32_t exit_before(const uint8_t* __restrict__ wire, uint64_t W, uint6
 // capacities and writes the totals. The chain (every entry its predecessor's exit) is checked by
 // the emit pass. Frames are shorter than 2^32 bytes here, so both halves stay in 32 bits.
 __global__ __launch_bounds__(TPB) void nxg_fmx_resolve_kernel(
-    const uint8_t* __restrict__ wire, uint64_t W, uint64_t nt, const TileDesc* __restrict__ td,
+    const uint8_t* __restrict__ wire, FRange rg, uint64_t nt, const TileDesc* __restrict__ td,
     TileDesc* __restrict__ td2, uint64_t* __restrict__ starts, uint64_t* __restrict__ tloc,
     uint64_t* __restrict__ bsum, uint64_t* __restrict__ bpre, uint64_t* __restrict__ wexit,
     uint64_t cap_rows,
@@ -462,7 +478,8 @@ __global__ __launch_bounds__(TPB) void nxg_fmx_resolve_kernel(
     uint8_t* img = lds[w].img;
     // the exit the chain leaves the wave's previous tile at (FAIL: unknown), by the whole wave
     const uint64_t tw = tl - lane;  // the wave's first tile
-    uint32_t px0 = tw > 0 && tw < nt ? exit_before(wire, W, nt, td, tw, img, lane) : FAIL;
+    const uint64_t W = rg.W;
+    uint32_t px0 = tw > 0 && tw < nt ? exit_before(wire, rg, nt, td, tw, img, lane) : FAIL;
     if (tw > 0 && tw < nt && px0 == FAIL) {
         // no tile of the count pass to start from within 64 (frames of long messages): the
         // previous wave's exit after its recounts, which it publishes below. Only lower-numbered
@@ -507,13 +524,13 @@ __global__ __launch_bounds__(TPB) void nxg_fmx_resolve_kernel(
             const uint32_t ej = (uint32_t)__builtin_amdgcn_readlane((int)d.entry, (int)j);
             if (px == FAIL || px - TILE == ej) continue;
             const uint64_t t0 = t * TILE;
-            const uint32_t lim = (uint32_t)min<uint64_t>(TILE, W - t0);
+            const uint32_t lim = rg.lim(t);
             TileRegs g;
             tile_load(g, wire, t0, W, lane);
             tile_store(img, g, lane);
             const Cands cd = lane_cands(img, lane, lim);
             uint64_t bits;
-            const TileDesc r = count_from(img, cd, px - TILE, lim, t + 1 == nt, lane, bits);
+            const TileDesc r = count_from(img, cd, px - TILE, lim, rg.last(t, nt), lane, bits);
             starts[t * 64 + lane] = bits;
             if (lane == j) d = r;
             if (lane == 0) atomicAdd(&st->diag[5], 1ull);  // recounted tiles (diagnostics)
@@ -584,7 +601,7 @@ __global__ __launch_bounds__(TPB) void nxg_fmx_resolve_kernel(
 // by the wave), the rows (64 consecutive per store), and the array elements: their starts by a
 // walk per lane (by size), then one element per lane.
 __global__ __launch_bounds__(TPB) void nxg_fmx_emit_kernel(
-    const uint8_t* __restrict__ wire, uint64_t W, uint64_t nt, const TileDesc* __restrict__ td,
+    const uint8_t* __restrict__ wire, FRange rg, uint64_t nt, const TileDesc* __restrict__ td,
     const uint64_t* __restrict__ tloc, const uint64_t* __restrict__ bpre,
     const uint64_t* __restrict__ starts, ColsDesc cols, bool ctl_on, DevStatus* __restrict__ st) {
     __shared__ __attribute__((aligned(16))) EmitLds lds[TPB / 64];
@@ -599,7 +616,9 @@ __global__ __launch_bounds__(TPB) void nxg_fmx_emit_kernel(
     uint16_t* msg = lds[w].msg;
     uint32_t* el = lds[w].el;
     const lds_bytes limg = (lds_bytes)img;
+    const uint64_t W = rg.W;
     const uint64_t t0 = t * TILE;
+    const uint64_t t0f = rg.base + t0;  // the tile's offset in the frame (text, control spans)
     // message ends past this tile offset lie past the frame
     const uint32_t wend = (uint32_t)min<uint64_t>(W - t0, IMG);
     TileRegs g;
@@ -608,7 +627,11 @@ __global__ __launch_bounds__(TPB) void nxg_fmx_emit_kernel(
     const TileDesc d = td[t];
     // the chain: this tile is entered at its predecessor's exit (tile 0 at 0); the count pass
     // made the last tile end exactly at W
-    const uint32_t px = t ? td[t - 1].exit : TILE;
+    // (a range that does not start the frame: tile 0 is entered at its counted entry, which the
+    // caller links with the previous range's exit)
+    const uint32_t px = t ? td[t - 1].exit : (rg.first ? TILE : TILE + d.entry);
+    if (lane == 0 && t == 0) st->diag[2] = (uint64_t)d.entry + 1;  // the range's entry (+1)
+    if (lane == 0 && t + 1 == nt) st->diag[3] = t0 + d.exit + 1;  // its exit (+1)
     const uint64_t base = bpre[2 * (t / TPB)] + tloc[2 * t];
     uint64_t hnext = bpre[2 * (t / TPB) + 1] + tloc[2 * t + 1];  // next ctl slot (Heartbeats)
     const uint32_t nm = (d.rows & 0xffffu) + (d.rows >> 16);    // Updates + Heartbeats
@@ -648,7 +671,7 @@ __global__ __launch_bounds__(TPB) void nxg_fmx_emit_kernel(
         if (ishb && ctl_on) {
             const uint64_t c = hnext + hbefore;
             cols.ctl_row[c] = row;
-            cols.ctl_off[c] = t0 + p0;
+            cols.ctl_off[c] = t0f + p0;
             cols.ctl_len[c] = 2u;
             cols.ctl_variant[c] = 5u;
         }
@@ -672,7 +695,7 @@ __global__ __launch_bounds__(TPB) void nxg_fmx_emit_kernel(
                        g3 = up ? 0u : h[4];
         const uint32_t su = u & 3u;
         FV o = val_decode(upd ? tg : 1u, alignbyte(g1, g0, su), alignbyte(g2, g1, su),
-                          alignbyte(g3, g2, su), p + u, upd ? lim : p + u + 12u, true, t0);
+                          alignbyte(g3, g2, su), p + u, upd ? lim : p + u + 12u, true, t0f);
         if (NXG_FMX_SKIP & 4) o = FV{g0, tg, g1, lim, 0, 0, 0, true};
         // past the image: text only (the count pass), checked here from global memory
         const bool far = upd && lim > wend;
@@ -715,7 +738,7 @@ __global__ __launch_bounds__(TPB) void nxg_fmx_emit_kernel(
             cnext += rk;
             continue;
         }
-        bad = round_elements(img, lds[w].mark, el, kd, kpre, rk, o.end, lim, cnext, cols, t0, lane,
+        bad = round_elements(img, lds[w].mark, el, kd, kpre, rk, o.end, lim, cnext, cols, t0f, lane,
                              ntxt, st);
         if (bad) break;
         PMARK(5);
@@ -757,9 +780,16 @@ void nxg_fmx_wgs(int ncu, int* wgs) {
     wgs[1] = std::max(1, b) * ncu;
 }
 
-hipError_t nxg_launch_dec_fmx(const uint8_t* wire, uint64_t W, const ColsDesc& cols,
-                              uint8_t* scratch, const int* wgs, DevStatus* st, hipStream_t s) {
-    const uint64_t nt = nxg_fmx_tiles(W);
+// The messages that start in [begin, end) of a frame of W bytes (a whole frame: 0, W); rows,
+// children and control spans numbered from 0, text and control offsets in frame bytes; the
+// range's entry / exit (+1, relative to begin) in DevStatus.diag[2] / diag[3].
+hipError_t nxg_launch_dec_fmx_range(const uint8_t* wire, uint64_t W, uint64_t begin, uint64_t end,
+                                    const ColsDesc& cols, uint8_t* scratch, const int* wgs,
+                                    DevStatus* st, hipStream_t s) {
+    if (begin > end || end > W) return hipErrorInvalidValue;
+    const FRange rg{W - begin, end - begin, begin, begin == 0};
+    wire += begin;
+    const uint64_t nt = nxg_fmx_tiles(rg.R);
     if (nt == 0) return hipSuccess;
     uint8_t* p = scratch;
     auto take = [&](uint64_t bytes) {
@@ -784,13 +814,18 @@ hipError_t nxg_launch_dec_fmx(const uint8_t* wire, uint64_t W, const ColsDesc& c
     // latency of their own LDS walks, which more resident waves hide better
     (void)wgs;
     const uint32_t gc = (uint32_t)((nt + WV - 1) / WV);
-    hipLaunchKernelGGL(nxg_fmx_count_kernel, dim3(gc), dim3(TPB), 0, s, wire, W, nt, td, starts,
+    hipLaunchKernelGGL(nxg_fmx_count_kernel, dim3(gc), dim3(TPB), 0, s, wire, rg, nt, td, starts,
                        nxg_take_zero_slot());
     const bool ctl_on = cols.ctl_row && cols.ctl_off && cols.ctl_len && cols.ctl_variant;
-    hipLaunchKernelGGL(nxg_fmx_resolve_kernel, dim3((uint32_t)nb), dim3(TPB), 0, s, wire, W, nt,
+    hipLaunchKernelGGL(nxg_fmx_resolve_kernel, dim3((uint32_t)nb), dim3(TPB), 0, s, wire, rg, nt,
                        td, td2, starts, tloc, bsum, bpre, wexit, cols.cap_rows, cols.cap_children,
                        cols.cap_ctl, ctl_on, st);
-    hipLaunchKernelGGL(nxg_fmx_emit_kernel, dim3(gc), dim3(TPB), 0, s, wire, W, nt, td2, tloc,
+    hipLaunchKernelGGL(nxg_fmx_emit_kernel, dim3(gc), dim3(TPB), 0, s, wire, rg, nt, td2, tloc,
                        bpre, starts, cols, ctl_on, st);
     return hipGetLastError();
+}
+
+hipError_t nxg_launch_dec_fmx(const uint8_t* wire, uint64_t W, const ColsDesc& cols,
+                              uint8_t* scratch, const int* wgs, DevStatus* st, hipStream_t s) {
+    return nxg_launch_dec_fmx_range(wire, W, 0, W, cols, scratch, wgs, st, s);
 }

@@ -75,9 +75,31 @@ NXG_DEV uint64_t scalar_len(const Slot& s) {
     }
 }
 
+// The general walk's stack: kStk levels of (children left, next child slot), in LDS, one stack
+// per wave (the walk runs one lane at a time: one_lane_at_a_time). Kept out of registers and
+// scratch: a dynamically indexed private array would be scratch memory in every wave.
+constexpr int kStk = NXG_MAX_DEPTH + 2;
+struct WalkStack {
+    uint64_t rem[kStk];
+    uint64_t slot[kStk];
+};
+// f() for each lane with `want`, one lane at a time (uniform loop; the others wait)
+template <typename F>
+NXG_DEV void one_lane_at_a_time(bool want, F&& f) {
+    uint64_t m = __ballot(want);
+#pragma unroll 1
+    while (m) {
+        const uint32_t j = (uint32_t)__builtin_ctzll(m);
+        m &= m - 1;
+        if (lane_id() == j) f();
+    }
+}
+
 // |Value| for the value in (row?, slot), children included; 0 => error (*err set)
-NXG_DEV uint64_t value_len(const ColsDesc& c, bool row, uint64_t slot, uint32_t* err) {
-    uint64_t frem[NXG_MAX_DEPTH + 2], fslot[NXG_MAX_DEPTH + 2];
+NXG_DEV uint64_t value_len(const ColsDesc& c, bool row, uint64_t slot, uint32_t* err,
+                           WalkStack* stk) {
+    uint64_t* frem = stk->rem;
+    uint64_t* fslot = stk->slot;
     int top = -1, depth = 0;
     bool is_row = row;
     uint64_t cur = slot, total = 0;
@@ -171,8 +193,10 @@ struct Out {
     }
 };
 
-NXG_DEV void value_write(const ColsDesc& c, const uint8_t* heap, bool row, uint64_t slot, Out& w) {
-    uint64_t frem[NXG_MAX_DEPTH + 2], fslot[NXG_MAX_DEPTH + 2];
+NXG_DEV void value_write(const ColsDesc& c, const uint8_t* heap, bool row, uint64_t slot, Out& w,
+                         WalkStack* stk) {
+    uint64_t* frem = stk->rem;
+    uint64_t* fslot = stk->slot;
     int top = -1;
     bool is_row = row;
     uint64_t cur = slot;
@@ -298,27 +322,29 @@ NXG_DEV uint64_t ctl_upto(const uint64_t* ctl_row, uint64_t n_ctl, uint64_t r) {
 
 // Row r's message length exactly as the rows kernel sizes it (0 for a row whose value errs:
 // that tile reports the error itself).
-NXG_DEV uint64_t row_msg_len(const ColsDesc& c, uint64_t r, bool arch) {
+NXG_DEV uint64_t row_msg_len(const ColsDesc& c, uint64_t r, bool arch, WalkStack* stk) {
     const Slot v = get_slot(c, true, r);
     uint64_t vlen = 0;
     uint32_t err = 0;
     const uint32_t cl = arch && v.tag == 0x40u ? (uint32_t)CLS_SCAL : value_class(v.tag);
+    bool gen = false;
     switch (cl) {
     case CLS_FIX8: vlen = 9; break;
     case CLS_TEXT: vlen = 1 + vl64(v.aux) + v.aux; break;
     case CLS_TIME: vlen = 13; break;
     case CLS_SCAL:
         vlen = arch && v.tag == 0x40u ? 1 : scalar_len(v);
-        if (!vlen) vlen = value_len(c, true, r, &err);
+        gen = !vlen;
         break;
     case CLS_ARR: {
         bool flat;
         vlen = row_len_flat(c, r, flat);
-        if (!flat) vlen = value_len(c, true, r, &err);
+        gen = !flat;
         break;
     }
-    default: vlen = value_len(c, true, r, &err); break;
+    default: gen = true; break;
     }
+    one_lane_at_a_time(gen, [&] { vlen = value_len(c, true, r, &err, stk); });
     const uint64_t ml = err ? 0ull : arch ? vl64((uint32_t)c.id[r]) + vlen : lwlen(1 + vl64(c.id[r]) + vlen);
     if (!err && ml > (arch ? 0xFFFFFFFFull : 0x3FFFFFFFull)) return 0;
     return ml;
@@ -356,8 +382,10 @@ __global__ __launch_bounds__(TPB) void nxg_enc_rows_kernel(
     __shared__ uint16_t off_lds[GTILE];  // staging offset per row (tile-local index)
     __shared__ uint32_t len_lds[GTILE];  // message length per row (0: absent or erroring)
     __shared__ uint8_t cls_lds[GTILE];   // value class per row (CLS_GEN: the general walk)
+    __shared__ WalkStack wstk[TPB / 64];  // the general walk's stack, one per wave
     static_assert(GSTG < 65536, "staging offsets fit 16 bits");
     const uint32_t tid = threadIdx.x, lane = tid & 63;
+    WalkStack* const stk = &wstk[tid >> 6];
     const uint64_t n = c.n_rows;
     for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const uint64_t rt = (uint64_t)tile * GTILE;
@@ -410,6 +438,7 @@ __global__ __launch_bounds__(TPB) void nxg_enc_rows_kernel(
             const Slot v = get_slot(c, true, r);
             uint64_t vlen = 0;
             uint32_t err = 0;
+            bool gen = false;
             switch (cls_lds[rl]) {
             case CLS_FIX8: vlen = 9; break;
             case CLS_TEXT: vlen = 1 + vl64(v.aux) + v.aux; break;
@@ -418,7 +447,7 @@ __global__ __launch_bounds__(TPB) void nxg_enc_rows_kernel(
                 vlen = arch && v.tag == 0x40u ? 1 : scalar_len(v);
                 if (!vlen) {  // a tag the encoder does not write (17): the walk reports it
                     cls_lds[rl] = CLS_GEN;
-                    vlen = value_len(c, true, r, &err);
+                    gen = true;
                 }
                 break;
             case CLS_ARR: {
@@ -426,12 +455,14 @@ __global__ __launch_bounds__(TPB) void nxg_enc_rows_kernel(
                 vlen = row_len_flat(c, r, flat);
                 if (!flat) {
                     cls_lds[rl] = CLS_GEN;
-                    vlen = value_len(c, true, r, &err);
+                    gen = true;
                 }
                 break;
             }
-            default: vlen = value_len(c, true, r, &err); break;
+            default: gen = true; break;
             }
+            // Map, Error, nested containers: the general walk, one lane of the wave at a time
+            one_lane_at_a_time(gen, [&] { vlen = value_len(c, true, r, &err, stk); });
             // queue_send refuses a message longer than MAX_BATCH (channel.rs:178-181); that bound
             // also keeps the 32-bit staged lengths exact
             const uint64_t ml = err    ? 0ull
@@ -468,7 +499,7 @@ __global__ __launch_bounds__(TPB) void nxg_enc_rows_kernel(
                         const uint64_t q0 = t * GTILE;
                         uint64_t b = 0;
                         for (uint64_t r = q0 + lane; r < q0 + GTILE && r < n; r += 64)
-                            b += row_msg_len(c, r, arch);
+                            b += row_msg_len(c, r, arch, &wstk[0]);
                         return wave_sum<uint64_t>(b);
                     });
 #endif
@@ -532,8 +563,10 @@ __global__ __launch_bounds__(TPB) void nxg_enc_rows_kernel(
                 }
                 case CLS_ARR: row_write_flat(c, heap, r, w); break;
                 case CLS_SCAL: scalar_write(get_slot(c, true, r), heap, w); break;
-                default: value_write(c, heap, true, r, w); break;
+                default: break;
                 }
+                one_lane_at_a_time(cls_lds[rl] == CLS_GEN,
+                                   [&] { value_write(c, heap, true, r, w, stk); });
             }
             __syncthreads();
             const uint64_t end = tbase + tot;
@@ -577,7 +610,8 @@ __global__ __launch_bounds__(TPB) void nxg_enc_rows_kernel(
                             w.var(c.id[r]);
                         }
                         if (cls_lds[tid * GRPT + k] != CLS_GEN) row_write_flat(c, heap, r, w);
-                        else value_write(c, heap, true, r, w);
+                        one_lane_at_a_time(cls_lds[tid * GRPT + k] == CLS_GEN,
+                                           [&] { value_write(c, heap, true, r, w, stk); });
                     }
                 }
                 rpos += L[k];

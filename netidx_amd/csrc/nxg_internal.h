@@ -101,6 +101,12 @@ inline DevStatus* nxg_take_zero_slot() {
 // f64 decode of any f64 frame in one pass (nxg_decode_f64_x.hip): `tstat` holds
 // nxg_dec_f64x_groups(W) epoch-tagged words (no initialisation needed).
 uint64_t nxg_dec_f64x_groups(uint64_t W);
+// the records that start in [begin, end) of a W-byte frame; entry / exit (+1, relative to begin)
+// in DevStatus.diag[2] / diag[3]
+hipError_t nxg_launch_dec_f64x_range(const uint8_t* wire, uint64_t W, uint64_t begin,
+                                     uint64_t end, uint64_t* oid, uint64_t* oval, uint64_t cap,
+                                     uint64_t* tstat, uint32_t epoch, DevStatus* st,
+                                     hipStream_t s);
 hipError_t nxg_launch_dec_f64x(const uint8_t* wire, uint64_t W, uint64_t* oid, uint64_t* oval,
                                uint64_t cap, uint64_t* tstat, uint32_t epoch, DevStatus* st,
                                hipStream_t s);
@@ -161,6 +167,11 @@ uint64_t nxg_fmx_scratch_bytes(uint64_t W);
 void nxg_fmx_wgs(int ncu, int* wgs);  // persistent grid sizes (count, emit)
 hipError_t nxg_launch_dec_fmx(const uint8_t* wire, uint64_t W, const ColsDesc& cols,
                               uint8_t* scratch, const int* wgs, DevStatus* st, hipStream_t s);
+// the messages that start in [begin, end) of a W-byte frame (rows etc. from 0, text / control
+// offsets in frame bytes); entry / exit (+1, relative to begin) in DevStatus.diag[2] / diag[3]
+hipError_t nxg_launch_dec_fmx_range(const uint8_t* wire, uint64_t W, uint64_t begin, uint64_t end,
+                                    const ColsDesc& cols, uint8_t* scratch, const int* wgs,
+                                    DevStatus* st, hipStream_t s);
 // subscriber dispatch (nxg_dispatch.hip): `scratch` holds nxg_disp_scratch_bytes(n, n_chans)
 // bytes (no initialisation needed); `unmatched` one u64.
 uint64_t nxg_disp_scratch_bytes(uint64_t n, uint32_t n_chans);

@@ -386,8 +386,9 @@ bool nxg_decode_sharded(NxgCtx* ctx, NxgComm* comm, const uint8_t* dframe, uint6
         for (int i = 0; i < n; i++) memcpy(&all[i], &buf[(size_t)i * kSlotWords], sizeof(NxgRange));
         for (int i = 0; i < n; i++)
             if (!all[i].ok) {
-                set_err(err, "range %d is not a homogeneous-f64 range: decode the whole frame "
-                             "with nxg_decode_updates", i);
+                set_err(err, "range %d is not one the range decoders take (f64 frames; mixed "
+                             "frames of short Updates into mixed columns): decode the whole "
+                             "frame with nxg_decode_updates", i);
                 return false;
             }
         uint32_t bad = 0;

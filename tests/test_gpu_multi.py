@@ -1,5 +1,7 @@
 """Multi-GPU calls on one GPU: the byte-range decode of one frame (nxg_decode_range +
-nxg_range_link, the per-rank half of nxg_decode_sharded) and a one-rank RCCL communicator.
+nxg_range_link, the per-rank half of nxg_decode_sharded) -- ids counting up (the length-run
+decoder) and ids in any order (the single-pass decoder in range mode) -- and a one-rank RCCL
+communicator.
 
 The ranges of a frame are decoded one after another here, as N ranks would decode them at once;
 the cuts fall inside records (f64 records are 12-16 bytes), and the linked rows must be the
@@ -75,17 +77,114 @@ def test_byte_ranges_tiny_frames(codec):
         assert np.array_equal(np.concatenate([p["fixed"] for p in parts]), vals)
 
 
-def test_byte_ranges_irregular_frame_reports_not_ok(codec):
-    """Record lengths varying record to record: the length-run decoder declines (ok = 0) and
-    the caller decodes the whole frame."""
+@pytest.mark.parametrize("world", [2, 3, 8, 37])
+@pytest.mark.parametrize("kind", ["perm", "perm35", "planted"])
+def test_byte_ranges_random_order_ids(codec, world, kind):
+    """Ids in any order (a batch updating an arbitrary subset of a publisher's values,
+    publisher/mod.rs:776-845): record lengths vary record to record, the length-run probe
+    declines, and each range is decoded by the single-pass decoder in range mode (its entry from
+    the merge point of the 64 bytes before the range). Every row against the oracle; the ranges
+    meet. `planted`: f64 values whose bytes read as record headers (false starts) everywhere."""
     import nxo
     from netidx_amd import synth
-    n = 200_000
-    ids, vals = synth.f64_columns(n, 9)
-    ids = np.random.default_rng(3).permutation(ids)
+    n = 300_007
+    ids, vals = synth.f64_columns(n, 111)
+    rng = np.random.default_rng(world)
+    if kind == "perm35":
+        ids = rng.integers(0, 2**35, n, dtype=np.uint64)
+    else:
+        ids = rng.permutation(ids)
+    if kind == "planted":  # each value's bytes: 0x0c 0x04 ... (a 12-byte record header)
+        vals = (vals & np.uint64(0x0000ffffffffffff)) | np.uint64(0x0c04 << 48)
     wire = nxo.encode_f64(ids, vals)
-    rngs, parts, offs, bad = _ranges_decode(codec, wire, 2)
-    assert not all(r.ok for r in rngs) and offs is None
+    rngs, parts, offs, bad = _ranges_decode(codec, wire, world)
+    assert bad is None and all(r.ok for r in rngs), [(r.ok, r.entry, r.exit) for r in rngs]
+    got_id = np.concatenate([p["id"] for p in parts])
+    got_val = np.concatenate([p["fixed"] for p in parts])
+    o = nxo.decode(wire, cap_rows=n + 1, cap_children=1, cap_ctl=1).trim()
+    assert np.array_equal(got_id, o["id"]) and np.array_equal(got_val, o["fixed"])
+    assert rngs[0].entry == 0 and rngs[-1].exit == len(wire)
+    for a, b in zip(rngs, rngs[1:]):
+        assert a.exit == b.entry and b.begin <= b.entry < b.begin + 16
+
+
+def _mixed_wire(n, seed, ctl=False):
+    import nxo
+    from netidx_amd import synth
+    m = synth.mixed_columns(n, seed)
+    d = nxo.Decoded(len(m.id), len(m.ctag) + 1, 1)
+    for name in ("id", "tag", "fixed", "aux"):
+        getattr(d, name)[:len(m.id)] = getattr(m, name)
+    d.ctag[:len(m.ctag)] = m.ctag
+    d.cfixed[:len(m.ctag)] = m.cfixed
+    d.caux[:len(m.ctag)] = m.caux
+    d.s.n_rows, d.s.n_children, d.s.n_ctl = len(m.id), len(m.ctag), 0
+    w = nxo.encode(d, m.heap)
+    if ctl:  # a Heartbeat (02 05) after every 97th message
+        o = nxo.decode(np.frombuffer(w, np.uint8), cap_rows=n + 1, cap_children=len(m.ctag) + 1,
+                       cap_ctl=1)
+        b = np.frombuffer(w, np.uint8)
+        parts, p = [], 0
+        for k in range(n):
+            L = int(b[p]) if b[p] < 0x80 else (int(b[p]) & 0x7f) | (int(b[p + 1]) << 7)
+            parts.append(bytes(b[p:p + L]))
+            if k % 97 == 96:
+                parts.append(b"\x02\x05")
+            p += L
+        w = b"".join(parts)
+    return np.frombuffer(w, np.uint8)
+
+
+@pytest.mark.parametrize("world", [2, 3, 8, 37])
+@pytest.mark.parametrize("ctl", [False, True])
+def test_byte_ranges_mixed_frame(codec, world, ctl):
+    """A config-3 mixed frame (i64 / f64 / string / datetime / array values, ids in any order;
+    with `ctl` a Heartbeat every 97 messages) cut into byte ranges: the f64 decoders decline, the
+    fast mixed decoder takes each range in range mode (tile 0's entry guessed from its
+    candidates), the ranges meet, and every column of the concatenated ranges equals the
+    oracle's decode of the whole frame (child indices are per range: offset by the children of
+    the ranges before)."""
+    import netidx_amd
+    import nxo
+    import torch
+    from netidx_amd import shard
+    from netidx_amd.codec import Columns
+    n = 60_000
+    wire = _mixed_wire(n, 57 + world, ctl)
+    W = len(wire)
+    dw = torch.from_numpy(wire.copy()).cuda()
+    rngs, parts = [], []
+    for r in range(world):
+        b, e = shard.shard_range(W, world, r)
+        cols = Columns.for_frame(max(e - b, 16) + 64, netidx_amd.LAYOUT_MIXED, "cuda")
+        rng = codec.decode_range(dw, W, b, e, cols)
+        if not rng.ok:  # a false guessed entry: decoded again from the predecessor's exit
+            assert r > 0
+            at = rngs[-1].exit
+            rng = codec.decode_range(dw, W, min(at, e), e, cols)
+            rng.begin = b
+        rngs.append(rng)
+        parts.append(cols.numpy())
+    offs, bad = netidx_amd.range_link(rngs, W)
+    assert bad is None and all(r.ok for r in rngs), [(r.ok, r.entry, r.exit) for r in rngs]
+    o = nxo.decode(wire, cap_rows=n + 1, cap_children=8 * n + 1, cap_ctl=n + 1).trim()
+    cat = {k: np.concatenate([p[k] for p in parts]) for k in ("id", "tag", "aux", "ctag",
+                                                             "cfixed", "caux")}
+    for k in ("id", "tag", "aux", "ctag", "cfixed", "caux"):
+        assert np.array_equal(cat[k], o[k]), k
+    coff, fixed = 0, []
+    for p in parts:
+        f = p["fixed"].copy()
+        f[p["tag"] == 19] += np.uint64(coff)
+        fixed.append(f)
+        coff += len(p["ctag"])
+    assert np.array_equal(np.concatenate(fixed), o["fixed"])
+    if ctl:
+        assert sum(len(p["ctl_row"]) for p in parts) == len(o["ctl_row"])
+        assert np.array_equal(np.concatenate([p["ctl_off"] for p in parts]), o["ctl_off"])
+    assert rngs[0].entry == 0 and rngs[-1].exit == W
+    for a, b in zip(rngs, rngs[1:]):
+        assert a.exit == b.entry
 
 
 def test_rccl_one_rank_comm(codec):

@@ -101,3 +101,72 @@ def test_library_protocols_on_real_kernels(tmp_path, world):
     assert int(res[0][7]) == 0 and int(res[-1][8]) == W
     for a, b in zip(res, res[1:]):
         assert int(a[8]) == int(b[7])  # each range leaves where the next enters
+
+
+def _rank_mixed(rank, world, port, n_per, outdir):
+    """Config 3 over the library protocols: each rank's shard of a mixed batch encoded straight
+    into its place in the full frame (nxg_encode_allgather, the general encoder with the rank's
+    text heap), then the frame decoded in byte ranges (nxg_decode_sharded: the fast mixed decoder
+    in range mode, each range's entry guessed and linked, a range off the chain decoded again)."""
+    import torch
+    import torch.distributed as dist
+    import netidx_amd
+    import nxo
+    from netidx_amd import shard, synth
+    from netidx_amd.codec import Columns
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        codec = netidx_amd.Codec(0)
+        m = synth.mixed_columns(n_per, 700 + rank)
+        mc = netidx_amd.columns_from_arrays(m.id, m.fixed, m.tag, m.aux, m.ctag, m.cfixed, m.caux)
+        heap = torch.from_numpy(m.heap.copy()).cuda()
+        cap = 64 * n_per * world + 4096
+        dout = torch.zeros(cap, dtype=torch.uint8, device="cuda")
+        comm = shard.gloo_comm(codec, world, rank, [dout])
+        W, offs = comm.encode_allgather(mc, heap, dout.data_ptr(), cap)
+        frame = dout[:W].cpu().numpy()
+        o = nxo.decode(frame, cap_rows=n_per * world + 1, cap_children=16 * n_per * world + 1,
+                       cap_ctl=1).trim()
+        out = Columns.for_frame(W // world + 4096, netidx_amd.LAYOUT_MIXED, "cuda")
+        row_off, rng = comm.decode_sharded(dout, W, out)
+        g = out.numpy()
+        nr = int(rng.n_rows)
+        sl = slice(row_off, row_off + nr)
+        ok = all(np.array_equal(g[k], o[k][sl]) for k in ("id", "tag", "aux"))
+        arr = g["tag"] == 19
+        txt = ~arr
+        ok &= np.array_equal(g["fixed"][txt], o["fixed"][sl][txt])
+        if arr.any():
+            c0 = int(o["fixed"][sl][arr][0]) - int(g["fixed"][arr][0])  # children before the range
+            ok &= np.array_equal(g["fixed"][arr] + np.uint64(c0), o["fixed"][sl][arr])
+            nc = len(g["ctag"])
+            for k in ("ctag", "cfixed", "caux"):
+                ok &= np.array_equal(g[k], o[k][c0:c0 + nc])
+        np.save(os.path.join(outdir, f"m{rank}.npy"),
+                np.array([W, row_off, nr, int(ok), rng.entry, rng.exit], dtype=np.int64))
+        comm.close()
+        codec.close()
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_library_protocols_mixed_frame(tmp_path, world):
+    import torch.multiprocessing as mp
+    n_per = 300_000
+    mp.spawn(_rank_mixed, args=(world, _free_port(), n_per, str(tmp_path)), nprocs=world,
+             join=True)
+    res = [np.load(tmp_path / f"m{r}.npy") for r in range(world)]
+    rows = 0
+    for r, x in enumerate(res):
+        assert int(x[3]) == 1, f"rank {r}: its rows differ from the oracle's decode"
+        assert int(x[1]) == rows
+        rows += int(x[2])
+    assert rows == n_per * world
+    assert int(res[0][4]) == 0 and int(res[-1][5]) == int(res[0][0])
+    for a, b in zip(res, res[1:]):
+        assert int(a[5]) == int(b[4])

@@ -18,7 +18,9 @@ pytestmark = [pytest.mark.gpu, pytest.mark.timeout(300)]
 
 
 def _codec(patience):
+    import torch
     import netidx_amd
+    assert torch.cuda.is_available()  # torch's HIP runtime first (netidx_amd.codec.lib)
     os.environ["NXG_LOOKBACK_PATIENCE"] = str(patience)
     try:
         return netidx_amd.Codec(0)
