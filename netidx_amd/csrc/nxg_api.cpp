@@ -85,6 +85,12 @@ struct NxgCtx {
     // (NXG_MIXED_PATH=general: always the general decoder)
     uint32_t mix_left = 0;
     bool no_fmx = false;
+    // the fast mixed decoder's count pass: lean (one-byte-prefix Update candidates only) unless a
+    // recent frame of this connection made the resolve pass recount many tiles (Heartbeats, long
+    // text): then the full candidate set for the next kFullCountCalls calls (NXG_FMX_COUNT=full
+    // always, =lean always)
+    uint32_t fmx_full_left = 0;
+    int fmx_count_mode = 0;  // 0 adaptive, 1 full, 2 lean
     int wgs_fmx[2] = {0, 0};
     uint32_t f64r_flags = 0;  // NXG_F64R_FLAGS (tests): 1 every tile exact, 2 never hand over
     uint8_t* dframe = nullptr;
@@ -296,6 +302,7 @@ NxgColumns staged_view(NxgCtx* c, const NxgColumns* like) {
 constexpr uint32_t kIrregularCalls = 64;
 constexpr uint32_t kMixFailCalls = 16;
 constexpr uint32_t kSeqSkipCalls = 64;
+constexpr uint32_t kFullCountCalls = 16;
 
 // path codes of a fast attempt (Pending::fast): homogeneous f64 (SEQ, RUN, X) or mixed (MIX)
 enum { FAST_NONE = 0, FAST_RUN = 1, FAST_X = 2, FAST_MIX = 3, FAST_SEQ = 4 };
@@ -382,8 +389,10 @@ bool enqueue_dec_mixed(NxgCtx* c, const uint8_t* f, uint64_t len, NxgColumns* ou
         // one buffer for both, so that a fallback does not reallocate
         const uint64_t need = std::max(nxg_fmx_scratch_bytes(len), nxg_dec_gen_scratch_bytes(len));
         if (!ensure_glws(c, need, err)) return false;
+        const bool lean = c->fmx_count_mode == 2 || (c->fmx_count_mode == 0 && c->fmx_full_left == 0);
+        if (c->fmx_full_left) c->fmx_full_left--;
         HIPCHK(nxg_launch_dec_fmx(f, len, d, reinterpret_cast<uint8_t*>(c->glws), c->wgs_fmx, st,
-                                  c->stream));
+                                  c->stream, lean));
         return true;
     }
     if (c->mix_left) c->mix_left--;
@@ -455,6 +464,10 @@ bool finish_decode(NxgCtx* c, const uint8_t* f, uint64_t len, NxgColumns* out, i
         h = c->hst[slot2];
         tried_fast = next;
     }
+    // a fast mixed decode whose resolve pass recounted more than 1 tile in 32 (the lean count
+    // found no chain there: Heartbeats, long text): the full count for the next calls
+    if (h.path == 4 && len > 0 && h.diag[5] * 32 > (len + 4095) / 4096)
+        c->fmx_full_left = kFullCountCalls;
     if (h.err_key) {  // general decode: the earliest (offset, kind) on the true chain
         h.err_kind = (uint32_t)(~h.err_key & 0xffu);
         h.err_offset = ~h.err_key >> 8;
@@ -686,6 +699,8 @@ NxgCtx* nxg_ctx_new(int device, NetidxError* err) {
     c->no_seq = fp && (strcmp(fp, "run") == 0 || strcmp(fp, "x") == 0);
     const char* mp = getenv("NXG_MIXED_PATH");
     c->no_fmx = mp && strcmp(mp, "general") == 0;
+    const char* fc = getenv("NXG_FMX_COUNT");
+    c->fmx_count_mode = fc && strcmp(fc, "full") == 0 ? 1 : (fc && strcmp(fc, "lean") == 0 ? 2 : 0);
     const char* ap = getenv("NXG_ARCH_PATH");
     c->no_fa = ap && strcmp(ap, "exact") == 0;
     // (process-wide, set by every context created: tests make one with 0 and then a default one)

@@ -30,7 +30,7 @@
 namespace f64s {
 constexpr int TPB = 256;
 #ifndef NXG_F64S_R
-#define NXG_F64S_R 4  // records per lane loaded together
+#define NXG_F64S_R 8  // records per lane loaded together (4 pairs)
 #endif
 constexpr int R = NXG_F64S_R;
 constexpr uint32_t WREC = 64 * R;   // records per wave

@@ -36,11 +36,15 @@
 //           packed wave pass); array elements found by stride speculation (each element's tag
 //           confirms the size) and decoded one per lane, the exact walk as the fallback
 #include <algorithm>
+#include <type_traits>
 
 #include "nxg_fmx_common.h"
 
 #ifndef NXG_FMX_CAND
 #define NXG_FMX_CAND 7  // candidate rules (A/B timing only): 1 one-byte prefix, 2 Heartbeat, 4 two-byte
+#endif
+#ifndef NXG_FMX_LEAN
+#define NXG_FMX_LEAN 1  // the emit's lean rounds for tiles of one-byte-prefix Updates (A/B: 0)
 #endif
 #ifndef NXG_FMX_SKIP
 #define NXG_FMX_SKIP 0  // timing experiments only: 1 elements, 2 text, 4 row values, 8 row stores
@@ -84,6 +88,10 @@ struct EmitLds {
 // The lanes' chunks are 64 bytes (16 banks) apart, so lane j reads its words in the order
 // k + j / 2 (mod 16): at each step the 32 lanes of a half-wave read 32 different banks
 // (ds_read_b32: bank = dword address mod 32), where the plain order put 16 lanes on one bank.
+// FULL = false (a lean count): one-byte-prefix Update candidates only -- what most tiles of most
+// frames hold; a tile with anything else then has no lean chain and is recounted by the resolve
+// pass from every candidate kind.
+template <bool FULL = true>
 NXG_DEV uint64_t cand_mask(const uint8_t* img, uint32_t c, uint64_t& two) {
     const uint32_t* w = reinterpret_cast<const uint32_t*>(img + c);
     const uint32_t rot = (c >> 7) & 15u;  // (c / 64) / 2
@@ -96,11 +104,18 @@ NXG_DEV uint64_t cand_mask(const uint8_t* img, uint32_t c, uint64_t& two) {
         const uint32_t a1 = alignbyte(b, a, 1), a2 = alignbyte(b, a, 2);
         const uint32_t len = ((a & 0x7f7f7f7fu) + 0x7c7c7c7cu) & ~a & 0x80808080u;
         const uint32_t var = zero_bytes(a1 ^ 0x04040404u);
-        const uint32_t hb = zero_bytes(a ^ 0x02020202u) & zero_bytes(a1 ^ 0x05050505u);
-        const uint32_t tw = a & ~a1 & ~zero_bytes(a1) & zero_bytes(a2 ^ 0x04040404u) & 0x80808080u;
-        m |= (uint64_t)nib(((NXG_FMX_CAND & 1) ? (len & var) : 0u) | ((NXG_FMX_CAND & 2) ? hb : 0u))
-             << (4 * kk);
-        two |= (uint64_t)nib((NXG_FMX_CAND & 4) ? tw : 0u) << (4 * kk);
+        if (FULL) {
+            const uint32_t hb = zero_bytes(a ^ 0x02020202u) & zero_bytes(a1 ^ 0x05050505u);
+            const uint32_t tw =
+                a & ~a1 & ~zero_bytes(a1) & zero_bytes(a2 ^ 0x04040404u) & 0x80808080u;
+            m |= (uint64_t)nib(((NXG_FMX_CAND & 1) ? (len & var) : 0u) |
+                               ((NXG_FMX_CAND & 2) ? hb : 0u))
+                 << (4 * kk);
+            two |= (uint64_t)nib((NXG_FMX_CAND & 4) ? tw : 0u) << (4 * kk);
+        } else {
+            (void)a2;
+            m |= (uint64_t)nib(len & var) << (4 * kk);
+        }
     }
     return m;
 }
@@ -157,10 +172,11 @@ struct Cands {
     uint64_t m;
     uint32_t c0, x0, c1, x1;
 };
+template <bool FULL = true>
 NXG_DEV Cands lane_cands(const uint8_t* img, uint32_t lane, uint32_t lim) {
     Cands r;
     uint64_t two;
-    uint64_t m = cand_mask(img, lane * CH, two);
+    uint64_t m = cand_mask<FULL>(img, lane * CH, two);
     r.m = m | two;
     r.c0 = r.c1 = r.x0 = r.x1 = FAIL;
     if (m) {
@@ -286,11 +302,12 @@ NXG_DEV uint32_t msg_kids(const uint8_t* img, uint32_t p) {
 // the messages of the lane's chunk from its entry: Updates, Heartbeats, child slots, and their
 // starts as bits of the chunk (bit i: chunk byte i)
 NXG_DEV bool chunk_msgs(const uint8_t* img, uint32_t ce, uint32_t lane, uint32_t lim, uint32_t& n,
-                        uint32_t& nhb, uint32_t& kids, uint64_t& bits) {
+                        uint32_t& nhb, uint32_t& kids, uint64_t& bits, bool& two) {
     n = 0;
     nhb = 0;
     kids = 0;
     bits = 0;
+    two = false;
     if (ce == NONE) return true;
     uint32_t x = ce;
     const uint32_t c = lane * CH, end = min(c + CH, lim);
@@ -299,6 +316,7 @@ NXG_DEV bool chunk_msgs(const uint8_t* img, uint32_t ce, uint32_t lane, uint32_t
         const uint32_t k = msg_kids(img, x);
         if (k == FAIL) return false;
         bits |= 1ull << (x - c);
+        two |= img[x] >= 0x80u;
         if (k == HB) {
             nhb++;
         } else {
@@ -330,8 +348,11 @@ struct FRange {
 struct TileDesc {
     uint32_t entry, exit;  // tile offsets
     uint32_t rows;         // Updates | Heartbeats << 16
-    uint32_t kids;
+    uint32_t kids;         // child slots | kTwoByte (a message with a two-byte prefix)
 };
+constexpr uint32_t kTwoByte = 1u << 31;
+// a tile of one-byte-prefix Updates only: the emit pass's lean variant
+NXG_DEV bool lean_tile(const TileDesc& d) { return (d.rows >> 16) == 0 && !(d.kids & kTwoByte); }
 
 // The tile's descriptor for the chain from entry e: exit, messages, child slots (FAIL entry and
 // exit when the chain breaks, or does not end exactly at the frame end in the last tile).
@@ -343,14 +364,15 @@ NXG_DEV TileDesc count_from(const uint8_t* img, const Cands& cd, uint32_t e, uin
     if (x == FAIL) x = tile_chain(img, e, lim, lane, cd.m, cd.c0, cd.x0, cd.c1, cd.x1, ce);
     bool bad = x == FAIL || (last && x != lim);
     uint32_t n = 0, h = 0, k = 0;
+    bool two = false;
     bits = 0;
-    if (!bad) bad = !chunk_msgs(img, ce, lane, lim, n, h, k, bits);
+    if (!bad) bad = !chunk_msgs(img, ce, lane, lim, n, h, k, bits, two);
     bad = __any(bad);
     if (bad) return TileDesc{FAIL, FAIL, 0, 0};
     const uint32_t nh = wave_sum<uint32_t>(n | (h << 16));
     // more messages than the emit pass's list holds (Heartbeats are 2 bytes): the general decoder
     if ((nh & 0xffffu) + (nh >> 16) > MAXM) return TileDesc{FAIL, FAIL, 0, 0};
-    return TileDesc{e, x, nh, wave_sum<uint32_t>(k)};
+    return TileDesc{e, x, nh, wave_sum<uint32_t>(k) | (__any(two) ? kTwoByte : 0u)};
 }
 
 
@@ -360,11 +382,12 @@ NXG_DEV TileDesc count_from(const uint8_t* img, const Cands& cd, uint32_t e, uin
 // its entry: the first candidates of its first two chunks, in order, until one gives a complete
 // chain. A false guess whose chain merges into the true one gives the true exit but wrong counts:
 // the fix pass recounts such tiles from their predecessor's exit.
+template <bool FULL>
 NXG_DEV TileDesc count_tile(const uint8_t* img, uint64_t t, uint64_t nt, const FRange& rg,
                             uint32_t lane, uint64_t& bits) {
     const uint32_t lim = rg.lim(t);
     const bool last = rg.last(t, nt);
-    const Cands cd = lane_cands(img, lane, lim);
+    const Cands cd = lane_cands<FULL>(img, lane, lim);
     TileDesc d{FAIL, FAIL, 0, 0};
     bits = 0;
     if (t == 0 && rg.first) return count_from(img, cd, 0, lim, last, lane, bits);
@@ -391,6 +414,7 @@ NXG_DEV TileDesc count_tile(const uint8_t* img, uint64_t t, uint64_t nt, const F
 }
 
 // count pass: one wave per tile
+template <bool FULL>
 __global__ __launch_bounds__(TPB) void nxg_fmx_count_kernel(const uint8_t* __restrict__ wire,
                                                             FRange rg, uint64_t nt,
                                                             TileDesc* __restrict__ td,
@@ -406,7 +430,7 @@ __global__ __launch_bounds__(TPB) void nxg_fmx_count_kernel(const uint8_t* __res
     tile_load(g, wire, t * TILE, rg.W, lane);
     tile_store(img, g, lane);
     uint64_t bits;
-    const TileDesc d = count_tile(img, t, nt, rg, lane, bits);
+    const TileDesc d = count_tile<FULL>(img, t, nt, rg, lane, bits);
     starts[t * 64 + lane] = bits;
     if (lane == 0) td[t] = d;
 }
@@ -542,7 +566,8 @@ __global__ __launch_bounds__(TPB) void nxg_fmx_resolve_kernel(
         if (lane == 0 && tw < nt) st_agent(&wexit[tw / 64], (1ull << 63) | lx);
     }
     // two scans: (Updates | child slots << 32) and Heartbeats
-    const uint64_t v = tl < nt ? (uint64_t)(d.rows & 0xffffu) | ((uint64_t)d.kids << 32) : 0ull;
+    const uint64_t v =
+        tl < nt ? (uint64_t)(d.rows & 0xffffu) | ((uint64_t)(d.kids & ~kTwoByte) << 32) : 0ull;
     const uint64_t vh = tl < nt ? (uint64_t)(d.rows >> 16) : 0ull;
     uint64_t tot, toth;
     const uint64_t ex = block_excl_scan<uint64_t, TPB>(v, scan_tmp, &tot);
@@ -654,100 +679,107 @@ __global__ __launch_bounds__(TPB) void nxg_fmx_emit_kernel(
     }
     wave_lds_order();
     PMARK(0);
-    uint32_t ntxt = 0;  // deferred text checks in el[0, ntxt)
-#pragma unroll 1
-    for (uint32_t k = 0; k < nm && !bad; k += 64) {
-        const uint32_t i = k + lane;
-        const bool has = i < nm;
-        const uint32_t p0 = has ? msg[i] : 0u;
-        // a Heartbeat (02 05, checked by the count pass): a control span before the next row
-        const uint32_t c0 = img[p0];
-        const bool ishb = has && c0 == 2u;
-        const bool upd = has && !ishb;
-        const uint64_t hm = __ballot(ishb);
-        const uint32_t hbefore = __builtin_amdgcn_mbcnt_hi((uint32_t)(hm >> 32),
-                                                           __builtin_amdgcn_mbcnt_lo((uint32_t)hm, 0u));
-        const uint64_t row = rnext + (lane - hbefore);  // Updates before this lane in the round
-        if (ishb && ctl_on) {
-            const uint64_t c = hnext + hbefore;
-            cols.ctl_row[c] = row;
-            cols.ctl_off[c] = t0f + p0;
-            cols.ctl_len[c] = 2u;
-            cols.ctl_variant[c] = 5u;
-        }
-        // header: length (one or two bytes), Update variant (both checked by the count pass), id
-        // varint (at most 5 bytes: the count pass), value tag, then the 12 bytes after the tag;
-        // read from p, the last length byte
-        const uint32_t nbp = c0 < 0x80u ? 1u : 2u;
-        const uint32_t p = p0 + nbp - 1u;
-        uint32_t h[5];
-        win_words<5>(limg, p, h);
-        const uint32_t lim = p0 + (nbp == 1u ? c0 : (c0 & 0x7fu) | ((h[0] & 0xffu) << 7));
-        const uint32_t a = alignbyte(h[1], h[0], 2), b = alignbyte(h[2], h[1], 2);  // bytes 2..9
-        const uint32_t sa = ~a & 0x80808080u;
-        const uint32_t nb = sa ? ((uint32_t)__builtin_ctz(sa) >> 3) + 1 : 5u;
-        const uint64_t id = (uint64_t)compress7_32(nb >= 4u ? a : (a & ((1u << (8u * nb)) - 1u))) |
-                            (nb == 5u ? (uint64_t)(b & 0x7fu) << 28 : 0ull);
-        const uint32_t tg = (uint32_t)(((((uint64_t)b << 32) | a) >> (8u * nb)) & 0xffu);
-        const uint32_t u = 3u + nb;  // the payload, relative to p: 4..8
-        const bool up = u >= 8u;
-        const uint32_t g0 = up ? h[2] : h[1], g1 = up ? h[3] : h[2], g2 = up ? h[4] : h[3],
-                       g3 = up ? 0u : h[4];
-        const uint32_t su = u & 3u;
-        FV o = val_decode(upd ? tg : 1u, alignbyte(g1, g0, su), alignbyte(g2, g1, su),
-                          alignbyte(g3, g2, su), p + u, upd ? lim : p + u + 12u, true, t0f);
-        if (NXG_FMX_SKIP & 4) o = FV{g0, tg, g1, lim, 0, 0, 0, true};
-        // past the image: text only (the count pass), checked here from global memory
-        const bool far = upd && lim > wend;
-        bool ok = !upd || ((sa != 0u || !(b & 0x80u)) && u <= (lim - p) && lim <= fend && o.ok);
-        if (far && ok && o.slen) ok = utf8_ok(GlbSrc{(gbl_bytes)wire}, t0 + o.soff, o.slen);
-        PMARK(1);
-        // text: checked once per tile (text_flush) from a list in `el`
-        bad = __any(!ok);
-        if (!bad && !(NXG_FMX_SKIP & 2)) {
-            const bool tx = upd && !far && o.slen;
-            const uint64_t tm = __ballot(tx);
-            const uint32_t tn = (uint32_t)__popcll(tm);
-            if (ntxt + tn > MAXC) {
-                bad = !text_flush(limg, el, ntxt, lds[w].mark, lane, st);
-                ntxt = 0;
-                wave_lds_order();
+    // the rounds, in a lean variant for tiles of one-byte-prefix Updates only (no Heartbeat, no
+    // two-byte prefix, no text past the image: most tiles), chosen per tile
+    auto rounds = [&](auto lean_c) {
+        constexpr bool LEAN = decltype(lean_c)::value;
+        uint32_t ntxt = 0;  // deferred text checks in el[0, ntxt)
+    #pragma unroll 1
+        for (uint32_t k = 0; k < nm && !bad; k += 64) {
+            const uint32_t i = k + lane;
+            const bool has = i < nm;
+            const uint32_t p0 = has ? msg[i] : 0u;
+            // a Heartbeat (02 05, checked by the count pass): a control span before the next row
+            const uint32_t c0 = img[p0];
+            const bool ishb = !LEAN && has && c0 == 2u;
+            const bool upd = has && !ishb;
+            const uint64_t hm = LEAN ? 0ull : __ballot(ishb);
+            const uint32_t hbefore = LEAN ? 0u : __builtin_amdgcn_mbcnt_hi((uint32_t)(hm >> 32),
+                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)hm, 0u));
+            const uint64_t row = rnext + (lane - hbefore);  // Updates before this lane in the round
+            if (ishb && ctl_on) {
+                const uint64_t c = hnext + hbefore;
+                cols.ctl_row[c] = row;
+                cols.ctl_off[c] = t0f + p0;
+                cols.ctl_len[c] = 2u;
+                cols.ctl_variant[c] = 5u;
             }
-            if (tx) el[ntxt + __builtin_amdgcn_mbcnt_hi((uint32_t)(tm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)tm, 0u))] = o.soff | (o.slen << 16);
-            ntxt += tn;
-        }
-        PMARK(2);
-        if (bad) break;
-        const uint32_t kd = upd ? o.kids : 0u;
-        const uint32_t kinc = wave_incl_scan<uint32_t>(kd);
-        const uint32_t kpre = kinc - kd;
-        const uint32_t rk = wave_last<uint32_t>(kinc);
-        {
-            const uint32_t nh = (uint32_t)__popcll(hm);
-            rnext += min(nm - k, 64u) - nh;
-            hnext += nh;
-        }
-        if (upd && !(NXG_FMX_SKIP & 8)) {
-            cols.id[row] = id;
-            cols.tag[row] = (uint8_t)o.tag;
-            cols.fixed[row] = o.tag == 19u ? cnext + kpre : o.fixed;
-            cols.aux[row] = o.aux;
-        }
-        PMARK(3);
-        if (rk == 0 || (NXG_FMX_SKIP & 1)) {
+            // header: length (one or two bytes), Update variant (both checked by the count pass), id
+            // varint (at most 5 bytes: the count pass), value tag, then the 12 bytes after the tag;
+            // read from p, the last length byte
+            const uint32_t nbp = LEAN || c0 < 0x80u ? 1u : 2u;
+            const uint32_t p = p0 + nbp - 1u;
+            uint32_t h[5];
+            win_words<5>(limg, p, h);
+            const uint32_t lim = p0 + (nbp == 1u ? c0 : (c0 & 0x7fu) | ((h[0] & 0xffu) << 7));
+            const uint32_t a = alignbyte(h[1], h[0], 2), b = alignbyte(h[2], h[1], 2);  // bytes 2..9
+            const uint32_t sa = ~a & 0x80808080u;
+            const uint32_t nb = sa ? ((uint32_t)__builtin_ctz(sa) >> 3) + 1 : 5u;
+            const uint64_t id = (uint64_t)compress7_32(nb >= 4u ? a : (a & ((1u << (8u * nb)) - 1u))) |
+                                (nb == 5u ? (uint64_t)(b & 0x7fu) << 28 : 0ull);
+            const uint32_t tg = (uint32_t)(((((uint64_t)b << 32) | a) >> (8u * nb)) & 0xffu);
+            const uint32_t u = 3u + nb;  // the payload, relative to p: 4..8
+            const bool up = u >= 8u;
+            const uint32_t g0 = up ? h[2] : h[1], g1 = up ? h[3] : h[2], g2 = up ? h[4] : h[3],
+                           g3 = up ? 0u : h[4];
+            const uint32_t su = u & 3u;
+            FV o = val_decode(upd ? tg : 1u, alignbyte(g1, g0, su), alignbyte(g2, g1, su),
+                              alignbyte(g3, g2, su), p + u, upd ? lim : p + u + 12u, true, t0f);
+            if (NXG_FMX_SKIP & 4) o = FV{g0, tg, g1, lim, 0, 0, 0, true};
+            // past the image: text only (the count pass), checked here from global memory
+            const bool far = !LEAN && upd && lim > wend;
+            bool ok = !upd || ((sa != 0u || !(b & 0x80u)) && u <= (lim - p) && lim <= fend && o.ok);
+            if (far && ok && o.slen) ok = utf8_ok(GlbSrc{(gbl_bytes)wire}, t0 + o.soff, o.slen);
+            PMARK(1);
+            // text: checked once per tile (text_flush) from a list in `el`
+            bad = __any(!ok);
+            if (!bad && !(NXG_FMX_SKIP & 2)) {
+                const bool tx = upd && !far && o.slen;
+                const uint64_t tm = __ballot(tx);
+                const uint32_t tn = (uint32_t)__popcll(tm);
+                if (ntxt + tn > MAXC) {
+                    bad = !text_flush(limg, el, ntxt, lds[w].mark, lane, st);
+                    ntxt = 0;
+                    wave_lds_order();
+                }
+                if (tx) el[ntxt + __builtin_amdgcn_mbcnt_hi((uint32_t)(tm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)tm, 0u))] = o.soff | (o.slen << 16);
+                ntxt += tn;
+            }
+            PMARK(2);
+            if (bad) break;
+            const uint32_t kd = upd ? o.kids : 0u;
+            const uint32_t kinc = wave_incl_scan<uint32_t>(kd);
+            const uint32_t kpre = kinc - kd;
+            const uint32_t rk = wave_last<uint32_t>(kinc);
+            {
+                const uint32_t nh = (uint32_t)__popcll(hm);
+                rnext += min(nm - k, 64u) - nh;
+                hnext += nh;
+            }
+            if (upd && !(NXG_FMX_SKIP & 8)) {
+                cols.id[row] = id;
+                cols.tag[row] = (uint8_t)o.tag;
+                cols.fixed[row] = o.tag == 19u ? cnext + kpre : o.fixed;
+                cols.aux[row] = o.aux;
+            }
+            PMARK(3);
+            if (rk == 0 || (NXG_FMX_SKIP & 1)) {
+                cnext += rk;
+                continue;
+            }
+            bad = round_elements(img, lds[w].mark, el, kd, kpre, rk, o.end, lim, cnext, cols, t0f, lane,
+                                 ntxt, st);
+            if (bad) break;
+            PMARK(5);
             cnext += rk;
-            continue;
         }
-        bad = round_elements(img, lds[w].mark, el, kd, kpre, rk, o.end, lim, cnext, cols, t0f, lane,
-                             ntxt, st);
-        if (bad) break;
-        PMARK(5);
-        cnext += rk;
-    }
-#if NXG_FMX_PROF
-    _acc[3] += (uint64_t)ntxt << 40;
-#endif
-    if (!bad && ntxt) bad = !text_flush(limg, el, ntxt, lds[w].mark, lane, st);
+    #if NXG_FMX_PROF
+        _acc[3] += (uint64_t)ntxt << 40;
+    #endif
+        if (!bad && ntxt) bad = !text_flush(limg, el, ntxt, lds[w].mark, lane, st);
+    };
+    if (NXG_FMX_LEAN && lean_tile(d)) rounds(std::integral_constant<bool, true>{});
+    else rounds(std::integral_constant<bool, false>{});
 #if NXG_FMX_PROF
     _acc[6] = 1;
     _acc[4] = 0;
@@ -771,7 +803,7 @@ uint64_t nxg_fmx_scratch_bytes(uint64_t W) {
 // persistent grids: every workgroup co-resident (count: [0], emit: [1])
 void nxg_fmx_wgs(int ncu, int* wgs) {
     int a = 0, b = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, nxg_fmx_count_kernel, TPB, 0) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, nxg_fmx_count_kernel<true>, TPB, 0) !=
             hipSuccess ||
         hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, nxg_fmx_emit_kernel, TPB, 0) != hipSuccess) {
         a = b = 1;
@@ -785,7 +817,7 @@ void nxg_fmx_wgs(int ncu, int* wgs) {
 // range's entry / exit (+1, relative to begin) in DevStatus.diag[2] / diag[3].
 hipError_t nxg_launch_dec_fmx_range(const uint8_t* wire, uint64_t W, uint64_t begin, uint64_t end,
                                     const ColsDesc& cols, uint8_t* scratch, const int* wgs,
-                                    DevStatus* st, hipStream_t s) {
+                                    DevStatus* st, hipStream_t s, bool lean_count) {
     if (begin > end || end > W) return hipErrorInvalidValue;
     const FRange rg{W - begin, end - begin, begin, begin == 0};
     wire += begin;
@@ -814,8 +846,12 @@ hipError_t nxg_launch_dec_fmx_range(const uint8_t* wire, uint64_t W, uint64_t be
     // latency of their own LDS walks, which more resident waves hide better
     (void)wgs;
     const uint32_t gc = (uint32_t)((nt + WV - 1) / WV);
-    hipLaunchKernelGGL(nxg_fmx_count_kernel, dim3(gc), dim3(TPB), 0, s, wire, rg, nt, td, starts,
-                       nxg_take_zero_slot());
+    if (lean_count)
+        hipLaunchKernelGGL(nxg_fmx_count_kernel<false>, dim3(gc), dim3(TPB), 0, s, wire, rg, nt, td,
+                           starts, nxg_take_zero_slot());
+    else
+        hipLaunchKernelGGL(nxg_fmx_count_kernel<true>, dim3(gc), dim3(TPB), 0, s, wire, rg, nt, td,
+                           starts, nxg_take_zero_slot());
     const bool ctl_on = cols.ctl_row && cols.ctl_off && cols.ctl_len && cols.ctl_variant;
     hipLaunchKernelGGL(nxg_fmx_resolve_kernel, dim3((uint32_t)nb), dim3(TPB), 0, s, wire, rg, nt,
                        td, td2, starts, tloc, bsum, bpre, wexit, cols.cap_rows, cols.cap_children,
@@ -826,6 +862,7 @@ hipError_t nxg_launch_dec_fmx_range(const uint8_t* wire, uint64_t W, uint64_t be
 }
 
 hipError_t nxg_launch_dec_fmx(const uint8_t* wire, uint64_t W, const ColsDesc& cols,
-                              uint8_t* scratch, const int* wgs, DevStatus* st, hipStream_t s) {
-    return nxg_launch_dec_fmx_range(wire, W, 0, W, cols, scratch, wgs, st, s);
+                              uint8_t* scratch, const int* wgs, DevStatus* st, hipStream_t s,
+                              bool lean_count) {
+    return nxg_launch_dec_fmx_range(wire, W, 0, W, cols, scratch, wgs, st, s, lean_count);
 }

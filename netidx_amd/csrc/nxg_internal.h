@@ -165,13 +165,16 @@ int nxg_dec_gen_wgs(int ncu);
 // flat values; sets fast_fail for anything else. `scratch`: nxg_fmx_scratch_bytes(W), no zeroing.
 uint64_t nxg_fmx_scratch_bytes(uint64_t W);
 void nxg_fmx_wgs(int ncu, int* wgs);  // persistent grid sizes (count, emit)
+// lean_count: the count pass from one-byte-prefix Update candidates only (tiles holding anything
+// else are recounted by the resolve pass; DevStatus.diag[5] counts the recounts)
 hipError_t nxg_launch_dec_fmx(const uint8_t* wire, uint64_t W, const ColsDesc& cols,
-                              uint8_t* scratch, const int* wgs, DevStatus* st, hipStream_t s);
+                              uint8_t* scratch, const int* wgs, DevStatus* st, hipStream_t s,
+                              bool lean_count = false);
 // the messages that start in [begin, end) of a W-byte frame (rows etc. from 0, text / control
 // offsets in frame bytes); entry / exit (+1, relative to begin) in DevStatus.diag[2] / diag[3]
 hipError_t nxg_launch_dec_fmx_range(const uint8_t* wire, uint64_t W, uint64_t begin, uint64_t end,
                                     const ColsDesc& cols, uint8_t* scratch, const int* wgs,
-                                    DevStatus* st, hipStream_t s);
+                                    DevStatus* st, hipStream_t s, bool lean_count = false);
 // subscriber dispatch (nxg_dispatch.hip): `scratch` holds nxg_disp_scratch_bytes(n, n_chans)
 // bytes (no initialisation needed); `unmatched` one u64.
 uint64_t nxg_disp_scratch_bytes(uint64_t n, uint32_t n_chans);
