@@ -85,11 +85,12 @@ struct NxgCtx {
     // (NXG_MIXED_PATH=general: always the general decoder)
     uint32_t mix_left = 0;
     bool no_fmx = false;
-    // the fast mixed decoder's count pass: lean (one-byte-prefix Update candidates only) unless a
-    // recent frame of this connection made the resolve pass recount many tiles (Heartbeats, long
-    // text): then the full candidate set for the next kFullCountCalls calls (NXG_FMX_COUNT=full
+    // the fast mixed decoder's count pass: lean (one-byte-prefix Update candidates only, then the
+    // tiles where that found no chain recounted from every kind) while this connection's last
+    // decoded frame had at most 1 tile in 32 holding a Heartbeat or a two-byte prefix
+    // (DevStatus.diag[0], from the resolve pass), else every candidate kind (NXG_FMX_COUNT=full
     // always, =lean always)
-    uint32_t fmx_full_left = 0;
+    bool fmx_full = false;
     int fmx_count_mode = 0;  // 0 adaptive, 1 full, 2 lean
     int wgs_fmx[2] = {0, 0};
     uint32_t f64r_flags = 0;  // NXG_F64R_FLAGS (tests): 1 every tile exact, 2 never hand over
@@ -302,7 +303,6 @@ NxgColumns staged_view(NxgCtx* c, const NxgColumns* like) {
 constexpr uint32_t kIrregularCalls = 64;
 constexpr uint32_t kMixFailCalls = 16;
 constexpr uint32_t kSeqSkipCalls = 64;
-constexpr uint32_t kFullCountCalls = 16;
 
 // path codes of a fast attempt (Pending::fast): homogeneous f64 (SEQ, RUN, X) or mixed (MIX)
 enum { FAST_NONE = 0, FAST_RUN = 1, FAST_X = 2, FAST_MIX = 3, FAST_SEQ = 4 };
@@ -389,8 +389,7 @@ bool enqueue_dec_mixed(NxgCtx* c, const uint8_t* f, uint64_t len, NxgColumns* ou
         // one buffer for both, so that a fallback does not reallocate
         const uint64_t need = std::max(nxg_fmx_scratch_bytes(len), nxg_dec_gen_scratch_bytes(len));
         if (!ensure_glws(c, need, err)) return false;
-        const bool lean = c->fmx_count_mode == 2 || (c->fmx_count_mode == 0 && c->fmx_full_left == 0);
-        if (c->fmx_full_left) c->fmx_full_left--;
+        const bool lean = c->fmx_count_mode == 2 || (c->fmx_count_mode == 0 && !c->fmx_full);
         HIPCHK(nxg_launch_dec_fmx(f, len, d, reinterpret_cast<uint8_t*>(c->glws), c->wgs_fmx, st,
                                   c->stream, lean));
         return true;
@@ -449,7 +448,10 @@ bool finish_decode(NxgCtx* c, const uint8_t* f, uint64_t len, NxgColumns* out, i
     // a rejected frame: after the f64 decoders the mixed fast path (mixed columns), after that
     // the general decoder
     while (tried_fast && len > 0 && h.fast_fail) {
-        if (tried_fast == FAST_MIX) c->mix_left = kMixFailCalls;
+        if (tried_fast == FAST_MIX) {
+            c->mix_left = kMixFailCalls;
+            c->fmx_full = true;  // its next attempt with every candidate kind
+        }
         DevStatus* st2;
         uint32_t slot2;
         if (!begin_call(c, &st2, &slot2, err)) return false;
@@ -464,10 +466,8 @@ bool finish_decode(NxgCtx* c, const uint8_t* f, uint64_t len, NxgColumns* out, i
         h = c->hst[slot2];
         tried_fast = next;
     }
-    // a fast mixed decode whose resolve pass recounted more than 1 tile in 32 (the lean count
-    // found no chain there: Heartbeats, long text): the full count for the next calls
-    if (h.path == 4 && len > 0 && h.diag[5] * 32 > (len + 4095) / 4096)
-        c->fmx_full_left = kFullCountCalls;
+    // the next fast mixed decode's count pass from this frame's mix of tiles
+    if (h.path == 4 && len > 0) c->fmx_full = h.diag[0] * 32 > (len + 4095) / 4096;
     if (h.err_key) {  // general decode: the earliest (offset, kind) on the true chain
         h.err_kind = (uint32_t)(~h.err_key & 0xffu);
         h.err_offset = ~h.err_key >> 8;

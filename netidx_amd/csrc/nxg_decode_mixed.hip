@@ -413,18 +413,26 @@ NXG_DEV TileDesc count_tile(const uint8_t* img, uint64_t t, uint64_t nt, const F
     return d;
 }
 
-// count pass: one wave per tile
-template <bool FULL>
+// count pass: one wave per tile. MODE 0: the lean count (one-byte-prefix Update candidates);
+// 1: every candidate kind; 2: the recount after a lean count -- only the tiles whose lean count
+// found no chain (a Heartbeat, a two-byte prefix, a long message), from every candidate kind, each
+// counted in DevStatus.diag[5] (`sz` is the call's status slot there, the zero slot otherwise)
+template <int MODE>
 __global__ __launch_bounds__(TPB) void nxg_fmx_count_kernel(const uint8_t* __restrict__ wire,
                                                             FRange rg, uint64_t nt,
                                                             TileDesc* __restrict__ td,
                                                             uint64_t* __restrict__ starts,
-                                                            DevStatus* zst) {
-    zero_status(zst);
+                                                            DevStatus* sz) {
+    constexpr bool FULL = MODE != 0;
+    if (MODE != 2) zero_status(sz);
     __shared__ __attribute__((aligned(16))) CountLds lds[TPB / 64];
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const uint64_t t = (uint64_t)blockIdx.x * (TPB / 64) + w;
     if (t >= nt) return;
+    if (MODE == 2) {
+        if (td[t].entry != FAIL) return;
+        if (lane == 0) atomicAdd(&sz->diag[5], 1ull);
+    }
     uint8_t* img = lds[w].img;
     TileRegs g;
     tile_load(g, wire, t * TILE, rg.W, lane);
@@ -561,6 +569,11 @@ __global__ __launch_bounds__(TPB) void nxg_fmx_resolve_kernel(
         }
     }
     if (tl < nt) td2[tl] = d;
+    {  // tiles holding a Heartbeat or a two-byte prefix (DevStatus.diag[0]: the host's choice of
+       // count pass for the connection's next frame)
+        const uint64_t nl = __ballot(tl < nt && !lean_tile(d));
+        if (lane == 0 && nl) atomicAdd(&st->diag[0], (unsigned long long)__popcll(nl));
+    }
     {  // the exit the chain leaves the wave's last tile at (FAIL: broken), for the next wave
         const uint32_t lx = (uint32_t)__builtin_amdgcn_readlane((int)d.exit, 63);
         if (lane == 0 && tw < nt) st_agent(&wexit[tw / 64], (1ull << 63) | lx);
@@ -803,7 +816,7 @@ uint64_t nxg_fmx_scratch_bytes(uint64_t W) {
 // persistent grids: every workgroup co-resident (count: [0], emit: [1])
 void nxg_fmx_wgs(int ncu, int* wgs) {
     int a = 0, b = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, nxg_fmx_count_kernel<true>, TPB, 0) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, nxg_fmx_count_kernel<1>, TPB, 0) !=
             hipSuccess ||
         hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, nxg_fmx_emit_kernel, TPB, 0) != hipSuccess) {
         a = b = 1;
@@ -846,12 +859,15 @@ hipError_t nxg_launch_dec_fmx_range(const uint8_t* wire, uint64_t W, uint64_t be
     // latency of their own LDS walks, which more resident waves hide better
     (void)wgs;
     const uint32_t gc = (uint32_t)((nt + WV - 1) / WV);
-    if (lean_count)
-        hipLaunchKernelGGL(nxg_fmx_count_kernel<false>, dim3(gc), dim3(TPB), 0, s, wire, rg, nt, td,
+    if (lean_count) {
+        hipLaunchKernelGGL(nxg_fmx_count_kernel<0>, dim3(gc), dim3(TPB), 0, s, wire, rg, nt, td,
                            starts, nxg_take_zero_slot());
-    else
-        hipLaunchKernelGGL(nxg_fmx_count_kernel<true>, dim3(gc), dim3(TPB), 0, s, wire, rg, nt, td,
+        hipLaunchKernelGGL(nxg_fmx_count_kernel<2>, dim3(gc), dim3(TPB), 0, s, wire, rg, nt, td,
+                           starts, st);
+    } else {
+        hipLaunchKernelGGL(nxg_fmx_count_kernel<1>, dim3(gc), dim3(TPB), 0, s, wire, rg, nt, td,
                            starts, nxg_take_zero_slot());
+    }
     const bool ctl_on = cols.ctl_row && cols.ctl_off && cols.ctl_len && cols.ctl_variant;
     hipLaunchKernelGGL(nxg_fmx_resolve_kernel, dim3((uint32_t)nb), dim3(TPB), 0, s, wire, rg, nt,
                        td, td2, starts, tloc, bsum, bpre, wexit, cols.cap_rows, cols.cap_children,

@@ -165,8 +165,9 @@ int nxg_dec_gen_wgs(int ncu);
 // flat values; sets fast_fail for anything else. `scratch`: nxg_fmx_scratch_bytes(W), no zeroing.
 uint64_t nxg_fmx_scratch_bytes(uint64_t W);
 void nxg_fmx_wgs(int ncu, int* wgs);  // persistent grid sizes (count, emit)
-// lean_count: the count pass from one-byte-prefix Update candidates only (tiles holding anything
-// else are recounted by the resolve pass; DevStatus.diag[5] counts the recounts)
+// lean_count: the count pass from one-byte-prefix Update candidates only, then a recount of the
+// tiles where that found no chain from every candidate kind (DevStatus.diag[5] counts them, with
+// the resolve pass's recounts)
 hipError_t nxg_launch_dec_fmx(const uint8_t* wire, uint64_t W, const ColsDesc& cols,
                               uint8_t* scratch, const int* wgs, DevStatus* st, hipStream_t s,
                               bool lean_count = false);

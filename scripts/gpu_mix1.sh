@@ -5,13 +5,15 @@ set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd $R
 mkdir -p gpurun_out/mix1
+timeout -k 10 400 python3 -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_mixed_fast.py tests/test_gpu_dispatch.py tests/test_gpu_multi.py > gpurun_out/mix1/tests.log 2>&1 || { tail -30 gpurun_out/mix1/tests.log; exit 1; }
+tail -2 gpurun_out/mix1/tests.log
 for rep in 1 2; do
-  for v in base fullcount nolean_fullcount; do
+  for v in base fullcount lean; do
     lib=$R/netidx_amd/lib/libnxg_codec.so
     env=""
     case $v in
       fullcount) env="NXG_FMX_COUNT=full";;
-      nolean_fullcount) lib=$R/netidx_amd/build_ab/nolean/libnxg_codec.so; env="NXG_FMX_COUNT=full";;
+      lean) env="NXG_FMX_COUNT=lean";;
     esac
     env $env NXG_LIB=$lib timeout -k 10 300 python3 -u scripts/ab_mixed.py $v 2>&1 | grep -v amdgpu.ids | tee -a gpurun_out/mix1/ab.log || exit 1
   done
