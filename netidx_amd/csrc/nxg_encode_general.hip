@@ -30,6 +30,9 @@
 #ifndef NXG_ENC_SKIP
 #define NXG_ENC_SKIP 0  // timing experiments only
 #endif
+#ifndef NXG_ENC_EB
+#define NXG_ENC_EB 4  // array elements loaded together (sizing and writing flat arrays)
+#endif
 #ifndef NXG_ENC_LBU
 #define NXG_ENC_LBU 1  // look-back window, 64 * NXG_ENC_LBU tiles per round trip (1, 4 and 8 measured equal)
 #endif
@@ -272,14 +275,27 @@ NXG_DEV uint64_t row_len_flat(const ColsDesc& c, uint64_t r, bool& flat) {
         return 0;
     }
     uint64_t total = 1 + vl64(s.aux);
-    for (uint64_t k = 0; k < s.aux; k++) {
-        const Slot e = get_slot(c, false, s.fixed + k);
-        const uint64_t l = is_container(e.tag) ? 0 : scalar_len(e);
-        if (!l) {
+    // the elements NXG_ENC_EB at a time: their loads in flight together (one memory round trip
+    // per group, not per element)
+#pragma unroll 1
+    for (uint64_t k0 = 0; k0 < s.aux; k0 += NXG_ENC_EB) {
+        Slot e[NXG_ENC_EB];
+#pragma unroll
+        for (int j = 0; j < NXG_ENC_EB; j++)
+            if (k0 + j < s.aux) e[j] = get_slot(c, false, s.fixed + k0 + j);
+        bool ok = true;
+#pragma unroll
+        for (int j = 0; j < NXG_ENC_EB; j++) {
+            if (k0 + j < s.aux) {
+                const uint64_t l = is_container(e[j].tag) ? 0 : scalar_len(e[j]);
+                ok = ok && l != 0;
+                total += l;
+            }
+        }
+        if (!ok) {
             flat = false;
             return 0;
         }
-        total += l;
     }
     return total;
 }
@@ -291,7 +307,16 @@ NXG_DEV void row_write_flat(const ColsDesc& c, const uint8_t* heap, uint64_t r, 
     }
     w.b(19);
     w.var(s.aux);
-    for (uint64_t k = 0; k < s.aux; k++) scalar_write(get_slot(c, false, s.fixed + k), heap, w);
+#pragma unroll 1
+    for (uint64_t k0 = 0; k0 < s.aux; k0 += NXG_ENC_EB) {
+        Slot e[NXG_ENC_EB];
+#pragma unroll
+        for (int j = 0; j < NXG_ENC_EB; j++)
+            if (k0 + j < s.aux) e[j] = get_slot(c, false, s.fixed + k0 + j);
+#pragma unroll
+        for (int j = 0; j < NXG_ENC_EB; j++)
+            if (k0 + j < s.aux) scalar_write(e[j], heap, w);
+    }
 }
 
 // Value classes by tag (CLS_GEN: Map, Error, nested containers and unknown tags, which take
@@ -484,45 +509,15 @@ __global__ __launch_bounds__(TPB) void nxg_enc_rows_kernel(
         uint64_t tot;
         const uint64_t off = block_excl_scan<uint64_t, TPB>(mine, tmp, &tot);
         if (tid == 0) st_agent(&tstat[tile], lb_word(tile == 0 ? kFlagInc : kFlagAgg, epoch, tot));
-        if (tid < 64) {
-            uint64_t base = 0;
-            if (tile != 0) {
-                bool give_up;
-#if NXG_ENC_SKIP & 1
-                give_up = false;  // timing experiments only: no look-back (wrong offsets)
-#else
-                // no wait on a workgroup that may not be running: an unpublished predecessor's
-                // byte count is computed here from its rows (self-help)
-                give_up = false;
-                base = lookback_selfhelp_fn(
-                    tstat, tile, epoch, patience, [&](uint64_t t) -> uint64_t {
-                        const uint64_t q0 = t * GTILE;
-                        uint64_t b = 0;
-                        for (uint64_t r = q0 + lane; r < q0 + GTILE && r < n; r += 64)
-                            b += row_msg_len(c, r, arch, &wstk[0]);
-                        return wave_sum<uint64_t>(b);
-                    });
-#endif
-                if (give_up && lane == 0) atomicOr(&st->timeout, 1u);
-                if (lane == 0) st_agent(&tstat[tile], lb_word(kFlagInc, epoch, base + tot));
-            }
-            if (lane == 0) sh_base = base;
-        }
-        __syncthreads();
-        const uint64_t tbase = sh_base + arch_base;
-        const uint32_t phase = (uint32_t)(tbase & 15u);
-        const bool staged = out && c.n_ctl == 0 && phase + tot <= (uint64_t)(GSTG - 16) &&
-                            tbase + tot <= cap;
-        if (staged) {
-            // 4. rows into the staging at their offsets, class by class, then aligned
-            //    nontemporal 16-byte stores (edge blocks shared with the neighbours: bytes)
+        // 4a. without control messages: the rows into the staging at their tile-local offsets
+        //     first, so that the look-back below finds its predecessors mostly done
+        const bool stage = out && c.n_ctl == 0 && tot <= (uint64_t)(GSTG - 32);
+        if (stage) {
             {
-                uint32_t o = phase + (uint32_t)off;
+                uint32_t o = (uint32_t)off;
 #pragma unroll
                 for (int k = 0; k < GRPT; k++) {
                     off_lds[tid * GRPT + k] = (uint16_t)o;
-                    if (!arch && tbase <= kMaxBatch && kMaxBatch < tbase + tot)
-                        note_split(st, tbase + off + (o - phase - (uint32_t)off), L[k]);
                     o += (uint32_t)L[k];
                 }
             }
@@ -568,21 +563,70 @@ __global__ __launch_bounds__(TPB) void nxg_enc_rows_kernel(
                 one_lane_at_a_time(cls_lds[rl] == CLS_GEN,
                                    [&] { value_write(c, heap, true, r, w, stk); });
             }
-            __syncthreads();
+        }
+        // 3b. the tile's base: look-back over the tiles' byte counts
+        if (tid < 64) {
+            uint64_t base = 0;
+            if (tile != 0) {
+                bool give_up;
+#if NXG_ENC_SKIP & 1
+                give_up = false;  // timing experiments only: no look-back (wrong offsets)
+#else
+                // no wait on a workgroup that may not be running: an unpublished predecessor's
+                // byte count is computed here from its rows (self-help)
+                give_up = false;
+                base = lookback_selfhelp_fn(
+                    tstat, tile, epoch, patience, [&](uint64_t t) -> uint64_t {
+                        const uint64_t q0 = t * GTILE;
+                        uint64_t b = 0;
+                        for (uint64_t r = q0 + lane; r < q0 + GTILE && r < n; r += 64)
+                            b += row_msg_len(c, r, arch, &wstk[0]);
+                        return wave_sum<uint64_t>(b);
+                    });
+#endif
+                if (give_up && lane == 0) atomicOr(&st->timeout, 1u);
+                if (lane == 0) st_agent(&tstat[tile], lb_word(kFlagInc, epoch, base + tot));
+            }
+            if (lane == 0) sh_base = base;
+        }
+        __syncthreads();
+        const uint64_t tbase = sh_base + arch_base;
+        if (stage && tbase + tot <= cap) {
+            // 4b. the staging out as aligned nontemporal 16-byte stores: global block g holds the
+            //     staged bytes from g - tbase; the two edge blocks (shared with the neighbours)
+            //     by bytes
+            if (!arch && tbase <= kMaxBatch && kMaxBatch < tbase + tot) {
+                uint64_t o = tbase + off;
+#pragma unroll
+                for (int k = 0; k < GRPT; k++) {
+                    const uint32_t lk = len_lds[tid * GRPT + k];
+                    note_split(st, o, lk);
+                    o += lk;
+                }
+            }
             const uint64_t end = tbase + tot;
             if (tot) {
                 const uint64_t gb0 = tbase & ~15ull;
+                const uint32_t phase = (uint32_t)(tbase & 15u);
                 const uint32_t nblk = (uint32_t)((end - gb0 + 15) >> 4);
+                typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
                 for (uint32_t b = tid; b < nblk; b += TPB) {
                     const uint64_t g = gb0 + 16ull * b;
-                    const uint8_t* src = stg + 16 * b;
                     if (g >= tbase && g + 16 <= end) {
-                        typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
-                        __builtin_nontemporal_store(*reinterpret_cast<const u32x4v*>(src),
-                                                    reinterpret_cast<u32x4v*>(out + g));
+                        // local bytes [16 b - phase, + 16): five aligned dwords from LDS, realigned
+                        const uint32_t ls = 16u * b - phase, a = ls >> 2, sb = ls & 3u;
+                        const uint32_t* s32 = reinterpret_cast<const uint32_t*>(stg);
+                        const uint32_t e0 = s32[a], e1 = s32[a + 1], e2 = s32[a + 2], e3 = s32[a + 3],
+                                       e4 = s32[a + 4];
+                        u32x4v v;
+                        v[0] = __builtin_amdgcn_alignbyte(e1, e0, sb);
+                        v[1] = __builtin_amdgcn_alignbyte(e2, e1, sb);
+                        v[2] = __builtin_amdgcn_alignbyte(e3, e2, sb);
+                        v[3] = __builtin_amdgcn_alignbyte(e4, e3, sb);
+                        __builtin_nontemporal_store(v, reinterpret_cast<u32x4v*>(out + g));
                     } else {
                         for (int k = 0; k < 16; k++)
-                            if (g + k >= tbase && g + k < end) out[g + k] = src[k];
+                            if (g + k >= tbase && g + k < end) out[g + k] = stg[g + k - tbase];
                     }
                 }
             }
@@ -593,19 +637,20 @@ __global__ __launch_bounds__(TPB) void nxg_enc_rows_kernel(
 #pragma unroll
             for (int k = 0; k < GRPT; k++) {
                 const uint64_t r = r0 + k;
+                const uint64_t Lk = len_lds[tid * GRPT + k];
                 if (r < n && row_off) row_off[r] = rpos;  // ctl placement needs every row's base
-                if (r < n && L[k] && out) {
+                if (r < n && Lk && out) {
                     uint64_t pos = rpos;
                     if (c.n_ctl) pos += ctl_pre[ctl_upto(c.ctl_row, c.n_ctl, r)];
-                    if (!arch) note_split(st, pos, L[k]);
-                    if (pos + L[k] > cap) {
+                    if (!arch) note_split(st, pos, Lk);
+                    if (pos + Lk > cap) {
                         atomicOr(&st->capacity, 1u);
                     } else {
                         Out w{out, pos};
                         if (arch) {
                             w.var((uint32_t)c.id[r]);
                         } else {
-                            w.var(L[k]);
+                            w.var(Lk);
                             w.b(4);
                             w.var(c.id[r]);
                         }
@@ -614,7 +659,7 @@ __global__ __launch_bounds__(TPB) void nxg_enc_rows_kernel(
                                            [&] { value_write(c, heap, true, r, w, stk); });
                     }
                 }
-                rpos += L[k];
+                rpos += Lk;
             }
         }
         if (tile == ntiles - 1 && tid == 0) {
