@@ -410,13 +410,54 @@ NXG_DEV TileDesc count_tile(const uint8_t* img, uint64_t t, uint64_t nt, const F
         }
         d = count_from(img, cd, g, lim, last, lane, bits);
     }
+    if (FULL && d.entry != FAIL && d.entry < 2 * CH) {
+        // a message with a two-byte prefix (long text) that ends where the guessed chain starts
+        // is the tile's entry (the guesses use one-byte candidates only): the chain from there,
+        // so that the tile needs no recount in the resolve pass
+        const uint32_t g = d.entry;
+        uint32_t x2 = FAIL;
+        if (lane < 2) {
+#pragma unroll 1
+            for (uint64_t m = cd.m; m; m &= m - 1) {
+                const uint32_t p = lane * CH + (uint32_t)__builtin_ctzll(m);
+                if (p >= g) break;
+                if (img[p] >= 0x80u && p + msg_len(img, p) == g) {
+                    x2 = p;
+                    break;
+                }
+            }
+        }
+        x2 = wave_min_u32(x2);
+        if (x2 != FAIL) {
+            uint64_t b2;
+            const TileDesc d2 = count_from(img, cd, x2, lim, last, lane, b2);
+            if (d2.entry != FAIL) {
+                d = d2;
+                bits = b2;
+            }
+        }
+    }
+    if (d.entry == FAIL) {
+        // chunks 0 and 1 hold no candidate (the tile starts inside a long text): the first
+        // candidate of a later chunk, so that the tile needs no recount in the resolve pass
+        const uint64_t cm = __ballot(cd.c0 != FAIL) & ~3ull;
+        if (cm) {
+            const uint32_t g = (uint32_t)__builtin_amdgcn_readlane((int)cd.c0, (int)__builtin_ctzll(cm));
+            d = count_from(img, cd, g, lim, last, lane, bits);
+        }
+    }
     return d;
 }
 
 // count pass: one wave per tile. MODE 0: the lean count (one-byte-prefix Update candidates);
-// 1: every candidate kind; 2: the recount after a lean count -- only the tiles whose lean count
-// found no chain (a Heartbeat, a two-byte prefix, a long message), from every candidate kind, each
-// counted in DevStatus.diag[5] (`sz` is the call's status slot there, the zero slot otherwise)
+// 1: every candidate kind; 2: the fix pass after either -- the tiles whose count found no chain (a
+// lean count on a Heartbeat, a two-byte prefix, a long message) or whose guessed entry is not
+// their predecessor's counted exit (a false guess that merged into the chain) are recounted, from
+// that exit when it is known, all at once instead of one after another in the resolve pass's
+// waves; each counted in DevStatus.diag[5] (`sz` is the call's status slot there, the zero slot
+// otherwise). A predecessor being recounted at the same moment may be read before or after its
+// rewrite: every descriptor written is a complete count from some entry, and the resolve pass
+// checks the chain and recounts in order whatever still disagrees.
 template <int MODE>
 __global__ __launch_bounds__(TPB) void nxg_fmx_count_kernel(const uint8_t* __restrict__ wire,
                                                             FRange rg, uint64_t nt,
@@ -429,8 +470,15 @@ __global__ __launch_bounds__(TPB) void nxg_fmx_count_kernel(const uint8_t* __res
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const uint64_t t = (uint64_t)blockIdx.x * (TPB / 64) + w;
     if (t >= nt) return;
+    // (MODE 2) the predecessor's counted exit, when it enters this tile: the tile's entry
+    uint32_t pe = FAIL;
     if (MODE == 2) {
-        if (td[t].entry != FAIL) return;
+        const uint32_t e = __builtin_amdgcn_readfirstlane(td[t].entry);
+        if (t > 0) {
+            const uint32_t px = __builtin_amdgcn_readfirstlane(td[t - 1].exit);
+            if (px != FAIL && px - TILE < TILE) pe = px - TILE;
+        }
+        if (e != FAIL && (pe == FAIL || pe == e)) return;
         if (lane == 0) atomicAdd(&sz->diag[5], 1ull);
     }
     uint8_t* img = lds[w].img;
@@ -438,7 +486,13 @@ __global__ __launch_bounds__(TPB) void nxg_fmx_count_kernel(const uint8_t* __res
     tile_load(g, wire, t * TILE, rg.W, lane);
     tile_store(img, g, lane);
     uint64_t bits;
-    const TileDesc d = count_tile<FULL>(img, t, nt, rg, lane, bits);
+    TileDesc d;
+    if (MODE == 2 && pe != FAIL) {
+        const Cands cd = lane_cands<true>(img, lane, rg.lim(t));
+        d = count_from(img, cd, pe, rg.lim(t), rg.last(t, nt), lane, bits);
+    } else {
+        d = count_tile<FULL>(img, t, nt, rg, lane, bits);
+    }
     starts[t * 64 + lane] = bits;
     if (lane == 0) td[t] = d;
 }
@@ -867,6 +921,8 @@ hipError_t nxg_launch_dec_fmx_range(const uint8_t* wire, uint64_t W, uint64_t be
     } else {
         hipLaunchKernelGGL(nxg_fmx_count_kernel<1>, dim3(gc), dim3(TPB), 0, s, wire, rg, nt, td,
                            starts, nxg_take_zero_slot());
+        hipLaunchKernelGGL(nxg_fmx_count_kernel<2>, dim3(gc), dim3(TPB), 0, s, wire, rg, nt, td,
+                           starts, st);
     }
     const bool ctl_on = cols.ctl_row && cols.ctl_off && cols.ctl_len && cols.ctl_variant;
     hipLaunchKernelGGL(nxg_fmx_resolve_kernel, dim3((uint32_t)nb), dim3(TPB), 0, s, wire, rg, nt,

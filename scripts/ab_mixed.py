@@ -25,7 +25,8 @@ def main():
     codec = netidx_amd.Codec(0)
     stream = torch.cuda.Stream()
     codec.set_stream(stream.cuda_stream)
-    for kind in ("plain", "ctl"):
+    kinds = ("ctl",) if tag == "ctlonly" else ("plain", "ctl")
+    for kind in kinds:
         if kind == "plain":
             m = synth.mixed_columns(n)
             cr = np.zeros(0, np.uint64)
@@ -43,7 +44,8 @@ def main():
         g = out.numpy()
         ok = all(np.array_equal(g[k], o[k]) for k in ("id", "tag", "fixed", "aux", "ctag",
                                                       "cfixed", "caux", "ctl_row", "ctl_off"))
-        res = {"tag": tag, "kind": kind, "path": st.path, "ok": bool(ok)}
+        res = {"tag": tag, "kind": kind, "path": st.path, "ok": bool(ok), "diag": [int(x) for x in codec.last_diag()],
+               "tiles": (wire.numel() + 4095) // 4096}
         for rep in range(3):
             k = 20
             torch.cuda.synchronize()
@@ -58,6 +60,7 @@ def main():
             if rep:
                 res[f"ms{rep}"] = round(e0.elapsed_time(e1) / k, 4)
         res["path_after"] = st.path
+        res["diag_after"] = [int(x) for x in codec.last_diag()]
         print(json.dumps(res), flush=True)
         del mc, heap, wire, out
         torch.cuda.empty_cache()
