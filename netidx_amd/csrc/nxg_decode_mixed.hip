@@ -232,9 +232,19 @@ NXG_DEV SMap sscan(SMap T) {  // inclusive: lane j gets T_j o ... o T_0
     return T;
 }
 
-NXG_DEV uint32_t tile_chain_scan(uint32_t e, uint32_t lim, uint32_t lane, uint32_t c0, uint32_t x0,
-                                 uint32_t c1, uint32_t x1, uint32_t& ce) {
+constexpr uint32_t GIVEUP = 0xfffffffdu;  // tile_chain_scan: too many resumes (tile_chain decides)
+NXG_DEV SMap sconst(uint32_t st) { return SMap{st * 0x01010101u, st * 0x01010101u}; }
+
+// The tile's chain from entry e (as tile_chain, without its serial loop over the chunks): from a
+// resume point -- the entry, or where a message leaves the model (it lands more than two chunks
+// on, or at a chunk's third candidate: long text) -- the chain is followed through that chunk
+// exactly, then the state maps of the chunks after it are scanned; the first chunk whose chain
+// leaves the model is the next resume point. A tile of short messages takes one scan, each long
+// message one more. Returns the exit, FAIL (the chain breaks), or GIVEUP (more than 64 resumes).
+NXG_DEV uint32_t tile_chain_scan(const uint8_t* img, uint32_t e, uint32_t lim, uint32_t lane,
+                                 const Cands& cd, uint32_t& ce) {
     ce = NONE;
+    const uint32_t c0 = cd.c0, x0 = cd.x0, c1 = cd.c1, x1 = cd.x1;
     // the candidates of chunks j+1 and j+2 (none past the tile)
     const uint32_t c0n = dpp_fill<0x130, 0xf>(c0, FAIL), c1n = dpp_fill<0x130, 0xf>(c1, FAIL);
     const uint32_t c0nn = dpp_fill<0x130, 0xf>(c0n, FAIL), c1nn = dpp_fill<0x130, 0xf>(c1n, FAIL);
@@ -249,33 +259,75 @@ NXG_DEV uint32_t tile_chain_scan(uint32_t e, uint32_t lim, uint32_t lane, uint32
     // F0 -> N0, F1 -> N1, FAIL and END (and the unused 6, 7) stay
     const SMap T{out(x0) | (out(x1) << 8) | (S_N0 << 16) | (S_N1 << 24),
                  S_FAIL | (S_END << 8) | (6u << 16) | (7u << 24)};
-    // the state in front of chunk 0
-    uint32_t s0;
-    if (e >= lim) {
-        return e;  // no message starts in this tile
-    } else if (e < CH) {
-        const uint32_t a0 = (uint32_t)__builtin_amdgcn_readlane((int)c0, 0);
-        const uint32_t a1 = (uint32_t)__builtin_amdgcn_readlane((int)c1, 0);
-        s0 = e == a0 ? S_N0 : (e == a1 ? S_N1 : S_FAIL);
-    } else if (e < 2 * CH) {
-        const uint32_t a0 = (uint32_t)__builtin_amdgcn_readlane((int)c0, 1);
-        const uint32_t a1 = (uint32_t)__builtin_amdgcn_readlane((int)c1, 1);
-        s0 = e == a0 ? S_F0 : (e == a1 ? S_F1 : S_FAIL);
-    } else {
-        s0 = S_FAIL;
+    if (e >= lim) return e;  // no message starts in this tile
+    uint32_t sout = S_FAIL;            // the state behind the lane's chunk
+    uint32_t cin = NONE, cout = FAIL;  // where the chain enters / leaves the lane's chunk
+    uint32_t k = e >> 6, xs = e;       // the resume point: chunk k, entered at xs (uniform)
+    bool done = false;
+#pragma unroll 1
+    for (int it = 0; it < 64 && !done; it++) {
+        // the chain from xs through chunk k
+        const uint32_t a0 = (uint32_t)__builtin_amdgcn_readlane((int)c0, (int)k);
+        const uint32_t a1 = (uint32_t)__builtin_amdgcn_readlane((int)c1, (int)k);
+        uint32_t xe;
+        if (xs == a0) {
+            xe = (uint32_t)__builtin_amdgcn_readlane((int)x0, (int)k);
+        } else if (xs == a1) {
+            xe = (uint32_t)__builtin_amdgcn_readlane((int)x1, (int)k);
+        } else {
+            const uint32_t mlo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)cd.m, (int)k);
+            const uint32_t mhi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(cd.m >> 32), (int)k);
+            xe = chunk_exit(img, xs, k, ((uint64_t)mhi << 32) | mlo, lim);
+        }
+        if (xe == FAIL) return FAIL;
+        const uint32_t sk = (uint32_t)__builtin_amdgcn_readlane((int)out(xe), (int)k);
+        if (lane == k) {
+            cin = xs;
+            cout = xe;
+            sout = sk;
+        }
+        if (sk == S_END) {
+            if (lane > k) sout = S_END;
+            break;
+        }
+        if (sk == S_FAIL) {  // a long message (or a third candidate): resume where it lands
+            k = xe >> 6;
+            xs = xe;
+            continue;
+        }
+        // the chunks after k: a scan of their maps from the state sk behind chunk k
+        const SMap Tk = lane <= k ? sconst(sk) : T;
+        const uint32_t so = sget(sscan(Tk), S_FAIL);
+        const uint32_t si = dpp_fill<0x138, 0xf>(so, sk);  // the state in front of the chunk
+        if (lane > k) {
+            sout = so;
+            cin = si == S_N0 ? c0 : (si == S_N1 ? c1 : NONE);
+            cout = si == S_N0 ? x0 : (si == S_N1 ? x1 : FAIL);
+        }
+        // the first chunk after k whose chain leaves the model: the next resume point
+        const uint64_t off = __ballot(lane > k && (si == S_N0 || si == S_N1) && so == S_FAIL);
+        if (!off) {
+            done = true;
+            break;
+        }
+        const uint32_t l = (uint32_t)__builtin_ctzll(off);
+        const uint32_t xl = (uint32_t)__builtin_amdgcn_readlane((int)cout, (int)l);
+        if (xl == FAIL) return FAIL;
+        if (lane > l) {
+            sout = S_FAIL;
+            cin = NONE;
+            cout = FAIL;
+        }
+        k = xl >> 6;
+        xs = xl;
     }
-    if (s0 == S_FAIL) return FAIL;
-    const uint32_t sout = sget(sscan(T), s0);          // state behind chunk j
-    const uint32_t sin = dpp_fill<0x138, 0xf>(sout, s0);  // in front of chunk j (wave_shr:1)
+    if (!done && wave_last<uint32_t>(sout) != S_END) return GIVEUP;
     if (wave_last<uint32_t>(sout) != S_END) return FAIL;
-    if (sin == S_N0) ce = c0;
-    else if (sin == S_N1) ce = c1;
+    ce = cin;
     // the exit: the last start's chunk, whose state behind is the first END
-    const bool last = (sin == S_N0 || sin == S_N1) && sout == S_END;
-    const uint64_t lm = __ballot(last);
+    const uint64_t lm = __ballot(cin != NONE && sout == S_END);
     if (!lm) return FAIL;
-    const uint32_t xl = sin == S_N0 ? x0 : x1;
-    return (uint32_t)__builtin_amdgcn_readlane((int)xl, (int)__builtin_ctzll(lm));
+    return (uint32_t)__builtin_amdgcn_readlane((int)cout, (int)__builtin_ctzll(lm));
 }
 
 // Header of the message at tile offset p: child slots (Array element count), HB for a
@@ -360,8 +412,8 @@ NXG_DEV bool lean_tile(const TileDesc& d) { return (d.rows >> 16) == 0 && !(d.ki
 NXG_DEV TileDesc count_from(const uint8_t* img, const Cands& cd, uint32_t e, uint32_t lim,
                             bool last, uint32_t lane, uint64_t& bits) {
     uint32_t ce;
-    uint32_t x = tile_chain_scan(e, lim, lane, cd.c0, cd.x0, cd.c1, cd.x1, ce);
-    if (x == FAIL) x = tile_chain(img, e, lim, lane, cd.m, cd.c0, cd.x0, cd.c1, cd.x1, ce);
+    uint32_t x = tile_chain_scan(img, e, lim, lane, cd, ce);
+    if (x == GIVEUP) x = tile_chain(img, e, lim, lane, cd.m, cd.c0, cd.x0, cd.c1, cd.x1, ce);
     bool bad = x == FAIL || (last && x != lim);
     uint32_t n = 0, h = 0, k = 0;
     bool two = false;
