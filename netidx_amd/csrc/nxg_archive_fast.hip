@@ -40,7 +40,10 @@ namespace fa {
 constexpr uint32_t UNSUB = 0x40;         // Event::Unsubscribed (subscriber/mod.rs:168)
 constexpr uint32_t BROKEN = 0x80000000u;  // FaDesc.items: the chain stops at `exit`
 constexpr uint32_t IMGL = fmx::IMG - 24;  // emit image: items end before this (text aside)
-constexpr uint32_t PRE = 128;             // count image: bytes before the tile
+#ifndef NXG_FA_PRE
+#define NXG_FA_PRE 128
+#endif
+constexpr uint32_t PRE = NXG_FA_PRE;      // count image: bytes before the tile (walked for the entry)
 constexpr uint32_t CIMG = PRE + fmx::IMG;  // count image bytes
 constexpr uint32_t CIMGL = CIMG - 24;      // count image: items end before this (text aside)
 }  // namespace fa
@@ -242,8 +245,27 @@ NXG_DEV FaDesc chain_from(lds_bytes img, uint32_t E, uint32_t lim, uint32_t wl, 
                           uint32_t A, uint32_t X, uint32_t n, uint32_t kids, uint64_t bits,
                           uint32_t brk, uint64_t& obits) {
     uint32_t x = E, ce = NONE, bp = FAIL;
+    // Every chunk entered where its predecessor's walk left it (the usual case: the guesses
+    // synchronised): the chain is the lanes' own walks, from one ballot. Otherwise the uniform
+    // loop below takes over from the first chunk that is not.
+    uint32_t j0 = 0;
+    {
+        const uint32_t cl = PRE + lane * CH;
+        const bool act = cl < lim;
+        const uint32_t xp = (uint32_t)__shfl_up((int)X, 1, 64);
+        const uint32_t pin = lane == 0 ? E : xp;  // where the chain enters the lane's chunk
+        const bool cov = pin >= min(cl + CH, lim);  // an item covers the whole chunk
+        const uint64_t bad = __ballot(act && !(pin == A && X != FAIL));
+        j0 = bad ? (uint32_t)__builtin_ctzll(bad) : TILE / CH;
+        if (lane < j0 && act && !cov) ce = A;
+        if (j0 > 0) x = (uint32_t)__builtin_amdgcn_readlane((int)X, (int)(j0 - 1));
+        if (j0 == TILE / CH) {
+            const uint64_t am = __ballot(act);
+            x = (uint32_t)__builtin_amdgcn_readlane((int)X, 63 - (int)__builtin_clzll(am));
+        }
+    }
 #pragma unroll 1
-    for (uint32_t j = 0; j < TILE / CH && x < lim; j++) {
+    for (uint32_t j = j0; j < TILE / CH && x < lim; j++) {
         const uint32_t cj = PRE + j * CH;
         const uint32_t endj = min(cj + CH, lim);
         if (x >= endj) continue;  // an item covers the whole chunk
