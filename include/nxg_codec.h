@@ -191,13 +191,16 @@ bool nxg_encode_frames(NxgCtx* ctx, const NxgColumns* in, const uint8_t* heap, u
  * straddle frames, channel.rs:187-201, but they do straddle ranges). A range's summary says
  * where its chain enters (the first message start >= begin) and leaves (the first start >= end,
  * or the frame end); nxg_range_link checks that consecutive ranges meet and numbers their rows.
- * Homogeneous-f64 frames only (the length-run decoder); others report ok = 0. */
+ * Any f64 frame (the length-run decoder, or the single-pass decoder when ids come in any order)
+ * into f64 or mixed columns, and frames of short Updates / Heartbeats (the fast mixed decoder)
+ * into mixed columns; a range those decoders decline (Maps, nested containers, content errors)
+ * reports ok = 0, for the caller to decode the frame whole. */
 typedef struct NxgRange {
     uint64_t begin, end; /* the byte range [begin, end) of the frame */
     uint64_t entry;      /* first message start >= begin (absolute byte offset) */
     uint64_t exit;       /* first message start >= end, or the frame end */
     uint64_t n_rows;     /* rows decoded from the range (at dout rows 0 .. n_rows) */
-    uint32_t ok;         /* 1: decoded; 0: not a homogeneous-f64 range (decode the frame) */
+    uint32_t ok;         /* 1: decoded; 0: a range these decoders decline (decode the frame) */
     uint32_t err_kind;   /* NxgErrKind when ok = 1 but the columns overflowed, else 0 */
 } NxgRange;
 /* Device frame and device columns; synchronous. */

@@ -25,7 +25,7 @@ def main():
     codec = netidx_amd.Codec(0)
     stream = torch.cuda.Stream()
     codec.set_stream(stream.cuda_stream)
-    kinds = ("ctl",) if tag == "ctlonly" else ("plain", "ctl")
+    kinds = {"ctlonly": ("ctl",), "plainonly": ("plain",)}.get(tag, ("plain", "ctl"))
     for kind in kinds:
         if kind == "plain":
             m = synth.mixed_columns(n)
