@@ -1061,6 +1061,10 @@ def main():
     _, kms_same, st1 = time_decode(codec, wire, outs[0], n, max(20, args.steps // 4), 2, world,
                                    stream, stream_of_frames=True)
     assert st1.err_kind == 0 and st1.path == 1 and st1.n_rows == n, st1
+    # one nxg_decode_updates_async per frame (no backlog), the same frames in rotation
+    _, kms_call, st3 = time_decode(codec, wires, outs, n, max(20, args.steps // 4), 2, world,
+                                   stream, stream_of_frames=False)
+    assert st3.err_kind == 0 and st3.path == 1 and st3.n_rows == n, st3
     # the length-run decoder (any f64 frame; probe of frame j + 1 fused into the emit of frame j)
     crun = codec_run_path(local)
     crun.set_stream(stream.cuda_stream)
@@ -1110,6 +1114,11 @@ def main():
                      "timed": "HIP events on the codec stream around the whole backlog of frames "
                               "(nxg_decode_frames_async), divided by the frames; 3 distinct "
                               "frames and column sets in rotation (every decode from HBM)"},
+        "method": "stream of frames: a connection's backlog through nxg_decode_frames_async "
+                  "(round 3 on); per_call: one nxg_decode_updates_async per frame",
+        "per_call": {"kernel_ms": round(kms_call, 4), "frac": frac(kms_call),
+                     "timed": "one nxg_decode_updates_async per frame, the 3 frames in rotation, "
+                              "HIP events on the codec stream"},
         "same_frame": {"kernel_ms": round(kms_same, 4), "frac": frac(kms_same),
                        "timed": "one frame into one column set every time (rounds 1-3's method: "
                                 "partly served by the Infinity Cache)"},
