@@ -437,7 +437,7 @@ __global__ __launch_bounds__(TPB) void nxg_fa_count_kernel(const uint8_t* __rest
 }
 
 #ifndef NXG_FA_FIX_PASSES
-#define NXG_FA_FIX_PASSES 1  // (2: a second pass for tiles whose predecessor the first recounted)
+#define NXG_FA_FIX_PASSES 2  // a second pass for tiles whose predecessor the first recounted (fix 69 -> 2 x 64, resolve 134 -> 52 us)
 #endif
 // fix: one wave per tile, all tiles at once. A tile whose guessed entry is not its predecessor's
 // counted exit is recounted from that exit. A false guess almost always merges into the true

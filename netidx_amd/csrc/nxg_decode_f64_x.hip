@@ -52,7 +52,7 @@ constexpr uint32_t MAXR = SUB / 12 + 2;  // rows per sub-tile (records start in 
 #define NXG_F64X_CHEAP 1  // 0: every candidate checked as a record before it counts as a start
 #endif                    // (10^7 random-order ids: 128.6 us, against 105.6 us for 1)
 #ifndef NXG_F64X_LASTX
-#define NXG_F64X_LASTX 0  // 1: the 16 positions after a sub-tile are read only after the wave's last (A/B)
+#define NXG_F64X_LASTX 1  // 1: the 16 positions after a sub-tile read only after the wave's last (0.121-0.122 vs 0.1245 ms)
 #endif
 constexpr int CB = NXG_F64X_CB;          // candidates checked together (independent loads)
 }  // namespace f64x
@@ -208,7 +208,7 @@ NXG_DEV void subtile_starts(const uint8_t* __restrict__ wire, const XRange& rg, 
     starts_of<16>(im, r, fp, W, S, slo, shi);
     // lane 63: the starts among the 16 positions after the sub-tile. Inside the wave the next
     // sub-tile's entry check covers them (LASTX), so only the wave's last sub-tile reads them.
-    const bool need_x = !NXG_F64X_LASTX || last_sub || a0 + SUB >= W;
+    const bool need_x = !NXG_F64X_LASTX || last_sub || a0 + SUB >= W || a0 + SUB >= R;
     uint64_t Sx = 0, xlo, xhi;
     if (need_x) starts_of<4>(im, XHI, ib + XHI, W, Sx, xlo, xhi);
     // False starts -- bytes inside a record that read as one (an f64's bytes may) -- are
