@@ -659,7 +659,11 @@ __global__ __launch_bounds__(TPB) void nxg_fa_emit_kernel(
         const bool arr = o.tag == 19u;
         bool ok = !has || ((sa != 0u || !(b & 0x80u)) && o.ok && (!far || !arr) &&
                            (!arr || o.end <= elim));
-        if (far && ok && o.slen) ok = utf8_ok(GlbSrc{(gbl_bytes)buf}, t0 + o.soff, o.slen);
+        {  // (text past the image: the whole wave, one text after the other)
+            const bool fw = far && ok && o.slen;
+            const bool fo = far_text_ok(buf, fw, t0 + o.soff, o.slen, lane);
+            if (fw) ok = fo;
+        }
         bad = __any(!ok);
         if (bad) why |= 8u | (__any(has && !o.ok) ? 16u : 0u) | (__any(far && arr) ? 32u : 0u);
         if (!bad) {

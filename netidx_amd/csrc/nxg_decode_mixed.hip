@@ -848,7 +848,11 @@ __global__ __launch_bounds__(TPB) void nxg_fmx_emit_kernel(
             // past the image: text only (the count pass), checked here from global memory
             const bool far = !LEAN && upd && lim > wend;
             bool ok = !upd || ((sa != 0u || !(b & 0x80u)) && u <= (lim - p) && lim <= fend && o.ok);
-            if (far && ok && o.slen) ok = utf8_ok(GlbSrc{(gbl_bytes)wire}, t0 + o.soff, o.slen);
+            if (!LEAN) {  // (text past the image: the whole wave, one text after the other)
+                const bool fw = far && ok && o.slen;
+                const bool fo = far_text_ok(wire, fw, t0 + o.soff, o.slen, lane);
+                if (fw) ok = fo;
+            }
             PMARK(1);
             // text: checked once per tile (text_flush) from a list in `el`
             bad = __any(!ok);

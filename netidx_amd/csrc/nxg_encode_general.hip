@@ -40,9 +40,18 @@
 namespace {
 
 constexpr int TPB = 256;
-constexpr int GRPT = 4;                  // rows per thread
+#ifndef NXG_ENC_GRPT
+#define NXG_ENC_GRPT 4
+#endif
+#ifndef NXG_ENC_OCC
+#define NXG_ENC_OCC 1  // waves per SIMD asked of the register allocator (launch bounds)
+#endif
+#ifndef NXG_ENC_BPR
+#define NXG_ENC_BPR 28  // staging bytes per row
+#endif
+constexpr int GRPT = NXG_ENC_GRPT;       // rows per thread
 constexpr int GTILE = TPB * GRPT;        // rows per tile
-constexpr int GSTG = GTILE * 28 + 32;    // staging: 28 bytes per row (config 3 averages 21.5)
+constexpr int GSTG = GTILE * NXG_ENC_BPR + 32;  // staging (config 3 averages 21.5 bytes per row)
 constexpr uint64_t kMaxVec = 2ull * 1024 * 1024 * 1024;
 
 struct Slot {
@@ -392,7 +401,7 @@ __global__ __launch_bounds__(TPB) void nxg_enc_ctl_scan_kernel(ColsDesc c, uint6
     if (threadIdx.x == 0) ctl_pre[c.n_ctl] = carry;
 }
 
-__global__ __launch_bounds__(TPB) void nxg_enc_rows_kernel(
+__global__ __launch_bounds__(TPB, NXG_ENC_OCC) void nxg_enc_rows_kernel(
     ColsDesc c, const uint8_t* __restrict__ heap, uint8_t* __restrict__ out, uint64_t cap,
     const uint64_t* __restrict__ ctl_pre, uint64_t* __restrict__ row_off,
     uint64_t* __restrict__ tstat, uint32_t ntiles, uint32_t epoch, DevStatus* __restrict__ st,

@@ -347,6 +347,35 @@ NXG_DEV bool utf8_packed(lds_bytes img, uint8_t* mark, bool na, uint32_t soff, u
 
 // The deferred text checks of a tile: entries soff | slen << 16 in `list`, 64 per pass (ASCII per
 // lane, the rest by utf8_packed). Uniform; false on invalid UTF-8.
+// Text that leaves the tile's image (lanes with `want`: n bytes at frame offset off): the ASCII
+// check by the whole wave from global memory, 4 bytes per lane, one text after the other; a text
+// holding a byte >= 0x80 is then checked exactly (std::str::from_utf8 rules, utf8_ok) by its own
+// lane. All 64 lanes active. Returns the lane's verdict (true when it has no such text).
+NXG_DEV bool far_text_ok(const uint8_t* wire, bool want, uint64_t off, uint32_t n, uint32_t lane) {
+    bool ok = true;
+#pragma unroll 1
+    for (uint64_t m = __ballot(want); m; m &= m - 1) {
+        const uint32_t j = (uint32_t)__builtin_ctzll(m);
+        const uint64_t sj =
+            (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)off, (int)j) |
+            ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(off >> 32), (int)j) << 32);
+        const uint32_t nj = (uint32_t)__builtin_amdgcn_readlane((int)n, (int)j);
+        bool hi = false;
+#pragma unroll 1
+        for (uint32_t k = 0; k < nj; k += 256) {
+            const uint32_t o = k + 4u * lane;
+            if (o < nj) {
+                const uint32_t rem = nj - o;
+#pragma unroll
+                for (uint32_t q = 0; q < 4; q++)
+                    if (q < rem) hi |= wire[sj + o + q] >= 0x80u;
+            }
+        }
+        if (__any(hi) && lane == j) ok = utf8_ok(GlbSrc{(gbl_bytes)wire}, sj, nj);
+    }
+    return ok;
+}
+
 NXG_DEV bool text_flush(lds_bytes img, const uint32_t* list, uint32_t ntxt, uint8_t* mark,
                         uint32_t lane, DevStatus* st) {
     bool good = true;
@@ -355,7 +384,30 @@ NXG_DEV bool text_flush(lds_bytes img, const uint32_t* list, uint32_t ntxt, uint
         const uint32_t i = b + lane;
         const uint32_t e = i < ntxt ? list[i] : 0u;
         const uint32_t so = e & 0xffffu, sl = e >> 16;
-        const bool na = sl && !ascii_ok(img, so, sl);
+        // texts longer than 32 bytes: the ASCII check by the whole wave, 4 bytes per lane, one
+        // text after the other (a lane alone would take a round of 32 bytes each while the
+        // others wait)
+        bool na_long = false;
+#pragma unroll 1
+        for (uint64_t lm = __ballot(sl > 32u); lm; lm &= lm - 1) {
+            const uint32_t j = (uint32_t)__builtin_ctzll(lm);
+            const uint32_t sj = (uint32_t)__builtin_amdgcn_readlane((int)so, (int)j);
+            const uint32_t nj = (uint32_t)__builtin_amdgcn_readlane((int)sl, (int)j);
+            bool hi = false;
+#pragma unroll 1
+            for (uint32_t k = 0; k < nj; k += 256) {
+                const uint32_t off = k + 4u * lane;
+                if (off < nj) {
+                    uint32_t q[1];
+                    win_words<1>(img, sj + off, q);
+                    const uint32_t rem = nj - off;
+                    const uint32_t keep = rem >= 4u ? 0xffffffffu : (1u << (8u * rem)) - 1u;
+                    hi |= (q[0] & keep & 0x80808080u) != 0u;
+                }
+            }
+            if (__any(hi) && lane == j) na_long = true;
+        }
+        const bool na = sl && (sl > 32u ? na_long : !ascii_ok(img, so, sl));
 #if NXG_FMX_PROF
         {
             const uint64_t nm = __ballot(na);
