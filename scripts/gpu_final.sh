@@ -1,12 +1,10 @@
 #!/bin/bash
-# round-end rehearsal: smoke(), the GPU suite, the default bench line
+# round 4 final: mixed / archive tests and timings, then the whole GPU suite, smoke() and the bench
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd $R
-mkdir -p gpurun_out
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
-rc=$?; tail -2 gpurun_out/smoke.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 900 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
-rc=$?; tail -2 gpurun_out/pytest_gpu.log; [ $rc -eq 0 ] || { grep -E "FAILED|Error" gpurun_out/pytest_gpu.log | head -20; exit $rc; }
-timeout -k 10 600 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err
-rc=$?; cat gpurun_out/bench.json; [ $rc -eq 0 ] || { tail -5 gpurun_out/bench.err; exit $rc; }
+scripts/gpu_mix3.sh || exit 1
+timeout -k 10 300 python3 -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_archive.py > gpurun_out/ta.log 2>&1 || { tail -20 gpurun_out/ta.log; exit 1; }
+tail -1 gpurun_out/ta.log
+scripts/trace_arch.sh base || true
+TAG=${TAG:-r04e} scripts/gpu_r04b.sh
