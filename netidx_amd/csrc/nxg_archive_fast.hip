@@ -342,15 +342,33 @@ NXG_DEV FaDesc count_tile(lds_bytes img, uint64_t t, uint64_t W, uint32_t E, uin
                                            rbits, rkids)
                                : c;
     uint32_t ge = 0;
-    if (E == NONE) {  // lane 0 also walks the bytes before the tile (two 64-byte halves)
-        uint32_t f2, k2;
-        uint64_t b2;
-        if (lane == 0) {
-            ge = spec_walk(img, 0, 0, CH, wl, f2, item_cands((lds_bytes)img, 0), b2, k2);
-            if (ge < PRE)
-                ge = spec_walk(img, ge, CH, PRE, wl, f2, item_cands((lds_bytes)img, CH), b2, k2);
+    if (E == NONE) {
+        // the walk over the two 64-byte halves before the tile: lanes 0 and 1 walk one half each
+        // at the same time; when the first half's exit is an item of the second half's last
+        // unbroken run, the exact walk from there is that run, so the guess is that walk's exit
+        // (else lane 0 walks on from the first half's exit)
+        static_assert(PRE == 2 * CH, "two halves before the tile");
+        uint32_t f2 = 0, k2 = 0;
+        uint64_t b2 = 0;
+        if (lane < 2) {
+            const uint32_t cb = lane * CH;
+            ge = spec_walk(img, cb, cb, cb + CH, wl, f2, item_cands((lds_bytes)img, cb), b2, k2);
         }
-        E = (uint32_t)__builtin_amdgcn_readlane((int)ge, 0);
+        const uint32_t ge1 = (uint32_t)__builtin_amdgcn_readlane((int)ge, 0);
+        const uint32_t ge2 = (uint32_t)__builtin_amdgcn_readlane((int)ge, 1);
+        const uint32_t fr2 = (uint32_t)__builtin_amdgcn_readlane((int)f2, 1);
+        const uint64_t rb2 =
+            (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b2, 1) |
+            ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b2 >> 32), 1) << 32);
+        if (ge1 >= PRE) {
+            E = ge1;  // an item covers the second half
+        } else if (ge1 >= fr2 && ((rb2 >> (ge1 - CH)) & 1ull)) {
+            E = ge2;
+        } else {
+            if (lane == 0)
+                ge = spec_walk(img, ge1, CH, PRE, wl, f2, item_cands((lds_bytes)img, CH), b2, k2);
+            E = (uint32_t)__builtin_amdgcn_readlane((int)ge, 0);
+        }
     } else {
         E += PRE;
     }

@@ -462,13 +462,22 @@ NXG_DEV TileDesc count_tile(const uint8_t* img, uint64_t t, uint64_t nt, const F
         }
         d = count_from(img, cd, g, lim, last, lane, bits);
     }
-    if (FULL && d.entry != FAIL && d.entry < 2 * CH) {
+    if (d.entry == FAIL) {
+        // chunks 0 and 1 hold no candidate (the tile starts inside a long text): the first
+        // candidate of a later chunk, so that the tile needs no recount in the resolve pass
+        const uint64_t cm = __ballot(cd.c0 != FAIL) & ~3ull;
+        if (cm) {
+            const uint32_t g = (uint32_t)__builtin_amdgcn_readlane((int)cd.c0, (int)__builtin_ctzll(cm));
+            d = count_from(img, cd, g, lim, last, lane, bits);
+        }
+    }
+    if (FULL && d.entry != FAIL) {
         // a message with a two-byte prefix (long text) that ends where the guessed chain starts
         // is the tile's entry (the guesses use one-byte candidates only): the chain from there,
-        // so that the tile needs no recount in the resolve pass
+        // so that the tile needs no recount
         const uint32_t g = d.entry;
         uint32_t x2 = FAIL;
-        if (lane < 2) {
+        if (lane <= (g >> 6)) {
 #pragma unroll 1
             for (uint64_t m = cd.m; m; m &= m - 1) {
                 const uint32_t p = lane * CH + (uint32_t)__builtin_ctzll(m);
@@ -487,15 +496,6 @@ NXG_DEV TileDesc count_tile(const uint8_t* img, uint64_t t, uint64_t nt, const F
                 d = d2;
                 bits = b2;
             }
-        }
-    }
-    if (d.entry == FAIL) {
-        // chunks 0 and 1 hold no candidate (the tile starts inside a long text): the first
-        // candidate of a later chunk, so that the tile needs no recount in the resolve pass
-        const uint64_t cm = __ballot(cd.c0 != FAIL) & ~3ull;
-        if (cm) {
-            const uint32_t g = (uint32_t)__builtin_amdgcn_readlane((int)cd.c0, (int)__builtin_ctzll(cm));
-            d = count_from(img, cd, g, lim, last, lane, bits);
         }
     }
     return d;
