@@ -37,6 +37,7 @@ def main():
             res = {"tag": tag, "path": path, "n": n, "W": W}
             for o in outs:
                 o.id.zero_()
+            torch.cuda.synchronize()  # (the zeroing runs on torch's stream, the decode on ours)
             st = codec.decode_into(wires[0].data_ptr(), W, outs[0])
             res["diag1"] = codec.last_diag()[1]
             res["ok"] = bool(st.n_rows == n and torch.equal(outs[0].id[:n], cols.id[:n])
