@@ -30,14 +30,17 @@
 namespace f64s {
 constexpr int TPB = 256;
 #ifndef NXG_F64S_R
-#define NXG_F64S_R 8  // records per lane loaded together (4 pairs)
+#define NXG_F64S_R 8  // records per lane loaded together (4 pairs), frames past the Infinity Cache
 #endif
-constexpr int R = NXG_F64S_R;
-constexpr uint32_t WREC = 64 * R;   // records per wave
+#ifndef NXG_F64S_R_SMALL
+#define NXG_F64S_R_SMALL 4  // ... and frames within it (A/B: 4 is 2 % faster at 10^7, 8 at 10^8)
+#endif
 #ifndef NXG_F64S_NT
 #define NXG_F64S_NT 1  // bit 0: nontemporal column stores, bit 1: nontemporal wire loads
 #endif
 constexpr uint64_t kXcdMin = 256ull << 20;  // frames past the Infinity Cache (256 MiB)
+// records per lane for a frame of W bytes
+inline int r_for(uint64_t W) { return W >= kXcdMin ? NXG_F64S_R : NXG_F64S_R_SMALL; }
 #ifndef NXG_F64S_XCD
 #define NXG_F64S_XCD 1  // XCD-contiguous record ranges for frames past the Infinity Cache
 #endif
@@ -116,6 +119,7 @@ NXG_DEV bool emit_edge(const uint8_t* __restrict__ wire, uint64_t W, uint64_t p0
 // scalar base and the wave keeps only the R blocks it loaded in registers: lane j's record's second
 // block is lane j + 1's first (DPP), and lane 63's is lane 0's of the next batch (readlane), or
 // for the last batch one more block that lane 63 loads.
+template <int R>
 NXG_DEV bool emit_full(const uint8_t* __restrict__ wire, uint64_t W, uint64_t p0, uint32_t L,
                        uint32_t ks, uint64_t k0, uint64_t i0, uint64_t* __restrict__ oid,
                        uint64_t* __restrict__ oval, uint64_t cap, uint32_t lane, bool& over) {
@@ -186,6 +190,7 @@ NXG_DEV bool emit_full(const uint8_t* __restrict__ wire, uint64_t W, uint64_t p0
 // even: one 16-byte aligned store per column). The two records lie in the 48 bytes from the
 // aligned block of the first: blocks A and B are loaded, C is the next lane's A or B (DPP; its
 // first record starts 24..32 bytes after ours), lane 63 loads its C itself.
+template <int R>
 NXG_DEV bool emit_full_pairs(const uint8_t* __restrict__ wire, uint64_t W, uint64_t p0, uint32_t L,
                              uint32_t ks, uint64_t k0, uint64_t i0, uint64_t* __restrict__ oid,
                              uint64_t* __restrict__ oval, uint64_t cap, uint32_t lane,
@@ -276,6 +281,7 @@ NXG_DEV bool emit_full_pairs(const uint8_t* __restrict__ wire, uint64_t W, uint6
 // waves past the frame's last record exit after the head read. Everything before the loads is
 // wave-uniform (scalar registers): the head, the closed-form position of the wave's first record
 // and the width change inside the wave.
+template <int R>
 __global__ __launch_bounds__(f64s::TPB) void nxg_f64s_kernel(const uint8_t* __restrict__ wire,
                                                              uint64_t W, uint64_t* __restrict__ oid,
                                                              uint64_t* __restrict__ oval,
@@ -284,6 +290,7 @@ __global__ __launch_bounds__(f64s::TPB) void nxg_f64s_kernel(const uint8_t* __re
                                                              DevStatus* zst) {
     using namespace f64s;
     using namespace f64rec16;
+    constexpr uint32_t WREC = 64 * R;  // records per wave
     // another wave rejected the frame already (a plain read before any store: a scalar load)
     const uint32_t failed = st->fast_fail;
     zero_status(zst);
@@ -336,8 +343,8 @@ __global__ __launch_bounds__(f64s::TPB) void nxg_f64s_kernel(const uint8_t* __re
     const uint64_t pend = p0 + (uint64_t)ks * L + (uint64_t)(WREC - ks) * (L + 1);  // pos(k0 + WREC)
     bool over = false, bad = b > 5;
     if (!bad && pend + 48 <= W) {
-        bad = NXG_F64S_PAIR ? emit_full_pairs(wire, W, p0, L, ks, k0, i0, oid, oval, cap, lane, over)
-                            : emit_full(wire, W, p0, L, ks, k0, i0, oid, oval, cap, lane, over);
+        bad = NXG_F64S_PAIR ? emit_full_pairs<R>(wire, W, p0, L, ks, k0, i0, oid, oval, cap, lane, over)
+                            : emit_full<R>(wire, W, p0, L, ks, k0, i0, oid, oval, cap, lane, over);
     } else if (!bad) {
         // near the frame's end: n = #{k < WREC : pos(k0 + k) < W} (pos increases by 12..16 per
         // record); the frame's last record must end exactly at W
@@ -370,7 +377,8 @@ __global__ __launch_bounds__(f64s::TPB) void nxg_f64s_kernel(const uint8_t* __re
 
 uint64_t nxg_dec_f64s_groups(uint64_t W) {
     const uint64_t maxrec = W / 12 + 1;
-    const uint64_t waves = (maxrec + f64s::WREC - 1) / f64s::WREC;
+    const uint64_t wrec = 64ull * (uint64_t)f64s::r_for(W);
+    const uint64_t waves = (maxrec + wrec - 1) / wrec;
     return (waves + f64s::TPB / 64 - 1) / (f64s::TPB / 64);
 }
 
@@ -382,7 +390,11 @@ hipError_t nxg_launch_dec_f64s(const uint8_t* wire, uint64_t W, uint64_t* oid, u
     const uint64_t ng = nxg_dec_f64s_groups(W);
     if (ng > 0x7fffffffull) return hipErrorInvalidValue;
     const uint32_t flags = NXG_F64S_XCD && W > f64s::kXcdMin ? f64s::F_XCD : 0u;
-    hipLaunchKernelGGL(nxg_f64s_kernel, dim3((uint32_t)ng), dim3(f64s::TPB), NXG_F64S_LDS, s, wire,
-                       W, oid, oval, cap, flags, st, zst);
+    if (f64s::r_for(W) == NXG_F64S_R)
+        hipLaunchKernelGGL(nxg_f64s_kernel<NXG_F64S_R>, dim3((uint32_t)ng), dim3(f64s::TPB),
+                           NXG_F64S_LDS, s, wire, W, oid, oval, cap, flags, st, zst);
+    else
+        hipLaunchKernelGGL(nxg_f64s_kernel<NXG_F64S_R_SMALL>, dim3((uint32_t)ng), dim3(f64s::TPB),
+                           NXG_F64S_LDS, s, wire, W, oid, oval, cap, flags, st, zst);
     return hipGetLastError();
 }
