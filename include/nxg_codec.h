@@ -193,19 +193,35 @@ bool nxg_encode_frames(NxgCtx* ctx, const NxgColumns* in, const uint8_t* heap, u
  * or the frame end); nxg_range_link checks that consecutive ranges meet and numbers their rows.
  * Any f64 frame (the length-run decoder, or the single-pass decoder when ids come in any order)
  * into f64 or mixed columns, and frames of short Updates / Heartbeats (the fast mixed decoder)
- * into mixed columns; a range those decoders decline (Maps, nested containers, content errors)
- * reports ok = 0, for the caller to decode the frame whole. */
+ * into mixed columns; a range those decoders decline (Maps, nested containers, rare control
+ * messages, content errors) reports ok = 0 (err_kind NXG_CAPACITY when it was declined because
+ * the columns are too small). nxg_decode_sharded then falls back to row shares
+ * (nxg_decode_share). */
 typedef struct NxgRange {
     uint64_t begin, end; /* the byte range [begin, end) of the frame */
     uint64_t entry;      /* first message start >= begin (absolute byte offset) */
     uint64_t exit;       /* first message start >= end, or the frame end */
     uint64_t n_rows;     /* rows decoded from the range (at dout rows 0 .. n_rows) */
-    uint32_t ok;         /* 1: decoded; 0: a range these decoders decline (decode the frame) */
-    uint32_t err_kind;   /* NxgErrKind when ok = 1 but the columns overflowed, else 0 */
+    uint32_t ok;         /* 1: decoded by bytes; 2: decoded as a row share (nxg_decode_sharded's
+                            fallback: entry = exit = UINT64_MAX); 0: declined */
+    uint32_t err_kind;   /* NxgErrKind: the columns overflowed (ok = 1, or ok = 0 when that is why
+                            the range was declined); the frame's error (ok = 2); else 0 */
+    uint64_t err_offset; /* ok = 2: the frame's error offset */
 } NxgRange;
 /* Device frame and device columns; synchronous. */
 bool nxg_decode_range(NxgCtx* ctx, const uint8_t* dframe, uint64_t frame_len, uint64_t begin,
                       uint64_t end, NxgColumns* dout, NxgRange* rng, NetidxError* err);
+/* One share of a frame's rows: the frame (device) decoded whole, as nxg_decode_updates does
+ * (every decoder, every error), then rows [N*share/shares, N*(share+1)/shares) of its N rows, the
+ * children of their values and the control spans before them (the last share: also those after
+ * the last row) into dout (device columns) from row 0, child indices and ctl_row re-based;
+ * *row_off = the share's first row. The frame's error (status->err_kind / err_offset) leaves no
+ * rows in any share; a share that does not fit dout reports NXG_CAPACITY (NXG_NOT_F64 for mixed
+ * content in f64 columns). The ctx grows its own whole-frame columns on demand (first `shares`
+ * times dout's capacities). Synchronous. */
+bool nxg_decode_share(NxgCtx* ctx, const uint8_t* dframe, uint64_t frame_len, uint32_t share,
+                      uint32_t shares, NxgColumns* dout, uint64_t* row_off, NxgStatus* status,
+                      NetidxError* err);
 /* Ranges in frame order, contiguous from 0 to frame_len: checks ranges[0].entry == 0,
  * ranges[i].exit == ranges[i+1].entry and the last exit == frame_len; row_off[i] = rows before
  * range i. Returns false (and *bad = the first range whose entry is off the chain) otherwise. */
@@ -243,6 +259,10 @@ typedef struct NxgCommOps {
                    uint64_t cap, uint64_t* len);
     bool (*decode_range)(void* user, const uint8_t* frame, uint64_t frame_len, uint64_t begin,
                          uint64_t end, NxgColumns* out, NxgRange* rng);
+    /* optional with the codec hooks (NULL: a declined range fails nxg_decode_sharded): the
+     * contract of nxg_decode_share */
+    bool (*decode_share)(void* user, const uint8_t* frame, uint64_t frame_len, uint32_t share,
+                         uint32_t shares, NxgColumns* out, uint64_t* row_off, NxgStatus* status);
 } NxgCommOps;
 /* Not collective. ctx may be NULL when ops carries the local codec. The ops struct is copied. */
 NxgComm* nxg_comm_init_ops(NxgCtx* ctx, int nranks, int rank, const NxgCommOps* ops,
@@ -258,9 +278,13 @@ bool nxg_encode_allgather(NxgCtx* ctx, NxgComm* comm, const NxgColumns* din, con
                           NetidxError* err);
 /* One frame (on every rank's device) decoded in nranks byte ranges: rank r decodes range r,
  * the summaries are all-gathered and linked; a range whose guessed entry is off the chain is
- * decoded again from its predecessor's exit. *row_off = this rank's first global row. Every rank
- * returns the same verdict: a range that fails to decode, is not a homogeneous-f64 range, or a
- * frame that does not link makes all of them return false. */
+ * decoded again from its predecessor's exit. *row_off = this rank's first global row. When a
+ * range is declined (rng->ok 0 on some rank: content the byte-range decoders do not take), every
+ * rank sees it in the same exchange and falls back to nxg_decode_share(rank, nranks): the frame
+ * decoded whole on every rank (the frame is there already; no data moves), rows in nranks row
+ * shares, rng->ok = 2, the frame's error in rng->err_kind / err_offset. Every rank returns the
+ * same verdict: a local failure on any rank (a launch, a range declined for capacity), or a frame
+ * that does not link makes all of them return false. */
 bool nxg_decode_sharded(NxgCtx* ctx, NxgComm* comm, const uint8_t* dframe, uint64_t frame_len,
                         NxgColumns* dout, uint64_t* row_off, NxgRange* rng, NetidxError* err);
 

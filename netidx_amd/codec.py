@@ -67,10 +67,11 @@ class NxgColumns(C.Structure):
 class NxgRange(C.Structure):
     _fields_ = [("begin", C.c_uint64), ("end", C.c_uint64), ("entry", C.c_uint64),
                 ("exit", C.c_uint64), ("n_rows", C.c_uint64), ("ok", C.c_uint32),
-                ("err_kind", C.c_uint32)]
+                ("err_kind", C.c_uint32), ("err_offset", C.c_uint64)]
 
     def tuple(self):
-        return (self.begin, self.end, self.entry, self.exit, self.n_rows, self.ok, self.err_kind)
+        return (self.begin, self.end, self.entry, self.exit, self.n_rows, self.ok, self.err_kind,
+                self.err_offset)
 
     @classmethod
     def of(cls, t):
@@ -158,6 +159,9 @@ SIGNATURES = {
     "nxg_decode_range": (C.c_bool, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint64,
                                     C.POINTER(NxgColumns), C.POINTER(NxgRange),
                                     C.POINTER(NetidxError)]),
+    "nxg_decode_share": (C.c_bool, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, C.c_uint32,
+                                    C.POINTER(NxgColumns), C.POINTER(C.c_uint64),
+                                    C.POINTER(NxgStatus), C.POINTER(NetidxError)]),
     "nxg_range_link": (C.c_bool, [C.POINTER(NxgRange), C.c_uint32, C.c_uint64, C.c_void_p,
                                   C.POINTER(C.c_uint32), C.POINTER(NetidxError)]),
     "nxg_comm_unique_id": (C.c_bool, [C.c_void_p, C.POINTER(NetidxError)]),
@@ -613,6 +617,16 @@ class Codec:
                                       C.byref(cols.s), C.byref(rng), C.byref(err)), err)
         return rng
 
+    def decode_share(self, dframe, frame_len, share, shares, cols):
+        """nxg_decode_share: the frame decoded whole, row share `share` of `shares` into cols;
+        returns (first row of the share, NxgStatus)."""
+        ptr = dframe.data_ptr() if hasattr(dframe, "data_ptr") else int(dframe)
+        off, st, err = C.c_uint64(0), NxgStatus(), NetidxError()
+        _check(lib().nxg_decode_share(self.ctx, C.c_void_p(ptr), frame_len, share, shares,
+                                      C.byref(cols.s), C.byref(off), C.byref(st), C.byref(err)),
+               err)
+        return off.value, st
+
     def encode_frames(self, cols, heap, out_ptr, cap, max_frames=16):
         """Encode into out_ptr and return (total length, [frame payload lengths]) as
         WriteChannel::queue_send / try_flush would cut them (MAX_BATCH, channel.rs:177-257)."""
@@ -1023,11 +1037,14 @@ _ENC = C.CFUNCTYPE(C.c_bool, C.c_void_p, C.POINTER(NxgColumns), C.c_void_p, C.c_
                    C.c_uint64, C.POINTER(C.c_uint64))
 _DRNG = C.CFUNCTYPE(C.c_bool, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint64,
                     C.POINTER(NxgColumns), C.POINTER(NxgRange))
+_DSHR = C.CFUNCTYPE(C.c_bool, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, C.c_uint32,
+                    C.POINTER(NxgColumns), C.POINTER(C.c_uint64), C.POINTER(NxgStatus))
 
 
 class NxgCommOps(C.Structure):
     _fields_ = [("user", C.c_void_p), ("allgather", _AG), ("allgatherv", _AGV),
-                ("encoded_len", _ELEN), ("encode", _ENC), ("decode_range", _DRNG)]
+                ("encoded_len", _ELEN), ("encode", _ENC), ("decode_range", _DRNG),
+                ("decode_share", _DSHR)]
 
 
 def _guard(fn):
@@ -1063,12 +1080,14 @@ class Comm:
 
     @classmethod
     def with_ops(cls, codec, nranks, rank, allgather, allgatherv, encoded_len=None, encode=None,
-                 decode_range=None):
+                 decode_range=None, decode_share=None):
         """nxg_comm_init_ops. allgather(mine: bytes) -> bytes of every rank's, in rank order;
         allgatherv(buf_ptr, offsets, nranks, rank) fills every shard of the buffer at its
         offset. The optional local codec: encoded_len(NxgColumns) -> int; encode(NxgColumns,
         out_ptr, cap) -> int; decode_range(frame_ptr, frame_len, begin, end, NxgColumns) ->
-        (begin, end, entry, exit, n_rows, ok, err_kind). codec may be None with the codec."""
+        (begin, end, entry, exit, n_rows, ok, err_kind); and, optionally with it,
+        decode_share(frame_ptr, frame_len, share, shares, NxgColumns) -> (row_off, n_rows,
+        err_kind, err_offset). codec may be None with the codec."""
         self = cls.__new__(cls)
 
         def ag(user, mine, all_, nbytes):
@@ -1094,6 +1113,16 @@ class Comm:
             fns += [_ELEN(_guard(elen)), _ENC(_guard(enc)), _DRNG(_guard(drng))]
         else:
             fns += [_ELEN(), _ENC(), _DRNG()]
+        if decode_share is not None:
+            def dshr(user, frame, flen, share, shares, cols, off, st):
+                o, nr, ek, eo = decode_share(int(frame or 0), int(flen), int(share), int(shares),
+                                             cols.contents)
+                off[0] = int(o)
+                st[0] = NxgStatus(n_rows=int(nr), err_kind=int(ek), err_offset=int(eo))
+
+            fns.append(_DSHR(_guard(dshr)))
+        else:
+            fns.append(_DSHR())
         self._fns = fns  # the C function pointers live as long as the communicator
         self.ops = NxgCommOps(None, *fns)
         err = NetidxError()
@@ -1128,7 +1157,8 @@ class Comm:
         return n.value, [int(x) for x in offs]
 
     def decode_sharded(self, dframe, frame_len, cols):
-        """This rank's byte range of one frame; returns (first global row, NxgRange)."""
+        """This rank's byte range of one frame (or, for a frame the byte-range decoders decline,
+        its row share: rng.ok == 2); returns (first global row, NxgRange)."""
         ptr = dframe.data_ptr() if hasattr(dframe, "data_ptr") else int(dframe)
         off, rng, err = C.c_uint64(0), NxgRange(), NetidxError()
         cs = cols.s if hasattr(cols, "s") else cols

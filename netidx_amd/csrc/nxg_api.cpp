@@ -43,7 +43,7 @@ constexpr int kStatusRing = 1024;  // at most kStatusRing/2 async calls in fligh
 
 }  // namespace
 
-uint32_t nxg_patience = 128;
+thread_local uint32_t nxg_patience = 128;  // the calling ctx's, set by begin_call
 thread_local DevStatus* nxg_zero_slot = nullptr;
 thread_local bool nxg_zero_used = false;
 
@@ -94,6 +94,7 @@ struct NxgCtx {
     int fmx_count_mode = 0;  // 0 adaptive, 1 full, 2 lean
     int wgs_fmx[2] = {0, 0};
     uint32_t f64r_flags = 0;  // NXG_F64R_FLAGS (tests): 1 every tile exact, 2 never hand over
+    uint32_t patience = 128;  // NXG_LOOKBACK_PATIENCE: look-back polls before self-help
     uint8_t* dframe = nullptr;
     size_t dframe_cap = 0;
     uint64_t* escratch = nullptr;
@@ -113,6 +114,9 @@ struct NxgCtx {
         uint64_t cap;  // encode: the output capacity
         DevStatus* st;
         uint32_t slot;
+        uint32_t flags = 0;            // decode: the caller's NXG_DECODE_* flags
+        const uint8_t* heap = nullptr;  // encode: the heap and the output buffer
+        uint8_t* out = nullptr;
     };
     std::vector<Pending> pending;
     // zstd (compressed archive records): predefined tables, literal buffers, descriptors
@@ -139,6 +143,7 @@ bool set_device(NxgCtx* c, NetidxError* err) {
 bool begin_call(NxgCtx* c, DevStatus** st, uint32_t* slot, NetidxError* err) {
     *slot = c->calls % kStatusRing;
     *st = c->dst + *slot;
+    nxg_patience = c->patience;
     nxg_zero_slot = c->dst + (c->calls + kStatusRing / 2) % kStatusRing;
     nxg_zero_used = false;
     c->calls++;
@@ -342,7 +347,9 @@ bool enqueue_dec_fast(NxgCtx* c, const uint8_t* f, uint64_t len, NxgColumns* out
                                    nxg_take_zero_slot(), c->stream));
         return true;
     }
-    if (c->seq_left) c->seq_left--;
+    // (a rerun right after the sequential-id decoder declined does not count: the skip lasts
+    // kSeqSkipCalls calls after the one that declined)
+    if (try_seq && c->seq_left) c->seq_left--;
     if (!c->force_x && c->irregular_left == 0) {
         *path = FAST_RUN;
         if (!ensure_tstat(c, nxg_dec_f64r_groups(len), err)) return false;
@@ -402,9 +409,12 @@ bool enqueue_dec_mixed(NxgCtx* c, const uint8_t* f, uint64_t len, NxgColumns* ou
 // finish a device decode: read status, fall back to the general kernel if the f64 kernel
 // rejected the frame, fill the user-visible status
 // `fetched`: the caller has already copied the status ring to c->hst after the stream drained.
+// `redone` (optional) is set when a fallback decoder rewrote the columns here, i.e. after every
+// call enqueued behind this one had already run.
 bool finish_decode(NxgCtx* c, const uint8_t* f, uint64_t len, NxgColumns* out, int tried_fast,
                    DevStatus* st, uint32_t slot, NxgStatus* ust, NetidxError* err,
-                   bool fetched = false) {
+                   bool fetched = false, bool* redone = nullptr) {
+    if (redone) *redone = false;
     if (!fetched) {
         HIPCHK(hipMemcpyAsync(c->hst + slot, st, sizeof(DevStatus), hipMemcpyDeviceToHost,
                               c->stream));
@@ -424,6 +434,7 @@ bool finish_decode(NxgCtx* c, const uint8_t* f, uint64_t len, NxgColumns* out, i
             if (!begin_call(c, &st2, &slot2, err)) return false;
             const bool ok = enqueue_dec_fast(c, f, len, out, st2, &tried_fast, err, false);
             if (!end_call(c, err) || !ok) return false;
+            if (redone) *redone = true;
             HIPCHK(hipMemcpyAsync(c->hst + slot2, st2, sizeof(DevStatus), hipMemcpyDeviceToHost,
                                   c->stream));
             HIPCHK(hipStreamSynchronize(c->stream));
@@ -440,6 +451,7 @@ bool finish_decode(NxgCtx* c, const uint8_t* f, uint64_t len, NxgColumns* out, i
         if (!begin_call(c, &st2, &slot2, err)) return false;
         const bool ok = enqueue_dec_x(c, f, len, out, st2, err);
         if (!end_call(c, err) || !ok) return false;
+        if (redone) *redone = true;
         HIPCHK(hipMemcpyAsync(c->hst + slot2, st2, sizeof(DevStatus), hipMemcpyDeviceToHost,
                               c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
@@ -460,6 +472,7 @@ bool finish_decode(NxgCtx* c, const uint8_t* f, uint64_t len, NxgColumns* out, i
                             ? enqueue_dec_general(c, f, len, out, st2, err)
                             : enqueue_dec_mixed(c, f, len, out, st2, &next, err);
         if (!end_call(c, err) || !ok) return false;
+        if (redone) *redone = true;
         HIPCHK(hipMemcpyAsync(c->hst + slot2, st2, sizeof(DevStatus), hipMemcpyDeviceToHost,
                               c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
@@ -616,6 +629,61 @@ bool finish_encode(NxgCtx* c, const NxgColumns* in, DevStatus* st, uint32_t slot
     return true;
 }
 
+
+// ---- memory touched by a call (nxg_ctx_sync's ordering of late fallbacks) ---------------------
+struct Span {
+    uintptr_t lo, hi;
+};
+
+Span span_of(const void* p, uint64_t bytes) {
+    const uintptr_t a = (uintptr_t)p;
+    return Span{a, p ? a + bytes : a};
+}
+
+// every column array of `c`, sized by its capacity (or its count, if larger)
+void cols_spans(const NxgColumns* c, std::vector<Span>* v) {
+    const uint64_t r = std::max(c->cap_rows, c->n_rows);
+    const uint64_t k = std::max(c->cap_children, c->n_children);
+    const uint64_t q = std::max(c->cap_ctl, c->n_ctl);
+    const std::pair<const void*, uint64_t> a[] = {
+        {c->id, r * 8},      {c->fixed, r * 8},   {c->tag, r},         {c->aux, r * 4},
+        {c->ctag, k},        {c->cfixed, k * 8},  {c->caux, k * 4},    {c->ctl_row, q * 8},
+        {c->ctl_off, q * 8}, {c->ctl_len, q * 4}, {c->ctl_variant, q}};
+    for (const auto& x : a)
+        if (x.first && x.second) v->push_back(span_of(x.first, x.second));
+}
+
+bool overlaps(const std::vector<Span>& a, const std::vector<Span>& b) {
+    for (const Span& x : a)
+        for (const Span& y : b)
+            if (x.lo < y.hi && y.lo < x.hi) return true;
+    return false;
+}
+
+// a pending decode done again from the start, synchronously (its first attempt's columns were
+// overwritten by an earlier frame's late fallback)
+bool redo_decode(NxgCtx* c, const NxgCtx::Pending& p, NxgStatus* s, NetidxError* err) {
+    DevStatus* st;
+    uint32_t slot;
+    if (!begin_call(c, &st, &slot, err)) return false;
+    int fast = FAST_NONE;
+    const bool ok = !(p.flags & NXG_DECODE_HINT_MIXED)
+                        ? enqueue_dec_fast(c, p.frame, p.len, p.cols, st, &fast, err)
+                        : enqueue_dec_mixed(c, p.frame, p.len, p.cols, st, &fast, err);
+    if (!end_call(c, err) || !ok) return false;
+    return finish_decode(c, p.frame, p.len, p.cols, fast, st, slot, s, err);
+}
+
+// a pending encode done again, synchronously (its input columns were rewritten after it ran)
+bool redo_encode(NxgCtx* c, const NxgCtx::Pending& p, const NxgColumns* in, NetidxError* err) {
+    DevStatus* st;
+    uint32_t slot;
+    if (!begin_call(c, &st, &slot, err)) return false;
+    const bool ok = enqueue_encode(c, in, p.heap, p.out, p.cap, st, err);
+    if (!end_call(c, err) || !ok) return false;
+    return finish_encode(c, in, st, slot, p.len_out, p.cap, true, err);
+}
+
 }  // namespace
 
 extern "C" {
@@ -703,9 +771,9 @@ NxgCtx* nxg_ctx_new(int device, NetidxError* err) {
     c->fmx_count_mode = fc && strcmp(fc, "full") == 0 ? 1 : (fc && strcmp(fc, "lean") == 0 ? 2 : 0);
     const char* ap = getenv("NXG_ARCH_PATH");
     c->no_fa = ap && strcmp(ap, "exact") == 0;
-    // (process-wide, set by every context created: tests make one with 0 and then a default one)
+    // (per context: a test context with patience 0 leaves every other context's alone)
     const char* lp = getenv("NXG_LOOKBACK_PATIENCE");
-    nxg_patience = lp ? (uint32_t)strtoul(lp, nullptr, 0) : 128u;
+    c->patience = lp ? (uint32_t)strtoul(lp, nullptr, 0) : 128u;
     const char* ff = getenv("NXG_F64R_FLAGS");
     c->f64r_flags = ff ? (uint32_t)strtoul(ff, nullptr, 0) : 0u;
     return c;
@@ -851,7 +919,7 @@ bool nxg_decode_updates_async(NxgCtx* c, const uint8_t* dframe, uint64_t len, Nx
                         ? enqueue_dec_fast(c, dframe, len, dout, st, &fast, err)
                         : enqueue_dec_mixed(c, dframe, len, dout, st, &fast, err);
     if (!end_call(c, err) || !ok) return false;
-    c->pending.push_back({1, fast, dframe, len, dout, nullptr, 0, st, slot});
+    c->pending.push_back({1, fast, dframe, len, dout, nullptr, 0, st, slot, flags});
     return true;
 }
 
@@ -917,6 +985,8 @@ bool nxg_decode_frames_async(NxgCtx* c, uint32_t n, const uint8_t* const* dframe
     // (the frames become pending only once their launches are enqueued: a failed launch leaves
     // no call behind whose status slot no kernel wrote)
     HIPCHK(nxg_launch_dec_f64r_stream(fr.data(), n, c->tstat, c->f64r_flags, c->stream));
+    // (these frames skipped the sequential-id decoder: they count toward its skip)
+    c->seq_left = c->seq_left > n ? c->seq_left - n : 0;
     c->pending.insert(c->pending.end(), pend.begin(), pend.end());
     return true;
 }
@@ -924,6 +994,12 @@ bool nxg_decode_frames_async(NxgCtx* c, uint32_t n, const uint8_t* const* dframe
 // Completes every in-flight call in order (every one, even after a failure, so that each decode
 // gets its fallback and each encode its length); the status returned is the last call's, or the
 // first failing call's, and the first error is the one reported.
+//
+// A decode that falls back here rewrites its columns after every later call of the backlog has
+// run. Later calls that touched the same memory are therefore done again, in order: a decode
+// whose columns (or frame) overlap what was rewritten, and an encode whose input columns do; what
+// those rewrite joins the set. (nxg_codec.h allows a backlog to reuse columns, the later frame's
+// rows being the ones left.)
 bool nxg_ctx_sync(NxgCtx* c, NxgStatus* ust, NetidxError* err) {
     if (!c) {
         set_err(err, "null ctx");
@@ -934,6 +1010,7 @@ bool nxg_ctx_sync(NxgCtx* c, NxgStatus* ust, NetidxError* err) {
     ps.swap(c->pending);
     HIPCHK(hipStreamSynchronize(c->stream));
     // the in-flight calls used consecutive ring slots: at most two copies cover them
+    std::vector<DevStatus> hs(ps.size());
     if (!ps.empty()) {
         const uint32_t s0 = ps.front().slot, s1 = ps.back().slot;
         if (s0 <= s1) {
@@ -946,15 +1023,32 @@ bool nxg_ctx_sync(NxgCtx* c, NxgStatus* ust, NetidxError* err) {
                                   hipMemcpyDeviceToHost, c->stream));
         }
         HIPCHK(hipStreamSynchronize(c->stream));
+        // (kept aside: the fallbacks below take ring slots of their own, which may wrap)
+        for (size_t i = 0; i < ps.size(); i++) hs[i] = c->hst[ps[i].slot];
     }
     if (ust) memset(ust, 0, sizeof *ust);
     bool reported = false, ok = true;
-    for (auto& p : ps) {
+    std::vector<Span> dirty;  // memory rewritten by a call completed out of order
+    for (size_t i = 0; i < ps.size(); i++) {
+        auto& p = ps[i];
+        c->hst[p.slot] = hs[i];
         NetidxError e{nullptr};
         bool r;
         if (p.kind == 1) {
+            std::vector<Span> w;
+            cols_spans(p.cols, &w);
+            const bool stale =
+                !dirty.empty() && (overlaps(dirty, w) || overlaps(dirty, {span_of(p.frame, p.len)}));
             NxgStatus s;
-            r = finish_decode(c, p.frame, p.len, p.cols, p.fast, p.st, p.slot, &s, &e, true);
+            bool redone = false;
+            if (stale) {
+                r = redo_decode(c, p, &s, &e);
+                redone = true;
+            } else {
+                r = finish_decode(c, p.frame, p.len, p.cols, p.fast, p.st, p.slot, &s, &e, true,
+                                  &redone);
+            }
+            if (redone) dirty.insert(dirty.end(), w.begin(), w.end());
             if (r) {
                 p.cols->layout =
                     (!mixed_capable(p.cols) || s.path == 1) ? NXG_LAYOUT_F64 : NXG_LAYOUT_MIXED;
@@ -964,8 +1058,16 @@ bool nxg_ctx_sync(NxgCtx* c, NxgStatus* ust, NetidxError* err) {
         } else {
             NxgColumns dummy{};
             dummy.layout = NXG_LAYOUT_F64;
-            r = finish_encode(c, p.cols ? p.cols : &dummy, p.st, p.slot, p.len_out, p.cap, true,
-                              &e, true);
+            const NxgColumns* in = p.cols ? p.cols : &dummy;
+            std::vector<Span> rd;
+            cols_spans(in, &rd);
+            if (!dirty.empty() && overlaps(dirty, rd)) {
+                // its input columns were rewritten after it ran: encode again
+                r = redo_encode(c, p, in, &e);
+                dirty.push_back(span_of(p.out, p.cap));
+            } else {
+                r = finish_encode(c, in, p.st, p.slot, p.len_out, p.cap, true, &e, true);
+            }
         }
         if (!r && ok) {
             ok = false;
@@ -1623,7 +1725,8 @@ bool nxg_encode_updates_async(NxgCtx* c, const NxgColumns* din, const uint8_t* d
     if (!begin_call(c, &st, &slot, err)) return false;
     const bool ok = enqueue_encode(c, din, dheap, dout, cap, st, err);
     if (!end_call(c, err) || !ok) return false;
-    c->pending.push_back({2, 0, nullptr, 0, const_cast<NxgColumns*>(din), len_out, cap, st, slot});
+    c->pending.push_back({2, 0, nullptr, 0, const_cast<NxgColumns*>(din), len_out, cap, st, slot,
+                          0, dheap, dout});
     return true;
 }
 
@@ -1786,7 +1889,10 @@ bool nxg_decode_range(NxgCtx* c, const uint8_t* dframe, uint64_t W, uint64_t beg
         HIPCHK(hipStreamSynchronize(c->stream));
         const DevStatus& h2 = c->hst[slot2];
         c->last = h2;
-        if (h2.fast_fail || h2.path != 4 || !h2.diag[2] || !h2.diag[3]) return true;  // ok = 0
+        if (h2.fast_fail || h2.path != 4 || !h2.diag[2] || !h2.diag[3]) {  // ok = 0
+            if (h2.capacity) rng->err_kind = NXG_CAPACITY;  // declined: the columns are short
+            return true;
+        }
         rng->entry = begin + h2.diag[2] - 1;
         rng->exit = begin + h2.diag[3] - 1;
         rng->n_rows = h2.n_rows;
@@ -1845,6 +1951,125 @@ bool nxg_range_link(const NxgRange* r, uint32_t n, uint64_t W, uint64_t* row_off
                 (unsigned long long)W);
         return false;
     }
+    return true;
+}
+
+// ---- one share of a frame's rows (nxg_decode_sharded's fallback) --------------------------------
+// The frame decoded whole (every decoder in turn, as nxg_decode_updates), into ctx-owned device
+// columns sized `shares` times the caller's (each rank's share should fit its own columns), or to
+// the frame's totals when that is short; then rows [N*share/shares, N*(share+1)/shares) with their
+// children and the control spans before them (the last share: also those after the last row)
+// into `out`, re-based (nxg_share.hip).
+bool nxg_decode_share(NxgCtx* c, const uint8_t* dframe, uint64_t W, uint32_t share,
+                      uint32_t shares, NxgColumns* out, uint64_t* row_off, NxgStatus* ust,
+                      NetidxError* err) {
+    if (!c || !out || (!dframe && W) || shares == 0 || share >= shares) {
+        set_err(err, "bad argument (share %u of %u)", share, shares);
+        return false;
+    }
+    if (!c->pending.empty()) {
+        set_err(err, "an async operation is pending on this ctx; call nxg_ctx_sync first");
+        return false;
+    }
+    if (W >= (1ull << 40)) {
+        set_err(err, "frame too large (%llu bytes)", (unsigned long long)W);
+        return false;
+    }
+    if (out->mem != NXG_MEM_DEVICE || (W && !is_device_ptr(dframe))) {
+        set_err(err, "share decode needs a device frame and device columns");
+        return false;
+    }
+    if (!set_device(c, err)) return false;
+    if (row_off) *row_off = 0;
+    // the whole-frame columns: the caller's shape, `shares` times its capacities (at most the
+    // frame's bounds, include/nxg_codec.h), grown to the frame's totals after a capacity miss
+    auto times = [&](uint64_t x, uint64_t bound) {
+        return std::max<uint64_t>(1, std::min<uint64_t>(x > bound / shares ? bound : x * shares, bound));
+    };
+    NxgColumns like = *out;
+    like.cap_rows = times(out->cap_rows, W / 4 + 1);
+    like.cap_children = times(out->cap_children, W + 1);
+    like.cap_ctl = times(out->cap_ctl, W / 2 + 1);
+    NxgColumns v{};
+    NxgStatus s{};
+    for (int attempt = 0;; attempt++) {
+        if (!ensure_dcols(c, &like, err)) return false;
+        v = staged_view(c, &like);
+        DevStatus* st;
+        uint32_t slot;
+        if (!begin_call(c, &st, &slot, err)) return false;
+        int fast = FAST_NONE;
+        const bool ok = enqueue_dec_fast(c, dframe, W, &v, st, &fast, err);
+        if (!end_call(c, err) || !ok) return false;
+        if (!finish_decode(c, dframe, W, &v, fast, st, slot, &s, err)) return false;
+        if (s.err_kind != NXG_CAPACITY || attempt == 2) break;
+        const uint64_t r = std::min<uint64_t>(std::max(s.n_rows, 2 * like.cap_rows), W / 4 + 1);
+        const uint64_t k = std::min<uint64_t>(std::max(s.n_children, 2 * like.cap_children), W + 1);
+        const uint64_t q = std::min<uint64_t>(std::max(s.n_ctl, 2 * like.cap_ctl), W / 2 + 1);
+        if (r == like.cap_rows && k == like.cap_children && q == like.cap_ctl) break;
+        like.cap_rows = r;
+        like.cap_children = k;
+        like.cap_ctl = q;
+    }
+    NxgStatus o{};
+    o.path = s.path;
+    o.err_kind = s.err_kind;
+    o.err_offset = s.err_offset;
+    if (s.err_kind) {  // the frame fails as a whole (connection.rs:228-231): no rows in any share
+        out->n_rows = out->n_children = out->n_ctl = out->n_heartbeat = 0;
+        if (ust) *ust = o;
+        return true;
+    }
+    const uint64_t N = s.n_rows;
+    const uint64_t r0 = (uint64_t)((unsigned __int128)N * share / shares);
+    const uint64_t r1 = (uint64_t)((unsigned __int128)N * (share + 1) / shares);
+    const bool last = share + 1 == shares;
+    const bool f64_rows = s.path == 1 || !mixed_capable(&v);  // tag / children not written
+    ColsDesc src = desc_of(&v);
+    src.n_rows = N;
+    src.n_children = f64_rows ? 0 : s.n_children;
+    src.n_ctl = f64_rows ? 0 : s.n_ctl;
+    if (f64_rows) src.tag = nullptr;
+    uint64_t c0 = 0, c1 = 0, k0 = 0, k1 = 0;
+    if (!ensure_escratch(c, 8, err)) return false;
+    if (!f64_rows && (src.n_children || src.n_ctl)) {
+        uint64_t b[4];
+        HIPCHK(nxg_launch_share_bounds(src, r0, r1, c->escratch, c->stream));
+        HIPCHK(hipMemcpyAsync(b, c->escratch, sizeof b, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        c0 = std::min<uint64_t>(b[0], src.n_children);
+        c1 = std::min<uint64_t>(b[1], src.n_children);
+        k0 = std::min<uint64_t>(b[2], src.n_ctl);
+        k1 = last ? src.n_ctl : std::min<uint64_t>(b[3], src.n_ctl);
+    }
+    const uint64_t nr = r1 - r0, nc = c1 - c0, nk = k1 - k0;
+    if (nr > out->cap_rows || nc > out->cap_children || nk > out->cap_ctl ||
+        ((nc || nk) && !mixed_capable(out))) {
+        o.err_kind = (nc || nk) && !mixed_capable(out) ? NXG_NOT_F64 : NXG_CAPACITY;
+        o.n_rows = nr;
+        o.n_children = nc;
+        o.n_ctl = nk;
+        out->n_rows = out->n_children = out->n_ctl = out->n_heartbeat = 0;
+        if (ust) *ust = o;
+        return true;
+    }
+    ColsDesc dst = desc_of(out);
+    if (f64_rows) dst.tag = nullptr;
+    HIPCHK(nxg_launch_share_copy(src, dst, r0, nr, c0, nc, k0, nk, c->escratch + 4, c->stream));
+    uint64_t hb = 0;
+    HIPCHK(hipMemcpyAsync(&hb, c->escratch + 4, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    out->n_rows = nr;
+    out->n_children = nc;
+    out->n_ctl = nk;
+    out->n_heartbeat = hb;
+    out->layout = f64_rows ? NXG_LAYOUT_F64 : NXG_LAYOUT_MIXED;
+    o.n_rows = nr;
+    o.n_children = nc;
+    o.n_ctl = nk;
+    o.n_heartbeat = hb;
+    if (row_off) *row_off = r0;
+    if (ust) *ust = o;
     return true;
 }
 

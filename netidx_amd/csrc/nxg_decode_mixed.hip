@@ -725,8 +725,10 @@ __global__ __launch_bounds__(TPB) void nxg_fmx_resolve_kernel(
     }
     if (threadIdx.x == 0) {
         const uint64_t nr = run & 0xffffffffull, nc = run >> 32;
-        // columns too small: the general decoder reports the capacity error
+        // columns too small: the general decoder reports the capacity error (a range decode
+        // reports it itself: capacity set)
         if (nr > cap_rows || nc > cap_children || runh > cap_ctl || (runh && !ctl_ok)) {
+            if (nr > cap_rows || nc > cap_children || runh > cap_ctl) st->capacity = 1u;
             atomicOr(&st->fast_fail, 1u);
         } else {
             st->n_rows = nr;

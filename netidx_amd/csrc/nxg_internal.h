@@ -81,7 +81,7 @@ constexpr int MAXB = TILE * 15 + 32;   // staging bytes (f64 records <= 15 B for
 // Polls of an unpublished look-back predecessor before its aggregate is computed by the waiting
 // workgroup itself (self-help look-backs); NXG_LOOKBACK_PATIENCE at context creation (tests: 0,
 // every unpublished predecessor computed).
-extern uint32_t nxg_patience;
+extern thread_local uint32_t nxg_patience;
 
 // launchers (each defined next to its kernel)
 struct ColsDesc;
@@ -245,6 +245,15 @@ int nxg_zstd_grid(int ncu);
 hipError_t nxg_launch_zstd(const uint8_t* dsrc, const void* drecs, uint32_t n, const void* ddict,
                            const void* ddefs, uint8_t* dout, uint8_t* dlit, void* dres, int grid,
                            hipStream_t s);
+// one share of a decoded frame's rows (nxg_share.hip): bounds (4 u64 in device memory: the first
+// child slot of a container row >= r0 / >= r1, the first control span with ctl_row >= r0 / >= r1;
+// ~0 for none), then the copy of rows [r0, r0 + nr), children [c0, c0 + nc) and control spans
+// [k0, k0 + nk), re-based, with the Heartbeats among those spans counted into *hb (device u64)
+hipError_t nxg_launch_share_bounds(const ColsDesc& src, uint64_t r0, uint64_t r1, uint64_t* b,
+                                   hipStream_t s);
+hipError_t nxg_launch_share_copy(const ColsDesc& src, const ColsDesc& dst, uint64_t r0,
+                                 uint64_t nr, uint64_t c0, uint64_t nc, uint64_t k0, uint64_t nk,
+                                 uint64_t* hb, hipStream_t s);
 int nxg_occupancy_enc_f64();
 int nxg_occupancy_enc_general();
 

@@ -202,6 +202,25 @@ bool local_decode_range(NxgComm* comm, const uint8_t* f, uint64_t W, uint64_t b,
     return nxg_decode_range(comm->ctx, f, W, b, e, out, rng, err);
 }
 
+bool local_decode_share(NxgComm* comm, const uint8_t* f, uint64_t W, NxgColumns* out,
+                        uint64_t* row_off, NxgStatus* st, NetidxError* err) {
+    if (has_codec_hooks(comm)) {
+        if (!comm->ops.decode_share) {
+            set_err(err, "rank %d: a byte range was declined and the ops carry no decode_share",
+                    comm->rank);
+            return false;
+        }
+        if (!comm->ops.decode_share(comm->ops.user, f, W, (uint32_t)comm->rank,
+                                    (uint32_t)comm->nranks, out, row_off, st)) {
+            set_err(err, "rank %d: decode_share failed", comm->rank);
+            return false;
+        }
+        return true;
+    }
+    return nxg_decode_share(comm->ctx, f, W, (uint32_t)comm->rank, (uint32_t)comm->nranks, out,
+                            row_off, st, err);
+}
+
 // After a gather: the first rank whose status word is set, or -1.
 int first_failed(const NxgComm* comm, const std::vector<uint64_t>& all) {
     for (int i = 0; i < comm->nranks; i++)
@@ -356,6 +375,35 @@ bool nxg_encode_allgather(NxgCtx* ctx, NxgComm* comm, const NxgColumns* din, con
     return true;
 }
 
+// nxg_decode_sharded's fallback: rank r keeps row share r of the whole frame's decode; the ranks
+// agree on any local failure in one more exchange. Every rank decodes the same frame with the
+// same decoders, so the frame's error (if any) is the same on every rank.
+static bool share_fallback(NxgComm* comm, const uint8_t* dframe, uint64_t W, uint64_t b,
+                           uint64_t e, NxgColumns* dout, uint64_t* row_off, NxgRange* rng,
+                           NetidxError* err) {
+    NxgStatus s{};
+    uint64_t off = 0;
+    uint64_t slot[kSlotWords] = {0};
+    if (!local_decode_share(comm, dframe, W, dout, &off, &s, err)) slot[kStatusWord] = 1;
+    std::vector<uint64_t> buf((size_t)comm->nranks * kSlotWords);
+    if (!gather_slots(comm, slot, buf.data(), err)) return false;
+    const int who = first_failed(comm, buf);
+    if (who >= 0) return fail_together(comm, who, "to decode its row share", err);
+    if (row_off) *row_off = off;
+    if (rng) {
+        NxgRange m{};
+        m.begin = b;
+        m.end = e;
+        m.entry = m.exit = ~0ull;
+        m.n_rows = s.n_rows;
+        m.ok = 2;
+        m.err_kind = (uint32_t)s.err_kind;
+        m.err_offset = s.err_offset;
+        *rng = m;
+    }
+    return true;
+}
+
 bool nxg_decode_sharded(NxgCtx* ctx, NxgComm* comm, const uint8_t* dframe, uint64_t frame_len,
                         NxgColumns* dout, uint64_t* row_off, NxgRange* rng, NetidxError* err) {
     if (!comm_ready(ctx, comm, err)) return false;
@@ -384,13 +432,19 @@ bool nxg_decode_sharded(NxgCtx* ctx, NxgComm* comm, const uint8_t* dframe, uint6
         const int who = first_failed(comm, buf);
         if (who >= 0) return fail_together(comm, who, "to decode its byte range", err);
         for (int i = 0; i < n; i++) memcpy(&all[i], &buf[(size_t)i * kSlotWords], sizeof(NxgRange));
-        for (int i = 0; i < n; i++)
-            if (!all[i].ok) {
-                set_err(err, "range %d is not one the range decoders take (f64 frames; mixed "
-                             "frames of short Updates into mixed columns): decode the whole "
-                             "frame with nxg_decode_updates", i);
+        int declined = -1;
+        for (int i = 0; i < n; i++) {
+            if (all[i].ok) continue;
+            if (all[i].err_kind == NXG_CAPACITY) {
+                set_err(err, "range %d: the columns of rank %d are too small for its rows", i, i);
                 return false;
             }
+            if (declined < 0) declined = i;
+        }
+        // content the byte-range decoders do not take: every rank saw it in this exchange, so
+        // every rank takes the row-share fallback (the frame decoded whole, rows in shares)
+        if (declined >= 0) return share_fallback(comm, dframe, frame_len, b, e, dout, row_off, rng,
+                                                 err);
         uint32_t bad = 0;
         NetidxError e2{nullptr};
         const bool linked = nxg_range_link(all.data(), (uint32_t)n, frame_len, offs.data(), &bad,

@@ -223,6 +223,7 @@ struct NxgResolver {
         Addr4 addr;
         uint32_t priority;
         uint64_t last_seen;  // seconds: the last message on its write connection (writer TTL)
+        int fd;              // its write connection
     };
     std::vector<Pub> pubs;                                  // by connection, PublisherId order
     std::map<std::string, std::pair<uint64_t, uint32_t>> published;  // path -> (id, flags)
@@ -238,14 +239,24 @@ struct NxgResolver {
         for (auto it = pubs.begin(); it != pubs.end();)
             it = it->id == id ? pubs.erase(it) : std::next(it);
     }
-    // (under mu) publishers silent for longer than the writer TTL are expired (the reference's
-    // resolver drops a writer's data when its TTL runs out without heartbeats)
+    // (under mu) publishers silent for longer than the writer TTL are expired: their data is
+    // dropped and their write connection shut down, as the reference's resolver times out a
+    // silent writer's connection (resolver_server/mod.rs:289-299) -- the publisher reconnects
+    // and is told ttl_expired; its serving thread sees the socket end and leaves
     void expire(uint64_t now) {
         if (!ttl) return;
-        std::vector<uint64_t> dead;
+        std::vector<std::pair<uint64_t, int>> dead;
         for (const Pub& p : pubs)
-            if (now > p.last_seen + ttl) dead.push_back(p.id);
-        for (uint64_t id : dead) drop_publisher(id);
+            if (now > p.last_seen + ttl) dead.push_back({p.id, p.fd});
+        for (const auto& d : dead) {
+            drop_publisher(d.first);
+            shutdown(d.second, SHUT_RDWR);
+        }
+    }
+    bool live(uint64_t id) const {
+        for (const Pub& p : pubs)
+            if (p.id == id) return true;
+        return false;
     }
     void touch(uint64_t id, uint64_t now) {
         for (Pub& p : pubs)
@@ -350,7 +361,7 @@ void NxgResolver::serve_write(int fd, const Addr4& write_addr, uint32_t priority
     {
         std::lock_guard<std::mutex> g(mu);
         id = next_id++;
-        pubs.push_back(Pub{id, write_addr, priority, (uint64_t)time(nullptr)});
+        pubs.push_back(Pub{id, write_addr, priority, (uint64_t)time(nullptr), fd});
     }
     // a write connection that ends (peer gone, or dropped on a PackError) takes its paths with it
     struct Drop {
@@ -376,6 +387,7 @@ void NxgResolver::serve_write(int fd, const Addr4& write_addr, uint32_t priority
         size_t n_msgs = 0, n_heartbeat = 0;
         {
             std::lock_guard<std::mutex> g(mu);
+            if (!live(id)) return;  // expired while this batch was on its way
             touch(id, (uint64_t)time(nullptr));
         }
         while (in.left()) {
@@ -391,6 +403,7 @@ void NxgResolver::serve_write(int fd, const Addr4& write_addr, uint32_t priority
                 if ((variant == 5 || variant == 6) && !in.be(flags, 4)) return;
                 {
                     std::lock_guard<std::mutex> g(mu);
+                    if (!live(id)) return;  // expired: no path under an id resolve cannot map
                     published[path] = {id, (uint32_t)flags};
                 }
                 reply.bytes(unit(0).data(), 2);  // FromWrite::Published

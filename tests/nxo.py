@@ -280,3 +280,41 @@ def publish_unsubscribes(ids, clients, n_clients):
     if r < 0:
         raise ValueError(-r)
     return off, ent[:r]
+
+
+CONTAINER_TAGS = (19, 21, 22)  # Array, Map, Error(Value): `fixed` is the first child slot
+
+
+def share(o, k, shares):
+    """Row share k of `shares` of a trimmed decode `o` (the contract of nxg_decode_share,
+    include/nxg_codec.h), restated on numpy: rows [N*k/shares, N*(k+1)/shares), the child slots
+    of their subtrees (children are allocated depth-first in row order), the control spans with
+    ctl_row in the share (the last share: also those after the last row); child indices and
+    ctl_row re-based. Returns (first row, dict of columns + n_heartbeat)."""
+    N = len(o["id"])
+    r0, r1 = N * k // shares, N * (k + 1) // shares
+    tag, fixed = o["tag"], o["fixed"]
+    cont = np.isin(tag, CONTAINER_TAGS)
+    nch = len(o["ctag"])
+
+    def first_child(r):
+        idx = np.flatnonzero(cont[r:])
+        return int(fixed[r + idx[0]]) if len(idx) else nch
+
+    c0, c1 = first_child(r0), first_child(r1)
+    ctl_row = o["ctl_row"]
+    k0 = int(np.searchsorted(ctl_row, r0, "left"))
+    k1 = len(ctl_row) if k == shares - 1 else int(np.searchsorted(ctl_row, r1, "left"))
+    ct = o["ctag"][c0:c1]
+    out = {
+        "id": o["id"][r0:r1], "tag": tag[r0:r1],
+        "fixed": np.where(cont[r0:r1], fixed[r0:r1] - np.uint64(c0), fixed[r0:r1]),
+        "aux": o["aux"][r0:r1], "ctag": ct,
+        "cfixed": np.where(np.isin(ct, CONTAINER_TAGS), o["cfixed"][c0:c1] - np.uint64(c0),
+                           o["cfixed"][c0:c1]),
+        "caux": o["caux"][c0:c1], "ctl_row": ctl_row[k0:k1] - np.uint64(r0),
+        "ctl_off": o["ctl_off"][k0:k1], "ctl_len": o["ctl_len"][k0:k1],
+        "ctl_variant": o["ctl_variant"][k0:k1],
+    }
+    out["n_heartbeat"] = int((out["ctl_variant"] == 5).sum())
+    return r0, out

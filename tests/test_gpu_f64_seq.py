@@ -260,3 +260,62 @@ def test_seq_async_and_frames_async(codec):
     codec.sync()
     for j in range(3):
         assert np.array_equal(outs[j].numpy()["id"], refs[j][0])
+
+
+def test_async_backlog_keeps_wire_order_after_a_late_fallback():
+    """a frame the sequential-id kernel declines is decoded again at sync,
+    after the frames behind it. A later frame into the same columns must still be the one left
+    in them, and an async encode that read those columns must see the frame decoded before it.
+    A fresh context, so the sequential-id kernel is tried first on every frame."""
+    import torch
+    import netidx_amd
+    import nxo
+    from netidx_amd import synth
+    from netidx_amd.codec import Columns
+    n = 150_000
+    codec = netidx_amd.Codec(0)
+    try:
+        ids_a, vals_a = synth.f64_columns(n, 31)
+        perm = np.random.default_rng(5).permutation(n)
+        ids_a = ids_a[perm]
+        wire_a = nxo.encode_f64(ids_a, vals_a)  # ids in random order: declined, rerun at sync
+        ids_b, vals_b, wire_b = _seq_wire(n, 500, 32)
+        fa = torch.from_numpy(np.ascontiguousarray(wire_a)).cuda()
+        fb = torch.from_numpy(np.ascontiguousarray(wire_b)).cuda()
+        cols = Columns(n, 0, 0, netidx_amd.LAYOUT_F64, "cuda")
+        codec.decode_frames_async([fa.data_ptr(), fb.data_ptr()], [fa.numel(), fb.numel()],
+                                  [cols, cols])
+        st = codec.sync()
+        assert st.err_kind == 0
+        g = cols.numpy()
+        assert np.array_equal(g["id"], ids_b) and np.array_equal(g["fixed"], vals_b)
+        # the same through single async calls, then an async encode of the declined frame's
+        # columns: the encode must read the rerun's rows, not the declined attempt's (a fresh
+        # context: this one now skips the sequential-id kernel for a while)
+        codec.close()
+        codec = netidx_amd.Codec(0)
+        other = Columns(n, 0, 0, netidx_amd.LAYOUT_F64, "cuda")
+        out = torch.zeros(len(wire_a) + 64, dtype=torch.uint8, device="cuda")
+        codec.decode_async(fa.data_ptr(), fa.numel(), other)
+        n_len = codec.encode_async(other, None, out.data_ptr(), out.numel())
+        codec.decode_async(fb.data_ptr(), fb.numel(), cols)
+        codec.sync()
+        assert n_len.value == len(wire_a)
+        assert np.array_equal(out[:len(wire_a)].cpu().numpy(), wire_a)
+        g = other.numpy()
+        assert np.array_equal(g["id"], ids_a) and np.array_equal(g["fixed"], vals_a)
+        # a mixed frame (declined by the f64 decoders) before a sequential one, same columns
+        codec.close()
+        codec = netidx_amd.Codec(0)
+        m = synth.mixed_columns(20_000, 9)
+        mc = netidx_amd.columns_from_arrays(m.id, m.fixed, m.tag, m.aux, m.ctag, m.cfixed,
+                                            m.caux)
+        mw = codec.encode_batch(mc, torch.from_numpy(m.heap.copy()).cuda())
+        mixed = Columns.for_frame(max(mw.numel(), len(wire_b)), netidx_amd.LAYOUT_MIXED, "cuda")
+        codec.decode_frames_async([mw.data_ptr(), fb.data_ptr()], [mw.numel(), fb.numel()],
+                                  [mixed, mixed])
+        codec.sync()
+        g = mixed.numpy()
+        assert np.array_equal(g["id"], ids_b) and np.array_equal(g["fixed"], vals_b)
+    finally:
+        codec.close()

@@ -210,3 +210,119 @@ def test_rccl_one_rank_comm(codec):
         assert np.array_equal(g["id"], ids) and np.array_equal(g["fixed"], vals)
     finally:
         comm.close()
+
+
+# ---- row shares (nxg_decode_share): nxg_decode_sharded's fallback ------------------------------
+
+def _share_cols(codec, wire, shares, cols_of):
+    """Every row share of one device frame, each into its own columns."""
+    import torch
+    dw = torch.from_numpy(np.ascontiguousarray(wire)).cuda()
+    out = []
+    for k in range(shares):
+        cols = cols_of(k)
+        off, st = codec.decode_share(dw, len(wire), k, shares, cols)
+        out.append((off, st, cols.numpy() if st.err_kind == 0 else None))
+    return out
+
+
+def _check_shares(got, o, shares):
+    import nxo
+    rows = 0
+    for k, (off, st, g) in enumerate(got):
+        r0, want = nxo.share(o, k, shares)
+        assert st.err_kind == 0 and off == r0 == rows
+        assert st.n_rows == len(want["id"]) and st.n_heartbeat == want["n_heartbeat"]
+        for f in ("id", "tag", "fixed", "aux", "ctag", "cfixed", "caux", "ctl_row", "ctl_off",
+                  "ctl_len", "ctl_variant"):
+            assert np.array_equal(g[f], want[f]), (k, f)
+        assert g["n_heartbeat"] == want["n_heartbeat"]
+        rows += st.n_rows
+    assert rows == len(o["id"])
+
+
+@pytest.mark.parametrize("shares", [1, 2, 3, 8, 37])
+def test_decode_share_rich_frame(codec, shares):
+    """Maps, nested arrays, Error(Value), Heartbeats, Unsubscribed, wide ids: the frame decoded
+    whole (the general decoder) and cut into row shares, children and control spans re-based,
+    against the oracle's decode cut by the restated contract (nxo.share)."""
+    import netidx_amd
+    import nxo
+    from frames import rich_wire
+    from netidx_amd.codec import Columns
+    wire = rich_wire(20_000, 51)
+    o = nxo.decode(wire).trim()
+    assert o["err_kind"] == 0
+    got = _share_cols(codec, wire, shares,
+                      lambda k: Columns.for_frame(len(wire), netidx_amd.LAYOUT_MIXED, "cuda"))
+    _check_shares(got, o, shares)
+
+
+@pytest.mark.parametrize("shares", [3, 8])
+def test_decode_share_f64_and_config3_frames(codec, shares):
+    """The fast decoders' frames through the same call: an f64 frame (rows only, F64 layout)
+    and a config-3 frame with Heartbeats and long strings."""
+    import netidx_amd
+    import nxo
+    from netidx_amd import synth
+    from netidx_amd.codec import Columns
+    ids, vals = synth.f64_columns(300_001, 77)
+    wire = nxo.encode_f64(ids, vals)
+    got = _share_cols(codec, wire, shares,
+                      lambda k: Columns(300_001 // shares + 2, 0, 0, netidx_amd.LAYOUT_F64, "cuda"))
+    rows = 0
+    for k, (off, st, g) in enumerate(got):
+        assert st.err_kind == 0 and st.path == 1 and off == rows
+        assert np.array_equal(g["id"], ids[off:off + st.n_rows])
+        assert np.array_equal(g["fixed"], vals[off:off + st.n_rows])
+        rows += st.n_rows
+    assert rows == len(ids)
+    wire = _mixed_wire(100_000, 5, ctl=True)
+    o = nxo.decode(wire).trim()
+    got = _share_cols(codec, wire, shares,
+                      lambda k: Columns.for_frame(len(wire) // shares + 65536,
+                                                  netidx_amd.LAYOUT_MIXED, "cuda"))
+    _check_shares(got, o, shares)
+
+
+def test_decode_share_errors_and_capacity(codec):
+    """A frame error leaves no rows in any share (the oracle's kind and offset); a share larger
+    than its columns reports NXG_CAPACITY; mixed content into f64 columns NXG_NOT_F64."""
+    import netidx_amd
+    import nxo
+    import torch
+    from frames import rich_wire
+    from netidx_amd.codec import Columns
+    wire = rich_wire(5000, 52, corrupt_at=3100)
+    o = nxo.decode(wire).trim()
+    assert o["err_kind"] == 1
+    for k in range(3):
+        cols = Columns.for_frame(len(wire), netidx_amd.LAYOUT_MIXED, "cuda")
+        dw = torch.from_numpy(wire).cuda()
+        off, st = codec.decode_share(dw, len(wire), k, 3, cols)
+        assert (st.err_kind, st.err_offset, st.n_rows, off) == (o["err_kind"], o["err_offset"], 0, 0)
+    wire = rich_wire(5000, 53)
+    dw = torch.from_numpy(wire).cuda()
+    small = Columns(100, 10_000, 10_000, netidx_amd.LAYOUT_MIXED, "cuda")
+    off, st = codec.decode_share(dw, len(wire), 1, 4, small)
+    assert st.err_kind == 7 and st.n_rows > 100  # NXG_CAPACITY, with the share's size
+    f64 = Columns(5000, 0, 0, netidx_amd.LAYOUT_F64, "cuda")
+    off, st = codec.decode_share(dw, len(wire), 0, 2, f64)
+    assert st.err_kind == 8  # NXG_NOT_F64
+
+
+def test_decode_range_mixed_capacity_is_reported(codec):
+    """A mixed range declined because its columns are too small says so (err_kind NXG_CAPACITY),
+    so nxg_decode_sharded reports the capacity, not an unsupported range."""
+    import netidx_amd
+    import torch
+    from netidx_amd.codec import Columns
+    wire = _mixed_wire(50_000, 6)
+    dw = torch.from_numpy(np.ascontiguousarray(wire)).cuda()
+    W = len(wire)
+    small = Columns(1000, 100_000, 1000, netidx_amd.LAYOUT_MIXED, "cuda")
+    rng = codec.decode_range(dw, W, 0, W // 2, small)
+    assert rng.ok == 0 and rng.err_kind == 7
+    big = Columns.for_frame(W, netidx_amd.LAYOUT_MIXED, "cuda")
+    rng = codec.decode_range(dw, W, 0, W // 2, big)
+    assert rng.ok == 1 and rng.err_kind == 0

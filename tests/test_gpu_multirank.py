@@ -170,3 +170,144 @@ def test_library_protocols_mixed_frame(tmp_path, world):
     assert int(res[0][4]) == 0 and int(res[-1][5]) == int(res[0][0])
     for a, b in zip(res, res[1:]):
         assert int(a[5]) == int(b[4])
+
+
+def _rank_rich(rank, world, port, outdir):
+    """A frame the byte-range decoders decline (Maps, nested arrays, Error(Value), Unsubscribed,
+    ids past 35 bits): nxg_decode_sharded falls back to row shares on every rank at once."""
+    import torch
+    import torch.distributed as dist
+    import netidx_amd
+    import nxo
+    from frames import rich_wire
+    from netidx_amd import shard
+    from netidx_amd.codec import Columns
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        codec = netidx_amd.Codec(0)
+        wire = rich_wire(30_000, 61)
+        W = len(wire)
+        dw = torch.from_numpy(wire).cuda()
+        out = Columns.for_frame(W // world + 65536, netidx_amd.LAYOUT_MIXED, "cuda")
+        comm = shard.gloo_comm(codec, world, rank, [dw])
+        row_off, rng = comm.decode_sharded(dw, W, out)
+        o = nxo.decode(wire).trim()
+        r0, want = nxo.share(o, rank, world)
+        g = out.numpy()
+        ok = rng.ok == 2 and row_off == r0 and rng.n_rows == len(want["id"]) and all(
+            np.array_equal(g[f], want[f]) for f in ("id", "tag", "fixed", "aux", "ctag",
+                                                    "cfixed", "caux", "ctl_row", "ctl_off",
+                                                    "ctl_len", "ctl_variant"))
+        np.save(os.path.join(outdir, f"s{rank}.npy"),
+                np.array([int(ok), row_off, rng.n_rows, len(o["id"])], dtype=np.int64))
+        comm.close()
+        codec.close()
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_library_sharded_decode_falls_back_to_row_shares(tmp_path, world):
+    import torch.multiprocessing as mp
+    mp.spawn(_rank_rich, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    res = [np.load(tmp_path / f"s{r}.npy") for r in range(world)]
+    rows = 0
+    for r, x in enumerate(res):
+        assert int(x[0]) == 1, f"rank {r}: its row share differs from the oracle's"
+        assert int(x[1]) == rows
+        rows += int(x[2])
+    assert rows == int(res[0][3])
+
+
+def _rank_config5(rank, world, port, total, want_path, outdir):
+    """BASELINE configs[4] at its own size and width: 10^8 f64 records (seed 0x5EED0005) over 8
+    ranks sharing device 0. Each rank's 1.25*10^7-record shard is encoded on the GPU straight
+    into its place in the 1.498 GB frame (nxg_encode_allgather), the frame checked byte for byte
+    against the oracle's encoder, then decoded in 8 byte ranges (nxg_decode_sharded) and every
+    rank's rows checked against the batch at its global offset."""
+    import torch
+    import torch.distributed as dist
+    import netidx_amd
+    from netidx_amd import shard, synth
+    from netidx_amd.codec import Columns
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        codec = netidx_amd.Codec(0)
+
+        def say(msg):  # progress (a quiet minute reads as a hang on the GPU box)
+            if rank == 0:
+                print(f"config5: {msg}", flush=True)
+
+        b, e = shard.shard_range(total, world, rank)
+        ids, vals = synth.f64_columns(e - b, synth.SEED_8GPU, id_offset=b)
+        cols = netidx_amd.columns_from_arrays(ids, vals)
+        del ids, vals
+        want = np.load(want_path, mmap_mode="r")
+        say("shards built")
+        cap = len(want) + 64
+        dout = torch.zeros(cap, dtype=torch.uint8, device="cuda")
+        comm = shard.gloo_comm(codec, world, rank, [dout])
+        W, offs = comm.encode_allgather(cols, None, dout.data_ptr(), cap)
+        say(f"encoded and gathered: {W} bytes")
+        del cols
+        host = dout[:W].cpu().numpy()
+        frame_ok = W == len(want) and np.array_equal(host, want)
+        del host
+        say(f"frame checked: {frame_ok}")
+        out = Columns((W // world) // 12 + 1024, 0, 0, netidx_amd.LAYOUT_F64, "cuda")
+        row_off, rng = comm.decode_sharded(dout, W, out)
+        say(f"decoded: rows {row_off}..{row_off + int(rng.n_rows)}")
+        n = int(rng.n_rows)
+        ids, vals = synth.f64_columns(n, synth.SEED_8GPU, id_offset=row_off)
+        rows_ok = rng.ok == 1 and \
+            np.array_equal(out.id[:n].cpu().numpy().view(np.uint64), ids) and \
+            np.array_equal(out.fixed[:n].cpu().numpy().view(np.uint64), vals)
+        np.save(os.path.join(outdir, f"c{rank}.npy"),
+                np.array([W, int(frame_ok), row_off, n, int(rows_ok), rng.begin, rng.end,
+                          rng.entry, rng.exit] + list(offs), dtype=np.int64))
+        comm.close()
+        codec.close()
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(900)
+def test_config5_full_size_eight_ranks(tmp_path):
+    """configs[4] as BASELINE.json names it: 10^8 records, 8 ranks (processes sharing the one
+    GPU of this pool; gloo behind NxgCommOps, since RCCL refuses two ranks on one device)."""
+    import torch.multiprocessing as mp
+    import nxo
+    from netidx_amd import shard, synth
+    total, world = 100_000_000, 8
+    ids, vals = synth.f64_columns(total, synth.SEED_8GPU)
+    want = nxo.encode_f64(ids, vals)
+    del ids, vals
+    assert len(want) == 1_497_886_336
+    want_path = str(tmp_path / "want.npy")
+    np.save(want_path, want)
+    del want
+    mp.spawn(_rank_config5, args=(world, _free_port(), total, want_path, str(tmp_path)),
+             nprocs=world, join=True)
+    res = [np.load(tmp_path / f"c{r}.npy") for r in range(world)]
+    W = int(res[0][0])
+    rows = 0
+    for r, x in enumerate(res):
+        assert int(x[0]) == W == 1_497_886_336 and int(x[1]) == 1, \
+            f"rank {r}: the gathered frame differs from the oracle's"
+        assert int(x[4]) == 1, f"rank {r}: its rows differ from the batch"
+        assert int(x[2]) == rows
+        rows += int(x[3])
+        assert (int(x[5]), int(x[6])) == shard.shard_range(W, world, r)
+        assert list(x[9:]) == list(res[0][9:])
+    assert rows == total
+    assert int(res[0][7]) == 0 and int(res[-1][8]) == W
+    for a, b in zip(res, res[1:]):
+        assert int(a[8]) == int(b[7])

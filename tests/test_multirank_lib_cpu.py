@@ -22,6 +22,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 import nxo
+from frames import rich_wire
 from netidx_amd import shard, synth
 
 pytestmark = pytest.mark.timeout(240)
@@ -197,6 +198,98 @@ def test_library_decode_sharded_links_and_redecodes(tmp_path, world, total, liar
 @pytest.mark.parametrize("world,fail_rank,liar", [(2, 0, -1), (3, 2, -1), (3, 1, -1)])
 def test_library_decode_sharded_fails_on_every_rank(tmp_path, world, fail_rank, liar):
     mp.spawn(_rank_decode, args=(world, _free_port(), 9000, 92, liar, fail_rank, str(tmp_path)),
+             nprocs=world, join=True)
+    for r in range(world):
+        msg = (tmp_path / f"err{r}.txt").read_text()
+        assert not (tmp_path / f"dec{r}.npy").exists()
+        if r != fail_rank:
+            assert f"rank {fail_rank} failed" in msg
+
+
+def _rank_share(rank, world, port, seed, decline_rank, fail_rank, corrupt_at, outdir):
+    import netidx_amd
+    from netidx_amd.codec import NxgColumns
+    _init(rank, world, port)
+    try:
+        wire = rich_wire(3000, seed, corrupt_at)
+        W = len(wire)
+
+        def decode_range(frame_ptr, flen, b, e, cols):
+            # the byte-range decoders decline on rank `decline_rank` (-1: every rank)
+            ok = 0 if decline_rank in (-1, rank) else 1
+            return (b, e, b, e, 0, ok, 0)
+
+        def decode_share(frame_ptr, flen, k, shares, cols):
+            """nxg_decode_share's contract from the oracle: the frame whole, then row share k."""
+            assert flen == W and frame_ptr == wire.ctypes.data and shares == world
+            if rank == fail_rank:
+                raise RuntimeError("this rank's share decode failed")
+            o = nxo.decode(wire).trim()
+            if o["err_kind"]:
+                return 0, 0, o["err_kind"], o["err_offset"]
+            r0, part = nxo.share(o, k, shares)
+            np.savez(os.path.join(outdir, f"share{rank}.npz"), **part)
+            return r0, len(part["id"]), 0, 0
+
+        comm = netidx_amd.Comm.with_ops(None, world, rank, gloo_allgather(world), gloo_allgatherv,
+                                        lambda c: 0, lambda c, p, n: 0, decode_range,
+                                        decode_share)
+        try:
+            off, rng = comm.decode_sharded(wire.ctypes.data, W, NxgColumns())
+            np.save(os.path.join(outdir, f"dec{rank}.npy"),
+                    np.array([off] + list(rng.tuple()), dtype=np.uint64))
+        except netidx_amd.CodecError as ex:
+            with open(os.path.join(outdir, f"err{rank}.txt"), "w") as f:
+                f.write(str(ex))
+        comm.close()
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,decline_rank", [(2, -1), (3, 1), (3, 0)])
+def test_library_decode_sharded_falls_back_to_row_shares(tmp_path, world, decline_rank):
+    """A range the byte-range decoders decline (ok = 0) on any rank: every rank takes its row
+    share of the whole frame's decode (rng.ok = 2), and the shares put back together are the
+    whole frame's decode."""
+    mp.spawn(_rank_share, args=(world, _free_port(), 41, decline_rank, -1, None, str(tmp_path)),
+             nprocs=world, join=True)
+    whole = nxo.decode(rich_wire(3000, 41)).trim()
+    assert whole["err_kind"] == 0 and len(whole["ctag"]) > 0 and len(whole["ctl_row"]) > 0
+    rows = 0
+    for r in range(world):
+        assert not (tmp_path / f"err{r}.txt").exists()
+        d = np.load(tmp_path / f"dec{r}.npy").astype(np.int64)
+        off, ok, n_rows = int(d[0]), int(d[6]), int(d[5])
+        assert ok == 2 and off == rows
+        got = np.load(tmp_path / f"share{r}.npz")
+        r0, want = nxo.share(whole, r, world)
+        assert r0 == off and n_rows == len(want["id"])
+        for k in want:
+            if k != "n_heartbeat":
+                assert np.array_equal(got[k], want[k]), k
+        rows += n_rows
+    assert rows == len(whole["id"])
+
+
+def test_library_decode_sharded_share_reports_the_frame_error(tmp_path):
+    """The frame fails as a whole: every rank reports the oracle's (kind, offset), no rows."""
+    world = 3
+    mp.spawn(_rank_share, args=(world, _free_port(), 42, -1, -1, 1500, str(tmp_path)),
+             nprocs=world, join=True)
+    whole = nxo.decode(rich_wire(3000, 42, 1500)).trim()
+    assert whole["err_kind"] == 1  # UnknownTag
+    for r in range(world):
+        assert not (tmp_path / f"err{r}.txt").exists()
+        d = np.load(tmp_path / f"dec{r}.npy").astype(np.int64)
+        assert int(d[6]) == 2 and int(d[5]) == 0
+        assert (int(d[7]), int(d[8])) == (whole["err_kind"], whole["err_offset"])
+
+
+@pytest.mark.parametrize("fail_rank", [0, 2])
+def test_library_decode_sharded_share_failure_on_every_rank(tmp_path, fail_rank):
+    world = 3
+    mp.spawn(_rank_share, args=(world, _free_port(), 43, 1, fail_rank, None, str(tmp_path)),
              nprocs=world, join=True)
     for r in range(world):
         msg = (tmp_path / f"err{r}.txt").read_text()

@@ -9,6 +9,8 @@ shard_store.rs:160-193 and 600-640.
 import socket
 import struct
 
+import pytest
+
 import netidx_amd
 
 VERSION = bytes.fromhex("00000008" "0000000000000003")
@@ -178,7 +180,18 @@ def test_writer_ttl_expires_a_silent_publisher():
         assert rc.resolve("/quiet").n_publishers == 1
         time.sleep(2.2)
         assert rc.resolve("/quiet").n_publishers == 0
-        rc.close()
+        # the expired publisher's write connection is shut down (resolver_server/mod.rs:289-299):
+        # publishing on it again fails, so no path is stored under an id resolve cannot map
+        with pytest.raises(netidx_amd.CodecError):
+            w.publish("/again")
+        assert rc.resolve("/again").n_publishers == 0
         w.close()
+        # it reconnects and publishes again: resolve names a publisher it can describe
+        w2 = netidx_amd.ResolverClient.write("127.0.0.1", res.port, ("127.0.0.1", 7201))
+        w2.publish("/quiet")
+        r = rc.resolve("/quiet")
+        assert r.n_publishers == 1 and r.addr == ("127.0.0.1", 7201)
+        rc.close()
+        w2.close()
     finally:
         res.stop()
