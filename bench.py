@@ -25,7 +25,8 @@ Also reported on the same JSON line:
                  host-memory (PCIe-inclusive) decode path, f64 encode (config 4), subscriber
                  dispatch and publisher commit, the oracle on 16 host threads; with N>1, the
                  config-5 sharded encode + RCCL all-gather, the 10^8 batch decoded sharded by
-                 record, and mixed decode at 10^7 records per GPU.
+                 record, mixed decode at 10^7 records per GPU (weak) and one 10^7-record mixed
+                 frame decoded in N byte ranges (strong).
 """
 import argparse
 import json
@@ -297,13 +298,13 @@ def cpu_baseline_threads(wire_host, ids, seconds, threads=16):
 
 def read_traffic(records, kernel):
     """HBM bytes per launch from the committed rocprofv3 PMC summary, if it matches."""
-    p = os.path.join(ROOT, "profiles", "pmc_dec_f64.json")
-    try:
-        j = json.load(open(p))
-        if j.get("records") == records and j.get("kernel") == kernel:
-            return j.get("hbm_bytes_per_launch")
-    except Exception:
-        pass
+    for f in ("pmc_dec_f64.json", "pmc_dec_f64_100000000.json"):
+        try:
+            j = json.load(open(os.path.join(ROOT, "profiles", f)))
+            if j.get("records") == records and j.get("kernel") == kernel:
+                return j.get("hbm_bytes_per_launch")
+        except Exception:
+            pass
     return None
 
 
@@ -411,6 +412,9 @@ def extras_single_gpu(codec, stream, steps, warmup):
                                     "per_call_kernel_ms": round(kms_run1, 4),
                                     "per_call_hbm_frac": fr(kms_run1)},
                                 "kernel_split": read_split(n),
+                                "traffic": read_traffic(n, kname),
+                                "traffic_source": "profiles/pmc_dec_f64_100000000.json (FETCH_SIZE "
+                                                  "x2 + WRITE_SIZE per launch, committed)",
                                 "oracle_rows_checked": sum(oracle_check_decode(wire, o, n)
                                                            for o in outs)}
         del cols, wire, wires, outs
@@ -1023,8 +1027,63 @@ def extras_multi_gpu(codec, world, rank, stream):
     ex["decode_mixed_1e7_per_gpu"] = {
         "records_per_gpu": nm, "world": world, "kernel_ms_slowest_rank": round(kmax, 4),
         "M_updates_s": round(world * nm / (kmax / 1e3) / 1e6, 1)}
+    # config 3 strong-scaled: the SAME 10^7-record mixed frame (one connection's batch, as every
+    # rank holds config 5's frame after the all-gather) decoded in N byte ranges, one per GPU
+    # (nxg_decode_sharded: the fast mixed decoder in range mode, ranges linked)
+    comm.close()
+    comm = make_comm(codec, world, rank, [wire])
+    W = wire.numel()
+    sout = Columns.for_frame(W // world + 65536, netidx_amd.LAYOUT_MIXED, "cuda")
+
+    def decode_mixed_ranges():
+        return comm.decode_sharded(wire, W, sout)
+
+    decode_mixed_ranges()
+    times = []
+    for it in range(5):
+        barrier(world)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        row_off, rng = decode_mixed_ranges()
+        torch.cuda.synchronize()
+        times.append(time.perf_counter() - t0)
+    t = max_over_ranks(min(times), world)
+    check_mixed_range(wire, heap, mc, sout, row_off, rng, nm)
+    ex["decode_mixed_1e7_byte_ranges"] = {
+        "records": nm, "world": world, "wire_bytes": W, "range_path": int(rng.ok),
+        "via": ("rccl" if BACKEND != "gloo" else "gloo transport via nxg_comm_init_ops") +
+               " (nxg_decode_sharded: fast mixed decoder in range mode)",
+        "ms_slowest_rank": round(t * 1e3, 4), "M_updates_s": round(nm / t / 1e6, 1)}
     comm.close()
     return ex
+
+
+def check_mixed_range(wire, heap, mc, out, row_off, rng, nm):
+    """One rank's byte range of a mixed frame against the encode input it was made from: rows
+    [row_off, row_off + n) of every column (array child indices from the range's first child,
+    text compared byte for byte), and the children of those rows."""
+    import torch
+    n = int(rng.n_rows)
+    assert rng.ok == 1 and row_off + n <= nm, (row_off, n, rng.ok)
+    sl = slice(row_off, row_off + n)
+    for k in ("id", "tag", "aux"):
+        assert torch.equal(out.t[k][:n], mc.t[k][sl]), f"mixed range differs in column {k}"
+    tag = out.tag[:n]
+    arr, txt = tag == 19, tag == 12
+    plain = ~(arr | txt)
+    assert torch.equal(out.fixed[:n][plain], mc.fixed[sl][plain]), "mixed range differs in fixed"
+    if bool(arr.any()):
+        c0 = int(mc.fixed[sl][arr][0]) - int(out.fixed[:n][arr][0])
+        assert torch.equal(out.fixed[:n][arr] + c0, mc.fixed[sl][arr])
+        nc = int(out.s.n_children)
+        for k in ("ctag", "cfixed", "caux"):
+            assert torch.equal(out.t[k][:nc], mc.t[k][c0:c0 + nc]), f"range children differ: {k}"
+    lens = out.aux[:n][txt].long()
+    if len(lens):
+        rep = torch.repeat_interleave(torch.arange(len(lens), device=lens.device), lens)
+        pos = torch.arange(int(lens.sum()), device=lens.device) - (torch.cumsum(lens, 0) - lens)[rep]
+        assert torch.equal(wire[out.fixed[:n][txt][rep] + pos],
+                           heap[mc.fixed[sl][txt][rep] + pos]), "mixed range differs in text"
 
 
 def main():
