@@ -337,6 +337,10 @@ class Columns:
             self.caps["rows"], self.caps["children"], self.caps["ctl"])
         for name, _, _ in self.FIELDS:
             setattr(self.s, name, _ptr(self.t[name]).value)
+        if self.device.type == "cuda":
+            # the zero fill ran on torch's current stream; a codec on another stream (set_stream)
+            # must not start writing before it is done
+            torch.cuda.synchronize(self.device)
 
     @classmethod
     def for_frame(cls, nbytes, layout=LAYOUT_MIXED, device="cuda"):
@@ -483,6 +487,13 @@ class Codec:
         cols = Columns.for_frame(n, layout, device)
         st = self.decode_into(frame, n, cols, flags)
         return cols, st
+
+    def last_status(self):
+        """(fast_fail, irregular, path, n_rows, err_kind, timeout) of the last completed decode's
+        device status (diagnostics, not ABI)."""
+        a = (C.c_ulonglong * 6)()
+        lib().nxg_debug_status(C.c_void_p(self.ctx), a)
+        return list(a)
 
     def last_diag(self):
         """DevStatus.diag of the last completed decode (diagnostics, not ABI): for an f64 frame,

@@ -44,6 +44,12 @@ constexpr uint32_t IMGL = fmx::IMG - 24;  // emit image: items end before this (
 #define NXG_FA_PRE 128
 #endif
 constexpr uint32_t PRE = NXG_FA_PRE;      // count image: bytes before the tile (walked for the entry)
+#ifndef NXG_FA_WIN
+#define NXG_FA_WIN 1  // text / varint lengths from the item's own window in the item walks
+#endif
+#ifndef NXG_FA_STRIDE
+#define NXG_FA_STRIDE 1  // array elements by stride speculation in the item walks
+#endif
 constexpr uint32_t CIMG = PRE + fmx::IMG;  // count image bytes
 constexpr uint32_t CIMGL = CIMG - 24;      // count image: items end before this (text aside)
 }  // namespace fa
@@ -130,11 +136,40 @@ NXG_DEV uint32_t item_end(lds_bytes img, uint32_t p, uint32_t wl, uint32_t il, u
     const uint32_t q = p + k + 1;  // the Event's first byte
     const uint32_t t = (uint32_t)(w.lo >> (8 * (k + 1))) & 0xffu;
     if (t == UNSUB) return q + 1 <= wl ? q + 1 : FAIL;
+    if (NXG_FA_WIN && t < 28u && ((1u << t) & (kVarTags | kTextTags))) {
+        // a varint scalar or text: its varint from the same window (bytes k + 2 .. k + 11 of it,
+        // k <= 4), not a second window read as leaf_end makes
+        const uint32_t o = 8 * (k + 2);
+        uint64_t x;
+        const uint32_t nb = wvar((w.lo >> o) | (w.hi << (64 - o)), w.hi >> o, x);
+        if (nb == 0) return FAIL;
+        const uint32_t s = q + 1 + nb;
+        if ((1u << t) & kVarTags) return s <= min(wl, il) ? s : FAIL;
+        return s <= wl && x <= (uint64_t)(wl - s) ? s + (uint32_t)x : FAIL;
+    }
     if (t != 19u) return leaf_end(img, q, t, wl, il);
     const uint32_t c = img[q + 1];
     if (c >= 0x80u) return FAIL;
     kids = c;
     uint32_t e = q + 2;
+    if (NXG_FA_STRIDE && c) {
+        // stride speculation: an array whose first element has a fixed size f is taken to be c
+        // elements of that size, each element's tag then read independently (8 at a time, one
+        // LDS round trip instead of one per element); any other element falls to the exact walk
+        const uint32_t f = fixed_size1(img[e]);
+        if (f && e + c * f <= min(wl, il)) {
+            bool ok = true;
+#pragma unroll 1
+            for (uint32_t i0 = 1; i0 < c && ok; i0 += 8) {
+                uint32_t tg[8];
+#pragma unroll
+                for (int j = 0; j < 8; j++) tg[j] = img[i0 + j < c ? e + (i0 + j) * f : e];
+#pragma unroll
+                for (int j = 0; j < 8; j++) ok = ok && fixed_size1(tg[j]) == f;
+            }
+            if (ok) return e + c * f;
+        }
+    }
 #pragma unroll 1
     for (uint32_t i = 0; i < c && e != FAIL; i++) {
         if (e >= il) return FAIL;
@@ -486,6 +521,65 @@ __global__ __launch_bounds__(TPB) void nxg_fa_fix_kernel(const uint8_t* __restri
     if (lane == 0) td[t] = d;
 }
 
+#ifndef NXG_FA_FIXLIST
+#define NXG_FA_FIXLIST 1
+#endif
+// fix as two launches: a lane per tile lists the tiles entered elsewhere than their predecessor's
+// counted exit (wave-aggregated appends), then a persistent grid of waves takes the listed tiles by
+// ticket and recounts each from its predecessor's exit. The per-tile fix kernel launches a wave for
+// every tile of the batch (46,598 at 10^7 items) to recount about 2 % of them.
+// (A wave recounting its 64 tiles in order measured slower, 243 vs 112 us: the recounts of the
+// busiest wave set the pass.)
+__global__ __launch_bounds__(TPB) void nxg_fa_fixlist_kernel(uint64_t nt,
+                                                             const FaDesc* __restrict__ td,
+                                                             uint32_t* __restrict__ list,
+                                                             uint32_t* __restrict__ cnt) {
+    const uint64_t t = (uint64_t)blockIdx.x * TPB + threadIdx.x;
+    bool mis = false;
+    if (t >= 1 && t < nt) {
+        const FaDesc p = td[t - 1];
+        const uint32_t e = td[t].entry;
+        mis = !(p.exit == FAIL || (p.items & BROKEN) || p.exit - TILE == e || p.exit - TILE >= TILE);
+    }
+    const uint64_t m = __ballot(mis);
+    if (!m) return;
+    const uint32_t lane = threadIdx.x & 63, lead = (uint32_t)__builtin_ctzll(m);
+    uint32_t b0 = 0;
+    if (lane == lead) b0 = atomicAdd(cnt, (uint32_t)__popcll(m));
+    b0 = __shfl(b0, (int)lead);
+    if (mis) list[b0 + __popcll(m & ((1ull << lane) - 1))] = (uint32_t)t;
+}
+__global__ __launch_bounds__(TPB) void nxg_fa_fixrun_kernel(const uint8_t* __restrict__ buf,
+                                                            uint64_t W, FaDesc* __restrict__ td,
+                                                            uint64_t* __restrict__ starts,
+                                                            const uint32_t* __restrict__ list,
+                                                            const uint32_t* __restrict__ cnt,
+                                                            uint32_t* __restrict__ ticket) {
+    __shared__ __attribute__((aligned(16))) FaCountLds lds[TPB / 64];
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint8_t* img = lds[w].img;
+    const uint32_t n = __builtin_amdgcn_readfirstlane(*cnt);
+#pragma unroll 1
+    for (;;) {
+        uint32_t j = 0;
+        if (lane == 0) j = atomicAdd(ticket, 1u);
+        j = __builtin_amdgcn_readfirstlane(j);
+        if (j >= n) break;  // every wave ends once the list is taken
+        const uint64_t t = list[j];
+        const uint32_t px = __builtin_amdgcn_readfirstlane(td[t - 1].exit);
+        const uint32_t pi = __builtin_amdgcn_readfirstlane(td[t - 1].items);
+        const uint32_t e = __builtin_amdgcn_readfirstlane(td[t].entry);
+        if (px == FAIL || (pi & BROKEN) || px - TILE == e || px - TILE >= TILE) continue;
+        CountRegs g;
+        count_load(g, buf, t * TILE, W, lane);
+        count_store(img, g, lane);
+        uint64_t bits;
+        const FaDesc d = count_tile((lds_bytes)img, t, W, px - TILE, lane, bits);
+        starts[t * 64 + lane] = bits;
+        if (lane == 0) td[t] = d;
+    }
+}
+
 // resolve: a lane per tile. A tile whose entry is not its (unbroken) predecessor's exit is
 // recounted from that exit by its wave; then block scans of (items | child slots << 32) give each
 // tile its offset in the block (tloc), and the last block to arrive (FaHead.arrived) scans the
@@ -748,9 +842,9 @@ __global__ __launch_bounds__(TPB) void nxg_fa_emit_kernel(
 // ---- launch (host) --------------------------------------------------------------------------------
 uint64_t nxg_fa_scratch_bytes(uint64_t W) {
     const uint64_t nt = (W + TILE - 1) / TILE;
-    // head 64 B; 2 descs 32 B, starts 512 B, tloc 8 B per tile; bsum + bpre 16 B per 256 tiles;
-    // one exit word per 64 tiles
-    return 64 + nt * 552 + 16 * (nt / TPB + 1) + 8 * (nt / 64 + 1) + 7 * 16;
+    // head 64 B; 2 descs 32 B, starts 512 B, tloc 8 B, fix list 4 B per tile; bsum + bpre 16 B
+    // per 256 tiles; one exit word per 64 tiles; the fix passes' counters 64 B
+    return 64 + nt * 556 + 16 * (nt / TPB + 1) + 8 * (nt / 64 + 1) + 64 + 9 * 16;
 }
 
 // One pass of the fast path over buf[0, W) (W < 2^32; the batch's count and its varint's length
@@ -777,15 +871,28 @@ hipError_t nxg_launch_dec_fa(const uint8_t* buf, uint64_t W, uint32_t p0, uint64
     uint64_t* bpre = reinterpret_cast<uint64_t*>(take(8 * nb));
     const uint64_t nwv = (nt + 63) / 64;
     uint64_t* wexit = reinterpret_cast<uint64_t*>(take(8 * nwv));
+    uint32_t* fixl = reinterpret_cast<uint32_t*>(take(4 * nt));  // the fix passes' tile list
+    uint32_t* fixw = reinterpret_cast<uint32_t*>(take(64));      // its counts and tickets
     hipError_t e;
     if ((e = hipMemsetAsync(hp, 0, sizeof(FaHead), s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(fixw, 0, 64, s)) != hipSuccess) return e;
+    const uint64_t fix_grid = std::min<uint64_t>((nt + 3) / 4, 1024);
     if ((e = hipMemsetAsync(wexit, 0, 8 * nwv, s)) != hipSuccess) return e;
     constexpr uint64_t WV = TPB / 64;
     const uint32_t gc = (uint32_t)((nt + WV - 1) / WV);
     hipLaunchKernelGGL(nxg_fa_count_kernel, dim3(gc), dim3(TPB), 0, s, buf, W, nt, p0, td, starts);
     // (a second pass would catch the tiles whose predecessor the first one recounted)
-    for (int k = 0; k < NXG_FA_FIX_PASSES; k++)
-        hipLaunchKernelGGL(nxg_fa_fix_kernel, dim3(gc), dim3(TPB), 0, s, buf, W, nt, td, starts);
+    for (int k = 0; k < NXG_FA_FIX_PASSES; k++) {
+        if (NXG_FA_FIXLIST) {
+            uint32_t* c = fixw + 2 * k;  // [count, ticket] of this pass
+            hipLaunchKernelGGL(nxg_fa_fixlist_kernel, dim3((uint32_t)((nt + TPB - 1) / TPB)),
+                               dim3(TPB), 0, s, nt, td, fixl, c);
+            hipLaunchKernelGGL(nxg_fa_fixrun_kernel, dim3((uint32_t)fix_grid), dim3(TPB), 0, s, buf,
+                               W, td, starts, fixl, c, c + 1);
+        } else {
+            hipLaunchKernelGGL(nxg_fa_fix_kernel, dim3(gc), dim3(TPB), 0, s, buf, W, nt, td, starts);
+        }
+    }
     hipLaunchKernelGGL(nxg_fa_resolve_kernel, dim3((uint32_t)nb), dim3(TPB), 0, s, buf, W, nt, td,
                        td2, starts, tloc, bsum, bpre, wexit, hp);
     hipLaunchKernelGGL(nxg_fa_emit_kernel, dim3(gc), dim3(TPB), 0, s, buf, W, nt, p0, count, td2,

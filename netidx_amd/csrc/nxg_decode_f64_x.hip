@@ -42,6 +42,7 @@ constexpr int WAVES = TPB / 64;
 constexpr int SPW = NXG_F64X_SPW;       // sub-tiles per wave
 constexpr uint64_t WGB = (uint64_t)SUB * SPW * WAVES;  // bytes per workgroup
 constexpr uint32_t MAXR = SUB / 12 + 2;  // rows per sub-tile (records start in it, >= 12 bytes)
+constexpr uint32_t MAXW = MAXR * SPW;     // rows per wave
 #ifndef NXG_F64X_CB
 #define NXG_F64X_CB 6
 #endif
@@ -55,7 +56,44 @@ constexpr uint32_t MAXR = SUB / 12 + 2;  // rows per sub-tile (records start in 
 #define NXG_F64X_LASTX 1  // 1: the 16 positions after a sub-tile read only after the wave's last (0.121-0.122 vs 0.1245 ms)
 #endif
 constexpr int CB = NXG_F64X_CB;          // candidates checked together (independent loads)
+#ifndef NXG_F64X_EU
+#define NXG_F64X_EU 2  // emit rounds with loads in flight together (1 / 2 / 4 with pairs: 0.114 / 0.113 / 0.116 ms)
+#endif
+#ifndef NXG_F64X_CBATCH
+#define NXG_F64X_CBATCH 0
+#endif
+#ifndef NXG_F64X_PAIRS
+#define NXG_F64X_PAIRS 1  // emit two rows per lane as 16-byte stores (0.113 vs 0.118 ms at 10^7)
+#endif
+#ifndef NXG_F64X_NT
+#define NXG_F64X_NT 1  // nontemporal row stores (0.900-0.905 vs 0.928-0.931 ms at 10^8)
+#endif
+#ifndef NXG_F64X_PFD
+#define NXG_F64X_PFD 1  // sub-tile images loading ahead (registers; 2: no faster)
+#endif
+constexpr int PFD = NXG_F64X_PFD;
+
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+constexpr int EU = NXG_F64X_EU;          // emit rounds whose record loads are in flight together
 }  // namespace f64x
+
+#ifndef NXG_F64X_PROF
+#define NXG_F64X_PROF 0
+#endif
+#if NXG_F64X_PROF
+// diagnostic build only: per workgroup (the first 16384) s_memtime at the kernel's phase edges
+// (start, phase 1 done, block scan done, look-back done, emit done) and the XCC / CU it ran on
+__device__ unsigned long long nxg_f64x_st[6][16384];
+#define XSTAMP(k)                                                                                \
+    do {                                                                                         \
+        if (threadIdx.x == 0 && blockIdx.x < 16384)                                              \
+            nxg_f64x_st[k][blockIdx.x] = __builtin_amdgcn_s_memrealtime();                           \
+    } while (0)
+#else
+#define XSTAMP(k) \
+    do {          \
+    } while (0)
+#endif
 
 namespace {
 using namespace f64x;
@@ -126,12 +164,36 @@ NXG_DEV void starts_of(const SwzImg& im, uint32_t r, uint64_t fp, uint64_t W, ui
         // every candidate (a byte in 12..16 then 04) taken as a start, its successor from its
         // length byte; the records are checked completely where they are decoded
         S = cm;
+        if (!NXG_F64X_CBATCH) {
 #pragma unroll 1
-        for (uint64_t m = cm; m; m &= m - 1) {
-            const uint32_t p = (uint32_t)__builtin_ctzll(m);
-            const uint32_t nx = p + im.byte(r + p);
-            if (nx < 64u) slo |= 1ull << nx;
-            else shi |= 1ull << (nx - 64u);
+            for (uint64_t m = cm; m; m &= m - 1) {
+                const uint32_t p = (uint32_t)__builtin_ctzll(m);
+                const uint32_t nx = p + im.byte(r + p);
+                if (nx < 64u) slo |= 1ull << nx;
+                else shi |= 1ull << (nx - 64u);
+            }
+            return;
+        }
+        // (CB candidates at a time: their length bytes read from LDS together, one wait; A/B:
+        // slower, 0.122 vs 0.118 ms at 10^7 with the emit pipelining)
+#pragma unroll 1
+        for (uint64_t m = cm; m;) {
+            uint32_t pp[CB], ll[CB];
+#pragma unroll
+            for (int i = 0; i < CB; i++) {
+                pp[i] = m ? (uint32_t)__builtin_ctzll(m) : 64u;
+                m &= m - 1;
+            }
+#pragma unroll
+            for (int i = 0; i < CB; i++) ll[i] = im.byte(r + (pp[i] & 63u));
+#pragma unroll
+            for (int i = 0; i < CB; i++) {
+                if (pp[i] < 64u) {
+                    const uint32_t nx = pp[i] + ll[i];
+                    if (nx < 64u) slo |= 1ull << nx;
+                    else shi |= 1ull << (nx - 64u);
+                }
+            }
         }
         return;
     }
@@ -288,15 +350,20 @@ NXG_DEV void subtile_starts(const uint8_t* __restrict__ wire, const XRange& rg, 
 // (nxg_f64_rec16.h exact_tile: merge points and lane walks), which counts the records that start
 // in the range. On a valid frame that is g's own count (both are the true chain's starts in g's
 // bytes); if the walks find no chain the frame is rerun (fast_fail), as g itself would.
-NXG_DEV uint64_t wg_count(const uint8_t* __restrict__ wire, const XRange& rg, uint8_t* buf,
-                          uint64_t g, uint32_t lane, DevStatus* st) {
+template <uint32_t T>
+NXG_DEV uint64_t unit_count(const uint8_t* __restrict__ wire, const XRange& rg, uint8_t* buf,
+                            uint64_t g, uint32_t lane, DevStatus* st) {
     static_assert(IMGB == kXImg && SUB == kXSub && XLO == kXLo, "the exact path's image");
     uint32_t c, en, xx;
     bool b = false, ov = false;
-    exact_tile<false, (uint32_t)WGB>(wire, rg.W, rg.R, rg.first, rg.pre, g, buf, lane, 0, nullptr,
-                                     nullptr, 0, c, en, xx, b, ov);
+    exact_tile<false, T>(wire, rg.W, rg.R, rg.first, rg.pre, g, buf, lane, 0, nullptr, nullptr, 0,
+                         c, en, xx, b, ov);
     if (b && lane == 0) atomicOr(&st->fast_fail, 1u);
     return c;
+}
+NXG_DEV uint64_t wg_count(const uint8_t* __restrict__ wire, const XRange& rg, uint8_t* buf,
+                          uint64_t g, uint32_t lane, DevStatus* st) {
+    return unit_count<(uint32_t)WGB>(wire, rg, buf, g, lane, st);
 }
 
 __global__ __launch_bounds__(TPB, NXG_F64X_OCC) void nxg_f64x_kernel(const uint8_t* __restrict__ wire,
@@ -306,9 +373,11 @@ __global__ __launch_bounds__(TPB, NXG_F64X_OCC) void nxg_f64x_kernel(const uint8
                                                        DevStatus* __restrict__ st,
                                                        DevStatus* zst, uint32_t patience) {
     zero_status(zst);
+    XSTAMP(0);
     const uint64_t W = rg.W, R = rg.R;
     __shared__ __attribute__((aligned(16))) uint8_t img[WAVES][IMGB];
-    __shared__ __attribute__((aligned(16))) uint64_t rows[WAVES][MAXR][2];
+    // the wave's record starts in wire order, as offsets from its first byte (< SUB * SPW)
+    __shared__ uint16_t plist[WAVES][MAXW];
     __shared__ uint64_t scan_tmp[WAVES];
     __shared__ uint64_t sh_base;
     const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -316,47 +385,47 @@ __global__ __launch_bounds__(TPB, NXG_F64X_OCC) void nxg_f64x_kernel(const uint8
     const uint32_t bid = blockIdx.x;
     const uint64_t w0 = (uint64_t)bid * WGB + (uint64_t)w * SUB * SPW;  // the wave's bytes
     uint8_t* buf = img[w];
-    const SwzImg im{buf};
-    uint64_t Sm[SPW];
-    uint32_t n[SPW];
+    uint16_t* pl = plist[w];
     bool bad = false;
-    Prefetch pf;
-    fetch_image(pf, wire, w0, W, lane, rg.pre);
+    // the images of the next PFD sub-tiles in registers while one is checked
+    Prefetch pf[PFD];
+#pragma unroll
+    for (int s = 0; s < PFD && s < SPW; s++)
+        if (w0 + (uint64_t)s * SUB < R) fetch_image(pf[s], wire, w0 + (uint64_t)s * SUB, W, lane, rg.pre);
     // q: the frame position of the chain's first record start at or past the sub-tile, carried
     // from sub-tile to sub-tile of the wave (~0: not known -- the wave's first sub-tile)
     uint64_t q = ~0ull;
+    uint32_t tw = 0;  // the wave's records so far (wave-uniform)
 #pragma unroll
     for (int s = 0; s < SPW; s++) {
-        Sm[s] = 0;
-        n[s] = 0;
         const uint64_t a0 = w0 + (uint64_t)s * SUB;
-        if (a0 >= R) continue;
-        commit_image(buf, pf, lane);
-        if (s + 1 < SPW && a0 + SUB < R)
-            fetch_image(pf, wire, a0 + SUB, W, lane, rg.pre);  // the next, while checking
-        subtile_starts(wire, rg, buf, a0, s == SPW - 1, lane, q, Sm[s], n[s], bad, st);
+        if (a0 >= R) break;
+        commit_image(buf, pf[s % PFD], lane);
+        if (s + PFD < SPW && a0 + PFD * SUB < R)
+            fetch_image(pf[s % PFD], wire, a0 + PFD * SUB, W, lane, rg.pre);  // while checking
+        uint64_t Sm;
+        uint32_t n;
+        subtile_starts(wire, rg, buf, a0, s == SPW - 1, lane, q, Sm, n, bad, st);
+        // the sub-tile's starts into the wave's list, in wire order (a frame that is not a chain
+        // of records can hold more candidates than the list: those are dropped, and the frame is
+        // rerun anyway)
+        const uint32_t inc = wave_incl_scan<uint32_t>(n);
+        uint32_t k = tw + inc - n;
+        const uint32_t pb = (uint32_t)s * SUB + lane * 64;
+#pragma unroll 1
+        for (uint64_t m = Sm; m; m &= m - 1, k++)
+            if (k < MAXW) pl[k] = (uint16_t)(pb + (uint32_t)__builtin_ctzll(m));
+        tw += wave_last<uint32_t>(inc);
     }
+    bad |= tw > MAXW;
+    XSTAMP(1);
     const bool wbad = __any(bad);
     if (wbad && lane == 0) atomicOr(&st->fast_fail, 1u);
-    // rows: the block scan orders the lanes' counts wave by wave, sub-tile by sub-tile within a
-    // wave; here the lane's total, and below each sub-tile's wave-level offsets
-    uint32_t ntot = 0;
-#pragma unroll
-    for (int s = 0; s < SPW; s++) ntot += n[s];
-    // the first image of the emit pass, loading during the look-back (waves 1..3; wave 0 runs the
-    // look-back, whose self-help path needs the registers)
-    if (SPW > 1 && w != 0) fetch_image(pf, wire, w0, W, lane, rg.pre);
-    // the start masks wait in the wave's (still unused) row buffer across the look-back, so that
-    // they hold no registers there
-    uint32_t* stash = reinterpret_cast<uint32_t*>(rows[w]);
-#pragma unroll
-    for (int s = 0; s < SPW; s++) {
-        stash[(3 * s) * 64 + lane] = (uint32_t)Sm[s];
-        stash[(3 * s + 1) * 64 + lane] = (uint32_t)(Sm[s] >> 32);
-        stash[(3 * s + 2) * 64 + lane] = n[s];
-    }
+    // rows: one block scan of the waves' totals, one look-back per workgroup
     uint64_t total;
-    const uint64_t excl = block_excl_scan<uint64_t, TPB>((uint64_t)ntot, scan_tmp, &total);
+    const uint64_t excl =
+        block_excl_scan<uint64_t, TPB>(lane == 0 ? (uint64_t)tw : 0ull, scan_tmp, &total);
+    XSTAMP(2);
     if (w == 0) {
         uint64_t base = 0;
         if (bid == 0) {
@@ -377,73 +446,145 @@ __global__ __launch_bounds__(TPB, NXG_F64X_OCC) void nxg_f64x_kernel(const uint8
         }
     }
     __syncthreads();
+    XSTAMP(3);
     if (wbad) return;  // (a bad sub-tile has raised fast_fail: the frame is rerun)
-    if (SPW > 1 && w == 0) fetch_image(pf, wire, w0, W, lane, rg.pre);
-#pragma unroll
-    for (int s = 0; s < SPW; s++) {
-        Sm[s] = (uint64_t)stash[(3 * s) * 64 + lane] | ((uint64_t)stash[(3 * s + 1) * 64 + lane] << 32);
-        n[s] = stash[(3 * s + 2) * 64 + lane];
-    }
-    wave_lds_order();  // (the row buffer is written below)
     // the wave's first row: the block prefix of its lane 0
-    uint64_t row0 = sh_base + ((uint64_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)excl) |
-                               ((uint64_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(excl >> 32)) << 32));
+    const uint64_t row0 =
+        sh_base + ((uint64_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)excl) |
+                   ((uint64_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(excl >> 32)) << 32));
+    // emit: one record per lane, 64 consecutive rows per round; the record's 16 bytes by one
+    // (unaligned) load from the frame, which the wave read a moment ago (L2), and checked
+    // completely (CHEAP: a candidate counted as a start must be a whole record)
     bool over = false, vbad = false;
+#if NXG_F64X_PAIRS
+    // two consecutive rows per lane, stored as 16-byte pairs (half the store instructions): lane j
+    // of a round takes rows 2j, 2j + 1 counted from the even row at or before row0, so the pairs are
+    // 16-byte aligned; the half of a pair outside the wave's rows (the first, the last) is skipped
+    {
+        const uint32_t a = (uint32_t)(row0 & 1u);  // row0 odd: the first pair's first row is not ours
+        const uint64_t rb = row0 - a;              // even
+        const uint32_t np = (tw + a + 1) / 2;      // pairs
+#pragma unroll 1
+        for (uint32_t j0 = 0; j0 < np; j0 += 64 * EU) {
+            uint64_t p[EU][2];
+            uint4 e[EU][2];
 #pragma unroll
-    for (int s = 0; s < SPW; s++) {
-        const uint64_t a0 = w0 + (uint64_t)s * SUB;
-        if (a0 >= R) break;
-        const uint32_t inc = wave_incl_scan<uint32_t>(n[s]);
-        const uint32_t nw = wave_last<uint32_t>(inc);
-        if (SPW > 1) {
-            commit_image(buf, pf, lane);
-            if (s + 1 < SPW && a0 + SUB < R) fetch_image(pf, wire, a0 + SUB, W, lane, rg.pre);
-        }
-        // the lane's records (at most 6 start in 64 bytes), loaded together
-        uint32_t k = inc - n[s];
-        uint64_t m = Sm[s];
-        const uint32_t r = XLO + lane * 64;
-        uint32_t pp[6];
+            for (int u = 0; u < EU; u++) {
+                const uint32_t j = j0 + 64 * u + lane;
 #pragma unroll
-        for (int i = 0; i < 6; i++) {
-            pp[i] = m ? (uint32_t)__builtin_ctzll(m) : 0u;
-            m &= m - 1;
-        }
-        uint32_t e[6][4];
+                for (int h = 0; h < 2; h++) {
+                    const int32_t k = (int32_t)(2 * j + h) - (int32_t)a;  // record index in the wave
+                    const uint32_t kc = k < 0 ? 0u : ((uint32_t)k < tw ? (uint32_t)k : tw - 1);
+                    p[u][h] = w0 + pl[kc];
+                }
+            }
 #pragma unroll
-        for (int i = 0; i < 6; i++) lds16i(im, r + pp[i], e[i][0], e[i][1], e[i][2], e[i][3]);
+            for (int u = 0; u < EU; u++) {
+                e[u][0] = ld16g(wire, p[u][0], W);
+                e[u][1] = ld16g(wire, p[u][1], W);
+            }
 #pragma unroll
-        for (int i = 0; i < 6; i++) {
-            if ((uint32_t)i < n[s]) {
-                uint64_t id, val;
-                if (NXG_F64X_CHEAP)
-                    vbad |= rec_check16(e[i][0], e[i][1], W - (a0 + lane * 64 + pp[i])) !=
-                            (e[i][0] & 0xffu);
-                rec_decode16(e[i][0], e[i][1], e[i][2], e[i][3], e[i][0] & 0xffu, id, val);
-                rows[w][k + i][0] = id;
-                rows[w][k + i][1] = val;
+            for (int u = 0; u < EU; u++) {
+                const uint32_t j = j0 + 64 * u + lane;
+                uint64_t id[2], val[2];
+                bool in[2];
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    const int32_t k = (int32_t)(2 * j + h) - (int32_t)a;
+                    in[h] = k >= 0 && (uint32_t)k < tw;
+                    const uint32_t L = e[u][h].x & 0xffu;
+                    if (in[h]) vbad |= rec_check16(e[u][h].x, e[u][h].y, W - p[u][h]) != L;
+                    rec_decode16(e[u][h].x, e[u][h].y, e[u][h].z, e[u][h].w, L, id[h], val[h]);
+                }
+                const uint64_t row = rb + 2 * (uint64_t)j;
+                if (in[0] && in[1] && row + 1 < cap) {
+                    const v4u iv = {(uint32_t)id[0], (uint32_t)(id[0] >> 32), (uint32_t)id[1],
+                                    (uint32_t)(id[1] >> 32)};
+                    const v4u vv = {(uint32_t)val[0], (uint32_t)(val[0] >> 32), (uint32_t)val[1],
+                                    (uint32_t)(val[1] >> 32)};
+                    if (NXG_F64X_NT) {  // (rows are not read again: keep L2 for the frame)
+                        __builtin_nontemporal_store(iv, reinterpret_cast<v4u*>(oid + row));
+                        __builtin_nontemporal_store(vv, reinterpret_cast<v4u*>(oval + row));
+                    } else {
+                        *reinterpret_cast<v4u*>(oid + row) = iv;
+                        *reinterpret_cast<v4u*>(oval + row) = vv;
+                    }
+                } else {
+#pragma unroll
+                    for (int h = 0; h < 2; h++) {
+                        if (!in[h]) continue;
+                        if (row + h < cap) {
+                            oid[row + h] = id[h];
+                            oval[row + h] = val[h];
+                        } else {
+                            over = true;
+                        }
+                    }
+                }
             }
         }
-        wave_lds_order();
-        for (uint32_t i = lane; i < nw; i += 64) {
-            const uint64_t row = row0 + i;
-            if (row < cap) {
-                oid[row] = rows[w][i][0];
-                oval[row] = rows[w][i][1];
-            } else {
-                over = true;
-            }
-        }
-        wave_lds_order();
-        row0 += nw;
     }
+#else
+    // EU rounds at a time: their loads in flight together
+#pragma unroll 1
+    for (uint32_t k0 = 0; k0 < tw; k0 += 64 * EU) {
+        uint64_t p[EU];
+        uint4 e[EU];
+#pragma unroll
+        for (int u = 0; u < EU; u++) {
+            const uint32_t k = k0 + 64 * u + lane;
+            p[u] = w0 + pl[k < tw ? k : tw - 1];
+        }
+#pragma unroll
+        for (int u = 0; u < EU; u++) e[u] = ld16g(wire, p[u], W);
+#pragma unroll
+        for (int u = 0; u < EU; u++) {
+            const uint32_t k = k0 + 64 * u + lane;
+            if (k < tw) {
+                const uint32_t L = e[u].x & 0xffu;
+                vbad |= rec_check16(e[u].x, e[u].y, W - p[u]) != L;
+                uint64_t id, val;
+                rec_decode16(e[u].x, e[u].y, e[u].z, e[u].w, L, id, val);
+                const uint64_t row = row0 + k;
+                if (row < cap) {
+                    oid[row] = id;
+                    oval[row] = val;
+                } else {
+                    over = true;
+                }
+            }
+        }
+    }
+#endif
     if (__any(over) && lane == 0) atomicOr(&st->capacity, 1u);
     if (__any(vbad) && lane == 0) atomicOr(&st->fast_fail, 1u);  // (CHEAP: a start not a record)
+#if NXG_F64X_PROF
+    if (threadIdx.x == 0 && blockIdx.x < 16384) {
+        nxg_f64x_st[4][blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+        uint32_t hw;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        uint32_t xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        nxg_f64x_st[5][blockIdx.x] = ((uint64_t)xcc << 32) | hw;
+    }
+#endif
 }
 
 }  // namespace
 
-uint64_t nxg_dec_f64x_groups(uint64_t W) { return (W + WGB - 1) / WGB; }
+// workgroups of a range of R bytes (one look-back word each)
+static uint64_t f64x_wgs(uint64_t R) { return (R + WGB - 1) / WGB; }
+// (one look-back per wave instead, 16 KiB units: 0.120 vs 0.110 ms at 10^7 -- the inclusive front
+// crosses four times the units)
+uint64_t nxg_dec_f64x_groups(uint64_t W) { return f64x_wgs(W); }
+
+#if NXG_F64X_PROF
+// diagnostic build only (not ABI): the stamps of the last single-pass decode, 6 x 16384 u64
+extern "C" int nxg_debug_f64x_stamps(unsigned long long* out) {
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(nxg_f64x_st), sizeof(nxg_f64x_st), 0,
+                                    hipMemcpyDeviceToHost);
+}
+#endif
 
 // Decodes the records that start in [begin, end) of a frame of W bytes (a whole frame: 0, W).
 // `tstat` holds nxg_dec_f64x_groups(end - begin) epoch-tagged words (no initialisation needed).
@@ -454,7 +595,7 @@ hipError_t nxg_launch_dec_f64x_range(const uint8_t* wire, uint64_t W, uint64_t b
                                      uint64_t* tstat, uint32_t epoch, DevStatus* st,
                                      hipStream_t s) {
     if (begin > end || end > W) return hipErrorInvalidValue;
-    const uint64_t ng = nxg_dec_f64x_groups(end - begin);
+    const uint64_t ng = f64x_wgs(end - begin);
     if (ng == 0) return hipSuccess;
     if (ng > 0x7fffffffull) return hipErrorInvalidValue;
     const XRange rg{W - begin, end - begin, begin < 64 ? begin : 64, begin == 0};

@@ -24,6 +24,8 @@
 // The frame fails with the first error on the true chain, (PackError kind, offset of the
 // failing message), as the sequential reference stops at its first error
 // (netidx/src/subscriber/connection.rs:228-231).
+// (the resolve pass runs 8 waves per workgroup; each wave may decode values)
+#define NXG_DV_WAVES 8
 #include "nxg_msg.h"
 
 using namespace nxgmsg;
@@ -465,7 +467,10 @@ NXG_DEV RunSum run_tiles(const uint8_t* __restrict__ wire, uint64_t W, uint64_t 
 }  // namespace
 
 // ---- pass 1: count ---------------------------------------------------------------------------
-__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4))) void nxg_gen_count_kernel(
+#ifndef NXG_GEN_COUNT_OCC
+#define NXG_GEN_COUNT_OCC 3  // waves per SIMD (4: 128 VGPRs, and 128 B/lane of scratch)
+#endif
+__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(NXG_GEN_COUNT_OCC))) void nxg_gen_count_kernel(
     const uint8_t* __restrict__ wire, uint64_t W, uint64_t nt, uint32_t* __restrict__ lws,
     uint64_t* __restrict__ runs, DevStatus* __restrict__ st, DevStatus* zst, uint64_t* __restrict__ fix) {
     zero_status(zst);
@@ -501,7 +506,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4))) void n
 // from `from` on: a run whose guessed entry disagrees with its entering exit (wave 0 re-walks it
 // from that exit, rewriting its lane words and summary), or the first run with an error (the
 // frame's error). Then the run totals are prefix-summed into the emit pass's bases.
-constexpr int RES_TPB = 1024;
+constexpr int RES_TPB = 512;  // (1024: 128 VGPRs at most, and the re-walk spilled 296 B/lane)
 constexpr int RES_K = gdec2::MAX_RUNS / RES_TPB;
 static_assert(gdec2::MAX_RUNS % RES_TPB == 0, "resolve geometry");
 

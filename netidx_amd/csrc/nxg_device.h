@@ -267,6 +267,19 @@ NXG_DEV uint64_t lookback_selfhelp_fn(const uint64_t* tstat, uint32_t tile, uint
     return base;
 }
 
+// f() for each (active) lane with `want`, one lane at a time (uniform loop; the others wait):
+// lanes that share one per-wave resource (an LDS stack) take turns
+template <typename F>
+NXG_DEV void one_lane_at_a_time(bool want, F&& f) {
+    uint64_t m = __ballot(want);
+#pragma unroll 1
+    while (m) {
+        const uint32_t j = (uint32_t)__builtin_ctzll(m);
+        m &= m - 1;
+        if (lane_id() == j) f();
+    }
+}
+
 // exclusive scan over a 256-thread block; `tmp` = 4 (or more) T in LDS. Returns the exclusive
 // prefix, sets *total. Contains __syncthreads().
 template <typename T, int NT>

@@ -112,10 +112,12 @@ __global__ __launch_bounds__(TPB) void nxg_disp_count_kernel(
     NxgSubTable tb, Route rt, const uint64_t* __restrict__ id, uint64_t n, uint64_t seg_rows,
     uint64_t n_seg,
     uint32_t* __restrict__ hist, uint64_t* __restrict__ last_row, uint64_t* __restrict__ unmatched) {
-    __shared__ uint32_t cnt_lds[WAVES][LCH];
+    // (dynamic LDS: n_chans counters per wave, sized at launch, so that few channels leave room
+    // for more workgroups per CU)
+    extern __shared__ __attribute__((aligned(16))) uint64_t dyn_lds[];
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const bool lds = tb.n_chans <= LCH;
-    uint32_t* cnt = cnt_lds[w];
+    uint32_t* cnt = reinterpret_cast<uint32_t*>(dyn_lds) + (size_t)w * tb.n_chans;
     uint64_t um = 0;
 #pragma unroll 1
     for (uint64_t seg = (uint64_t)blockIdx.x * WAVES + w; seg < n_seg;
@@ -222,12 +224,12 @@ __global__ __launch_bounds__(TPB) void nxg_disp_scatter_kernel(
     uint64_t n_seg,
     uint64_t* __restrict__ off, uint64_t* __restrict__ ent_sub, uint64_t* __restrict__ ent_row,
     uint64_t cap) {
-    __shared__ uint64_t cur_lds[WAVES][LCH];
-    __shared__ uint64_t mask_lds[WAVES][LCH];
+    // (dynamic LDS: a cursor and a lane mask per channel and wave, sized at launch)
+    extern __shared__ __attribute__((aligned(16))) uint64_t dyn_lds[];
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const bool lds = tb.n_chans <= LCH;
-    uint64_t* cur = cur_lds[w];
-    uint64_t* mask = mask_lds[w];
+    uint64_t* cur = dyn_lds + (size_t)w * 2 * tb.n_chans;
+    uint64_t* mask = cur + tb.n_chans;
     const uint64_t lt = (1ull << lane) - 1;
 #pragma unroll 1
     for (uint64_t seg = (uint64_t)blockIdx.x * WAVES + w; seg < n_seg;
@@ -360,16 +362,19 @@ hipError_t nxg_launch_dispatch(const NxgSubTable& tb, const uint64_t* id, uint64
     if (tb.n_chans > LCH && (e = hipMemsetAsync(hist, 0, M * 4, s)) != hipSuccess) return e;
     const uint64_t want = (n_seg + WAVES - 1) / WAVES;
     const uint32_t g = (uint32_t)(want < (uint64_t)ncu * 8 ? want : (uint64_t)ncu * 8);
-    hipLaunchKernelGGL(nxg_disp_count_kernel, dim3(g), dim3(TPB), 0, s, tb, rt, id, n, seg, n_seg,
-                       hist, last_row, unmatched);
+    const bool in_lds = tb.n_chans <= LCH;
+    const size_t lds_count = in_lds ? (size_t)WAVES * tb.n_chans * 4 : 0;
+    const size_t lds_scatter = in_lds ? (size_t)WAVES * tb.n_chans * 16 : 0;
+    hipLaunchKernelGGL(nxg_disp_count_kernel, dim3(g), dim3(TPB), lds_count, s, tb, rt, id, n, seg,
+                       n_seg, hist, last_row, unmatched);
     if (M) {
         hipLaunchKernelGGL(nxg_disp_scan_block_kernel, dim3((uint32_t)nb), dim3(TPB), 0, s, hist, M,
                            off, bsum);
         hipLaunchKernelGGL(nxg_disp_scan_top_kernel, dim3(1), dim3(1024), 0, s, bsum, nb);
         hipLaunchKernelGGL(nxg_disp_scan_add_kernel, dim3((uint32_t)((M + TPB - 1) / TPB)),
                            dim3(TPB), 0, s, off, M, bsum, nb, n_seg, tb.n_chans, chan_off);
-        hipLaunchKernelGGL(nxg_disp_scatter_kernel, dim3(g), dim3(TPB), 0, s, tb, rt, id, n, seg,
-                           n_seg, off, ent_sub, ent_row, cap);
+        hipLaunchKernelGGL(nxg_disp_scatter_kernel, dim3(g), dim3(TPB), lds_scatter, s, tb, rt, id,
+                           n, seg, n_seg, off, ent_sub, ent_row, cap);
     }
     return hipGetLastError();
 }

@@ -33,8 +33,29 @@
 #ifndef NXG_ENC_EB
 #define NXG_ENC_EB 4  // array elements loaded together (sizing and writing flat arrays)
 #endif
+#ifndef NXG_ENC_TLS
+#define NXG_ENC_TLS 1  // each thread sizes its own rows from one batch of loads (then buckets)
+#endif
 #ifndef NXG_ENC_LBU
 #define NXG_ENC_LBU 1  // look-back window, 64 * NXG_ENC_LBU tiles per round trip (1, 4 and 8 measured equal)
+#endif
+
+#ifndef NXG_ENC_PROF
+#define NXG_ENC_PROF 0
+#endif
+#if NXG_ENC_PROF
+// diagnostic build only: per tile (the first 16384) s_memrealtime at the rows kernel's phase edges
+// (start, classified, sized, scanned, staged, look-back done, stored)
+__device__ unsigned long long nxg_enc_st[7][16384];
+#define ESTAMP(k)                                                                                \
+    do {                                                                                         \
+        if (threadIdx.x == 0 && tile < 16384)                                                    \
+            nxg_enc_st[k][tile] = __builtin_amdgcn_s_memrealtime();                              \
+    } while (0)
+#else
+#define ESTAMP(k) \
+    do {          \
+    } while (0)
 #endif
 
 namespace {
@@ -95,17 +116,6 @@ struct WalkStack {
     uint64_t rem[kStk];
     uint64_t slot[kStk];
 };
-// f() for each lane with `want`, one lane at a time (uniform loop; the others wait)
-template <typename F>
-NXG_DEV void one_lane_at_a_time(bool want, F&& f) {
-    uint64_t m = __ballot(want);
-#pragma unroll 1
-    while (m) {
-        const uint32_t j = (uint32_t)__builtin_ctzll(m);
-        m &= m - 1;
-        if (lane_id() == j) f();
-    }
-}
 
 // |Value| for the value in (row?, slot), children included; 0 => error (*err set)
 NXG_DEV uint64_t value_len(const ColsDesc& c, bool row, uint64_t slot, uint32_t* err,
@@ -424,9 +434,103 @@ __global__ __launch_bounds__(TPB, NXG_ENC_OCC) void nxg_enc_rows_kernel(
     for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const uint64_t rt = (uint64_t)tile * GTILE;
         const uint64_t r0 = rt + (uint64_t)tid * GRPT;
+        ESTAMP(0);
         // 1. classify by tag and bucket the rows (wave-ballot counting sort in LDS); a wave then
-        //    sizes and writes one class at a time
+        //    writes (and, without TLS, sizes) one class at a time
         if (tid < NCLS) cls_n[tid] = 0;
+#if NXG_ENC_TLS
+        // each thread sizes its own rows right away, from one batch of column loads (its rows'
+        // slots and ids in flight together): one memory round trip less than loading the tags
+        // first and sizing in class order (arrays load their elements; Map / Error / nested
+        // containers take the general walk, one lane of the wave at a time)
+        uint64_t Ltl[GRPT];
+        {
+            Slot v[GRPT];
+            uint64_t idv[GRPT];
+#pragma unroll
+            for (int k = 0; k < GRPT; k++) {
+                const uint64_t r = r0 + k;
+                v[k] = r < n ? get_slot(c, true, r) : Slot{NCLS, 0, 0};
+                idv[k] = r < n ? c.id[r] : 0ull;
+            }
+#pragma unroll
+            for (int k = 0; k < GRPT; k++) {
+                const uint64_t r = r0 + k;
+                uint64_t vlen = 0;
+                uint32_t err = 0;
+                bool gen = false;
+                const uint32_t cl = r >= n ? (uint32_t)NCLS
+                                           : (arch && v[k].tag == 0x40u ? (uint32_t)CLS_SCAL
+                                                                        : value_class(v[k].tag));
+                switch (cl) {
+                case CLS_FIX8: vlen = 9; break;
+                case CLS_TEXT: vlen = 1 + vl64(v[k].aux) + v[k].aux; break;
+                case CLS_TIME: vlen = 13; break;
+                case CLS_SCAL:
+                    vlen = arch && v[k].tag == 0x40u ? 1 : scalar_len(v[k]);
+                    gen = !vlen;  // a tag the encoder does not write (17): the walk reports it
+                    break;
+                case CLS_ARR: {
+                    bool flat;
+                    vlen = row_len_flat(c, r, flat);
+                    gen = !flat;
+                    break;
+                }
+                case NCLS: break;
+                default: gen = true; break;
+                }
+                one_lane_at_a_time(gen, [&] { vlen = value_len(c, true, r, &err, stk); });
+                const uint64_t ml = err    ? 0ull
+                                    : arch ? vl64((uint32_t)idv[k]) + vlen
+                                           : lwlen(1 + vl64(idv[k]) + vlen);
+                if (cl != NCLS && !err && ml > (arch ? 0xFFFFFFFFull : 0x3FFFFFFFull))
+                    err = NXG_TOO_BIG;
+                if (err) atomicMax(&st->err_kind, err);
+                Ltl[k] = (cl == NCLS || err) ? 0ull : ml;
+                v[k].tag = gen ? (uint32_t)CLS_GEN : cl;  // (the class, for the buckets below)
+            }
+#pragma unroll
+            for (int k = 0; k < GRPT; k++) idv[k] = v[k].tag;
+            __syncthreads();  // (cls_n cleared)
+            uint32_t cls[GRPT], pos[GRPT];
+#pragma unroll
+            for (int k = 0; k < GRPT; k++) {
+                cls[k] = (uint32_t)idv[k];
+                pos[k] = 0;
+#pragma unroll
+                for (uint32_t q = 0; q < NCLS; q++) {
+                    const uint64_t m = __ballot(cls[k] == q);
+                    if (!m) continue;
+                    const uint32_t lead = (uint32_t)__builtin_ctzll(m);
+                    uint32_t b0 = 0;
+                    if (lane == lead) b0 = atomicAdd(&cls_n[q], (uint32_t)__popcll(m));
+                    b0 = __shfl(b0, (int)lead);
+                    if (cls[k] == q) pos[k] = b0 + (uint32_t)__popcll(m & ((1ull << lane) - 1));
+                }
+            }
+            __syncthreads();
+            if (tid == 0) {
+                uint32_t acc = 0;
+                for (int q = 0; q < NCLS; q++) {
+                    cls_b[q] = acc;
+                    acc += cls_n[q];
+                }
+                cls_b[NCLS] = acc;
+            }
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < GRPT; k++) {
+                const uint32_t rl = tid * GRPT + k;
+                len_lds[rl] = (uint32_t)Ltl[k];
+                cls_lds[rl] = (uint8_t)cls[k];
+                if (cls[k] < NCLS) lst_row[cls_b[cls[k]] + pos[k]] = (uint16_t)rl;
+            }
+        }
+        __syncthreads();
+        ESTAMP(1);
+        ESTAMP(2);
+        const uint32_t ne = cls_b[NCLS];
+#else
         __syncthreads();
         uint32_t cls[GRPT], pos[GRPT];
 #pragma unroll
@@ -464,6 +568,7 @@ __global__ __launch_bounds__(TPB, NXG_ENC_OCC) void nxg_enc_rows_kernel(
             if (cls[k] < NCLS) lst_row[cls_b[cls[k]] + pos[k]] = (uint16_t)rl;
         }
         __syncthreads();
+        ESTAMP(1);
         const uint32_t ne = cls_b[NCLS];
         // 2. message lengths, class by class
         for (uint32_t e = tid; e < ne; e += TPB) {
@@ -507,6 +612,8 @@ __global__ __launch_bounds__(TPB, NXG_ENC_OCC) void nxg_enc_rows_kernel(
             len_lds[rl] = err ? 0u : (uint32_t)ml;
         }
         __syncthreads();
+        ESTAMP(2);
+#endif
         // 3. the tile's byte offsets: block scan, then look-back over the tiles' byte counts
         uint64_t L[GRPT];
         uint64_t mine = 0;
@@ -518,6 +625,7 @@ __global__ __launch_bounds__(TPB, NXG_ENC_OCC) void nxg_enc_rows_kernel(
         uint64_t tot;
         const uint64_t off = block_excl_scan<uint64_t, TPB>(mine, tmp, &tot);
         if (tid == 0) st_agent(&tstat[tile], lb_word(tile == 0 ? kFlagInc : kFlagAgg, epoch, tot));
+        ESTAMP(3);
         // 4a. without control messages: the rows into the staging at their tile-local offsets
         //     first, so that the look-back below finds its predecessors mostly done
         const bool stage = out && c.n_ctl == 0 && tot <= (uint64_t)(GSTG - 32);
@@ -574,6 +682,7 @@ __global__ __launch_bounds__(TPB, NXG_ENC_OCC) void nxg_enc_rows_kernel(
             }
         }
         // 3b. the tile's base: look-back over the tiles' byte counts
+        ESTAMP(4);
         if (tid < 64) {
             uint64_t base = 0;
             if (tile != 0) {
@@ -599,6 +708,7 @@ __global__ __launch_bounds__(TPB, NXG_ENC_OCC) void nxg_enc_rows_kernel(
             if (lane == 0) sh_base = base;
         }
         __syncthreads();
+        ESTAMP(5);
         const uint64_t tbase = sh_base + arch_base;
         if (stage && tbase + tot <= cap) {
             // 4b. the staging out as aligned nontemporal 16-byte stores: global block g holds the
@@ -675,6 +785,7 @@ __global__ __launch_bounds__(TPB, NXG_ENC_OCC) void nxg_enc_rows_kernel(
             st->total_bytes = sh_base + tot + arch_base;  // rows (+ archive header); ctl: host
             st->n_rows = n;
         }
+        ESTAMP(6);
         __syncthreads();
     }
 }
@@ -701,6 +812,14 @@ __global__ __launch_bounds__(TPB) void nxg_enc_ctl_write_kernel(
 }
 
 uint64_t nxg_enc_general_tiles(uint64_t n) { return (n + GTILE - 1) / GTILE; }
+
+#if NXG_ENC_PROF
+// diagnostic build only (not ABI): the stamps of the last general encode, 7 x 16384 u64
+extern "C" int nxg_debug_enc_stamps(unsigned long long* out) {
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(nxg_enc_st), sizeof(nxg_enc_st), 0,
+                                    hipMemcpyDeviceToHost);
+}
+#endif
 
 hipError_t nxg_launch_enc_general(const ColsDesc& cd, const uint8_t* heap, uint8_t* out,
                                   uint64_t cap, uint64_t* scratch, uint64_t* tstat,

@@ -9,8 +9,10 @@
 //                              array.rs:595-612, pack.rs:1225-1239, pbuf.rs:139-147,
 //                              pack.rs:457-469, 1567-1575, 1591-1595, 614-622,
 //                              abstract_type.rs:280-298
-// Values are walked iteratively; the top level and the first container level live in registers
-// and only deeper nesting uses an explicit stack. Children are allocated depth-first, the same
+// Values are walked iteratively; the top level and the first container level live in registers.
+// A value nested deeper than that is decoded again with an explicit stack that lives in LDS, one
+// per wave (DMode.stk, kStk levels), by one lane of the wave at a time: no lane keeps a private
+// stack, so no kernel needs scratch memory for it. Children are allocated depth-first, the same
 // order as the recursive reference decoder, which produces them as it goes.
 //
 // Byte sources. A message whose bytes all lie in the wave's LDS image is decoded from LDS with
@@ -40,6 +42,19 @@ struct DMode {
     uint32_t write;   // with EMIT: write the decoded values to the sink
 };
 constexpr DMode kSpec{kSpecBudget, 1, 0}, kBounded{kWalkBudget, 0, 0}, kExact{0xffffffffu, 0, 0};
+
+// The explicit stack of a value nested two or more levels deep: kStk levels of (values left,
+// next slot), in LDS, one per wave of the workgroup (a translation unit whose kernels run more
+// than NXG_DV_WAVES waves per workgroup defines it before including this header). Only kernels
+// that decode values allocate it.
+constexpr int kStk = NXG_MAX_DEPTH + 2;
+#ifndef NXG_DV_WAVES
+#define NXG_DV_WAVES 4
+#endif
+typedef __attribute__((address_space(3))) uint64_t* lds_stk;
+static __shared__ uint64_t nxg_dv_stk[NXG_DV_WAVES * 2 * kStk];
+NXG_DEV lds_stk dv_stack() { return (lds_stk)(nxg_dv_stk + (threadIdx.x >> 6) * 2 * kStk); }
+constexpr uint32_t E_DEEP = 101;  // (internal) the value needs the stack
 
 typedef const __attribute__((address_space(3))) uint8_t* lds_bytes;
 typedef const __attribute__((address_space(3))) uint32_t* lds_words;
@@ -410,11 +425,13 @@ NXG_DEV uint32_t dcontainer(const S& s, uint32_t t, uint64_t& p, uint64_t lim, c
 // depth-first, the order in which the recursive reference decoder produces them. One leaf
 // decoder serves every level. The top level and the first container level live in registers;
 // only values nested two or more levels deep touch the stack arrays (scratch memory).
-template <bool EMIT, class S>
-NXG_DEV uint32_t dvalue(const S& s, uint64_t& p, uint64_t lim, const Sink* k, bool row,
-                        uint64_t slot, uint64_t& child_next, uint32_t& work, const DMode& md) {
-    uint64_t frem[NXG_MAX_DEPTH + 2];  // levels >= 2: values left, next slot
-    uint64_t fslot[NXG_MAX_DEPTH + 2];
+// STK false: a value that needs level 2 returns E_DEEP (dvalue then decodes it again with STK).
+template <bool EMIT, bool STK, class S>
+NXG_DEV uint32_t dvalue_impl(const S& s, uint64_t& p, uint64_t lim, const Sink* k, bool row,
+                             uint64_t slot, uint64_t& child_next, uint32_t& work,
+                             const DMode& md) {
+    const lds_stk frem = STK ? dv_stack() : nullptr;  // levels >= 2: values left,
+    const lds_stk fslot = frem + kStk;                 // next slot
     int top = -1;
     uint64_t left = 1, cur = slot;     // current level
     uint64_t sv_left = 0, sv_cur = 0;  // level 0 while level 1 is decoded
@@ -451,6 +468,7 @@ NXG_DEV uint32_t dvalue(const S& s, uint64_t& p, uint64_t lim, const Sink* k, bo
                     sv_left = left;
                     sv_cur = cur;
                 } else {
+                    if (!STK) return E_DEEP;
                     ++top;
                     frem[top] = left;
                     fslot[top] = cur;
@@ -467,6 +485,23 @@ NXG_DEV uint32_t dvalue(const S& s, uint64_t& p, uint64_t lim, const Sink* k, bo
         cur++;
         is_row = false;
     }
+}
+
+// Decode one Value (see dvalue_impl): in registers when it nests at most one level, else again
+// with the wave's LDS stack, one lane at a time (any lanes of the wave may be inactive here).
+template <bool EMIT, class S>
+NXG_DEV uint32_t dvalue(const S& s, uint64_t& p, uint64_t lim, const Sink* k, bool row,
+                        uint64_t slot, uint64_t& child_next, uint32_t& work, const DMode& md) {
+    const uint64_t p_in = p, cn_in = child_next;
+    const uint32_t w_in = work;
+    uint32_t e = dvalue_impl<EMIT, false>(s, p, lim, k, row, slot, child_next, work, md);
+    one_lane_at_a_time(e == E_DEEP, [&] {
+        p = p_in;
+        child_next = cn_in;
+        work = w_in;
+        e = dvalue_impl<EMIT, true>(s, p, lim, k, row, slot, child_next, work, md);
+    });
+    return e;
 }
 
 struct MsgInfo {
