@@ -378,32 +378,38 @@ NXG_DEV FaDesc count_tile(lds_bytes img, uint64_t t, uint64_t W, uint32_t E, uin
                                : c;
     uint32_t ge = 0;
     if (E == NONE) {
-        // the walk over the two 64-byte halves before the tile: lanes 0 and 1 walk one half each
-        // at the same time; when the first half's exit is an item of the second half's last
-        // unbroken run, the exact walk from there is that run, so the guess is that walk's exit
-        // (else lane 0 walks on from the first half's exit)
-        static_assert(PRE == 2 * CH, "two halves before the tile");
-        uint32_t f2 = 0, k2 = 0;
-        uint64_t b2 = 0;
-        if (lane < 2) {
+        // the walk over the PRE / 64 chunks before the tile: lane q walks chunk q, all at once;
+        // then from the first chunk's exit on: an exit that is an item of the next chunk's last
+        // unbroken run continues as that run (the exact walk from there is that run), anything
+        // else is walked on by lane 0 (rare: the walks merge within an item or two)
+        constexpr uint32_t NQ = PRE / CH;
+        static_assert(PRE % CH == 0 && NQ >= 1 && NQ <= 8, "whole chunks before the tile");
+        uint32_t fq = 0, kq = 0;
+        uint64_t bq = 0;
+        if (lane < NQ) {
             const uint32_t cb = lane * CH;
-            ge = spec_walk(img, cb, cb, cb + CH, wl, f2, item_cands((lds_bytes)img, cb), b2, k2);
+            ge = spec_walk(img, cb, cb, cb + CH, wl, fq, item_cands((lds_bytes)img, cb), bq, kq);
         }
-        const uint32_t ge1 = (uint32_t)__builtin_amdgcn_readlane((int)ge, 0);
-        const uint32_t ge2 = (uint32_t)__builtin_amdgcn_readlane((int)ge, 1);
-        const uint32_t fr2 = (uint32_t)__builtin_amdgcn_readlane((int)f2, 1);
-        const uint64_t rb2 =
-            (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b2, 1) |
-            ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b2 >> 32), 1) << 32);
-        if (ge1 >= PRE) {
-            E = ge1;  // an item covers the second half
-        } else if (ge1 >= fr2 && ((rb2 >> (ge1 - CH)) & 1ull)) {
-            E = ge2;
-        } else {
-            if (lane == 0)
-                ge = spec_walk(img, ge1, CH, PRE, wl, f2, item_cands((lds_bytes)img, CH), b2, k2);
-            E = (uint32_t)__builtin_amdgcn_readlane((int)ge, 0);
+        uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)ge, 0);
+#pragma unroll 1
+        for (uint32_t q = 1; q < NQ; q++) {
+            const uint32_t cq = q * CH;
+            if (x >= cq + CH) continue;  // an item covers chunk q
+            const uint32_t fr = (uint32_t)__builtin_amdgcn_readlane((int)fq, (int)q);
+            const uint64_t rb =
+                (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)bq, (int)q) |
+                ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(bq >> 32), (int)q)
+                 << 32);
+            if (x >= fr && ((rb >> (x - cq)) & 1ull)) {
+                x = (uint32_t)__builtin_amdgcn_readlane((int)ge, (int)q);
+                continue;
+            }
+            uint32_t f2 = 0, k2 = 0, g2 = 0;
+            uint64_t b2 = 0;
+            if (lane == 0) g2 = spec_walk(img, x, cq, cq + CH, wl, f2, item_cands((lds_bytes)img, cq), b2, k2);
+            x = (uint32_t)__builtin_amdgcn_readlane((int)g2, 0);
         }
+        E = x;
     } else {
         E += PRE;
     }
@@ -519,65 +525,6 @@ __global__ __launch_bounds__(TPB) void nxg_fa_fix_kernel(const uint8_t* __restri
     const FaDesc d = count_tile((lds_bytes)img, t, W, px - TILE, lane, bits);
     starts[t * 64 + lane] = bits;
     if (lane == 0) td[t] = d;
-}
-
-#ifndef NXG_FA_FIXLIST
-#define NXG_FA_FIXLIST 1
-#endif
-// fix as two launches: a lane per tile lists the tiles entered elsewhere than their predecessor's
-// counted exit (wave-aggregated appends), then a persistent grid of waves takes the listed tiles by
-// ticket and recounts each from its predecessor's exit. The per-tile fix kernel launches a wave for
-// every tile of the batch (46,598 at 10^7 items) to recount about 2 % of them.
-// (A wave recounting its 64 tiles in order measured slower, 243 vs 112 us: the recounts of the
-// busiest wave set the pass.)
-__global__ __launch_bounds__(TPB) void nxg_fa_fixlist_kernel(uint64_t nt,
-                                                             const FaDesc* __restrict__ td,
-                                                             uint32_t* __restrict__ list,
-                                                             uint32_t* __restrict__ cnt) {
-    const uint64_t t = (uint64_t)blockIdx.x * TPB + threadIdx.x;
-    bool mis = false;
-    if (t >= 1 && t < nt) {
-        const FaDesc p = td[t - 1];
-        const uint32_t e = td[t].entry;
-        mis = !(p.exit == FAIL || (p.items & BROKEN) || p.exit - TILE == e || p.exit - TILE >= TILE);
-    }
-    const uint64_t m = __ballot(mis);
-    if (!m) return;
-    const uint32_t lane = threadIdx.x & 63, lead = (uint32_t)__builtin_ctzll(m);
-    uint32_t b0 = 0;
-    if (lane == lead) b0 = atomicAdd(cnt, (uint32_t)__popcll(m));
-    b0 = __shfl(b0, (int)lead);
-    if (mis) list[b0 + __popcll(m & ((1ull << lane) - 1))] = (uint32_t)t;
-}
-__global__ __launch_bounds__(TPB) void nxg_fa_fixrun_kernel(const uint8_t* __restrict__ buf,
-                                                            uint64_t W, FaDesc* __restrict__ td,
-                                                            uint64_t* __restrict__ starts,
-                                                            const uint32_t* __restrict__ list,
-                                                            const uint32_t* __restrict__ cnt,
-                                                            uint32_t* __restrict__ ticket) {
-    __shared__ __attribute__((aligned(16))) FaCountLds lds[TPB / 64];
-    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    uint8_t* img = lds[w].img;
-    const uint32_t n = __builtin_amdgcn_readfirstlane(*cnt);
-#pragma unroll 1
-    for (;;) {
-        uint32_t j = 0;
-        if (lane == 0) j = atomicAdd(ticket, 1u);
-        j = __builtin_amdgcn_readfirstlane(j);
-        if (j >= n) break;  // every wave ends once the list is taken
-        const uint64_t t = list[j];
-        const uint32_t px = __builtin_amdgcn_readfirstlane(td[t - 1].exit);
-        const uint32_t pi = __builtin_amdgcn_readfirstlane(td[t - 1].items);
-        const uint32_t e = __builtin_amdgcn_readfirstlane(td[t].entry);
-        if (px == FAIL || (pi & BROKEN) || px - TILE == e || px - TILE >= TILE) continue;
-        CountRegs g;
-        count_load(g, buf, t * TILE, W, lane);
-        count_store(img, g, lane);
-        uint64_t bits;
-        const FaDesc d = count_tile((lds_bytes)img, t, W, px - TILE, lane, bits);
-        starts[t * 64 + lane] = bits;
-        if (lane == 0) td[t] = d;
-    }
 }
 
 // resolve: a lane per tile. A tile whose entry is not its (unbroken) predecessor's exit is
@@ -842,9 +789,9 @@ __global__ __launch_bounds__(TPB) void nxg_fa_emit_kernel(
 // ---- launch (host) --------------------------------------------------------------------------------
 uint64_t nxg_fa_scratch_bytes(uint64_t W) {
     const uint64_t nt = (W + TILE - 1) / TILE;
-    // head 64 B; 2 descs 32 B, starts 512 B, tloc 8 B, fix list 4 B per tile; bsum + bpre 16 B
-    // per 256 tiles; one exit word per 64 tiles; the fix passes' counters 64 B
-    return 64 + nt * 556 + 16 * (nt / TPB + 1) + 8 * (nt / 64 + 1) + 64 + 9 * 16;
+    // head 64 B; 2 descs 32 B, starts 512 B, tloc 8 B per tile; bsum + bpre 16 B per 256
+    // tiles; one exit word per 64 tiles
+    return 64 + nt * 552 + 16 * (nt / TPB + 1) + 8 * (nt / 64 + 1) + 7 * 16;
 }
 
 // One pass of the fast path over buf[0, W) (W < 2^32; the batch's count and its varint's length
@@ -871,27 +818,15 @@ hipError_t nxg_launch_dec_fa(const uint8_t* buf, uint64_t W, uint32_t p0, uint64
     uint64_t* bpre = reinterpret_cast<uint64_t*>(take(8 * nb));
     const uint64_t nwv = (nt + 63) / 64;
     uint64_t* wexit = reinterpret_cast<uint64_t*>(take(8 * nwv));
-    uint32_t* fixl = reinterpret_cast<uint32_t*>(take(4 * nt));  // the fix passes' tile list
-    uint32_t* fixw = reinterpret_cast<uint32_t*>(take(64));      // its counts and tickets
     hipError_t e;
     if ((e = hipMemsetAsync(hp, 0, sizeof(FaHead), s)) != hipSuccess) return e;
-    if ((e = hipMemsetAsync(fixw, 0, 64, s)) != hipSuccess) return e;
-    const uint64_t fix_grid = std::min<uint64_t>((nt + 3) / 4, 1024);
     if ((e = hipMemsetAsync(wexit, 0, 8 * nwv, s)) != hipSuccess) return e;
     constexpr uint64_t WV = TPB / 64;
     const uint32_t gc = (uint32_t)((nt + WV - 1) / WV);
     hipLaunchKernelGGL(nxg_fa_count_kernel, dim3(gc), dim3(TPB), 0, s, buf, W, nt, p0, td, starts);
     // (a second pass would catch the tiles whose predecessor the first one recounted)
     for (int k = 0; k < NXG_FA_FIX_PASSES; k++) {
-        if (NXG_FA_FIXLIST) {
-            uint32_t* c = fixw + 2 * k;  // [count, ticket] of this pass
-            hipLaunchKernelGGL(nxg_fa_fixlist_kernel, dim3((uint32_t)((nt + TPB - 1) / TPB)),
-                               dim3(TPB), 0, s, nt, td, fixl, c);
-            hipLaunchKernelGGL(nxg_fa_fixrun_kernel, dim3((uint32_t)fix_grid), dim3(TPB), 0, s, buf,
-                               W, td, starts, fixl, c, c + 1);
-        } else {
-            hipLaunchKernelGGL(nxg_fa_fix_kernel, dim3(gc), dim3(TPB), 0, s, buf, W, nt, td, starts);
-        }
+        hipLaunchKernelGGL(nxg_fa_fix_kernel, dim3(gc), dim3(TPB), 0, s, buf, W, nt, td, starts);
     }
     hipLaunchKernelGGL(nxg_fa_resolve_kernel, dim3((uint32_t)nb), dim3(TPB), 0, s, buf, W, nt, td,
                        td2, starts, tloc, bsum, bpre, wexit, hp);

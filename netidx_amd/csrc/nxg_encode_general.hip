@@ -33,9 +33,6 @@
 #ifndef NXG_ENC_EB
 #define NXG_ENC_EB 4  // array elements loaded together (sizing and writing flat arrays)
 #endif
-#ifndef NXG_ENC_TLS
-#define NXG_ENC_TLS 1  // each thread sizes its own rows from one batch of loads (then buckets)
-#endif
 #ifndef NXG_ENC_LBU
 #define NXG_ENC_LBU 1  // look-back window, 64 * NXG_ENC_LBU tiles per round trip (1, 4 and 8 measured equal)
 #endif
@@ -177,6 +174,7 @@ NXG_DEV uint64_t value_len(const ColsDesc& c, bool row, uint64_t slot, uint32_t*
 struct Out {
     uint8_t* o;
     uint64_t p;
+    NXG_DEV void done() {}
     NXG_DEV void b(uint32_t x) { o[p++] = (uint8_t)x; }
     NXG_DEV void be(uint64_t v, int n) {
         for (int i = n - 1; i >= 0; i--) o[p++] = (uint8_t)(v >> (8 * i));
@@ -215,7 +213,84 @@ struct Out {
     }
 };
 
-NXG_DEV void value_write(const ColsDesc& c, const uint8_t* heap, bool row, uint64_t slot, Out& w,
+#ifndef NXG_ENC_OR
+#define NXG_ENC_OR 0
+#endif
+// The staging writer of the rows kernel (NXG_ENC_OR): bytes gather in a 64-bit register and go
+// to LDS as aligned dwords by ds_or (the staging is zeroed first), two dwords per 8 bytes, instead
+// of one ds_write_b8 per byte; neighbouring rows share edge dwords, which the OR merges.
+struct OrOut {
+    uint32_t* o;    // the staging as dwords
+    uint32_t q;     // the dword that acc's byte 0 goes to
+    uint32_t fill;  // bytes held in acc (its first p & 3 are the previous row's: zero)
+    uint64_t acc;
+    NXG_DEV OrOut(uint8_t* stg, uint32_t p)
+        : o(reinterpret_cast<uint32_t*>(stg)), q(p >> 2), fill(p & 3u), acc(0) {}
+    NXG_DEV void put(uint64_t v, uint32_t n) {  // v's low n bytes (1..8, the rest zero), in order
+        const uint32_t sh = 8 * fill;
+        acc |= v << sh;
+        const uint64_t carry = sh ? v >> (64 - sh) : 0ull;
+        fill += n;
+        if (fill >= 8) {
+            atomicOr(&o[q], (uint32_t)acc);
+            atomicOr(&o[q + 1], (uint32_t)(acc >> 32));
+            q += 2;
+            acc = carry;
+            fill -= 8;
+        }
+    }
+    NXG_DEV void done() {
+        if (fill) atomicOr(&o[q], (uint32_t)acc);
+        if (fill > 4) atomicOr(&o[q + 1], (uint32_t)(acc >> 32));
+    }
+    NXG_DEV void b(uint32_t x) { put(x & 0xffu, 1); }
+    NXG_DEV void be(uint64_t v, int n) {  // n <= 8
+        put(__builtin_bswap64(v) >> (64 - 8 * n), (uint32_t)n);
+    }
+    NXG_DEV void var(uint64_t v) {
+        if (v < (1ull << 28)) {  // ids and lengths: 1..4 bytes in 32-bit arithmetic
+            const uint32_t u = (uint32_t)v;
+            const uint32_t nb = u < 0x80u ? 1u : u < 0x4000u ? 2u : u < 0x200000u ? 3u : 4u;
+            uint32_t x = (u & 0x7fu) | ((u << 1) & 0x7f00u) | ((u << 2) & 0x7f0000u) |
+                         ((u << 3) & 0x7f000000u);
+            x |= 0x80808080u & ((1u << (8 * (nb - 1))) - 1u);
+            put(x, nb);
+            return;
+        }
+        while (v >= 0x80) {
+            put((v & 0x7f) | 0x80, 1);
+            v >>= 7;
+        }
+        put(v, 1);
+    }
+    NXG_DEV void copy(const uint8_t* src, uint64_t n) {
+        constexpr int NW = 12;  // as Out::copy: the covering dwords of up to 44 bytes, realigned
+        if (n <= 4 * NW - 4) {
+            const uint32_t sh = (uint32_t)((uintptr_t)src & 3u);
+            const uint32_t* w = reinterpret_cast<const uint32_t*>((uintptr_t)src & ~(uintptr_t)3);
+            const uint32_t nw = (uint32_t)((sh + n + 3) >> 2);
+            uint32_t d[NW + 1];
+#pragma unroll
+            for (int i = 0; i < NW; i++) d[i] = (uint32_t)i < nw ? w[i] : 0u;
+            d[NW] = 0u;
+#pragma unroll
+            for (int i = 0; i < (NW - 1) / 2 + 1; i++) {
+                if ((uint64_t)(8 * i) < n) {
+                    const uint32_t lo = __builtin_amdgcn_alignbyte(d[2 * i + 1], d[2 * i], sh);
+                    const uint32_t hi = 2 * i + 2 <= NW ? __builtin_amdgcn_alignbyte(d[2 * i + 2], d[2 * i + 1], sh) : 0u;
+                    const uint32_t k = (uint32_t)min<uint64_t>(8, n - 8 * i);
+                    const uint64_t v = ((uint64_t)hi << 32) | lo;
+                    put(k == 8 ? v : v & ((1ull << (8 * k)) - 1ull), k);
+                }
+            }
+            return;
+        }
+        for (uint64_t i = 0; i < n; i++) put(src[i], 1);
+    }
+};
+
+template <typename W>
+NXG_DEV void value_write(const ColsDesc& c, const uint8_t* heap, bool row, uint64_t slot, W& w,
                          WalkStack* stk) {
     uint64_t* frem = stk->rem;
     uint64_t* fslot = stk->slot;
@@ -260,7 +335,8 @@ NXG_DEV void value_write(const ColsDesc& c, const uint8_t* heap, bool row, uint6
 }
 
 // Writes a non-container value (tag byte included).
-NXG_DEV void scalar_write(const Slot& s, const uint8_t* heap, Out& w) {
+template <typename W>
+NXG_DEV void scalar_write(const Slot& s, const uint8_t* heap, W& w) {
     w.b(s.tag);
     switch (s.tag) {
     case 0: case 2: case 8: w.be(s.fixed, 4); break;
@@ -318,7 +394,8 @@ NXG_DEV uint64_t row_len_flat(const ColsDesc& c, uint64_t r, bool& flat) {
     }
     return total;
 }
-NXG_DEV void row_write_flat(const ColsDesc& c, const uint8_t* heap, uint64_t r, Out& w) {
+template <typename W>
+NXG_DEV void row_write_flat(const ColsDesc& c, const uint8_t* heap, uint64_t r, W& w) {
     const Slot s = get_slot(c, true, r);
     if (s.tag != 19) {
         scalar_write(s, heap, w);
@@ -436,101 +513,8 @@ __global__ __launch_bounds__(TPB, NXG_ENC_OCC) void nxg_enc_rows_kernel(
         const uint64_t r0 = rt + (uint64_t)tid * GRPT;
         ESTAMP(0);
         // 1. classify by tag and bucket the rows (wave-ballot counting sort in LDS); a wave then
-        //    writes (and, without TLS, sizes) one class at a time
+        //    writes and sizes one class at a time
         if (tid < NCLS) cls_n[tid] = 0;
-#if NXG_ENC_TLS
-        // each thread sizes its own rows right away, from one batch of column loads (its rows'
-        // slots and ids in flight together): one memory round trip less than loading the tags
-        // first and sizing in class order (arrays load their elements; Map / Error / nested
-        // containers take the general walk, one lane of the wave at a time)
-        uint64_t Ltl[GRPT];
-        {
-            Slot v[GRPT];
-            uint64_t idv[GRPT];
-#pragma unroll
-            for (int k = 0; k < GRPT; k++) {
-                const uint64_t r = r0 + k;
-                v[k] = r < n ? get_slot(c, true, r) : Slot{NCLS, 0, 0};
-                idv[k] = r < n ? c.id[r] : 0ull;
-            }
-#pragma unroll
-            for (int k = 0; k < GRPT; k++) {
-                const uint64_t r = r0 + k;
-                uint64_t vlen = 0;
-                uint32_t err = 0;
-                bool gen = false;
-                const uint32_t cl = r >= n ? (uint32_t)NCLS
-                                           : (arch && v[k].tag == 0x40u ? (uint32_t)CLS_SCAL
-                                                                        : value_class(v[k].tag));
-                switch (cl) {
-                case CLS_FIX8: vlen = 9; break;
-                case CLS_TEXT: vlen = 1 + vl64(v[k].aux) + v[k].aux; break;
-                case CLS_TIME: vlen = 13; break;
-                case CLS_SCAL:
-                    vlen = arch && v[k].tag == 0x40u ? 1 : scalar_len(v[k]);
-                    gen = !vlen;  // a tag the encoder does not write (17): the walk reports it
-                    break;
-                case CLS_ARR: {
-                    bool flat;
-                    vlen = row_len_flat(c, r, flat);
-                    gen = !flat;
-                    break;
-                }
-                case NCLS: break;
-                default: gen = true; break;
-                }
-                one_lane_at_a_time(gen, [&] { vlen = value_len(c, true, r, &err, stk); });
-                const uint64_t ml = err    ? 0ull
-                                    : arch ? vl64((uint32_t)idv[k]) + vlen
-                                           : lwlen(1 + vl64(idv[k]) + vlen);
-                if (cl != NCLS && !err && ml > (arch ? 0xFFFFFFFFull : 0x3FFFFFFFull))
-                    err = NXG_TOO_BIG;
-                if (err) atomicMax(&st->err_kind, err);
-                Ltl[k] = (cl == NCLS || err) ? 0ull : ml;
-                v[k].tag = gen ? (uint32_t)CLS_GEN : cl;  // (the class, for the buckets below)
-            }
-#pragma unroll
-            for (int k = 0; k < GRPT; k++) idv[k] = v[k].tag;
-            __syncthreads();  // (cls_n cleared)
-            uint32_t cls[GRPT], pos[GRPT];
-#pragma unroll
-            for (int k = 0; k < GRPT; k++) {
-                cls[k] = (uint32_t)idv[k];
-                pos[k] = 0;
-#pragma unroll
-                for (uint32_t q = 0; q < NCLS; q++) {
-                    const uint64_t m = __ballot(cls[k] == q);
-                    if (!m) continue;
-                    const uint32_t lead = (uint32_t)__builtin_ctzll(m);
-                    uint32_t b0 = 0;
-                    if (lane == lead) b0 = atomicAdd(&cls_n[q], (uint32_t)__popcll(m));
-                    b0 = __shfl(b0, (int)lead);
-                    if (cls[k] == q) pos[k] = b0 + (uint32_t)__popcll(m & ((1ull << lane) - 1));
-                }
-            }
-            __syncthreads();
-            if (tid == 0) {
-                uint32_t acc = 0;
-                for (int q = 0; q < NCLS; q++) {
-                    cls_b[q] = acc;
-                    acc += cls_n[q];
-                }
-                cls_b[NCLS] = acc;
-            }
-            __syncthreads();
-#pragma unroll
-            for (int k = 0; k < GRPT; k++) {
-                const uint32_t rl = tid * GRPT + k;
-                len_lds[rl] = (uint32_t)Ltl[k];
-                cls_lds[rl] = (uint8_t)cls[k];
-                if (cls[k] < NCLS) lst_row[cls_b[cls[k]] + pos[k]] = (uint16_t)rl;
-            }
-        }
-        __syncthreads();
-        ESTAMP(1);
-        ESTAMP(2);
-        const uint32_t ne = cls_b[NCLS];
-#else
         __syncthreads();
         uint32_t cls[GRPT], pos[GRPT];
 #pragma unroll
@@ -613,7 +597,6 @@ __global__ __launch_bounds__(TPB, NXG_ENC_OCC) void nxg_enc_rows_kernel(
         }
         __syncthreads();
         ESTAMP(2);
-#endif
         // 3. the tile's byte offsets: block scan, then look-back over the tiles' byte counts
         uint64_t L[GRPT];
         uint64_t mine = 0;
@@ -638,13 +621,22 @@ __global__ __launch_bounds__(TPB, NXG_ENC_OCC) void nxg_enc_rows_kernel(
                     o += (uint32_t)L[k];
                 }
             }
+            if (NXG_ENC_OR) {  // the OR writer needs a zeroed staging
+                typedef uint32_t z4 __attribute__((ext_vector_type(4)));
+                for (uint32_t b = tid; b < (uint32_t)((tot + 31) >> 4); b += TPB)
+                    reinterpret_cast<z4*>(stg)[b] = z4{0u, 0u, 0u, 0u};
+            }
             __syncthreads();
             for (uint32_t e = tid; e < ne; e += TPB) {
                 const uint32_t rl = lst_row[e];
                 const uint32_t len = len_lds[rl];
                 if (!len) continue;
                 const uint64_t r = rt + rl;
+#if NXG_ENC_OR
+                OrOut w(stg, off_lds[rl]);
+#else
                 Out w{stg, off_lds[rl]};
+#endif
                 if (arch) {
                     w.var((uint32_t)c.id[r]);
                 } else {
@@ -679,6 +671,7 @@ __global__ __launch_bounds__(TPB, NXG_ENC_OCC) void nxg_enc_rows_kernel(
                 }
                 one_lane_at_a_time(cls_lds[rl] == CLS_GEN,
                                    [&] { value_write(c, heap, true, r, w, stk); });
+                w.done();
             }
         }
         // 3b. the tile's base: look-back over the tiles' byte counts
@@ -753,7 +746,7 @@ __global__ __launch_bounds__(TPB, NXG_ENC_OCC) void nxg_enc_rows_kernel(
             // control messages interleaved, or more bytes than the staging: straight to the
             // frame, each thread its own rows
             uint64_t rpos = tbase + off;  // rows-only prefix
-#pragma unroll
+#pragma unroll 1  // (a large body with a lane-serial walk: not worth unrolling)
             for (int k = 0; k < GRPT; k++) {
                 const uint64_t r = r0 + k;
                 const uint64_t Lk = len_lds[tid * GRPT + k];

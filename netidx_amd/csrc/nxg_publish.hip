@@ -157,17 +157,33 @@ NXG_DEV int node_eq(const VSrc& A, uint32_t ta, uint64_t fa, uint32_t aa, const 
 }
 
 // Value::eq with containers: 1 equal, 0 different, -1 nested deeper than MAX_DEPTH (or no
-// child columns)
-__attribute__((noinline)) NXG_DEV int deep_eq(const VSrc& A, uint64_t ia, const VSrc& B,
-                                              uint64_t ib) {
-    uint64_t sa[MAX_DEPTH + 1], sb[MAX_DEPTH + 1], sn[MAX_DEPTH + 1];  // pending child ranges
-    int sp = 0;
+// child columns). Without a stack (stk null) only one level of children is walked, and a child
+// container gives DEEP_MORE; with one, stk holds 3 * (MAX_DEPTH + 1) words of pending child
+// ranges (a per-wave LDS stack: the callers take turns, one_lane_at_a_time).
+constexpr int DEEP_MORE = 3;
+NXG_DEV int deep_eq(const VSrc& A, uint64_t ia, const VSrc& B, uint64_t ib, uint64_t* stk) {
     uint32_t ta, aa, tb, ab;
     uint64_t fa, fb, n = 0;
     slot_at(A, false, ia, ta, fa, aa);
     slot_at(B, false, ib, tb, fb, ab);
     int r = node_eq(A, ta, fa, aa, B, tb, fb, ab, n);
     if (r < 2) return r;
+    if (!stk) {  // the common case: a flat container, walked in registers
+        const uint64_t a0 = fa, b0 = fb;
+        for (uint64_t k = 0; k < n; k++) {
+            uint64_t m;
+            slot_at(A, true, a0 + k, ta, fa, aa);
+            slot_at(B, true, b0 + k, tb, fb, ab);
+            r = node_eq(A, ta, fa, aa, B, tb, fb, ab, m);
+            if (r <= 0) return r;
+            if (r == 2) return DEEP_MORE;
+        }
+        return 1;
+    }
+    uint64_t* sa = stk;
+    uint64_t* sb = stk + (MAX_DEPTH + 1);
+    uint64_t* sn = stk + 2 * (MAX_DEPTH + 1);
+    int sp = 0;
     sa[0] = fa, sb[0] = fb, sn[0] = n, sp = 1;
     while (sp > 0) {
         const int k = sp - 1;
@@ -185,14 +201,6 @@ __attribute__((noinline)) NXG_DEV int deep_eq(const VSrc& A, uint64_t ia, const 
         if (r == 2) sa[sp] = fa, sb[sp] = fb, sn[sp] = n, sp++;
     }
     return 1;
-}
-
-// Value::eq of top-level slot ia of A and ib of B: scalars inline, the rest by deep_eq
-NXG_DEV int val_eq(const VSrc& A, uint64_t ia, const VSrc& B, uint64_t ib) {
-    const uint32_t ta = A.tag ? A.tag[ia] : 9u, tb = B.tag ? B.tag[ib] : 9u;
-    if (heavy(ta) || heavy(tb)) return deep_eq(A, ia, B, ib);
-    return scalar_eq(ta, A.fixed[ia], A.aux ? A.aux[ia] : 0u, A.heap, tb, B.fixed[ib],
-                     B.aux ? B.aux[ib] : 0u, B.heap);
 }
 
 struct PubIn {
@@ -325,7 +333,12 @@ NXG_DEV int changed_eq(const NxgPubTable& tb, const PubIn& in, const uint32_t* p
     const uint32_t ta = A.tag ? A.tag[ia] : 9u, tb_ = in.v.tag ? in.v.tag[i] : 9u;
     if (heavy(ta) || heavy(tb_)) {
         if (!ALLOW_DEEP) return DEEP;
-        return deep_eq(A, ia, in.v, i);
+        // one level in registers; a nested container retries with the wave's LDS stack
+        __shared__ uint64_t stks[WAVES][3 * (MAX_DEPTH + 1)];
+        int r = deep_eq(A, ia, in.v, i, nullptr);
+        one_lane_at_a_time(r == DEEP_MORE,
+                           [&] { r = deep_eq(A, ia, in.v, i, stks[threadIdx.x >> 6]); });
+        return r;
     }
     return scalar_eq(ta, A.fixed[ia], A.aux ? A.aux[ia] : 0u, A.heap, tb_, in.v.fixed[i],
                      in.v.aux ? in.v.aux[i] : 0u, in.v.heap);

@@ -514,7 +514,7 @@ NXG_DEV uint32_t block_compressed(ZLds& L, Frame& f, const uint8_t* ip, uint32_t
                 f.rep[1] = f.rep[0];
                 f.rep[0] = (uint32_t)off;
             } else {
-                off = f.rep[idx];
+                off = idx == 1 ? f.rep[1] : f.rep[2];  // (no dynamic index: registers)
                 if (idx == 2) f.rep[2] = f.rep[1];
                 f.rep[1] = f.rep[0];
                 f.rep[0] = (uint32_t)off;
