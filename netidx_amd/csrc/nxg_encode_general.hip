@@ -33,6 +33,12 @@
 #ifndef NXG_ENC_EB
 #define NXG_ENC_EB 4  // array elements loaded together (sizing and writing flat arrays)
 #endif
+#ifndef NXG_ENC_PF
+#define NXG_ENC_PF 1  // the sizing and staging loops load their next entry's columns ahead
+#endif
+#ifndef NXG_ENC_CLS2
+#define NXG_ENC_CLS2 1  // class buckets from per-wave ballot counts (no LDS atomics)
+#endif
 #ifndef NXG_ENC_LBU
 #define NXG_ENC_LBU 1  // look-back window, 64 * NXG_ENC_LBU tiles per round trip (1, 4 and 8 measured equal)
 #endif
@@ -105,6 +111,28 @@ NXG_DEV uint64_t scalar_len(const Slot& s) {
     }
 }
 
+#ifndef NXG_ENC_AFAST
+#define NXG_ENC_AFAST 1  // arrays of 1..8 fixed-size elements sized from one load of their tags (the write path's version: 170 VGPRs)
+#endif
+// |Value| of a value of fixed size by its tag (tag byte included; Decimal 17), 0 for the others:
+// nibble tables, tag 20's 15 standing for 17
+NXG_DEV uint32_t fixed_len(uint32_t t) {
+    if (t < 16) return (uint32_t)(0x1100dd9509090505ull >> (4 * t)) & 15u;
+    const uint32_t v = t < 28 ? (uint32_t)(0x332200f0001ull >> (4 * (t - 16))) & 15u : 0u;
+    return v == 15u ? 17u : v;
+}
+// the tags of an array's 1..8 elements, ctag[p .. p + n), from the covering aligned dwords (a
+// dword-aligned read never leaves the page of the bytes it covers); bytes past n zero
+NXG_DEV uint64_t tags8(const uint8_t* p, uint32_t n) {
+    const uint32_t sh = (uint32_t)((uintptr_t)p & 3u);
+    const uint32_t* w = reinterpret_cast<const uint32_t*>((uintptr_t)p & ~(uintptr_t)3);
+    const uint32_t nw = (sh + n + 3) >> 2;
+    const uint32_t w0 = w[0], w1 = nw > 1 ? w[1] : 0u, w2 = nw > 2 ? w[2] : 0u;
+    const uint64_t v = (uint64_t)__builtin_amdgcn_alignbyte(w1, w0, sh) |
+                       ((uint64_t)__builtin_amdgcn_alignbyte(w2, w1, sh) << 32);
+    return n >= 8 ? v : v & ((1ull << (8 * n)) - 1ull);
+}
+
 // The general walk's stack: kStk levels of (children left, next child slot), in LDS, one stack
 // per wave (the walk runs one lane at a time: one_lane_at_a_time). Kept out of registers and
 // scratch: a dynamically indexed private array would be scratch memory in every wave.
@@ -174,7 +202,6 @@ NXG_DEV uint64_t value_len(const ColsDesc& c, bool row, uint64_t slot, uint32_t*
 struct Out {
     uint8_t* o;
     uint64_t p;
-    NXG_DEV void done() {}
     NXG_DEV void b(uint32_t x) { o[p++] = (uint8_t)x; }
     NXG_DEV void be(uint64_t v, int n) {
         for (int i = n - 1; i >= 0; i--) o[p++] = (uint8_t)(v >> (8 * i));
@@ -210,82 +237,6 @@ struct Out {
             return;
         }
         for (uint64_t i = 0; i < n; i++) o[p++] = src[i];
-    }
-};
-
-#ifndef NXG_ENC_OR
-#define NXG_ENC_OR 0
-#endif
-// The staging writer of the rows kernel (NXG_ENC_OR): bytes gather in a 64-bit register and go
-// to LDS as aligned dwords by ds_or (the staging is zeroed first), two dwords per 8 bytes, instead
-// of one ds_write_b8 per byte; neighbouring rows share edge dwords, which the OR merges.
-struct OrOut {
-    uint32_t* o;    // the staging as dwords
-    uint32_t q;     // the dword that acc's byte 0 goes to
-    uint32_t fill;  // bytes held in acc (its first p & 3 are the previous row's: zero)
-    uint64_t acc;
-    NXG_DEV OrOut(uint8_t* stg, uint32_t p)
-        : o(reinterpret_cast<uint32_t*>(stg)), q(p >> 2), fill(p & 3u), acc(0) {}
-    NXG_DEV void put(uint64_t v, uint32_t n) {  // v's low n bytes (1..8, the rest zero), in order
-        const uint32_t sh = 8 * fill;
-        acc |= v << sh;
-        const uint64_t carry = sh ? v >> (64 - sh) : 0ull;
-        fill += n;
-        if (fill >= 8) {
-            atomicOr(&o[q], (uint32_t)acc);
-            atomicOr(&o[q + 1], (uint32_t)(acc >> 32));
-            q += 2;
-            acc = carry;
-            fill -= 8;
-        }
-    }
-    NXG_DEV void done() {
-        if (fill) atomicOr(&o[q], (uint32_t)acc);
-        if (fill > 4) atomicOr(&o[q + 1], (uint32_t)(acc >> 32));
-    }
-    NXG_DEV void b(uint32_t x) { put(x & 0xffu, 1); }
-    NXG_DEV void be(uint64_t v, int n) {  // n <= 8
-        put(__builtin_bswap64(v) >> (64 - 8 * n), (uint32_t)n);
-    }
-    NXG_DEV void var(uint64_t v) {
-        if (v < (1ull << 28)) {  // ids and lengths: 1..4 bytes in 32-bit arithmetic
-            const uint32_t u = (uint32_t)v;
-            const uint32_t nb = u < 0x80u ? 1u : u < 0x4000u ? 2u : u < 0x200000u ? 3u : 4u;
-            uint32_t x = (u & 0x7fu) | ((u << 1) & 0x7f00u) | ((u << 2) & 0x7f0000u) |
-                         ((u << 3) & 0x7f000000u);
-            x |= 0x80808080u & ((1u << (8 * (nb - 1))) - 1u);
-            put(x, nb);
-            return;
-        }
-        while (v >= 0x80) {
-            put((v & 0x7f) | 0x80, 1);
-            v >>= 7;
-        }
-        put(v, 1);
-    }
-    NXG_DEV void copy(const uint8_t* src, uint64_t n) {
-        constexpr int NW = 12;  // as Out::copy: the covering dwords of up to 44 bytes, realigned
-        if (n <= 4 * NW - 4) {
-            const uint32_t sh = (uint32_t)((uintptr_t)src & 3u);
-            const uint32_t* w = reinterpret_cast<const uint32_t*>((uintptr_t)src & ~(uintptr_t)3);
-            const uint32_t nw = (uint32_t)((sh + n + 3) >> 2);
-            uint32_t d[NW + 1];
-#pragma unroll
-            for (int i = 0; i < NW; i++) d[i] = (uint32_t)i < nw ? w[i] : 0u;
-            d[NW] = 0u;
-#pragma unroll
-            for (int i = 0; i < (NW - 1) / 2 + 1; i++) {
-                if ((uint64_t)(8 * i) < n) {
-                    const uint32_t lo = __builtin_amdgcn_alignbyte(d[2 * i + 1], d[2 * i], sh);
-                    const uint32_t hi = 2 * i + 2 <= NW ? __builtin_amdgcn_alignbyte(d[2 * i + 2], d[2 * i + 1], sh) : 0u;
-                    const uint32_t k = (uint32_t)min<uint64_t>(8, n - 8 * i);
-                    const uint64_t v = ((uint64_t)hi << 32) | lo;
-                    put(k == 8 ? v : v & ((1ull << (8 * k)) - 1ull), k);
-                }
-            }
-            return;
-        }
-        for (uint64_t i = 0; i < n; i++) put(src[i], 1);
     }
 };
 
@@ -357,8 +308,7 @@ NXG_DEV void scalar_write(const Slot& s, const uint8_t* heap, W& w) {
 
 // Row r's |Value| without the stack when the value is a scalar, text, or an array whose
 // elements are not containers; `flat` false (and 0) otherwise, or on an unknown tag.
-NXG_DEV uint64_t row_len_flat(const ColsDesc& c, uint64_t r, bool& flat) {
-    const Slot s = get_slot(c, true, r);
+NXG_DEV uint64_t row_len_flat(const ColsDesc& c, const Slot& s, bool& flat) {
     flat = true;
     if (!is_container(s.tag)) {
         const uint64_t l = scalar_len(s);
@@ -368,6 +318,20 @@ NXG_DEV uint64_t row_len_flat(const ColsDesc& c, uint64_t r, bool& flat) {
     if (s.tag != 19 || (uint64_t)s.aux * 16 > kMaxVec) {
         flat = false;
         return 0;
+    }
+    if ((NXG_ENC_AFAST & 1) && s.aux - 1u < 8u) {  // 1..8 elements: their tags in one load
+        const uint64_t tg = tags8(c.ctag + s.fixed, s.aux);
+        uint32_t sum = 0;
+        bool ok = true;
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            if ((uint32_t)j < s.aux) {
+                const uint32_t f = fixed_len((uint32_t)(tg >> (8 * j)) & 0xffu);
+                ok = ok && f != 0;
+                sum += f;
+            }
+        }
+        if (ok) return 2 + sum;  // tag 19, the count (one byte), the elements
     }
     uint64_t total = 1 + vl64(s.aux);
     // the elements NXG_ENC_EB at a time: their loads in flight together (one memory round trip
@@ -395,14 +359,43 @@ NXG_DEV uint64_t row_len_flat(const ColsDesc& c, uint64_t r, bool& flat) {
     return total;
 }
 template <typename W>
-NXG_DEV void row_write_flat(const ColsDesc& c, const uint8_t* heap, uint64_t r, W& w) {
-    const Slot s = get_slot(c, true, r);
+NXG_DEV void row_write_flat(const ColsDesc& c, const uint8_t* heap, const Slot& s, W& w) {
     if (s.tag != 19) {
         scalar_write(s, heap, w);
         return;
     }
     w.b(19);
     w.var(s.aux);
+    if ((NXG_ENC_AFAST & 2) && s.aux - 1u < 8u) {
+        // 1..8 elements of fixed size without aux (not DateTime / Duration / Decimal): their tags
+        // in one load, then only their values, four at a time
+        const uint64_t tg = tags8(c.ctag + s.fixed, s.aux);
+        bool ok = true;
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const uint32_t t = (uint32_t)(tg >> (8 * j)) & 0xffu;
+            const uint32_t f = fixed_len(t);
+            if ((uint32_t)j < s.aux) ok = ok && f != 0 && f <= 9u && t != 10u && t != 11u;
+        }
+        if (ok) {
+#pragma unroll 1
+            for (uint32_t k0 = 0; k0 < s.aux; k0 += 4) {
+                uint64_t v[4];
+#pragma unroll
+                for (int j = 0; j < 4; j++) v[j] = k0 + j < s.aux ? c.cfixed[s.fixed + k0 + j] : 0ull;
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    if (k0 + j < s.aux) {
+                        const uint32_t t = (uint32_t)(tg >> (8 * (k0 + j))) & 0xffu;
+                        const uint32_t f = fixed_len(t);
+                        w.b(t);
+                        if (f > 1u) w.be(v[j], (int)f - 1);
+                    }
+                }
+            }
+            return;
+        }
+    }
 #pragma unroll 1
     for (uint64_t k0 = 0; k0 < s.aux; k0 += NXG_ENC_EB) {
         Slot e[NXG_ENC_EB];
@@ -459,7 +452,7 @@ NXG_DEV uint64_t row_msg_len(const ColsDesc& c, uint64_t r, bool arch, WalkStack
         break;
     case CLS_ARR: {
         bool flat;
-        vlen = row_len_flat(c, r, flat);
+        vlen = row_len_flat(c, v, flat);
         gen = !flat;
         break;
     }
@@ -499,6 +492,7 @@ __global__ __launch_bounds__(TPB, NXG_ENC_OCC) void nxg_enc_rows_kernel(
     __shared__ uint64_t sh_base;
     __shared__ __attribute__((aligned(16))) uint8_t stg[GSTG];
     __shared__ uint32_t cls_n[NCLS], cls_b[NCLS + 1];
+    __shared__ uint32_t cls_w[TPB / 64][NCLS];  // per wave: class counts, then first entries
     __shared__ uint16_t lst_row[GTILE];  // the tile's rows sorted by value class
     __shared__ uint16_t off_lds[GTILE];  // staging offset per row (tile-local index)
     __shared__ uint32_t len_lds[GTILE];  // message length per row (0: absent or erroring)
@@ -508,19 +502,73 @@ __global__ __launch_bounds__(TPB, NXG_ENC_OCC) void nxg_enc_rows_kernel(
     const uint32_t tid = threadIdx.x, lane = tid & 63;
     WalkStack* const stk = &wstk[tid >> 6];
     const uint64_t n = c.n_rows;
+    // the tags of the thread's rows in its next tile, loaded during this tile's look-back
+    uint32_t ntg[GRPT];
+#pragma unroll
+    for (int k = 0; k < GRPT; k++) {
+        const uint64_t r = (uint64_t)blockIdx.x * GTILE + (uint64_t)tid * GRPT + k;
+        ntg[k] = r < n ? c.tag[r] : 0u;
+    }
     for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const uint64_t rt = (uint64_t)tile * GTILE;
         const uint64_t r0 = rt + (uint64_t)tid * GRPT;
         ESTAMP(0);
         // 1. classify by tag and bucket the rows (wave-ballot counting sort in LDS); a wave then
         //    writes and sizes one class at a time
+        uint32_t cls[GRPT], pos[GRPT];
+#if NXG_ENC_CLS2
+        // per wave: class counts and ranks from ballots alone (uniform counters, no LDS atomics),
+        // then one table of the waves' offsets per class
+        {
+            uint32_t cnt[NCLS];
+#pragma unroll
+            for (int q = 0; q < NCLS; q++) cnt[q] = 0;
+#pragma unroll
+            for (int k = 0; k < GRPT; k++) {
+                const uint64_t r = r0 + k;
+                const uint32_t tg = NXG_ENC_PF ? ntg[k] : r < n ? c.tag[r] : 0u;
+                cls[k] = r < n ? (arch && tg == 0x40u ? (uint32_t)CLS_SCAL : value_class(tg)) : NCLS;
+                pos[k] = 0;
+#pragma unroll
+                for (uint32_t q = 0; q < NCLS; q++) {
+                    const uint64_t m = __ballot(cls[k] == q);
+                    if (cls[k] == q) pos[k] = cnt[q] + (uint32_t)__popcll(m & ((1ull << lane) - 1));
+                    cnt[q] += (uint32_t)__popcll(m);
+                }
+            }
+            if (lane == 0) {
+#pragma unroll
+                for (int q = 0; q < NCLS; q++) cls_w[tid >> 6][q] = cnt[q];
+            }
+        }
+        __syncthreads();
+        if (tid == 0) {
+            uint32_t acc = 0;
+            for (int q = 0; q < NCLS; q++) {
+                cls_b[q] = acc;
+                for (int v = 0; v < TPB / 64; v++) {
+                    const uint32_t x = cls_w[v][q];
+                    cls_w[v][q] = acc;  // the wave's first entry of class q
+                    acc += x;
+                }
+            }
+            cls_b[NCLS] = acc;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < GRPT; k++) {
+            const uint32_t rl = tid * GRPT + k;
+            len_lds[rl] = 0;
+            cls_lds[rl] = (uint8_t)cls[k];
+            if (cls[k] < NCLS) lst_row[cls_w[tid >> 6][cls[k]] + pos[k]] = (uint16_t)rl;
+        }
+#else
         if (tid < NCLS) cls_n[tid] = 0;
         __syncthreads();
-        uint32_t cls[GRPT], pos[GRPT];
 #pragma unroll
         for (int k = 0; k < GRPT; k++) {
             const uint64_t r = r0 + k;
-            const uint32_t tg = r < n ? c.tag[r] : 0u;
+            const uint32_t tg = NXG_ENC_PF ? ntg[k] : r < n ? c.tag[r] : 0u;
             cls[k] = r < n ? (arch && tg == 0x40u ? (uint32_t)CLS_SCAL : value_class(tg)) : NCLS;
             pos[k] = 0;
 #pragma unroll
@@ -551,14 +599,30 @@ __global__ __launch_bounds__(TPB, NXG_ENC_OCC) void nxg_enc_rows_kernel(
             cls_lds[rl] = (uint8_t)cls[k];
             if (cls[k] < NCLS) lst_row[cls_b[cls[k]] + pos[k]] = (uint16_t)rl;
         }
+#endif
         __syncthreads();
         ESTAMP(1);
         const uint32_t ne = cls_b[NCLS];
-        // 2. message lengths, class by class
+        // 2. message lengths, class by class. Each thread's next entry's slot and id are loaded
+        //    while it sizes the current one (NXG_ENC_PF: two memory round trips in flight)
+        uint32_t p_rl = 0;
+        Slot p_v{0, 0, 0};
+        uint64_t p_id = 0;
+        if (NXG_ENC_PF && tid < ne) {
+            p_rl = lst_row[tid];
+            p_v = get_slot(c, true, rt + p_rl);
+            p_id = c.id[rt + p_rl];
+        }
         for (uint32_t e = tid; e < ne; e += TPB) {
-            const uint32_t rl = lst_row[e];
+            const uint32_t rl = NXG_ENC_PF ? p_rl : lst_row[e];
             const uint64_t r = rt + rl;
-            const Slot v = get_slot(c, true, r);
+            const Slot v = NXG_ENC_PF ? p_v : get_slot(c, true, r);
+            const uint64_t idv = NXG_ENC_PF ? p_id : c.id[r];
+            if (NXG_ENC_PF && e + TPB < ne) {
+                p_rl = lst_row[e + TPB];
+                p_v = get_slot(c, true, rt + p_rl);
+                p_id = c.id[rt + p_rl];
+            }
             uint64_t vlen = 0;
             uint32_t err = 0;
             bool gen = false;
@@ -575,7 +639,7 @@ __global__ __launch_bounds__(TPB, NXG_ENC_OCC) void nxg_enc_rows_kernel(
                 break;
             case CLS_ARR: {
                 bool flat;
-                vlen = row_len_flat(c, r, flat);
+                vlen = row_len_flat(c, v, flat);
                 if (!flat) {
                     cls_lds[rl] = CLS_GEN;
                     gen = true;
@@ -589,8 +653,8 @@ __global__ __launch_bounds__(TPB, NXG_ENC_OCC) void nxg_enc_rows_kernel(
             // queue_send refuses a message longer than MAX_BATCH (channel.rs:178-181); that bound
             // also keeps the 32-bit staged lengths exact
             const uint64_t ml = err    ? 0ull
-                                : arch ? vl64((uint32_t)c.id[r]) + vlen
-                                       : lwlen(1 + vl64(c.id[r]) + vlen);
+                                : arch ? vl64((uint32_t)idv) + vlen
+                                       : lwlen(1 + vl64(idv) + vlen);
             if (!err && ml > (arch ? 0xFFFFFFFFull : 0x3FFFFFFFull)) err = NXG_TOO_BIG;
             if (err) atomicMax(&st->err_kind, err);
             len_lds[rl] = err ? 0u : (uint32_t)ml;
@@ -621,58 +685,62 @@ __global__ __launch_bounds__(TPB, NXG_ENC_OCC) void nxg_enc_rows_kernel(
                     o += (uint32_t)L[k];
                 }
             }
-            if (NXG_ENC_OR) {  // the OR writer needs a zeroed staging
-                typedef uint32_t z4 __attribute__((ext_vector_type(4)));
-                for (uint32_t b = tid; b < (uint32_t)((tot + 31) >> 4); b += TPB)
-                    reinterpret_cast<z4*>(stg)[b] = z4{0u, 0u, 0u, 0u};
-            }
             __syncthreads();
+            uint32_t q_rl = 0;
+            Slot q_v{0, 0, 0};
+            uint64_t q_id = 0;
+            if (NXG_ENC_PF && tid < ne) {
+                q_rl = lst_row[tid];
+                q_v = get_slot(c, true, rt + q_rl);
+                q_id = c.id[rt + q_rl];
+            }
             for (uint32_t e = tid; e < ne; e += TPB) {
-                const uint32_t rl = lst_row[e];
+                const uint32_t rl = NXG_ENC_PF ? q_rl : lst_row[e];
+                const uint64_t r = rt + rl;
+                const Slot v = NXG_ENC_PF ? q_v : get_slot(c, true, r);
+                const uint64_t idv = NXG_ENC_PF ? q_id : c.id[r];
+                if (NXG_ENC_PF && e + TPB < ne) {
+                    q_rl = lst_row[e + TPB];
+                    q_v = get_slot(c, true, rt + q_rl);
+                    q_id = c.id[rt + q_rl];
+                }
                 const uint32_t len = len_lds[rl];
                 if (!len) continue;
-                const uint64_t r = rt + rl;
-#if NXG_ENC_OR
-                OrOut w(stg, off_lds[rl]);
-#else
                 Out w{stg, off_lds[rl]};
-#endif
                 if (arch) {
-                    w.var((uint32_t)c.id[r]);
+                    w.var((uint32_t)idv);
                 } else {
                     w.var(len);
                     w.b(4);
-                    w.var(c.id[r]);
+                    w.var(idv);
                 }
                 switch (cls_lds[rl]) {
-                case CLS_FIX8: {
-                    const Slot v = get_slot(c, true, r);
+                case CLS_FIX8:
                     w.b(v.tag);
                     w.be(v.fixed, 8);
                     break;
-                }
-                case CLS_TEXT: {
-                    const Slot v = get_slot(c, true, r);
+                case CLS_TEXT:
                     w.b(v.tag);
                     w.var(v.aux);
                     w.copy(heap + v.fixed, v.aux);
                     break;
-                }
-                case CLS_TIME: {
-                    const Slot v = get_slot(c, true, r);
+                case CLS_TIME:
                     w.b(v.tag);
                     w.be(v.fixed, 8);
                     w.be(v.aux, 4);
                     break;
-                }
-                case CLS_ARR: row_write_flat(c, heap, r, w); break;
-                case CLS_SCAL: scalar_write(get_slot(c, true, r), heap, w); break;
+                case CLS_ARR: row_write_flat(c, heap, v, w); break;
+                case CLS_SCAL: scalar_write(v, heap, w); break;
                 default: break;
                 }
                 one_lane_at_a_time(cls_lds[rl] == CLS_GEN,
                                    [&] { value_write(c, heap, true, r, w, stk); });
-                w.done();
             }
+        }
+        if (NXG_ENC_PF) {  // the next tile's tags: their round trip overlaps the look-back
+            const uint64_t rn = (uint64_t)(tile + gridDim.x) * GTILE + (uint64_t)tid * GRPT;
+#pragma unroll
+            for (int k = 0; k < GRPT; k++) ntg[k] = rn + k < n ? c.tag[rn + k] : 0u;
         }
         // 3b. the tile's base: look-back over the tiles' byte counts
         ESTAMP(4);
@@ -766,7 +834,7 @@ __global__ __launch_bounds__(TPB, NXG_ENC_OCC) void nxg_enc_rows_kernel(
                             w.b(4);
                             w.var(c.id[r]);
                         }
-                        if (cls_lds[tid * GRPT + k] != CLS_GEN) row_write_flat(c, heap, r, w);
+                        if (cls_lds[tid * GRPT + k] != CLS_GEN) row_write_flat(c, heap, get_slot(c, true, r), w);
                         one_lane_at_a_time(cls_lds[tid * GRPT + k] == CLS_GEN,
                                            [&] { value_write(c, heap, true, r, w, stk); });
                     }
