@@ -68,6 +68,27 @@ struct FaHead {
 };
 static_assert(sizeof(FaHead) == 64, "FaHead layout");
 
+#ifndef NXG_FA_PROF
+#define NXG_FA_PROF 0  // diagnostic build only: per-section wave clocks of the count pass
+#endif
+#if NXG_FA_PROF
+// [0..4] clocks: image, own chunk's spec walk, walk before the tile, own exact walk, chain;
+// [8] waves, [9] lanes that walked their chunk again exactly, [10] waves whose chain left the
+// ballot path, [11] chunks walked by the whole wave in the chain loop
+__device__ unsigned long long nxg_fa_prof[16];
+#define FAP(k)                                                                   \
+    do {                                                                         \
+        if (prof) {                                                              \
+            const uint64_t _t = __builtin_amdgcn_s_memtime();                    \
+            prof[k] += _t - prof[15];                                            \
+            prof[15] = _t;                                                       \
+        }                                                                        \
+    } while (0)
+#else
+#define FAP(k) \
+    do {       \
+    } while (0)
+#endif
 namespace {
 using namespace fmx;
 using namespace fa;
@@ -278,7 +299,7 @@ NXG_DEV uint32_t spec_walk(lds_bytes img, uint32_t x0, uint32_t cb, uint32_t end
 // elsewhere walks again).
 NXG_DEV FaDesc chain_from(lds_bytes img, uint32_t E, uint32_t lim, uint32_t wl, uint32_t lane,
                           uint32_t A, uint32_t X, uint32_t n, uint32_t kids, uint64_t bits,
-                          uint32_t brk, uint64_t& obits) {
+                          uint32_t brk, uint64_t& obits, uint64_t* prof = nullptr) {
     uint32_t x = E, ce = NONE, bp = FAIL;
     // Every chunk entered where its predecessor's walk left it (the usual case: the guesses
     // synchronised): the chain is the lanes' own walks, from one ballot. Otherwise the uniform
@@ -292,6 +313,9 @@ NXG_DEV FaDesc chain_from(lds_bytes img, uint32_t E, uint32_t lim, uint32_t wl, 
         const bool cov = pin >= min(cl + CH, lim);  // an item covers the whole chunk
         const uint64_t bad = __ballot(act && !(pin == A && X != FAIL));
         j0 = bad ? (uint32_t)__builtin_ctzll(bad) : TILE / CH;
+#if NXG_FA_PROF
+        if (prof && bad) prof[10]++;
+#endif
         if (lane < j0 && act && !cov) ce = A;
         if (j0 > 0) x = (uint32_t)__builtin_amdgcn_readlane((int)X, (int)(j0 - 1));
         if (j0 == TILE / CH) {
@@ -314,6 +338,9 @@ NXG_DEV FaDesc chain_from(lds_bytes img, uint32_t E, uint32_t lim, uint32_t wl, 
             }
             x = Xj;
         } else {  // entered off the guess: every lane walks it (uniform addresses)
+#if NXG_FA_PROF
+            if (prof) prof[11]++;
+#endif
             uint32_t n2, k2, b2;
             uint64_t m2;
             const uint32_t y = chunk_walk(img, x, cj, endj, wl, n2, k2, m2, b2);
@@ -366,7 +393,7 @@ NXG_DEV void count_store(uint8_t* img, const CountRegs& g, uint32_t lane) {
 // the count for tile t from entry E (a tile offset; NONE: guess it); the count image is in LDS.
 // The guess: where the walk over the PRE bytes before the tile leaves them.
 NXG_DEV FaDesc count_tile(lds_bytes img, uint64_t t, uint64_t W, uint32_t E, uint32_t lane,
-                          uint64_t& obits) {
+                          uint64_t& obits, uint64_t* prof = nullptr) {
     const uint64_t t0 = t * TILE;
     const uint32_t lim = PRE + (uint32_t)min<uint64_t>(TILE, W - t0);
     const uint32_t wl = PRE + (uint32_t)min<uint64_t>(W - t0, 0xffffffffull - PRE);
@@ -376,6 +403,7 @@ NXG_DEV FaDesc count_tile(lds_bytes img, uint64_t t, uint64_t W, uint32_t E, uin
     const uint32_t g = c < lim ? spec_walk(img, c, c, end, wl, first, item_cands((lds_bytes)img, c),
                                            rbits, rkids)
                                : c;
+    FAP(1);
     uint32_t ge = 0;
     if (E == NONE) {
         // the walk over the PRE / 64 chunks before the tile: lane q walks chunk q, all at once;
@@ -413,6 +441,7 @@ NXG_DEV FaDesc count_tile(lds_bytes img, uint64_t t, uint64_t W, uint32_t E, uin
     } else {
         E += PRE;
     }
+    FAP(2);
     // the lane's guessed entry: its predecessor's guessed exit (lane 0: E)
     const uint32_t gp = (uint32_t)__shfl_up((int)g, 1, 64);
     const uint32_t A = lane == 0 ? E : gp;
@@ -429,10 +458,16 @@ NXG_DEV FaDesc count_tile(lds_bytes img, uint64_t t, uint64_t W, uint32_t E, uin
             kids = rkids;
             X = g;
         } else {
+#if NXG_FA_PROF
+            if (prof) prof[9] += __popcll(__ballot(true));
+#endif
             X = chunk_walk(img, A, c, end, wl, n, kids, bits, brk);
         }
     }
-    return chain_from(img, E, lim, wl, lane, A, X, n, kids, bits, brk, obits);
+    FAP(3);
+    const FaDesc r = chain_from(img, E, lim, wl, lane, A, X, n, kids, bits, brk, obits, prof);
+    FAP(4);
+    return r;
 }
 
 }  // namespace
@@ -486,14 +521,33 @@ __global__ __launch_bounds__(TPB) void nxg_fa_count_kernel(const uint8_t* __rest
     const uint64_t t = (uint64_t)blockIdx.x * (TPB / 64) + w;
     if (t >= nt) return;
     uint8_t* img = lds[w].img;
+#if NXG_FA_PROF
+    uint64_t pacc[16] = {};
+    uint64_t* prof = pacc;
+    prof[15] = __builtin_amdgcn_s_memtime();
+#else
+    uint64_t* prof = nullptr;
+#endif
     CountRegs g;
     count_load(g, buf, t * TILE, W, lane);
     count_store(img, g, lane);
+    FAP(0);
     uint64_t bits;
-    const FaDesc d = count_tile((lds_bytes)img, t, W, t == 0 ? p0 : NONE, lane, bits);
+    const FaDesc d = count_tile((lds_bytes)img, t, W, t == 0 ? p0 : NONE, lane, bits, prof);
     starts[t * 64 + lane] = bits;
     if (lane == 0) td[t] = d;
+#if NXG_FA_PROF
+    pacc[8] = 1;
+    if (lane == 0)
+        for (int k = 0; k < 12; k++) atomicAdd(&nxg_fa_prof[k], (unsigned long long)pacc[k]);
+#endif
 }
+#if NXG_FA_PROF
+extern "C" int nxg_debug_fa_prof(unsigned long long* out) {
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(nxg_fa_prof), sizeof(nxg_fa_prof), 0,
+                                    hipMemcpyDeviceToHost);
+}
+#endif
 
 #ifndef NXG_FA_FIX_PASSES
 #define NXG_FA_FIX_PASSES 2  // a second pass for tiles whose predecessor the first recounted (fix 69 -> 2 x 64, resolve 134 -> 52 us)

@@ -39,6 +39,9 @@
 #ifndef NXG_ENC_CLS2
 #define NXG_ENC_CLS2 1  // class buckets from per-wave ballot counts (no LDS atomics)
 #endif
+#ifndef NXG_ENC_LBW
+#define NXG_ENC_LBW 1  // with the staging: wave 0 runs the look-back while waves 1-3 stage the rows
+#endif
 #ifndef NXG_ENC_LBU
 #define NXG_ENC_LBU 1  // look-back window, 64 * NXG_ENC_LBU tiles per round trip (1, 4 and 8 measured equal)
 #endif
@@ -675,6 +678,31 @@ __global__ __launch_bounds__(TPB, NXG_ENC_OCC) void nxg_enc_rows_kernel(
         ESTAMP(3);
         // 4a. without control messages: the rows into the staging at their tile-local offsets
         //     first, so that the look-back below finds its predecessors mostly done
+        // the tile's base (wave 0)
+        auto lookback = [&]() {
+            uint64_t base = 0;
+            if (tile != 0) {
+                bool give_up;
+#if NXG_ENC_SKIP & 1
+                give_up = false;  // timing experiments only: no look-back (wrong offsets)
+#else
+                // no wait on a workgroup that may not be running: an unpublished predecessor's
+                // byte count is computed here from its rows (self-help)
+                give_up = false;
+                base = lookback_selfhelp_fn(
+                    tstat, tile, epoch, patience, [&](uint64_t t) -> uint64_t {
+                        const uint64_t q0 = t * GTILE;
+                        uint64_t b = 0;
+                        for (uint64_t r = q0 + lane; r < q0 + GTILE && r < n; r += 64)
+                            b += row_msg_len(c, r, arch, &wstk[0]);
+                        return wave_sum<uint64_t>(b);
+                    });
+#endif
+                if (give_up && lane == 0) atomicOr(&st->timeout, 1u);
+                if (lane == 0) st_agent(&tstat[tile], lb_word(kFlagInc, epoch, base + tot));
+            }
+            if (lane == 0) sh_base = base;
+        };
         const bool stage = out && c.n_ctl == 0 && tot <= (uint64_t)(GSTG - 32);
         if (stage) {
             {
@@ -686,21 +714,24 @@ __global__ __launch_bounds__(TPB, NXG_ENC_OCC) void nxg_enc_rows_kernel(
                 }
             }
             __syncthreads();
+            const bool lbw = NXG_ENC_LBW && tid < 64;  // wave 0: the look-back, meanwhile
+            if (lbw) lookback();
+            const uint32_t e0 = NXG_ENC_LBW ? tid - 64 : tid, es = NXG_ENC_LBW ? TPB - 64 : TPB;
             uint32_t q_rl = 0;
             Slot q_v{0, 0, 0};
             uint64_t q_id = 0;
-            if (NXG_ENC_PF && tid < ne) {
-                q_rl = lst_row[tid];
+            if (NXG_ENC_PF && !lbw && e0 < ne) {
+                q_rl = lst_row[e0];
                 q_v = get_slot(c, true, rt + q_rl);
                 q_id = c.id[rt + q_rl];
             }
-            for (uint32_t e = tid; e < ne; e += TPB) {
+            for (uint32_t e = e0; !lbw && e < ne; e += es) {
                 const uint32_t rl = NXG_ENC_PF ? q_rl : lst_row[e];
                 const uint64_t r = rt + rl;
                 const Slot v = NXG_ENC_PF ? q_v : get_slot(c, true, r);
                 const uint64_t idv = NXG_ENC_PF ? q_id : c.id[r];
-                if (NXG_ENC_PF && e + TPB < ne) {
-                    q_rl = lst_row[e + TPB];
+                if (NXG_ENC_PF && e + es < ne) {
+                    q_rl = lst_row[e + es];
                     q_v = get_slot(c, true, rt + q_rl);
                     q_id = c.id[rt + q_rl];
                 }
@@ -742,32 +773,10 @@ __global__ __launch_bounds__(TPB, NXG_ENC_OCC) void nxg_enc_rows_kernel(
 #pragma unroll
             for (int k = 0; k < GRPT; k++) ntg[k] = rn + k < n ? c.tag[rn + k] : 0u;
         }
-        // 3b. the tile's base: look-back over the tiles' byte counts
+        // 3b. the tile's base: look-back over the tiles' byte counts (with the staging: by wave 0
+        //     while the other waves stage, NXG_ENC_LBW)
         ESTAMP(4);
-        if (tid < 64) {
-            uint64_t base = 0;
-            if (tile != 0) {
-                bool give_up;
-#if NXG_ENC_SKIP & 1
-                give_up = false;  // timing experiments only: no look-back (wrong offsets)
-#else
-                // no wait on a workgroup that may not be running: an unpublished predecessor's
-                // byte count is computed here from its rows (self-help)
-                give_up = false;
-                base = lookback_selfhelp_fn(
-                    tstat, tile, epoch, patience, [&](uint64_t t) -> uint64_t {
-                        const uint64_t q0 = t * GTILE;
-                        uint64_t b = 0;
-                        for (uint64_t r = q0 + lane; r < q0 + GTILE && r < n; r += 64)
-                            b += row_msg_len(c, r, arch, &wstk[0]);
-                        return wave_sum<uint64_t>(b);
-                    });
-#endif
-                if (give_up && lane == 0) atomicOr(&st->timeout, 1u);
-                if (lane == 0) st_agent(&tstat[tile], lb_word(kFlagInc, epoch, base + tot));
-            }
-            if (lane == 0) sh_base = base;
-        }
+        if (!(stage && NXG_ENC_LBW) && tid < 64) lookback();
         __syncthreads();
         ESTAMP(5);
         const uint64_t tbase = sh_base + arch_base;

@@ -302,6 +302,36 @@ def test_encode_staged_every_tag(codec):
     assert codec.encode_batch(cols, heap).cpu().numpy().tobytes() == wire
 
 
+def test_encode_arrays_of_fixed_size_elements(codec):
+    """Arrays of 1..9 elements of every fixed-size tag (the encoder sizes arrays of up to 8 such
+    elements from one load of their tags, at any alignment of their first child), with a
+    varint or text element now and then (the element-by-element path), byte-identical."""
+    import torch
+    mg = _mg()
+    rng = random.Random(4321)
+    fixed_tags = [0, 2, 4, 6, 8, 9, 10, 11, 14, 15, 16, 20, 23, 24, 25, 26]
+    msgs = []
+    for i in range(8000):
+        k = rng.randrange(1, 10)
+        els = []
+        for _ in range(k):
+            v = mg.rand_value(rng, 3)
+            while v[0] not in fixed_tags:
+                v = mg.rand_value(rng)
+            els.append(v)
+        if rng.random() < 0.1:
+            els[rng.randrange(k)] = rng.choice([(1, rng.getrandbits(14)), (12, b"abc"),
+                                                (5, rng.getrandbits(40))])
+        msgs.append(("u", rng.getrandbits(rng.choice([7, 21, 30])), (19, els)))
+        if rng.random() < 0.3:  # scalars between them shift the arrays' first child slots
+            msgs.append(("u", i, (9, rng.getrandbits(64))))
+    wire, _ = mg.batch(msgs)
+    cols, st = gpu_decode(codec, wire)
+    assert_same_as_oracle(cols, st, wire)
+    heap = torch.from_numpy(np.frombuffer(wire, np.uint8).copy()).cuda()
+    assert codec.encode_batch(cols, heap).cpu().numpy().tobytes() == wire
+
+
 def test_encode_tiles_past_the_staging(codec):
     """Values longer than the encoder's LDS staging (28 bytes per row): those tiles write their
     rows straight to the frame; short tiles around them stay staged."""
