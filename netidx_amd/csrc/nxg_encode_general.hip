@@ -39,9 +39,6 @@
 #ifndef NXG_ENC_CLS2
 #define NXG_ENC_CLS2 1  // class buckets from per-wave ballot counts (no LDS atomics)
 #endif
-#ifndef NXG_ENC_LBW
-#define NXG_ENC_LBW 1  // with the staging: wave 0 runs the look-back while waves 1-3 stage the rows
-#endif
 #ifndef NXG_ENC_LBU
 #define NXG_ENC_LBU 1  // look-back window, 64 * NXG_ENC_LBU tiles per round trip (1, 4 and 8 measured equal)
 #endif
@@ -115,7 +112,7 @@ NXG_DEV uint64_t scalar_len(const Slot& s) {
 }
 
 #ifndef NXG_ENC_AFAST
-#define NXG_ENC_AFAST 1  // arrays of 1..8 fixed-size elements sized from one load of their tags (the write path's version: 170 VGPRs)
+#define NXG_ENC_AFAST 1  // arrays of 1..8 fixed-size elements sized from one load of their tags (the same on the write side: no gain)
 #endif
 // |Value| of a value of fixed size by its tag (tag byte included; Decimal 17), 0 for the others:
 // nibble tables, tag 20's 15 standing for 17
@@ -369,36 +366,6 @@ NXG_DEV void row_write_flat(const ColsDesc& c, const uint8_t* heap, const Slot& 
     }
     w.b(19);
     w.var(s.aux);
-    if ((NXG_ENC_AFAST & 2) && s.aux - 1u < 8u) {
-        // 1..8 elements of fixed size without aux (not DateTime / Duration / Decimal): their tags
-        // in one load, then only their values, four at a time
-        const uint64_t tg = tags8(c.ctag + s.fixed, s.aux);
-        bool ok = true;
-#pragma unroll
-        for (int j = 0; j < 8; j++) {
-            const uint32_t t = (uint32_t)(tg >> (8 * j)) & 0xffu;
-            const uint32_t f = fixed_len(t);
-            if ((uint32_t)j < s.aux) ok = ok && f != 0 && f <= 9u && t != 10u && t != 11u;
-        }
-        if (ok) {
-#pragma unroll 1
-            for (uint32_t k0 = 0; k0 < s.aux; k0 += 4) {
-                uint64_t v[4];
-#pragma unroll
-                for (int j = 0; j < 4; j++) v[j] = k0 + j < s.aux ? c.cfixed[s.fixed + k0 + j] : 0ull;
-#pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    if (k0 + j < s.aux) {
-                        const uint32_t t = (uint32_t)(tg >> (8 * (k0 + j))) & 0xffu;
-                        const uint32_t f = fixed_len(t);
-                        w.b(t);
-                        if (f > 1u) w.be(v[j], (int)f - 1);
-                    }
-                }
-            }
-            return;
-        }
-    }
 #pragma unroll 1
     for (uint64_t k0 = 0; k0 < s.aux; k0 += NXG_ENC_EB) {
         Slot e[NXG_ENC_EB];
@@ -714,18 +681,16 @@ __global__ __launch_bounds__(TPB, NXG_ENC_OCC) void nxg_enc_rows_kernel(
                 }
             }
             __syncthreads();
-            const bool lbw = NXG_ENC_LBW && tid < 64;  // wave 0: the look-back, meanwhile
-            if (lbw) lookback();
-            const uint32_t e0 = NXG_ENC_LBW ? tid - 64 : tid, es = NXG_ENC_LBW ? TPB - 64 : TPB;
+            const uint32_t e0 = tid, es = TPB;
             uint32_t q_rl = 0;
             Slot q_v{0, 0, 0};
             uint64_t q_id = 0;
-            if (NXG_ENC_PF && !lbw && e0 < ne) {
+            if (NXG_ENC_PF && e0 < ne) {
                 q_rl = lst_row[e0];
                 q_v = get_slot(c, true, rt + q_rl);
                 q_id = c.id[rt + q_rl];
             }
-            for (uint32_t e = e0; !lbw && e < ne; e += es) {
+            for (uint32_t e = e0; e < ne; e += es) {
                 const uint32_t rl = NXG_ENC_PF ? q_rl : lst_row[e];
                 const uint64_t r = rt + rl;
                 const Slot v = NXG_ENC_PF ? q_v : get_slot(c, true, r);
@@ -773,10 +738,10 @@ __global__ __launch_bounds__(TPB, NXG_ENC_OCC) void nxg_enc_rows_kernel(
 #pragma unroll
             for (int k = 0; k < GRPT; k++) ntg[k] = rn + k < n ? c.tag[rn + k] : 0u;
         }
-        // 3b. the tile's base: look-back over the tiles' byte counts (with the staging: by wave 0
-        //     while the other waves stage, NXG_ENC_LBW)
+        // 3b. the tile's base: look-back over the tiles' byte counts (wave 0; running it while
+        //     the other waves stage measured slower, 0.281 vs 0.245 ms)
         ESTAMP(4);
-        if (!(stage && NXG_ENC_LBW) && tid < 64) lookback();
+        if (tid < 64) lookback();
         __syncthreads();
         ESTAMP(5);
         const uint64_t tbase = sh_base + arch_base;
