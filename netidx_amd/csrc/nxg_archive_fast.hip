@@ -47,6 +47,12 @@ constexpr uint32_t PRE = NXG_FA_PRE;      // count image: bytes before the tile 
 #ifndef NXG_FA_WIN
 #define NXG_FA_WIN 1  // text / varint lengths from the item's own window in the item walks
 #endif
+#ifndef NXG_FA_SKIP
+#define NXG_FA_SKIP 1  // the chain loop jumps over chunks whose own walks continue the chain
+#endif
+#ifndef NXG_FA_RK
+#define NXG_FA_RK 1  // an entry inside the spec walk's last run takes that run's tail, arrays included
+#endif
 #ifndef NXG_FA_STRIDE
 #define NXG_FA_STRIDE 1  // array elements by stride speculation in the item walks
 #endif
@@ -265,7 +271,8 @@ NXG_DEV uint64_t item_cands(lds_bytes img, uint32_t c) {
 // there to the exit parsed in a row); rbits / rkids: that run's item starts (bit i = cb + i) and
 // child slots.
 NXG_DEV uint32_t spec_walk(lds_bytes img, uint32_t x0, uint32_t cb, uint32_t end, uint32_t wl,
-                           uint32_t& first, uint64_t cm, uint64_t& rbits, uint32_t& rkids) {
+                           uint32_t& first, uint64_t cm, uint64_t& rbits, uint32_t& rkids,
+                           uint64_t& rabits) {
     auto next = [&](uint32_t p) -> uint32_t {  // the first candidate at or after p
         const uint32_t d = p - cb;
         const uint64_t rest = d < 64 ? cm & (~0ull << d) : 0ull;
@@ -275,6 +282,7 @@ NXG_DEV uint32_t spec_walk(lds_bytes img, uint32_t x0, uint32_t cb, uint32_t end
     first = x;
     rbits = 0;
     rkids = 0;
+    rabits = 0;
 #pragma unroll 1
     while (x < end) {
         uint32_t k;
@@ -284,13 +292,25 @@ NXG_DEV uint32_t spec_walk(lds_bytes img, uint32_t x0, uint32_t cb, uint32_t end
             first = x;
             rbits = 0;
             rkids = 0;
+            rabits = 0;
             continue;
         }
-        if (x - cb < 64) rbits |= 1ull << (x - cb);
+        if (x - cb < 64) {
+            rbits |= 1ull << (x - cb);
+            if (k) rabits |= 1ull << (x - cb);  // an Array with elements
+        }
         rkids += k;
         x = e;
     }
     return x;
+}
+
+// the element count of the Array item at image offset p (its Id varint, tag 19, the count byte)
+NXG_DEV uint32_t arr_count(lds_bytes img, uint32_t p) {
+    const Win16 w = win16(img, p);
+    const uint64_t stop = ~w.lo & 0x8080808080808080ull;
+    const uint32_t k = (uint32_t)__builtin_ctzll(stop) >> 3;  // (< 5: the walk parsed it)
+    return (uint32_t)(w.lo >> (8 * (k + 2))) & 0xffu;
 }
 
 // The tile's chain from entry E (uniform; image offsets, chunk j at PRE + 64 j, the tile's end at
@@ -305,13 +325,19 @@ NXG_DEV FaDesc chain_from(lds_bytes img, uint32_t E, uint32_t lim, uint32_t wl, 
     // synchronised): the chain is the lanes' own walks, from one ballot. Otherwise the uniform
     // loop below takes over from the first chunk that is not.
     uint32_t j0 = 0;
+    uint64_t badm;  // chunks not entered at their guess (or whose walk broke)
+    bool cov;       // an item covers the lane's whole chunk
+    uint32_t jact;  // the last chunk in the tile
     {
         const uint32_t cl = PRE + lane * CH;
         const bool act = cl < lim;
         const uint32_t xp = (uint32_t)__shfl_up((int)X, 1, 64);
         const uint32_t pin = lane == 0 ? E : xp;  // where the chain enters the lane's chunk
-        const bool cov = pin >= min(cl + CH, lim);  // an item covers the whole chunk
+        cov = pin >= min(cl + CH, lim);
         const uint64_t bad = __ballot(act && !(pin == A && X != FAIL));
+        badm = bad;
+        const uint64_t am0 = __ballot(act);
+        jact = am0 ? 63u - (uint32_t)__builtin_clzll(am0) : 0u;
         j0 = bad ? (uint32_t)__builtin_ctzll(bad) : TILE / CH;
 #if NXG_FA_PROF
         if (prof && bad) prof[10]++;
@@ -337,6 +363,18 @@ NXG_DEV FaDesc chain_from(lds_bytes img, uint32_t E, uint32_t lim, uint32_t wl, 
                 break;
             }
             x = Xj;
+            if (NXG_FA_SKIP) {
+                // the chunks up to the next off-guess one continue the chain with their own
+                // walks (each entered at its guess, which its predecessor's walk reaches): as on
+                // the ballot path
+                const uint64_t rest = badm & ~(~0ull >> (63 - j));  // off-guess chunks after j
+                const uint32_t jn = min(rest ? (uint32_t)__builtin_ctzll(rest) : 64u, jact + 1);
+                if (jn > j + 1) {
+                    if (lane > j && lane < jn && !cov) ce = A;
+                    x = (uint32_t)__builtin_amdgcn_readlane((int)X, (int)(jn - 1));
+                    j = jn - 1;
+                }
+            }
         } else {  // entered off the guess: every lane walks it (uniform addresses)
 #if NXG_FA_PROF
             if (prof) prof[11]++;
@@ -399,9 +437,9 @@ NXG_DEV FaDesc count_tile(lds_bytes img, uint64_t t, uint64_t W, uint32_t E, uin
     const uint32_t wl = PRE + (uint32_t)min<uint64_t>(W - t0, 0xffffffffull - PRE);
     const uint32_t c = PRE + lane * CH, end = min(c + CH, lim);
     uint32_t first, rkids = 0;
-    uint64_t rbits = 0;
+    uint64_t rbits = 0, rabits = 0;
     const uint32_t g = c < lim ? spec_walk(img, c, c, end, wl, first, item_cands((lds_bytes)img, c),
-                                           rbits, rkids)
+                                           rbits, rkids, rabits)
                                : c;
     FAP(1);
     uint32_t ge = 0;
@@ -413,10 +451,10 @@ NXG_DEV FaDesc count_tile(lds_bytes img, uint64_t t, uint64_t W, uint32_t E, uin
         constexpr uint32_t NQ = PRE / CH;
         static_assert(PRE % CH == 0 && NQ >= 1 && NQ <= 8, "whole chunks before the tile");
         uint32_t fq = 0, kq = 0;
-        uint64_t bq = 0;
+        uint64_t bq = 0, aq = 0;
         if (lane < NQ) {
             const uint32_t cb = lane * CH;
-            ge = spec_walk(img, cb, cb, cb + CH, wl, fq, item_cands((lds_bytes)img, cb), bq, kq);
+            ge = spec_walk(img, cb, cb, cb + CH, wl, fq, item_cands((lds_bytes)img, cb), bq, kq, aq);
         }
         uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)ge, 0);
 #pragma unroll 1
@@ -433,8 +471,9 @@ NXG_DEV FaDesc count_tile(lds_bytes img, uint64_t t, uint64_t W, uint32_t E, uin
                 continue;
             }
             uint32_t f2 = 0, k2 = 0, g2 = 0;
-            uint64_t b2 = 0;
-            if (lane == 0) g2 = spec_walk(img, x, cq, cq + CH, wl, f2, item_cands((lds_bytes)img, cq), b2, k2);
+            uint64_t b2 = 0, a2 = 0;
+            if (lane == 0)
+                g2 = spec_walk(img, x, cq, cq + CH, wl, f2, item_cands((lds_bytes)img, cq), b2, k2, a2);
             x = (uint32_t)__builtin_amdgcn_readlane((int)g2, 0);
         }
         E = x;
@@ -452,10 +491,17 @@ NXG_DEV FaDesc count_tile(lds_bytes img, uint64_t t, uint64_t W, uint32_t E, uin
         // entered at an item of the spec walk's last unbroken run: the exact walk from there is
         // that run (the same parses), so its counts are the run's
         const uint32_t d = A - c;
-        if (d < 64 && ((rbits >> d) & 1ull) && (A == first || rkids == 0)) {
+        if (d < 64 && ((rbits >> d) & 1ull) && (A == first || rkids == 0 || NXG_FA_RK)) {
             bits = rbits & (~0ull << d);
             n = (uint32_t)__popcll(bits);
             kids = rkids;
+            if (NXG_FA_RK && A != first && rkids) {
+                // the run's tail from A: the element counts of its Arrays at or after A
+                kids = 0;
+#pragma unroll 1
+                for (uint64_t m = rabits & (~0ull << d); m; m &= m - 1)
+                    kids += arr_count(img, c + (uint32_t)__builtin_ctzll(m));
+            }
             X = g;
         } else {
 #if NXG_FA_PROF
