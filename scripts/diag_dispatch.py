@@ -14,7 +14,8 @@ n = int(sys.argv[1]) if len(sys.argv) > 1 else 10_000_000
 n_chans = int(sys.argv[2]) if len(sys.argv) > 2 else 16
 codec = netidx_amd.Codec(0)
 rng = np.random.default_rng(1)
-ids = torch.from_numpy(rng.permutation(n).astype(np.int64)).cuda()
+order = sys.argv[3] if len(sys.argv) > 3 else "random"
+ids = torch.from_numpy((np.arange(n) if order == "seq" else rng.permutation(n)).astype(np.int64)).cuda()
 tab = netidx_amd.SubTable(np.arange(n, dtype=np.uint32), rng.integers(0, 2**63, n, dtype=np.uint64),
                           np.arange(n + 1, dtype=np.uint32),
                           rng.integers(0, n_chans, n, dtype=np.uint32),
@@ -27,4 +28,4 @@ for _ in range(10):
     d = codec.dispatch_updates(tab, ids, n, cap=n)
 torch.cuda.synchronize()
 print(f"n={n} chans={n_chans} call={(time.perf_counter() - t0) / 10 * 1e3:.3f} ms "
-      f"entries={d.n_entries}", flush=True)
+      f"entries={d.n_entries} ids={order}", flush=True)

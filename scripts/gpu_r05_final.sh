@@ -8,3 +8,4 @@ export TMPDIR=/tmp
 TAG=${TAG:-r05z} scripts/gpu_r04b.sh || exit 1
 scripts/profile_cmd.sh ${TAG:-r05z}_bench python3 $R/bench.py --no-extras --cpu-seconds 2 --steps 100 || exit 1
 tail -3 gpurun_out/prof_${TAG:-r05z}_bench/trace.log
+scripts/gpu_r05h.sh || exit 1
