@@ -1592,7 +1592,7 @@ bool nxg_publish_commit(NxgCtx* c, const NxgPubTable* tab, const NxgColumns* bat
     }
     const NxgPubBatch b{batch->id,    batch->tag,   batch->fixed, batch->aux, batch->ctag,
                         batch->cfixed, batch->caux, heap,         kind,       n};
-    HIPCHK(nxg_launch_pub_stage1(*tab, b, c->dscratch, c->stream));
+    HIPCHK(nxg_launch_pub_stage1(*tab, b, c->dscratch, c->ncu, c->stream));
     uint32_t flags[4] = {0, 0, 0, 0};
     HIPCHK(hipMemcpyAsync(flags, nxg_pub_flags(c->dscratch), 12, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));

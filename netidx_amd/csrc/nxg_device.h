@@ -123,6 +123,17 @@ NXG_DEV uint32_t wave_min_u32(uint32_t x) {
     return (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
 }
 
+// wave OR (uniform), the same DPP pattern with 0 as the identity
+NXG_DEV uint32_t wave_or_u32(uint32_t x) {
+    x |= dpp0<0x111, 0xf>(x);
+    x |= dpp0<0x112, 0xf>(x);
+    x |= dpp0<0x114, 0xf>(x);
+    x |= dpp0<0x118, 0xf>(x);
+    x |= dpp0<0x142, 0xa>(x);
+    x |= dpp0<0x143, 0xc>(x);
+    return (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+}
+
 // the next lane's value (lane 63: 0) -- DPP wave_shl:1
 NXG_DEV uint32_t wave_next(uint32_t v) { return dpp0<0x130, 0xf>(v); }
 

@@ -202,7 +202,7 @@ struct NxgPubBatch {
 };
 uint64_t nxg_pub_scratch_bytes(uint64_t n, uint64_t n_slots);
 hipError_t nxg_launch_pub_stage1(const NxgPubTable& tb, const NxgPubBatch& b, uint8_t* scratch,
-                                 hipStream_t s);
+                                 int ncu, hipStream_t s);
 const uint32_t* nxg_pub_flags(uint8_t* scratch);
 hipError_t nxg_launch_pub_stage2(const NxgPubTable& tb, const NxgPubBatch& b, uint8_t* scratch,
                                  bool dup, bool changed, int ncu, hipStream_t s,

@@ -20,6 +20,8 @@
 // compared by an explicit stack (no device recursion), off the scalar path. Map entries are
 // compared in column order: the reference's encoder writes a map's entries sorted by key and
 // unique, so two encodings of equal maps hold the same entries in the same order.
+#include <algorithm>
+
 #include "nxg_device.h"
 #include "nxg_internal.h"
 
@@ -220,18 +222,50 @@ NXG_DEV uint32_t slot_of(const NxgPubTable& tb, uint64_t x) {
 // exist; flags[2]: a value nested deeper than MAX_DEPTH, or a container without child columns;
 // flags[3]: some UpdateChanged row compares a Decimal, container or Abstract (nxg_pub_deep_kernel)
 __global__ __launch_bounds__(TPB) void nxg_pub_count_kernel(NxgPubTable tb, PubIn in,
-                                                            uint32_t* __restrict__ cnt,
+                                                            uint32_t* __restrict__ bm,
                                                             uint32_t* __restrict__ flags) {
-    const uint64_t i = (uint64_t)blockIdx.x * TPB + threadIdx.x;
+    // a slot seen twice: its bit in the slot bitmap `bm` (zeroed) already set. 64 rows at a
+    // time: when their slots fall in a few runs of equal bitmap words (Ids in order: 2-3 words
+    // per 64 rows) each run's bits go in with one atomic from its first lane, otherwise one per
+    // lane. A bounded grid strides over the rows, so the two flag words are touched once per
+    // wave, not once per 64 rows (every wave of a one-row-per-thread grid reading one flag word
+    // made that word's L2 channel the kernel's bound: 147 us at 10^7 rows).
+    const uint32_t lane = threadIdx.x & 63;
     bool dup = false, chg = false;
-    if (i < in.n && in.kind[i] != NXG_PUB_UPDATE_CLIENT) {
-        chg = in.kind[i] == NXG_PUB_UPDATE_CHANGED;
-        const uint32_t s = slot_of(tb, in.id[i]);
-        if (s != NONE) dup = atomicAdd(&cnt[s], 1u) != 0;
+#pragma unroll 1
+    for (uint64_t i = (uint64_t)blockIdx.x * TPB + threadIdx.x; i - lane < in.n;
+         i += (uint64_t)gridDim.x * TPB) {
+        uint32_t s = NONE;
+        if (i < in.n && in.kind[i] != NXG_PUB_UPDATE_CLIENT) {
+            chg |= in.kind[i] == NXG_PUB_UPDATE_CHANGED;
+            s = slot_of(tb, in.id[i]);
+        }
+        const bool v = s != NONE;
+        const uint32_t wd = v ? s >> 5 : NONE, bit = v ? 1u << (s & 31u) : 0u;
+        const uint32_t pw = (uint32_t)__shfl_up((int)wd, 1, 64);
+        const uint64_t heads = __ballot(v && (lane == 0 || pw != wd));
+        if (__popcll(heads) <= 4) {
+#pragma unroll 1
+            for (uint64_t hm = heads; hm; hm &= hm - 1) {
+                const uint32_t h = (uint32_t)__builtin_ctzll(hm);
+                const uint32_t w0 = (uint32_t)__builtin_amdgcn_readlane((int)wd, (int)h);
+                const uint64_t after = hm & (hm - 1);  // the next run starts at the next head
+                const uint32_t hn = after ? (uint32_t)__builtin_ctzll(after) : 64u;
+                const bool in_run = lane >= h && lane < hn && wd == w0;
+                const uint64_t rm = __ballot(in_run);
+                const uint32_t orv = wave_or_u32(in_run ? bit : 0u);
+                uint32_t old = 0;
+                if (lane == h) old = atomicOr(&bm[w0], orv);
+                old = (uint32_t)__builtin_amdgcn_readlane((int)old, (int)h);
+                // a slot twice in the run, or already set
+                if ((uint32_t)__popcll(rm) != (uint32_t)__popc(orv) || (old & orv)) dup = true;
+            }
+        } else if (v) {
+            dup |= (atomicOr(&bm[wd], bit) & bit) != 0;
+        }
     }
-    // one flag word for the whole grid: read it first, so only the first few waves contend
-    if (__any(dup) && (threadIdx.x & 63) == 0 && !ld_agent32(&flags[0])) atomicOr(&flags[0], 1u);
-    if (__any(chg) && (threadIdx.x & 63) == 0 && !ld_agent32(&flags[1])) atomicOr(&flags[1], 1u);
+    if (__any(dup) && lane == 0 && !ld_agent32(&flags[0])) atomicOr(&flags[0], 1u);
+    if (__any(chg) && lane == 0 && !ld_agent32(&flags[1])) atomicOr(&flags[1], 1u);
 }
 
 // radix keys: the slot of every non-directed row with one, else NONE (sorted last, ignored)
@@ -460,14 +494,17 @@ static PubScratch pub_layout(uint8_t* p, uint64_t n, uint64_t n_slots) {
 }
 
 hipError_t nxg_launch_pub_stage1(const NxgPubTable& tb, const NxgPubBatch& b, uint8_t* scratch,
-                                 hipStream_t s) {
+                                 int ncu, hipStream_t s) {
     PubScratch sc = pub_layout(scratch, b.n_rows, tb.n_slots);
     const PubIn in{b.id, b.kind, b.n_rows, {b.tag, b.fixed, b.aux, b.ctag, b.cfixed, b.caux, b.heap}};
     hipError_t e;
     if ((e = hipMemsetAsync(sc.flags, 0, 64, s)) != hipSuccess) return e;
-    if (tb.n_slots && (e = hipMemsetAsync(sc.cnt, 0, 4 * tb.n_slots, s)) != hipSuccess) return e;
+    if (tb.n_slots && (e = hipMemsetAsync(sc.cnt, 0, 4 * ((tb.n_slots + 31) / 32), s)) != hipSuccess)
+        return e;  // (the slot bitmap)
     if (b.n_rows)
-        hipLaunchKernelGGL(nxg_pub_count_kernel, dim3((uint32_t)((b.n_rows + TPB - 1) / TPB)),
+        hipLaunchKernelGGL(nxg_pub_count_kernel,
+                           dim3((uint32_t)std::min<uint64_t>((b.n_rows + TPB - 1) / TPB,
+                                                             (uint64_t)ncu * 8)),
                            dim3(TPB), 0, s, tb, in, sc.cnt, sc.flags);
     return hipGetLastError();
 }
