@@ -36,6 +36,10 @@
 
 #include "nxg_fmx_common.h"
 
+#ifndef NXG_FF_CHECK
+#define NXG_FF_CHECK 1  // emit waves skip a batch already declined (one agent-scope load each)
+#endif
+
 namespace fa {
 constexpr uint32_t UNSUB = 0x40;         // Event::Unsubscribed (subscriber/mod.rs:168)
 constexpr uint32_t BROKEN = 0x80000000u;  // FaDesc.items: the chain stops at `exit`
@@ -778,7 +782,7 @@ __global__ __launch_bounds__(TPB) void nxg_fa_emit_kernel(
     if (rb + items < count && ((d.items & BROKEN) || t + 1 == nt)) bad = true, why |= 2u;
     const uint32_t nm = (uint32_t)min<uint64_t>(items, count - rb);  // the batch's items here
     uint64_t cnext = base >> 32;
-    if (ld_agent32(&hp->fast_fail)) return;
+    if (NXG_FF_CHECK && ld_agent32(&hp->fast_fail)) return;
     tile_store(img, g, lane);
     const uint32_t n0 = (uint32_t)__popcll(bits);
     uint32_t at = wave_incl_scan<uint32_t>(n0) - n0;
