@@ -940,62 +940,80 @@ def extras_multi_gpu(codec, world, rank, stream):
     from netidx_amd import shard, synth
     from netidx_amd.codec import Columns
     total = 100_000_000
+    ex = {}
+    # Each leg catches its own failure, after the leg's collectives (the library's protocols fail
+    # on every rank at the same step; the checks run after the timing's all-reduce), so one
+    # failing leg is reported and the ranks go on to the next leg together.
+    comm = None
+    dout = None
+    W = 0
     b, e = shard.shard_range(total, world, rank)
     n = e - b
-    ids, vals = synth.f64_columns(n, synth.SEED_8GPU, id_offset=b)
-    cols = netidx_amd.columns_from_arrays(ids, vals)
-    cap = 15 * total + 64
-    dout = torch.empty(cap, dtype=torch.uint8, device="cuda")
-    comm = make_comm(codec, world, rank, [dout])
     via = ("rccl (nxg_encode_allgather)" if BACKEND != "gloo" else
            "gloo transport via nxg_comm_init_ops (nxg_encode_allgather)")
+    try:
+        ids, vals = synth.f64_columns(n, synth.SEED_8GPU, id_offset=b)
+        cols = netidx_amd.columns_from_arrays(ids, vals)
+        del ids, vals
+        cap = 15 * total + 64
+        dout = torch.empty(cap, dtype=torch.uint8, device="cuda")
+        comm = make_comm(codec, world, rank, [dout])
 
-    def encode_gather():
-        return comm.encode_allgather(cols, None, dout.data_ptr(), cap)
+        def encode_gather():
+            return comm.encode_allgather(cols, None, dout.data_ptr(), cap)
 
-    times = []
-    for it in range(3):
-        barrier(world)
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        W, offs = encode_gather()
-        torch.cuda.synchronize()
-        times.append(time.perf_counter() - t0)
-    t = max_over_ranks(min(times), world)
-    # check: this rank's shard where it belongs, and the frame's length is the whole batch's
-    assert W == 1_497_886_336, W
-    ex = {"encode_allgather_1e8": {"records": total, "wire_bytes": W, "world": world, "via": via,
-                                   "encode_allgather_ms": round(t * 1e3, 3),
-                                   "M_updates_s": round(total / t / 1e6, 1)}}
-    del cols
+        times = []
+        for it in range(3):
+            barrier(world)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            W, offs = encode_gather()
+            torch.cuda.synchronize()
+            times.append(time.perf_counter() - t0)
+        t = max_over_ranks(min(times), world)
+        del cols
+        # check: the frame's length is the whole batch's
+        assert W == 1_497_886_336, W
+        ex["encode_allgather_1e8"] = {"records": total, "wire_bytes": W, "world": world,
+                                      "via": via, "encode_allgather_ms": round(t * 1e3, 3),
+                                      "M_updates_s": round(total / t / 1e6, 1)}
+    except Exception as err:
+        ex["encode_allgather_1e8"] = {"error": repr(err)}
     # the one frame decoded in byte ranges (strong scaling)
-    out = Columns(n + 2 * total // world // 100 + 1024, 0, 0, netidx_amd.LAYOUT_F64, "cuda")
+    if comm is not None and W:
+        try:
+            out = Columns(n + 2 * total // world // 100 + 1024, 0, 0, netidx_amd.LAYOUT_F64, "cuda")
 
-    def decode_ranges():
-        return comm.decode_sharded(dout, W, out)
+            def decode_ranges():
+                return comm.decode_sharded(dout, W, out)
 
-    decode_ranges()
-    times = []
-    for it in range(5):
-        barrier(world)
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        row_off, rng = decode_ranges()
-        torch.cuda.synchronize()
-        times.append(time.perf_counter() - t0)
-    t = max_over_ranks(min(times), world)
-    nr = int(rng.n_rows)
-    # checker: rows [row_off, row_off + nr) of the batch (ids are the global row numbers)
-    got_id = out.id[:nr].cpu().numpy().view(np.uint64)
-    got_val = out.fixed[:nr].cpu().numpy().view(np.uint64)
-    assert np.array_equal(got_id, np.arange(row_off, row_off + nr, dtype=np.uint64))
-    _, want_val = synth.f64_columns(nr, synth.SEED_8GPU, id_offset=row_off)
-    assert np.array_equal(got_val, want_val), "range decode is not bit-exact"
-    ex["decode_f64_1e8_byte_ranges"] = {
-        "records": total, "world": world, "via": via.replace("nxg_encode_allgather",
-                                                              "nxg_decode_sharded"),
-        "ms_slowest_rank": round(t * 1e3, 4), "M_updates_s": round(total / t / 1e6, 1)}
-    del dout, out
+            decode_ranges()
+            times = []
+            for it in range(5):
+                barrier(world)
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                row_off, rng = decode_ranges()
+                torch.cuda.synchronize()
+                times.append(time.perf_counter() - t0)
+            t = max_over_ranks(min(times), world)
+            nr = int(rng.n_rows)
+            # checker: rows [row_off, row_off + nr) of the batch (ids are the global row numbers)
+            got_id = out.id[:nr].cpu().numpy().view(np.uint64)
+            got_val = out.fixed[:nr].cpu().numpy().view(np.uint64)
+            assert np.array_equal(got_id, np.arange(row_off, row_off + nr, dtype=np.uint64))
+            _, want_val = synth.f64_columns(nr, synth.SEED_8GPU, id_offset=row_off)
+            assert np.array_equal(got_val, want_val), "range decode is not bit-exact"
+            ex["decode_f64_1e8_byte_ranges"] = {
+                "records": total, "world": world,
+                "via": via.replace("nxg_encode_allgather", "nxg_decode_sharded"),
+                "ms_slowest_rank": round(t * 1e3, 4), "M_updates_s": round(total / t / 1e6, 1)}
+            del out
+        except Exception as err:
+            ex["decode_f64_1e8_byte_ranges"] = {"error": repr(err)}
+    if comm is not None:
+        comm.close()
+    del dout
     torch.cuda.empty_cache()
     # config 3 per GPU (weak scaling): each rank decodes its own 10^7-record mixed batch
     nm = 10_000_000
@@ -1003,58 +1021,64 @@ def extras_multi_gpu(codec, world, rank, stream):
     mc = netidx_amd.columns_from_arrays(m.id, m.fixed, m.tag, m.aux, m.ctag, m.cfixed, m.caux)
     heap = torch.from_numpy(m.heap.copy()).cuda()
     wire = codec.encode_batch(mc, heap)
-    out = Columns(nm + 1, len(m.ctag) + 1, 1, netidx_amd.LAYOUT_MIXED, "cuda")
-    wall, kms, st = time_decode(codec, wire, out, nm, 5, 1, world, stream,
-                                flags=netidx_amd.HINT_MIXED)
-    assert st.path == 4 and st.n_rows == nm and st.err_kind == 0, st
-    # every column equals the encode input it was made from (the encoder is the oracle's, checked
-    # byte for byte on rank 0 in the N=1 extras)
-    nc = len(m.ctag)
-    for k in ("id", "tag", "aux"):
-        assert torch.equal(out.t[k][:nm], mc.t[k][:nm]), f"mixed decode differs in column {k}"
-    for k in ("ctag", "cfixed", "caux"):
-        assert torch.equal(out.t[k][:nc], mc.t[k][:nc]), f"mixed decode differs in column {k}"
-    # fixed: the value for scalars; for text the frame offset of the bytes (the input's is a heap
-    # offset), so the text itself is compared
-    txt = out.tag[:nm] == 12
-    assert torch.equal(out.fixed[:nm][~txt], mc.fixed[:nm][~txt]), "mixed decode differs in fixed"
-    lens = out.aux[:nm][txt].long()
-    rep = torch.repeat_interleave(torch.arange(len(lens), device=lens.device), lens)
-    pos = torch.arange(int(lens.sum()), device=lens.device) - (torch.cumsum(lens, 0) - lens)[rep]
-    assert torch.equal(wire[out.fixed[:nm][txt][rep] + pos], heap[mc.fixed[:nm][txt][rep] + pos]), \
-        "mixed decode differs in text bytes"
-    kmax = max_over_ranks(kms, world)
-    ex["decode_mixed_1e7_per_gpu"] = {
-        "records_per_gpu": nm, "world": world, "kernel_ms_slowest_rank": round(kmax, 4),
-        "M_updates_s": round(world * nm / (kmax / 1e3) / 1e6, 1)}
+    try:
+        out = Columns(nm + 1, len(m.ctag) + 1, 1, netidx_amd.LAYOUT_MIXED, "cuda")
+        wall, kms, st = time_decode(codec, wire, out, nm, 5, 1, world, stream,
+                                    flags=netidx_amd.HINT_MIXED)
+        kmax = max_over_ranks(kms, world)
+        assert st.path == 4 and st.n_rows == nm and st.err_kind == 0, st
+        # every column equals the encode input it was made from (the encoder is the oracle's,
+        # checked byte for byte on rank 0 in the N=1 extras)
+        nc = len(m.ctag)
+        for k in ("id", "tag", "aux"):
+            assert torch.equal(out.t[k][:nm], mc.t[k][:nm]), f"mixed decode differs in column {k}"
+        for k in ("ctag", "cfixed", "caux"):
+            assert torch.equal(out.t[k][:nc], mc.t[k][:nc]), f"mixed decode differs in column {k}"
+        # fixed: the value for scalars; for text the frame offset of the bytes (the input's is a
+        # heap offset), so the text itself is compared
+        txt = out.tag[:nm] == 12
+        assert torch.equal(out.fixed[:nm][~txt], mc.fixed[:nm][~txt]), "mixed decode differs in fixed"
+        lens = out.aux[:nm][txt].long()
+        rep = torch.repeat_interleave(torch.arange(len(lens), device=lens.device), lens)
+        pos = torch.arange(int(lens.sum()), device=lens.device) - (torch.cumsum(lens, 0) - lens)[rep]
+        assert torch.equal(wire[out.fixed[:nm][txt][rep] + pos], heap[mc.fixed[:nm][txt][rep] + pos]), \
+            "mixed decode differs in text bytes"
+        ex["decode_mixed_1e7_per_gpu"] = {
+            "records_per_gpu": nm, "world": world, "kernel_ms_slowest_rank": round(kmax, 4),
+            "M_updates_s": round(world * nm / (kmax / 1e3) / 1e6, 1)}
+        del out
+    except Exception as err:
+        ex["decode_mixed_1e7_per_gpu"] = {"error": repr(err)}
     # config 3 strong-scaled: the SAME 10^7-record mixed frame (one connection's batch, as every
     # rank holds config 5's frame after the all-gather) decoded in N byte ranges, one per GPU
     # (nxg_decode_sharded: the fast mixed decoder in range mode, ranges linked)
-    comm.close()
-    comm = make_comm(codec, world, rank, [wire])
-    W = wire.numel()
-    sout = Columns.for_frame(W // world + 65536, netidx_amd.LAYOUT_MIXED, "cuda")
+    try:
+        comm = make_comm(codec, world, rank, [wire])
+        Wm = wire.numel()
+        sout = Columns.for_frame(Wm // world + 65536, netidx_amd.LAYOUT_MIXED, "cuda")
 
-    def decode_mixed_ranges():
-        return comm.decode_sharded(wire, W, sout)
+        def decode_mixed_ranges():
+            return comm.decode_sharded(wire, Wm, sout)
 
-    decode_mixed_ranges()
-    times = []
-    for it in range(5):
-        barrier(world)
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        row_off, rng = decode_mixed_ranges()
-        torch.cuda.synchronize()
-        times.append(time.perf_counter() - t0)
-    t = max_over_ranks(min(times), world)
-    check_mixed_range(wire, heap, mc, sout, row_off, rng, nm)
-    ex["decode_mixed_1e7_byte_ranges"] = {
-        "records": nm, "world": world, "wire_bytes": W, "range_path": int(rng.ok),
-        "via": ("rccl" if BACKEND != "gloo" else "gloo transport via nxg_comm_init_ops") +
-               " (nxg_decode_sharded: fast mixed decoder in range mode)",
-        "ms_slowest_rank": round(t * 1e3, 4), "M_updates_s": round(nm / t / 1e6, 1)}
-    comm.close()
+        decode_mixed_ranges()
+        times = []
+        for it in range(5):
+            barrier(world)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            row_off, rng = decode_mixed_ranges()
+            torch.cuda.synchronize()
+            times.append(time.perf_counter() - t0)
+        t = max_over_ranks(min(times), world)
+        comm.close()
+        check_mixed_range(wire, heap, mc, sout, row_off, rng, nm)
+        ex["decode_mixed_1e7_byte_ranges"] = {
+            "records": nm, "world": world, "wire_bytes": Wm, "range_path": int(rng.ok),
+            "via": ("rccl" if BACKEND != "gloo" else "gloo transport via nxg_comm_init_ops") +
+                   " (nxg_decode_sharded: fast mixed decoder in range mode)",
+            "ms_slowest_rank": round(t * 1e3, 4), "M_updates_s": round(nm / t / 1e6, 1)}
+    except Exception as err:
+        ex["decode_mixed_1e7_byte_ranges"] = {"error": repr(err)}
     return ex
 
 
@@ -1204,7 +1228,10 @@ def main():
                 "sample": f"full {n}-record frame cut at record boundaries into 16 sub-frames, "
                           f"decoded {reps}x ({secs:.1f} s) by oracle/nx_oracle.c on 16 threads"}
     elif world > 1 and not args.no_extras:
-        ex = extras_multi_gpu(codec, world, rank, stream)
+        try:
+            ex = extras_multi_gpu(codec, world, rank, stream)
+        except Exception as e:  # report, never lose the line (each leg catches its own below)
+            ex = {"error": repr(e)}
         if rank == 0:
             line["extras"] = ex
     if rank == 0:
