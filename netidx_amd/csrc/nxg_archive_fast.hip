@@ -857,10 +857,10 @@ __global__ __launch_bounds__(TPB) void nxg_fa_emit_kernel(
         }
         const uint64_t row = rb + i;
         if (has) {
-            cols.id[row] = (uint32_t)id;  // Id(decode_varint as u32) (logfile/mod.rs:162-164)
-            cols.tag[row] = (uint8_t)o.tag;
-            cols.fixed[row] = arr ? cnext + kpre : o.fixed;
-            cols.aux[row] = o.aux;
+            col_st(&cols.id[row], (uint64_t)(uint32_t)id);  // Id(decode_varint as u32) (logfile/mod.rs:162-164)
+            col_st(&cols.tag[row], (uint8_t)o.tag);
+            col_st(&cols.fixed[row], (uint64_t)(arr ? cnext + kpre : o.fixed));
+            col_st(&cols.aux[row], (uint32_t)o.aux);
             if (row + 1 == count) {  // the batch's last item: where it ends
                 const uint32_t nx = i + 1 < items ? (uint32_t)msg[i + 1] : d.exit;
                 hp->end = t0 + nx + 1;

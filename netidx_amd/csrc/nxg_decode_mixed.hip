@@ -885,10 +885,10 @@ __global__ __launch_bounds__(TPB) void nxg_fmx_emit_kernel(
                 hnext += nh;
             }
             if (upd && !(NXG_FMX_SKIP & 8)) {
-                cols.id[row] = id;
-                cols.tag[row] = (uint8_t)o.tag;
-                cols.fixed[row] = o.tag == 19u ? cnext + kpre : o.fixed;
-                cols.aux[row] = o.aux;
+                col_st(&cols.id[row], (uint64_t)id);
+                col_st(&cols.tag[row], (uint8_t)o.tag);
+                col_st(&cols.fixed[row], (uint64_t)(o.tag == 19u ? cnext + kpre : o.fixed));
+                col_st(&cols.aux[row], (uint32_t)o.aux);
             }
             PMARK(3);
             if (rk == 0 || (NXG_FMX_SKIP & 1)) {

@@ -6,6 +6,14 @@
 #include "nxg_msg.h"
 
 namespace fmx {
+#ifndef NXG_COL_NT
+#define NXG_COL_NT 1  // column stores of the emit passes nontemporal (rows are not read again here)
+#endif
+template <typename T>
+NXG_DEV void col_st(T* p, T v) {
+    if (NXG_COL_NT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
 constexpr uint32_t TILE = 4096;
 constexpr uint32_t CH = 64;
 constexpr uint32_t IMG = TILE + 256;    // image: the tile + 256 B
@@ -508,9 +516,9 @@ NXG_DEV bool round_elements(uint8_t* img, uint8_t* mark, uint32_t* el, uint32_t 
                 if (bad) break;
                 const uint64_t slot = cnext + j;
                 if (he && slot < cols.cap_children) {
-                    cols.ctag[slot] = (uint8_t)e.tag;
-                    cols.cfixed[slot] = e.fixed;
-                    cols.caux[slot] = e.aux;
+                    col_st(&cols.ctag[slot], (uint8_t)e.tag);
+                    col_st(&cols.cfixed[slot], (uint64_t)e.fixed);
+                    col_st(&cols.caux[slot], (uint32_t)e.aux);
                 }
             }
             wave_lds_order();
@@ -589,9 +597,9 @@ NXG_DEV bool round_elements(uint8_t* img, uint8_t* mark, uint32_t* el, uint32_t 
             if (bad) break;
             const uint64_t slot = cnext + j;
             if (he && slot < cols.cap_children) {
-                cols.ctag[slot] = (uint8_t)e.tag;
-                cols.cfixed[slot] = e.fixed;
-                cols.caux[slot] = e.aux;
+                col_st(&cols.ctag[slot], (uint8_t)e.tag);
+                col_st(&cols.cfixed[slot], (uint64_t)e.fixed);
+                col_st(&cols.caux[slot], (uint32_t)e.aux);
             }
         }
         wave_lds_order();
@@ -608,9 +616,9 @@ NXG_DEV bool round_elements(uint8_t* img, uint8_t* mark, uint32_t* el, uint32_t 
             ok = e.ok && (!e.slen || utf8_ok(LdsSrc{limg, t0}, t0 + e.soff, e.slen));
             const uint64_t slot = cnext + kpre + c;
             if (ok && slot < cols.cap_children) {
-                cols.ctag[slot] = (uint8_t)e.tag;
-                cols.cfixed[slot] = e.fixed;
-                cols.caux[slot] = e.aux;
+                col_st(&cols.ctag[slot], (uint8_t)e.tag);
+                col_st(&cols.cfixed[slot], (uint64_t)e.fixed);
+                col_st(&cols.caux[slot], (uint32_t)e.aux);
             }
             ep = e.end;
         }
