@@ -37,7 +37,7 @@
 #include "nxg_fmx_common.h"
 
 #ifndef NXG_FF_CHECK
-#define NXG_FF_CHECK 1  // emit waves skip a batch already declined (one agent-scope load each)
+#define NXG_FF_CHECK 1  // emit waves skip a batch already declined
 #endif
 
 namespace fa {
@@ -782,7 +782,9 @@ __global__ __launch_bounds__(TPB) void nxg_fa_emit_kernel(
     if (rb + items < count && ((d.items & BROKEN) || t + 1 == nt)) bad = true, why |= 2u;
     const uint32_t nm = (uint32_t)min<uint64_t>(items, count - rb);  // the batch's items here
     uint64_t cnext = base >> 32;
-    if (NXG_FF_CHECK && ld_agent32(&hp->fast_fail)) return;
+    // a batch already declined by the resolve pass (a plain read: one scalar load per CU, not an
+    // agent-scope load per wave on one address)
+    if (NXG_FF_CHECK && hp->fast_fail) return;
     tile_store(img, g, lane);
     const uint32_t n0 = (uint32_t)__popcll(bits);
     uint32_t at = wave_incl_scan<uint32_t>(n0) - n0;

@@ -44,7 +44,7 @@
 #define NXG_FMX_CAND 7  // candidate rules (A/B timing only): 1 one-byte prefix, 2 Heartbeat, 4 two-byte
 #endif
 #ifndef NXG_FF_CHECK
-#define NXG_FF_CHECK 1  // emit waves skip a frame already declined (one agent-scope load each)
+#define NXG_FF_CHECK 1  // emit waves skip a frame already declined
 #endif
 #ifndef NXG_FMX_LEAN
 #define NXG_FMX_LEAN 1  // the emit's lean rounds for tiles of one-byte-prefix Updates (A/B: 0)
@@ -789,7 +789,9 @@ __global__ __launch_bounds__(TPB) void nxg_fmx_emit_kernel(
     // message ends past this tile offset lie past the frame (long text is checked from global
     // memory where it leaves the image)
     const uint32_t fend = (uint32_t)min<uint64_t>(W - t0, 0xffffffffull);
-    if (NXG_FF_CHECK && ld_agent32(&st->fast_fail)) return;
+    // a frame already declined by the resolve pass (a plain read: one scalar load per CU, not an
+    // agent-scope load per wave on one address)
+    if (NXG_FF_CHECK && st->fast_fail) return;
     tile_store(img, g, lane);
     // the message list in wire order
     const uint32_t n0 = (uint32_t)__popcll(bits);
