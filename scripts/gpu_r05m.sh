@@ -5,4 +5,4 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd $R
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-TAG=r05y scripts/gpu_r05_final2.sh || exit 1
+TAG=${TAG:-r05w} scripts/gpu_r05_final2.sh || exit 1
