@@ -1052,6 +1052,7 @@ def extras_multi_gpu(codec, world, rank, stream):
     # config 3 strong-scaled: the SAME 10^7-record mixed frame (one connection's batch, as every
     # rank holds config 5's frame after the all-gather) decoded in N byte ranges, one per GPU
     # (nxg_decode_sharded: the fast mixed decoder in range mode, ranges linked)
+    comm = None
     try:
         comm = make_comm(codec, world, rank, [wire])
         Wm = wire.numel()
@@ -1070,7 +1071,6 @@ def extras_multi_gpu(codec, world, rank, stream):
             torch.cuda.synchronize()
             times.append(time.perf_counter() - t0)
         t = max_over_ranks(min(times), world)
-        comm.close()
         check_mixed_range(wire, heap, mc, sout, row_off, rng, nm)
         ex["decode_mixed_1e7_byte_ranges"] = {
             "records": nm, "world": world, "wire_bytes": Wm, "range_path": int(rng.ok),
@@ -1079,6 +1079,9 @@ def extras_multi_gpu(codec, world, rank, stream):
             "ms_slowest_rank": round(t * 1e3, 4), "M_updates_s": round(nm / t / 1e6, 1)}
     except Exception as err:
         ex["decode_mixed_1e7_byte_ranges"] = {"error": repr(err)}
+    finally:
+        if comm is not None:
+            comm.close()
     return ex
 
 

@@ -145,7 +145,10 @@ bool nxg_decode_updates(NxgCtx* ctx, const uint8_t* frame, uint64_t len, NxgColu
 /* Asynchronous device-resident variant: enqueue on the ctx stream; no host sync. Only the
  * path selected up front runs (flags). nxg_ctx_sync completes it, runs the general fallback if
  * the homogeneous path rejected the frame, and fills the status. At most 512 async calls
- * (decode and encode together) may be in flight between syncs; the next one fails. */
+ * (decode and encode together) may be in flight between syncs; the next one fails. A frame must
+ * stay unchanged until nxg_ctx_sync: a fallback re-reads it there, after every later call has
+ * run, and a later call of the backlog that wrote into it makes nxg_ctx_sync fail that decode
+ * with an error (it never decodes the overwritten bytes). */
 bool nxg_decode_updates_async(NxgCtx* ctx, const uint8_t* dframe, uint64_t len, NxgColumns* dout,
                               uint32_t flags, NetidxError* err);
 bool nxg_ctx_sync(NxgCtx* ctx, NxgStatus* st, NetidxError* err);

@@ -502,6 +502,13 @@ class Codec:
         lib().nxg_debug_diag(C.c_void_p(self.ctx), a)
         return list(a)
 
+    def last_encode_kernel(self):
+        """Which f64 encoder wrote the last f64 encode (diagnostics, not ABI): "seq" for the
+        sequential-id kernel (nxg_encode_f64_seq.hip), "tile" for the tiled look-back kernel."""
+        f = lib().nxg_debug_enc_kernel
+        f.restype = C.c_uint
+        return {1: "seq", 2: "tile"}.get(f(C.c_void_p(self.ctx)), None)
+
     def decode_async(self, dframe_ptr, nbytes, cols, flags=0):
         err = NetidxError()
         _check(lib().nxg_decode_updates_async(self.ctx, C.c_void_p(dframe_ptr), nbytes,

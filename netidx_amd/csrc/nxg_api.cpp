@@ -80,6 +80,12 @@ struct NxgCtx {
     // skipped for the next kSeqSkipCalls calls (NXG_F64_PATH=run skips it always)
     uint32_t seq_left = 0;
     bool no_seq = false;
+    // the sequential-id f64 encoder (nxg_encode_f64_seq.hip): after it declines a batch (ids not
+    // counting up by one) it is skipped for the next kSeqSkipCalls f64 encodes; NXG_F64_ENC=tile
+    // skips it always
+    uint32_t enc_seq_left = 0;
+    uint32_t last_enc_kernel = 0;  // the last f64 encode: 1 sequential-id kernel, 2 tiled (debug)
+    bool no_enc_seq = false;
     // mixed decode: the fast decoder (nxg_decode_mixed.hip) unless it rejected a recent frame of
     // this connection; then the general decoder for the next kMixFailCalls calls
     // (NXG_MIXED_PATH=general: always the general decoder)
@@ -575,9 +581,20 @@ bool frame_to_device(NxgCtx* c, const uint8_t* frame, uint64_t len, const uint8_
     return true;
 }
 
+// *fast = 1 when the sequential-id f64 encoder was launched (finish_encode then reruns a batch it
+// declines on the tiled encoder); allow_seq = false forces the tiled encoder.
 bool enqueue_encode(NxgCtx* c, const NxgColumns* in, const uint8_t* heap, uint8_t* out,
-                    uint64_t cap, DevStatus* st, NetidxError* err) {
+                    uint64_t cap, DevStatus* st, NetidxError* err, int* fast = nullptr,
+                    bool allow_seq = true) {
+    if (fast) *fast = 0;
     if (in->layout == NXG_LAYOUT_F64) {
+        const bool try_seq = allow_seq && !c->no_enc_seq && in->n_rows > 0;
+        if (try_seq && c->enc_seq_left == 0) {
+            HIPCHK(nxg_launch_enc_f64s(in->id, in->fixed, in->n_rows, out, cap, st, c->stream));
+            if (fast) *fast = 1;
+            return true;
+        }
+        if (try_seq) c->enc_seq_left--;
         const uint64_t nt = nxg_enc_f64_tiles(in->n_rows);
         if (!ensure_tstat(c, nt, err)) return false;
         HIPCHK(nxg_launch_enc_f64(in->id, in->fixed, in->n_rows, out, cap, c->tstat, c->epoch, st,
@@ -595,7 +612,9 @@ bool enqueue_encode(NxgCtx* c, const NxgColumns* in, const uint8_t* heap, uint8_
 
 bool finish_encode(NxgCtx* c, const NxgColumns* in, DevStatus* st, uint32_t slot,
                    uint64_t* len_out, uint64_t cap, bool wrote, NetidxError* err,
-                   bool fetched = false) {
+                   bool fetched = false, int fast = 0, const uint8_t* heap = nullptr,
+                   uint8_t* out = nullptr, bool* redone = nullptr) {
+    if (redone) *redone = false;
     if (!fetched)
         HIPCHK(hipMemcpyAsync(c->hst + slot, st, sizeof(DevStatus), hipMemcpyDeviceToHost,
                               c->stream));
@@ -605,8 +624,24 @@ bool finish_encode(NxgCtx* c, const NxgColumns* in, DevStatus* st, uint32_t slot
                               c->stream));
     if (!fetched || (in->layout == NXG_LAYOUT_MIXED && in->n_ctl))
         HIPCHK(hipStreamSynchronize(c->stream));
-    const DevStatus& h = c->hst[slot];
+    DevStatus h = c->hst[slot];
+    if (fast && h.fast_fail) {
+        // the sequential-id encoder declined (ids that do not count up by one, or past 35 bits):
+        // the tiled encoder, and the sequential one skipped for the next kSeqSkipCalls encodes
+        c->enc_seq_left = kSeqSkipCalls;
+        DevStatus* st2;
+        uint32_t slot2;
+        if (!begin_call(c, &st2, &slot2, err)) return false;
+        const bool ok = enqueue_encode(c, in, heap, out, cap, st2, err, nullptr, false);
+        if (!end_call(c, err) || !ok) return false;
+        if (redone) *redone = true;
+        HIPCHK(hipMemcpyAsync(c->hst + slot2, st2, sizeof(DevStatus), hipMemcpyDeviceToHost,
+                              c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        h = c->hst[slot2];
+    }
     c->last_split = h.split_start;
+    if (in->layout == NXG_LAYOUT_F64) c->last_enc_kernel = fast && !h.fast_fail ? 1u : 2u;
     if (h.timeout) {
         set_err(err, "device look-back watchdog expired");
         return false;
@@ -679,9 +714,10 @@ bool redo_encode(NxgCtx* c, const NxgCtx::Pending& p, const NxgColumns* in, Neti
     DevStatus* st;
     uint32_t slot;
     if (!begin_call(c, &st, &slot, err)) return false;
-    const bool ok = enqueue_encode(c, in, p.heap, p.out, p.cap, st, err);
+    int fast = 0;
+    const bool ok = enqueue_encode(c, in, p.heap, p.out, p.cap, st, err, &fast);
     if (!end_call(c, err) || !ok) return false;
-    return finish_encode(c, in, st, slot, p.len_out, p.cap, true, err);
+    return finish_encode(c, in, st, slot, p.len_out, p.cap, true, err, false, fast, p.heap, p.out);
 }
 
 }  // namespace
@@ -701,6 +737,8 @@ void nxg_debug_status(NxgCtx* c, unsigned long long out[6]) {
     out[4] = h.err_kind;
     out[5] = h.timeout;
 }
+// Not part of the ABI: which f64 encoder wrote the last f64 encode (1 sequential-id, 2 tiled).
+unsigned nxg_debug_enc_kernel(NxgCtx* c) { return c ? c->last_enc_kernel : 0u; }
 void nxg_debug_diag(NxgCtx* c, unsigned long long out[8]) {
     for (int i = 0; i < 8; i++) out[i] = c ? c->last.diag[i] : 0;
 }
@@ -765,6 +803,8 @@ NxgCtx* nxg_ctx_new(int device, NetidxError* err) {
     const char* fp = getenv("NXG_F64_PATH");
     c->force_x = fp && strcmp(fp, "x") == 0;
     c->no_seq = fp && (strcmp(fp, "run") == 0 || strcmp(fp, "x") == 0);
+    const char* fe = getenv("NXG_F64_ENC");
+    c->no_enc_seq = fe && strcmp(fe, "tile") == 0;
     const char* mp = getenv("NXG_MIXED_PATH");
     c->no_fmx = mp && strcmp(mp, "general") == 0;
     const char* fc = getenv("NXG_FMX_COUNT");
@@ -1041,6 +1081,29 @@ bool nxg_ctx_sync(NxgCtx* c, NxgStatus* ust, NetidxError* err) {
                 !dirty.empty() && (overlaps(dirty, w) || overlaps(dirty, {span_of(p.frame, p.len)}));
             NxgStatus s;
             bool redone = false;
+            // write-after-read: a fallback re-reads the frame after every later call has run; if
+            // a later call wrote into the frame (stream-ordered reuse of the buffer as an encode
+            // output or as columns), those bytes are gone -- fail loudly instead of decoding them
+            if (!stale && hs[i].fast_fail && p.len > 0 && p.fast) {
+                const std::vector<Span> fr = {span_of(p.frame, p.len)};
+                bool clobbered = false;
+                for (size_t j = i + 1; j < ps.size() && !clobbered; j++) {
+                    std::vector<Span> wj;
+                    if (ps[j].kind == 1) cols_spans(ps[j].cols, &wj);
+                    else wj.push_back(span_of(ps[j].out, ps[j].cap));
+                    clobbered = overlaps(fr, wj);
+                }
+                if (clobbered) {
+                    if (ok) {
+                        ok = false;
+                        set_err(err, "decode of async call %zu needs its frame again (fallback), "
+                                     "but a later call in the backlog wrote into that frame "
+                                     "buffer; keep a frame unchanged until nxg_ctx_sync",
+                                i);
+                    }
+                    continue;
+                }
+            }
             if (stale) {
                 r = redo_decode(c, p, &s, &e);
                 redone = true;
@@ -1061,12 +1124,31 @@ bool nxg_ctx_sync(NxgCtx* c, NxgStatus* ust, NetidxError* err) {
             const NxgColumns* in = p.cols ? p.cols : &dummy;
             std::vector<Span> rd;
             cols_spans(in, &rd);
-            if (!dirty.empty() && overlaps(dirty, rd)) {
+            bool clobbered = false;
+            if (p.fast && hs[i].fast_fail && (dirty.empty() || !overlaps(dirty, rd))) {
+                // write-after-read: the fallback re-reads the input columns after every later
+                // call ran; a later call that wrote into them leaves nothing to encode
+                for (size_t j = i + 1; j < ps.size() && !clobbered; j++) {
+                    std::vector<Span> wj;
+                    if (ps[j].kind == 1) cols_spans(ps[j].cols, &wj);
+                    else wj.push_back(span_of(ps[j].out, ps[j].cap));
+                    clobbered = overlaps(rd, wj);
+                }
+            }
+            if (clobbered) {
+                r = false;
+                set_err(&e, "encode of async call %zu needs its columns again (fallback), but a "
+                            "later call in the backlog wrote into them; keep them unchanged until "
+                            "nxg_ctx_sync", i);
+            } else if (!dirty.empty() && overlaps(dirty, rd)) {
                 // its input columns were rewritten after it ran: encode again
                 r = redo_encode(c, p, in, &e);
                 dirty.push_back(span_of(p.out, p.cap));
             } else {
-                r = finish_encode(c, in, p.st, p.slot, p.len_out, p.cap, true, &e, true);
+                bool redone = false;
+                r = finish_encode(c, in, p.st, p.slot, p.len_out, p.cap, true, &e, true, p.fast,
+                                  p.heap, p.out, &redone);
+                if (redone) dirty.push_back(span_of(p.out, p.cap));
             }
         }
         if (!r && ok) {
@@ -1134,9 +1216,11 @@ static bool encode_impl(NxgCtx* c, const NxgColumns* in, const uint8_t* heap, ui
     // pass 1 (sizing) when writing to a host buffer; a device buffer is written directly
     if (host && out) {
         if (!begin_call(c, &st, &slot, err)) return false;
-        const bool ok = enqueue_encode(c, din, dheap, nullptr, 0, st, err);
+        int fast = 0;
+        const bool ok = enqueue_encode(c, din, dheap, nullptr, 0, st, err, &fast);
         if (!end_call(c, err) || !ok) return false;
-        if (!finish_encode(c, din, st, slot, &total, 0, false, err)) return false;
+        if (!finish_encode(c, din, st, slot, &total, 0, false, err, false, fast, dheap, nullptr))
+            return false;
         if (total > cap) {
             set_err(err, "output buffer too small: need %llu bytes, have %llu",
                     (unsigned long long)total, (unsigned long long)cap);
@@ -1154,9 +1238,12 @@ static bool encode_impl(NxgCtx* c, const NxgColumns* in, const uint8_t* heap, ui
         cap = total;
     }
     if (!begin_call(c, &st, &slot, err)) return false;
-    const bool ok = enqueue_encode(c, din, dheap, dout, out ? cap : 0, st, err);
+    int fast = 0;
+    const bool ok = enqueue_encode(c, din, dheap, dout, out ? cap : 0, st, err, &fast);
     if (!end_call(c, err) || !ok) return false;
-    if (!finish_encode(c, din, st, slot, &total, cap, dout != nullptr, err)) return false;
+    if (!finish_encode(c, din, st, slot, &total, cap, dout != nullptr, err, false, fast, dheap,
+                       dout))
+        return false;
     if (host && out && total) {
         HIPCHK(hipMemcpyAsync(out, dout, total, hipMemcpyDeviceToHost, c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
@@ -1723,10 +1810,11 @@ bool nxg_encode_updates_async(NxgCtx* c, const NxgColumns* din, const uint8_t* d
     DevStatus* st;
     uint32_t slot;
     if (!begin_call(c, &st, &slot, err)) return false;
-    const bool ok = enqueue_encode(c, din, dheap, dout, cap, st, err);
+    int fast = 0;
+    const bool ok = enqueue_encode(c, din, dheap, dout, cap, st, err, &fast);
     if (!end_call(c, err) || !ok) return false;
-    c->pending.push_back({2, 0, nullptr, 0, const_cast<NxgColumns*>(din), len_out, cap, st, slot,
-                          0, dheap, dout});
+    c->pending.push_back({2, fast, nullptr, 0, const_cast<NxgColumns*>(din), len_out, cap, st,
+                          slot, 0, dheap, dout});
     return true;
 }
 

@@ -53,19 +53,8 @@ constexpr uint32_t F_XCD = 1;
 #endif
 constexpr uint64_t XRUN = NXG_F64S_XRUN;
 
-// pos(k), the byte where record k starts: record j is 12 + #{t in 1..4 : i0 + j >= 2^(7t)} bytes
-// long (ids < 2^35), so pos(k) = 12 k + sum_t clamp(i0 + k - 2^(7t), 0, k). Wave-uniform callers
-// keep this in scalar registers.
-NXG_DEV uint64_t pos_of(uint64_t i0, uint64_t k) {
-    uint64_t p = 12 * k;
-#pragma unroll
-    for (uint32_t t = 1; t <= 4; t++) {
-        const uint64_t B = 1ull << (7 * t);
-        const uint64_t x = i0 + k > B ? i0 + k - B : 0ull;
-        p += x < k ? x : k;
-    }
-    return p;
-}
+// pos(k), the byte where record k starts (f64rec16::seq_pos)
+NXG_DEV uint64_t pos_of(uint64_t i0, uint64_t k) { return f64rec16::seq_pos(i0, k); }
 
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 NXG_DEV uint4 ld16s(const uint8_t* __restrict__ p) {

@@ -43,6 +43,7 @@ constexpr int SPW = NXG_F64X_SPW;       // sub-tiles per wave
 constexpr uint64_t WGB = (uint64_t)SUB * SPW * WAVES;  // bytes per workgroup
 constexpr uint32_t MAXR = SUB / 12 + 2;  // rows per sub-tile (records start in it, >= 12 bytes)
 constexpr uint32_t MAXW = MAXR * SPW;     // rows per wave
+static_assert((uint64_t)SUB * SPW <= 65536, "start-list offsets are u16 within the wave's bytes");
 #ifndef NXG_F64X_CB
 #define NXG_F64X_CB 6
 #endif
@@ -463,7 +464,7 @@ __global__ __launch_bounds__(TPB, NXG_F64X_OCC) void nxg_f64x_kernel(const uint8
     {
         const uint32_t a = (uint32_t)(row0 & 1u);  // row0 odd: the first pair's first row is not ours
         const uint64_t rb = row0 - a;              // even
-        const uint32_t np = (tw + a + 1) / 2;      // pairs
+        const uint32_t np = tw ? (tw + a + 1) / 2 : 0u;  // pairs (none for a wave without rows)
 #pragma unroll 1
         for (uint32_t j0 = 0; j0 < np; j0 += 64 * EU) {
             uint64_t p[EU][2];
@@ -474,7 +475,7 @@ __global__ __launch_bounds__(TPB, NXG_F64X_OCC) void nxg_f64x_kernel(const uint8
 #pragma unroll
                 for (int h = 0; h < 2; h++) {
                     const int32_t k = (int32_t)(2 * j + h) - (int32_t)a;  // record index in the wave
-                    const uint32_t kc = k < 0 ? 0u : ((uint32_t)k < tw ? (uint32_t)k : tw - 1);
+                    const uint32_t kc = k < 0 || tw == 0 ? 0u : ((uint32_t)k < tw ? (uint32_t)k : tw - 1);
                     p[u][h] = w0 + pl[kc];
                 }
             }

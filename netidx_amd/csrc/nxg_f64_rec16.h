@@ -13,6 +13,22 @@
 
 namespace f64rec16 {
 
+// A frame whose ids count up by one from i0 (a publisher updating all of its values in
+// publication order, netidx-core/src/utils.rs:130-134): record j is 12 + #{t in 1..4 :
+// i0 + j >= 2^(7t)} bytes long (ids < 2^35), so record k starts at
+//     seq_pos(i0, k) = 12 k + sum_t clamp(i0 + k - 2^(7t), 0, k).
+// Shared by the sequential-id decoder and encoder; wave-uniform callers keep it in scalar registers.
+NXG_DEV uint64_t seq_pos(uint64_t i0, uint64_t k) {
+    uint64_t p = 12 * k;
+#pragma unroll
+    for (uint32_t t = 1; t <= 4; t++) {
+        const uint64_t B = 1ull << (7 * t);
+        const uint64_t x = i0 + k > B ? i0 + k - B : 0ull;
+        p += x < k ? x : k;
+    }
+    return p;
+}
+
 NXG_DEV uint4 ld16r(const uint8_t* __restrict__ p) { return *reinterpret_cast<const uint4*>(p); }
 // the bytes of [off, off+16) that lie inside the frame, zero-filled (out of line: rare)
 __device__ __attribute__((noinline)) uint4 ld16_tail(const uint8_t* __restrict__ wire,

@@ -146,6 +146,11 @@ uint64_t nxg_enc_f64_tiles(uint64_t n);  // tiles (and tstat words) of an f64 en
 hipError_t nxg_launch_enc_f64(const uint64_t* id, const uint64_t* val, uint64_t n, uint8_t* out,
                               uint64_t cap, uint64_t* tstat, uint32_t epoch, DevStatus* st,
                               int grid, hipStream_t s);
+// f64 encode of a batch whose ids count up by one (nxg_encode_f64_seq.hip): one launch, no
+// look-back; declines with fast_fail + DevStatus.irregular bit 2 (out NULL: sizing only)
+uint64_t nxg_enc_f64s_groups(uint64_t n);
+hipError_t nxg_launch_enc_f64s(const uint64_t* id, const uint64_t* val, uint64_t n, uint8_t* out,
+                               uint64_t cap, DevStatus* st, hipStream_t s);
 uint64_t nxg_enc_general_tiles(uint64_t n);  // tiles (and tstat words) of a general encode
 // arch_base > 0: archive-batch rows after an arch_base-byte count header (nxg_encode_general.hip)
 hipError_t nxg_launch_enc_general(const ColsDesc& cols, const uint8_t* heap, uint8_t* out,

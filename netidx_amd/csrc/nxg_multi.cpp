@@ -384,7 +384,15 @@ static bool share_fallback(NxgComm* comm, const uint8_t* dframe, uint64_t W, uin
     NxgStatus s{};
     uint64_t off = 0;
     uint64_t slot[kSlotWords] = {0};
-    if (!local_decode_share(comm, dframe, W, dout, &off, &s, err)) slot[kStatusWord] = 1;
+    if (!local_decode_share(comm, dframe, W, dout, &off, &s, err)) {
+        slot[kStatusWord] = 1;
+    } else if (s.err_kind == NXG_CAPACITY || s.err_kind == NXG_NOT_F64) {
+        // this rank's share does not fit its columns: a local failure, agreed by every rank (the
+        // frame's own errors are the same on every rank and stay in rng)
+        set_err(err, "rank %d: its row share does not fit its columns (%s)", comm->rank,
+                s.err_kind == NXG_CAPACITY ? "capacity" : "f64-only columns for mixed rows");
+        slot[kStatusWord] = 1;
+    }
     std::vector<uint64_t> buf((size_t)comm->nranks * kSlotWords);
     if (!gather_slots(comm, slot, buf.data(), err)) return false;
     const int who = first_failed(comm, buf);

@@ -211,3 +211,42 @@ def test_decode_frames_stream_shared_columns_1e7(dcodec):
         st = dcodec.sync()
         assert st.path == 1 and st.n_rows == n
         assert torch.equal(out.id[:n], cols.id[:n]) and torch.equal(out.fixed[:n], cols.fixed[:n])
+
+
+def test_async_fallback_frame_overwritten_fails_loudly():
+    """A decode that falls back in nxg_ctx_sync re-reads its frame after the later calls of the
+    backlog ran. A later async encode that wrote into that frame buffer (stream-ordered reuse)
+    makes the sync fail with a clear error instead of decoding the overwritten bytes (ADVICE r5);
+    the context stays usable, and the same backlog without the reuse decodes bit-exact."""
+    import netidx_amd
+    import nxo
+    import torch
+    from netidx_amd import synth
+    from netidx_amd.codec import Columns
+    c = netidx_amd.Codec(0)
+    try:
+        rng = np.random.default_rng(77)
+        n = 50_000
+        ids, vals = synth.f64_columns(n, 78)
+        ids = rng.permutation(ids)  # the sequential-id kernel declines: a fallback at sync
+        w = nxo.encode_f64(ids, vals)
+        frame = torch.from_numpy(w.copy()).cuda()
+        out = Columns(n, 0, 0, netidx_amd.LAYOUT_F64, "cuda")
+        i2, v2 = synth.f64_columns(n, 79)
+        cols2 = netidx_amd.columns_from_arrays(i2, v2)
+        c.decode_async(frame.data_ptr(), frame.numel(), out)
+        c.encode_async(cols2, None, frame.data_ptr(), frame.numel())  # writes into the frame
+        with pytest.raises(netidx_amd.CodecError, match="wrote into that frame"):
+            c.sync()
+        # without the reuse: the same backlog shape decodes bit-exact
+        frame = torch.from_numpy(w.copy()).cuda()
+        eout = torch.empty(frame.numel() + 64, dtype=torch.uint8, device="cuda")
+        c.decode_async(frame.data_ptr(), frame.numel(), out)
+        c.encode_async(cols2, None, eout.data_ptr(), eout.numel())
+        st = c.sync()
+        ref = nxo.decode(w).trim()
+        assert st.n_rows == n
+        assert np.array_equal(out.numpy()["id"], ref["id"])
+        assert np.array_equal(out.numpy()["fixed"], ref["fixed"])
+    finally:
+        c.close()

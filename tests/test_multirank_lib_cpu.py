@@ -206,7 +206,8 @@ def test_library_decode_sharded_fails_on_every_rank(tmp_path, world, fail_rank, 
             assert f"rank {fail_rank} failed" in msg
 
 
-def _rank_share(rank, world, port, seed, decline_rank, fail_rank, corrupt_at, outdir):
+def _rank_share(rank, world, port, seed, decline_rank, fail_rank, corrupt_at, outdir,
+                cap_rank=-1):
     import netidx_amd
     from netidx_amd.codec import NxgColumns
     _init(rank, world, port)
@@ -224,6 +225,8 @@ def _rank_share(rank, world, port, seed, decline_rank, fail_rank, corrupt_at, ou
             assert flen == W and frame_ptr == wire.ctypes.data and shares == world
             if rank == fail_rank:
                 raise RuntimeError("this rank's share decode failed")
+            if rank == cap_rank:  # this rank's share does not fit its columns (NXG_CAPACITY)
+                return 0, 0, 7, 0
             o = nxo.decode(wire).trim()
             if o["err_kind"]:
                 return 0, 0, o["err_kind"], o["err_offset"]
@@ -296,3 +299,19 @@ def test_library_decode_sharded_share_failure_on_every_rank(tmp_path, fail_rank)
         assert not (tmp_path / f"dec{r}.npy").exists()
         if r != fail_rank:
             assert f"rank {fail_rank} failed" in msg
+
+
+def test_library_decode_sharded_share_capacity_on_one_rank(tmp_path):
+    """Only rank 1's row share overflows its columns (nxg_decode_share: true with NXG_CAPACITY):
+    a local failure, so every rank returns false at the same step, instead of rank 1
+    reporting ok = 2 with no rows while the others succeed."""
+    world = 3
+    mp.spawn(_rank_share, args=(world, _free_port(), 44, 1, -1, None, str(tmp_path), 1),
+             nprocs=world, join=True)
+    for r in range(world):
+        msg = (tmp_path / f"err{r}.txt").read_text()
+        assert not (tmp_path / f"dec{r}.npy").exists()
+        if r != 1:
+            assert "rank 1 failed" in msg
+        else:
+            assert "does not fit" in msg
