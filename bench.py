@@ -296,6 +296,158 @@ def cpu_baseline_threads(wire_host, ids, seconds, threads=16):
     return n * reps / t_total, reps, t_total
 
 
+# host threads for the all-cores CPU baselines: the GPU box's CPU share per GPU (the harness sets
+# OMP_NUM_THREADS = 16 there; os.cpu_count() reports the whole host, 256 on the driver's boxes, most
+# of it other GPUs' share), capped at what this host has
+def cpu_threads():
+    try:
+        t = int(os.environ.get("OMP_NUM_THREADS", "16"))
+    except ValueError:
+        t = 16
+    return max(1, min(t, os.cpu_count() or 1))
+
+
+CPU_THREADS_WHY = ("the GPU box's CPU share per GPU (OMP_NUM_THREADS there); os.cpu_count() "
+                   "counts the whole host's cores, most of them other GPUs' share")
+
+
+def _timed_reps(fn, seconds):
+    reps, t = 0, 0.0
+    while t < seconds or reps == 0:
+        t0 = time.perf_counter()
+        fn()
+        t += time.perf_counter() - t0
+        reps += 1
+    return reps, t
+
+
+def _decoded_of(m, rows=None):
+    """Oracle-shaped columns (nxo.Decoded) of a MixedColumns row share (children re-based)."""
+    import numpy as np
+    nxo = _nxo()
+    r0, r1 = rows if rows else (0, len(m.id))
+    n = r1 - r0
+    tag = m.tag[r0:r1]
+    arr = tag == 19
+    if arr.any():
+        c0 = int(m.fixed[r0:r1][arr][0])
+        last = np.flatnonzero(arr)[-1]
+        c1 = int(m.fixed[r0 + last]) + int(m.aux[r0 + last])
+    else:
+        c0 = c1 = 0
+    d = nxo.Decoded(n, c1 - c0 + 1, 1)
+    d.id[:n] = m.id[r0:r1]
+    d.tag[:n] = tag
+    d.fixed[:n] = m.fixed[r0:r1]
+    d.fixed[:n][arr] -= np.uint64(c0)
+    d.aux[:n] = m.aux[r0:r1]
+    d.ctag[:c1 - c0] = m.ctag[c0:c1]
+    d.cfixed[:c1 - c0] = m.cfixed[c0:c1]
+    d.caux[:c1 - c0] = m.caux[c0:c1]
+    d.s.n_rows, d.s.n_children, d.s.n_ctl = n, c1 - c0, 0
+    return d
+
+
+def cpu_baselines_mixed(m, wire_host, seconds=3.0):
+    """Config 3 beside the device numbers (north_star): the oracle's sequential decoder
+    (the reference's receive_batch_fn loop, channel.rs:504-521) and encoder (queue_send,
+    channel.rs:177-202) on 1 core and on cpu_threads() threads over row shares (each share its
+    own frame: the messages are independent). Bounded samples, outside every timed GPU region."""
+    import ctypes as C
+    from concurrent.futures import ThreadPoolExecutor
+    nxo = _nxo()
+    n = len(m.id)
+    nc = len(m.ctag)
+    d = nxo.Decoded(n + 1, nc + 1, 1)
+
+    def dec1():
+        nxo.lib().nxo_decode_frame(wire_host.ctypes.data, len(wire_host), C.byref(d.s))
+        assert d.s.err_kind == 0 and d.s.n_rows == n
+    reps, t = _timed_reps(dec1, seconds)
+    out = {"decode_1_core": {"value": round(n * reps / t / 1e6, 3), "unit": "M updates/s",
+                             "cores": 1, "kind": "port",
+                             "sample": f"the whole {n}-record mixed frame decoded {reps}x "
+                                       f"({t:.1f} s) by oracle/nx_oracle.c"}}
+    full = _decoded_of(m)
+
+    def enc1():
+        ln = nxo.lib().nxo_encoded_len(C.byref(full.s), m.heap.ctypes.data)
+        buf = enc1.buf
+        assert nxo.lib().nxo_encode(C.byref(full.s), m.heap.ctypes.data, buf.ctypes.data, ln) == ln
+    import numpy as np
+    enc1.buf = np.empty(len(wire_host) + 64, np.uint8)
+    reps, t = _timed_reps(enc1, seconds)
+    out["encode_1_core"] = {"value": round(n * reps / t / 1e6, 3), "unit": "M updates/s",
+                            "cores": 1, "kind": "port",
+                            "sample": f"the whole {n}-row batch encoded {reps}x ({t:.1f} s) by "
+                                      "oracle/nx_oracle.c (encoded_len + encode)"}
+    T = cpu_threads()
+    cuts = [n * k // T for k in range(T + 1)]
+    shares = [_decoded_of(m, (cuts[k], cuts[k + 1])) for k in range(T)]
+    frames = [np.frombuffer(nxo.encode(sh, m.heap), np.uint8) for sh in shares]
+    assert sum(len(f) for f in frames) == len(wire_host)
+    outs = [nxo.Decoded(cuts[k + 1] - cuts[k] + 1, sh.s.n_children + 1, 1)
+            for k, sh in enumerate(shares)]
+    bufs = [np.empty(len(f) + 64, np.uint8) for f in frames]
+
+    def dec_k(k):
+        nxo.lib().nxo_decode_frame(frames[k].ctypes.data, len(frames[k]), C.byref(outs[k].s))
+        assert outs[k].s.err_kind == 0
+
+    def enc_k(k):
+        ln = nxo.lib().nxo_encoded_len(C.byref(shares[k].s), m.heap.ctypes.data)
+        assert nxo.lib().nxo_encode(C.byref(shares[k].s), m.heap.ctypes.data,
+                                    bufs[k].ctypes.data, ln) == ln
+    with ThreadPoolExecutor(T) as ex:
+        reps, t = _timed_reps(lambda: list(ex.map(dec_k, range(T))), seconds)
+        out["decode_threads"] = {
+            "value": round(n * reps / t / 1e6, 3), "unit": "M updates/s", "cores": T,
+            "kind": "port", "why_this_many": CPU_THREADS_WHY,
+            "sample": f"the batch as {T} row-share frames decoded on {T} threads, {reps}x "
+                      f"({t:.1f} s) (an upper bound: the reference decodes a frame on one task)"}
+        reps, t = _timed_reps(lambda: list(ex.map(enc_k, range(T))), seconds)
+        out["encode_threads"] = {
+            "value": round(n * reps / t / 1e6, 3), "unit": "M updates/s", "cores": T,
+            "kind": "port", "why_this_many": CPU_THREADS_WHY,
+            "sample": f"the batch as {T} row shares encoded on {T} threads, {reps}x ({t:.1f} s)"}
+    return out
+
+
+def cpu_baselines_encode_f64(ids, vals, seconds=3.0):
+    """Config 4 beside the device number: the oracle's f64 encoder (handle_updates ->
+    queue_send, server.rs:604-629) on 1 core and on cpu_threads() threads over row shares."""
+    import ctypes as C
+    import numpy as np
+    from concurrent.futures import ThreadPoolExecutor
+    nxo = _nxo()
+    n = len(ids)
+    cap = 21 * n + 16
+    buf = np.empty(cap, np.uint8)
+
+    def enc1():
+        assert nxo.lib().nxo_encode_f64(ids.ctypes.data, vals.ctypes.data, n, buf.ctypes.data,
+                                        cap) > 0
+    reps, t = _timed_reps(enc1, seconds)
+    out = {"encode_1_core": {"value": round(n * reps / t / 1e6, 3), "unit": "M updates/s",
+                             "cores": 1, "kind": "port",
+                             "sample": f"the whole {n}-record batch encoded {reps}x ({t:.1f} s) "
+                                       "by oracle/nx_oracle.c"}}
+    T = cpu_threads()
+    cuts = [n * k // T for k in range(T + 1)]
+
+    def enc_k(k):
+        a, b = cuts[k], cuts[k + 1]
+        assert nxo.lib().nxo_encode_f64(ids[a:].ctypes.data, vals[a:].ctypes.data, b - a,
+                                        buf[21 * a:].ctypes.data, 21 * (b - a) + 16) >= 0
+    with ThreadPoolExecutor(T) as ex:
+        reps, t = _timed_reps(lambda: list(ex.map(enc_k, range(T))), seconds)
+    out["encode_threads"] = {
+        "value": round(n * reps / t / 1e6, 3), "unit": "M updates/s", "cores": T, "kind": "port",
+        "why_this_many": CPU_THREADS_WHY,
+        "sample": f"the batch as {T} row shares encoded on {T} threads, {reps}x ({t:.1f} s)"}
+    return out
+
+
 def read_traffic(records, kernel):
     """HBM bytes per launch from the committed rocprofv3 PMC summary, if it matches."""
     for f in ("pmc_dec_f64.json", "pmc_dec_f64_100000000.json"):
@@ -495,6 +647,14 @@ def extras_single_gpu(codec, stream, steps, warmup):
                                   "kernel_ms": round(ems, 4),
                                   "hbm_frac": round(be / (ems / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
                                   "oracle_bytes_checked": eb}
+        try:
+            cb = cpu_baselines_mixed(m, wire.cpu().numpy())
+            ex["decode_mixed_1e7"]["cpu_baseline"] = cb["decode_1_core"]
+            ex["decode_mixed_1e7"]["cpu_baseline_threads"] = cb["decode_threads"]
+            ex["encode_mixed_1e7"]["cpu_baseline"] = cb["encode_1_core"]
+            ex["encode_mixed_1e7"]["cpu_baseline_threads"] = cb["encode_threads"]
+        except Exception as e:
+            ex["decode_mixed_1e7"]["cpu_baseline"] = {"error": repr(e)}
         del mc, heap, wire, out, dout
         torch.cuda.empty_cache()
     except Exception as e:
@@ -796,7 +956,16 @@ def extras_single_gpu(codec, stream, steps, warmup):
         ex["encode_f64_1e7"] = {"records": n, "M_updates_s": round(n / (kms / 1e3) / 1e6, 1),
                                 "kernel_ms": round(kms, 4),
                                 "hbm_frac": round(b / (kms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                                "kernel": ("nxg_enc_f64s_kernel (sequential ids)"
+                                           if codec.last_encode_kernel() == "seq"
+                                           else "nxg_enc_f64_kernel (tiled look-back)"),
                                 "oracle_bytes_checked": eb}
+        try:
+            cb = cpu_baselines_encode_f64(ids_h, vals_h)
+            ex["encode_f64_1e7"]["cpu_baseline"] = cb["encode_1_core"]
+            ex["encode_f64_1e7"]["cpu_baseline_threads"] = cb["encode_threads"]
+        except Exception as e:
+            ex["encode_f64_1e7"]["cpu_baseline"] = {"error": repr(e)}
     except Exception as e:
         ex["encode_f64_1e7"] = {"error": repr(e)}
     # (d) SURVEY 8f row 2: subscriber dispatch (process_updates_batch, connection.rs:546-567) of
@@ -1223,13 +1392,14 @@ def main():
                                           f"({secs:.1f} s) by oracle/nx_oracle.c"}
         if not args.no_extras:
             line["extras"] = extras_single_gpu(codec, stream, min(args.steps, 40), args.warmup)
+            T = cpu_threads()
             ups, reps, secs = cpu_baseline_threads(host, cols.id.cpu().numpy().view("uint64"),
-                                                   min(args.cpu_seconds, 5.0))
-            line["extras"]["cpu_baseline_16_threads"] = {
-                "value": round(ups / 1e6, 3), "unit": "M updates/s", "cores": 16,
-                "kind": "port",
-                "sample": f"full {n}-record frame cut at record boundaries into 16 sub-frames, "
-                          f"decoded {reps}x ({secs:.1f} s) by oracle/nx_oracle.c on 16 threads"}
+                                                   min(args.cpu_seconds, 5.0), T)
+            line["extras"]["cpu_baseline_threads"] = {
+                "value": round(ups / 1e6, 3), "unit": "M updates/s", "cores": T,
+                "kind": "port", "why_this_many": CPU_THREADS_WHY, "host_nproc": nproc,
+                "sample": f"full {n}-record frame cut at record boundaries into {T} sub-frames, "
+                          f"decoded {reps}x ({secs:.1f} s) by oracle/nx_oracle.c on {T} threads"}
     elif world > 1 and not args.no_extras:
         try:
             ex = extras_multi_gpu(codec, world, rank, stream)

@@ -43,6 +43,9 @@
 #ifndef NXG_FMX_CAND
 #define NXG_FMX_CAND 7  // candidate rules (A/B timing only): 1 one-byte prefix, 2 Heartbeat, 4 two-byte
 #endif
+#ifndef NXG_FMX_CLS
+#define NXG_FMX_CLS 1  // the emit's row values by class (row_value_cls), val_decode for the rest
+#endif
 #ifndef NXG_FF_CHECK
 #define NXG_FF_CHECK 1  // emit waves skip a frame already declined
 #endif
@@ -123,6 +126,78 @@ NXG_DEV uint64_t cand_mask(const uint8_t* img, uint32_t c, uint64_t& two) {
     return m;
 }
 
+#ifndef NXG_FMX_CM
+#define NXG_FMX_CM 2  // candidate scan: 1 dword pairs in per-lane word order, 2 ds_read_b128 pieces
+#endif
+// 4 bits of x (flags at bits 7, 15, 23, 31 only) gathered into bits 28..31: the partial products
+// of x * 0x00204081 land at distinct positions below 32, so nothing carries
+NXG_DEV uint32_t nib4(uint32_t x) { return (x * 0x00204081u) >> 28; }
+// cand_mask, reading the lane's chunk as four 16-byte pieces (ds_read_b128). Lane j takes piece
+// (i + (j / 4) % 4) % 4 at step i: the 16 lanes of each ds_read_b128 lane group then cover the 64
+// banks once (MI355X_MICROARCH.md LDS table), where the plain order is 4-way. The nibbles are
+// placed in that rotated order (constant shifts) and the 64-bit mask rotated back once. The word
+// after the chunk (the next chunk's first) comes from the next lane (DPP); lane 63 reads it.
+template <bool FULL = true>
+NXG_DEV uint64_t cand_mask_b128(const uint8_t* img, uint32_t lane, uint64_t& two) {
+    const uint32_t c = lane * CH;
+    const uint32_t r = (lane >> 2) & 3u;
+    uint32_t P[4][4];
+#pragma unroll
+    for (uint32_t i = 0; i < 4; i++) {
+        const uint4 v = *reinterpret_cast<const uint4*>(img + c + 16u * ((i + r) & 3u));
+        P[i][0] = v.x, P[i][1] = v.y, P[i][2] = v.z, P[i][3] = v.w;
+    }
+    // the chunk's first word is in the piece read at step (4 - r) % 4
+    const uint32_t i0 = (4u - r) & 3u;
+    const uint32_t w0 = i0 == 0 ? P[0][0] : (i0 == 1 ? P[1][0] : (i0 == 2 ? P[2][0] : P[3][0]));
+    uint32_t w16 = wave_next(w0);
+    if (lane == 63) w16 = *reinterpret_cast<const uint32_t*>(img + c + 64);
+    uint32_t lo = 0, hi = 0, tlo = 0, thi = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < 4; i++) {
+        // the word after this piece: the next piece's first, or w16 after the chunk's last piece
+        const uint32_t nx = i == 3u - r ? w16 : P[(i + 1) & 3][0];
+#pragma unroll
+        for (uint32_t e = 0; e < 4; e++) {
+            const uint32_t a = P[i][e], b = e < 3 ? P[i][e + 1] : nx;
+            const uint32_t a1 = alignbyte(b, a, 1);
+            const uint32_t len = ((a & 0x7f7f7f7fu) + 0x7c7c7c7cu) & ~a & 0x80808080u;
+            const uint32_t var = zero_bytes(a1 ^ 0x04040404u);
+            uint32_t f = (NXG_FMX_CAND & 1) ? (len & var) : 0u, t = 0;
+            if (FULL) {
+                const uint32_t a2 = alignbyte(b, a, 2);
+                if (NXG_FMX_CAND & 2) f |= zero_bytes(a ^ 0x02020202u) & zero_bytes(a1 ^ 0x05050505u);
+                if (NXG_FMX_CAND & 4)
+                    t = a & ~a1 & ~zero_bytes(a1) & zero_bytes(a2 ^ 0x04040404u) & 0x80808080u;
+            }
+            const uint32_t sh = 4u * (4u * i + e);  // a constant
+            if (sh < 32) {
+                lo |= nib4(f) << sh;
+                if (FULL) tlo |= nib4(t) << sh;
+            } else {
+                hi |= nib4(f) << (sh - 32);
+                if (FULL) thi |= nib4(t) << (sh - 32);
+            }
+        }
+    }
+    // rotate left by 16 r bits: r & 2 swaps the halves, r & 1 rotates by 16 (v_alignbit)
+    auto rot = [&](uint32_t x, uint32_t y) -> uint64_t {
+        if (r & 2u) {
+            const uint32_t z = x;
+            x = y;
+            y = z;
+        }
+        if (r & 1u) {
+            const uint32_t nl = __builtin_amdgcn_alignbit(x, y, 16), nh = __builtin_amdgcn_alignbit(y, x, 16);
+            x = nl;
+            y = nh;
+        }
+        return ((uint64_t)y << 32) | x;
+    };
+    two = FULL ? rot(tlo, thi) : 0ull;
+    return rot(lo, hi);
+}
+
 // the length of the message at tile offset x (its canonical one- or two-byte prefix)
 NXG_DEV uint32_t msg_len(const uint8_t* img, uint32_t x) {
     const uint32_t b0 = img[x];
@@ -179,7 +254,8 @@ template <bool FULL = true>
 NXG_DEV Cands lane_cands(const uint8_t* img, uint32_t lane, uint32_t lim) {
     Cands r;
     uint64_t two;
-    uint64_t m = cand_mask<FULL>(img, lane * CH, two);
+    uint64_t m = NXG_FMX_CM == 2 ? cand_mask_b128<FULL>(img, lane, two)
+                                 : cand_mask<FULL>(img, lane * CH, two);
     r.m = m | two;
     r.c0 = r.c1 = r.x0 = r.x1 = FAIL;
     if (m) {
@@ -849,8 +925,12 @@ __global__ __launch_bounds__(TPB) void nxg_fmx_emit_kernel(
             const uint32_t g0 = up ? h[2] : h[1], g1 = up ? h[3] : h[2], g2 = up ? h[4] : h[3],
                            g3 = up ? 0u : h[4];
             const uint32_t su = u & 3u;
-            FV o = val_decode(upd ? tg : 1u, alignbyte(g1, g0, su), alignbyte(g2, g1, su),
-                              alignbyte(g3, g2, su), p + u, upd ? lim : p + u + 12u, true, t0f);
+            const uint32_t V0 = alignbyte(g1, g0, su), V1 = alignbyte(g2, g1, su),
+                           V2 = alignbyte(g3, g2, su);
+            FV o;
+            if (!NXG_FMX_CLS || !row_value_cls(upd ? tg : 1u, V0, V1, V2, p + u,
+                                               upd ? lim : p + u + 12u, t0f, upd, o))
+                o = val_decode(upd ? tg : 1u, V0, V1, V2, p + u, upd ? lim : p + u + 12u, true, t0f);
             if (NXG_FMX_SKIP & 4) o = FV{g0, tg, g1, lim, 0, 0, 0, true};
             // past the image: text only (the count pass), checked here from global memory
             const bool far = !LEAN && upd && lim > wend;

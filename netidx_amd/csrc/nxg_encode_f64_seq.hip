@@ -265,10 +265,11 @@ __global__ __launch_bounds__(f64es::TPB) void nxg_enc_f64s_kernel(
             st->split_start = f64rec16::seq_pos(i0, lo) + 1;
         }
     }
-    if (out && T > cap) {
-        if (lead) atomicOr(&st->capacity, 1u);
-        return;
-    }
+    // columns too large for `out`: nothing is written, but the ids are still checked, so that a
+    // batch that is not a run of consecutive ids (whose real length T does not give) goes to the
+    // tiled encoder, which sizes it exactly (fast_fail comes before capacity on the host)
+    const bool over = out && T > cap;
+    if (over && lead) atomicOr(&st->capacity, 1u);
     uint64_t blk = blockIdx.x;
     if (flags & F_XCD) {  // each XCD streams runs of XRUN consecutive workgroups' records
         const uint64_t full = (uint64_t)gridDim.x / (8 * XRUN) * (8 * XRUN);
@@ -308,7 +309,7 @@ __global__ __launch_bounds__(f64es::TPB) void nxg_enc_f64s_kernel(
         }
         return;
     }
-    if (!out) return;
+    if (!out || over) return;
     const uint64_t p0 = f64rec16::seq_pos(i0, k0);
     const uint32_t vl = vl64(i0 + k0);
     const uint32_t ph = (uint32_t)((uintptr_t)out & 15u);

@@ -229,6 +229,88 @@ NXG_DEV FV val_decode(uint32_t t, uint32_t P0, uint32_t P1, uint32_t P2, uint32_
     return o;
 }
 
+// val_decode for a round's row values when each lane's tag is in one of the common classes -- a
+// fixed-size scalar (F), DateTime / Duration (D), String / Bytes / Error(String) (S), Array (A):
+// each class's fields are computed only when the round holds that class (wave-uniform tests), so a
+// round pays for the classes present instead of every field of every tag. The same results as
+// val_decode(t, P0, P1, P2, u, lim, true, t0) for those tags (the same rules, restated per class:
+// dleaf / dcontainer in nxg_msg.h, netidx-value/src/lib.rs:470-506). Returns false (uniform) when
+// some lane holds another tag: the caller then runs val_decode.
+NXG_DEV bool row_value_cls(uint32_t t, uint32_t P0, uint32_t P1, uint32_t P2, uint32_t u,
+                           uint32_t lim, uint64_t t0, bool has, FV& o) {
+    const uint32_t f1 = fixed_size1(t);
+    const bool isD = t == 10u || t == 11u;
+    const bool isF = f1 != 0u && !isD;
+    const bool isS = t == 12u || t == 13u || t == 18u;
+    const bool isA = t == 19u;
+    if (__any(has && !(isF || isD || isS || isA))) return false;
+    const uint32_t room = lim > u ? lim - u : 0u;
+    const uint32_t b0 = bswap32(P0), b1 = bswap32(P1);
+    const uint32_t bit = 1u << (t & 31u);
+    {  // F (every lane: the cheapest class, and the default)
+        const uint32_t n = f1 - 1u;
+        const bool n8 = f1 == 9u;
+        const uint32_t sh = (32u - 8u * n) & 31u;
+        const bool sgn = bit & kSgnTags;
+        const uint32_t lo32 = f1 >= 2u ? (sgn ? (uint32_t)((int32_t)b0 >> sh) : b0 >> sh)
+                                       : ((bit & B(14)) ? 1u : 0u);
+        const uint32_t fhi = n8 ? b0 : (sgn ? (uint32_t)((int32_t)lo32 >> 31) : 0u);
+        o.fixed = ((uint64_t)fhi << 32) | (n8 ? b1 : lo32);
+        o.tag = t == 17u ? 16u : t;
+        o.aux = 0;
+        o.end = u + n;
+        o.kids = 0;
+        o.soff = 0;
+        o.slen = 0;
+        o.ok = room >= n;
+    }
+    if (__any(isD)) {  // DateTime (from_timestamp validity), Duration (Duration::new normalisation)
+        uint32_t ns = bswap32(P2);
+        const uint64_t secs = ((uint64_t)b0 << 32) | b1;
+        bool fok = room >= 12u;
+        const bool easy = ns < 1000000000u && secs + ((1ull << 42) - 1) < (1ull << 43) - 1;
+        if (__builtin_expect(t == 10u && !easy, 0)) fok = fok && datetime_valid((int64_t)secs, ns);
+        const bool dur = t == 11u;
+        const uint32_t add = dur ? (uint32_t)(ns >= 1000000000u) + (ns >= 2000000000u) +
+                                       (ns >= 3000000000u) + (ns >= 4000000000u)
+                                 : 0u;
+        const uint64_t s2 = secs + add;
+        fok = fok && s2 >= secs;
+        ns -= add * 1000000000u;
+        if (isD) {
+            o.fixed = dur ? s2 : secs;
+            o.aux = ns;
+            o.end = u + 12u;
+            o.ok = fok;
+        }
+    }
+    if (__any(isS || isA)) {  // a length / count varint
+        uint64_t v;
+        const uint32_t nb = var3(P0, P1, P2, v);
+        const bool vok = nb != 0 && nb <= room;
+        const uint32_t p = u + nb;
+        const uint32_t rest = lim > p ? lim - p : 0u;
+        const uint32_t v32 = (uint32_t)v;
+        if (isS) {
+            const bool tok = vok && v <= (uint64_t)(room - nb);
+            o.fixed = t0 + p;
+            o.aux = v32;
+            o.end = p + v32;
+            o.soff = p;
+            o.slen = tok && t != 13u ? v32 : 0u;
+            o.ok = tok;
+        } else if (isA) {
+            o.fixed = 0;
+            o.aux = v32;
+            o.kids = v32;
+            o.end = p;
+            o.soff = p;
+            o.ok = vok && v <= kMaxVec / 16 && v * 16 <= ((uint64_t)rest << 8);
+        }
+    }
+    return true;
+}
+
 // index of the first byte >= 0x80 among bytes 0..15 of the words q[0..3] (16: none)
 NXG_DEV uint32_t first_high16(const uint32_t* q) {
     const uint64_t lo = (((uint64_t)q[1] << 32) | q[0]) & 0x8080808080808080ull;

@@ -49,6 +49,7 @@ def _encode(codec, ids, vals, off=0, cap=None):
     cols = netidx_amd.columns_from_arrays(ids, vals)
     n = codec.encoded_len(cols)
     buf = torch.full((n + off + 64,), SENT, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()  # (the fill runs on torch's stream, the encode on the codec's)
     m = codec.encode_into(cols, None, buf.data_ptr() + off, n if cap is None else cap)
     assert m == n
     h = buf.cpu().numpy()
@@ -134,6 +135,7 @@ def test_seq_encode_capacity_and_sizing(codec):
     cols = netidx_amd.columns_from_arrays(ids, vals)
     assert codec.encoded_len(cols) == len(ref)
     buf = torch.full((len(ref) + 64,), SENT, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
     with pytest.raises(netidx_amd.CodecError, match="too small"):
         codec.encode_into(cols, None, buf.data_ptr(), len(ref) - 1)
     assert (buf.cpu().numpy() == SENT).all(), "a declined encode wrote bytes"
@@ -163,6 +165,7 @@ def test_seq_encode_async_backlog_with_late_fallback():
         refs = [nxo.encode_f64(i, v) for i, v in batches]
         cols = [netidx_amd.columns_from_arrays(i, v) for i, v in batches]
         outs = [torch.zeros(len(r) + 64, dtype=torch.uint8, device="cuda") for r in refs]
+        torch.cuda.synchronize()
         lens = [c.encode_async(cl, None, o.data_ptr(), o.numel()) for cl, o in zip(cols, outs)]
         dec = Columns(n, 0, 0, netidx_amd.LAYOUT_F64, "cuda")
         c.decode_async(outs[1].data_ptr(), len(refs[1]), dec)
