@@ -623,6 +623,37 @@ def extras_single_gpu(codec, stream, steps, warmup):
                                   "n_children": len(m.ctag),
                                   "oracle_rows_checked": checked,
                                   "oracle_columns_checked": "all"}
+        # the type-partitioned view of the decoded columns (nxg_partition_by_tag: per-tile LDS tag
+        # histogram + scan, SURVEY 8a's optional output), checked against its numpy restatement
+        try:
+            view = codec.partition_by_tag(out)
+            torch.cuda.synchronize()
+            kp = max(3, steps // 4)
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for _ in range(kp):
+                view = codec.partition_by_tag(out, view)
+            e1.record(stream)
+            torch.cuda.synchronize()
+            pms = e0.elapsed_time(e1) / kp
+            g = out.numpy()
+            want = _nxo().partition_by_tag(g["tag"][:n], g["fixed"][:n], g["aux"][:n])
+            got = view.numpy()
+            assert all(np.array_equal(got[k], want[k]) for k in want), "partition differs"
+            pb = n * (1 + 13 + 20)
+            ex["partition_mixed_1e7"] = {
+                "records": n, "call_ms": round(pms, 4),
+                "M_rows_s": round(n / (pms / 1e3) / 1e6, 1),
+                "hbm_frac": round(pb / (pms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                "algorithmic_bytes": pb,
+                "kernels": "nxg_part_count / scan / offsets / place",
+                "tags": {int(t): int(c) for t, c in enumerate(view.count) if c},
+                "timed": "synchronous calls (host sync each), HIP events on the codec stream",
+                "checked": "every array vs tests/nxo.py partition_by_tag (stable sort by tag)"}
+            del view, g, want, got
+        except Exception as e:
+            ex["partition_mixed_1e7"] = {"error": repr(e)}
         # the mixed encode of the same columns (nxg_enc_rows_kernel), byte-identical to the wire
         dout = torch.empty(wire.numel() + 64, dtype=torch.uint8, device="cuda")
         for _ in range(2):
@@ -930,9 +961,16 @@ def extras_single_gpu(codec, stream, steps, warmup):
         torch.cuda.empty_cache()
     except Exception as e:
         ex["socket_e2e_f64_1e7"] = {"error": repr(e)}
-    # (c) config 4: f64 encode from device columns, byte-identical round trip
+    # (c) config 4: f64 encode from device columns, byte-identical round trip. A context of its
+    # own, as a publisher's connection has: the random-order legs above made this one's encodes
+    # skip the sequential-id encoder for a while (it declined their batches)
+    enc = None
+    codec_main = codec
     try:
         n = 10_000_000
+        enc = netidx_amd.Codec(0)
+        enc.set_stream(stream.cuda_stream)
+        codec = enc
         cols, wire = make_f64_wire(codec, n, 0)
         dout = torch.empty(wire.numel() + 64, dtype=torch.uint8, device="cuda")
         for _ in range(2):
@@ -966,8 +1004,51 @@ def extras_single_gpu(codec, stream, steps, warmup):
             ex["encode_f64_1e7"]["cpu_baseline_threads"] = cb["encode_threads"]
         except Exception as e:
             ex["encode_f64_1e7"]["cpu_baseline"] = {"error": repr(e)}
+        del cols, wire, dout
+        torch.cuda.empty_cache()
+        # (c2) the north-star size: 10^8 records, 1.5 GB of wire
+        try:
+            n = 100_000_000
+            ids_h, vals_h = synth.f64_columns(n, synth.SEED_F64)
+            cols = netidx_amd.columns_from_arrays(ids_h, vals_h)
+            W = codec.encoded_len(cols)
+            dout = torch.empty(W + 64, dtype=torch.uint8, device="cuda")
+            for _ in range(2):
+                codec.encode_async(cols, None, dout.data_ptr(), dout.numel())
+                codec.sync()
+            torch.cuda.synchronize()
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            k = max(4, steps // 4)
+            e0.record(stream)
+            for _ in range(k):
+                codec.encode_async(cols, None, dout.data_ptr(), dout.numel())
+            e1.record(stream)
+            codec.sync()
+            torch.cuda.synchronize()
+            kms = e0.elapsed_time(e1) / k
+            eb = oracle_check_encode(dout[:W], ids_h, vals_h)
+            b = W + 16 * n
+            ex["encode_f64_1e8"] = {"records": n, "wire_bytes": W,
+                                    "M_updates_s": round(n / (kms / 1e3) / 1e6, 1),
+                                    "kernel_ms": round(kms, 4),
+                                    "hbm_frac": round(b / (kms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                                    "kernel": ("nxg_enc_f64s_kernel (sequential ids)"
+                                               if codec.last_encode_kernel() == "seq"
+                                               else "nxg_enc_f64_kernel (tiled look-back)"),
+                                    "timed": f"{k} async encodes of one column set into one "
+                                             "buffer, HIP events on the codec stream",
+                                    "oracle_bytes_checked": eb}
+            del cols, dout
+            torch.cuda.empty_cache()
+        except Exception as e:
+            ex["encode_f64_1e8"] = {"error": repr(e)}
     except Exception as e:
         ex["encode_f64_1e7"] = {"error": repr(e)}
+    finally:
+        codec = codec_main
+        if enc is not None:
+            enc.close()
     # (d) SURVEY 8f row 2: subscriber dispatch (process_updates_batch, connection.rs:546-567) of
     # 10^7 decoded updates: every id subscribed once, its stream on one of 16 channels, half of
     # the subscriptions keeping `last`. Checked against the oracle, which is also timed (1 core).

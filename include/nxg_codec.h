@@ -332,6 +332,32 @@ typedef struct NxgDispatch {
 bool nxg_dispatch_updates(NxgCtx* ctx, const NxgSubTable* tab, const uint64_t* id,
                           uint64_t n_rows, NxgDispatch* out, NetidxError* err);
 
+/* ---- type-partitioned view of decoded mixed columns (optional output) --------
+ * Replaces the per-value 28-way `match` on the tag (Value::decode, netidx-value/src/lib.rs:470-506)
+ * for a consumer that handles values by type: the rows of `cols` grouped by their tag column, on
+ * the device, from a per-tile LDS tag histogram + scan (the mechanism BASELINE configs[2] names).
+ * Device memory, capacities >= cols->n_rows (rows < 2^32):
+ *   rank[i]      row i's index among the rows of its tag (record -> (tag[i], rank[i]))
+ *   row_of[d]    the row at dense index d; tag t's rows are d in [off[t], off[t+1]), in record
+ *                order
+ *   fixed[d], aux[d]   the rows' fixed / aux columns at their dense index
+ * off[] and count[] are filled on the host (off[NXG_TAG_BINS] = n_rows). Children (array
+ * elements) and text stay where the decode put them (fixed / aux of a row still point at them).
+ * Synchronous. Returns false on API misuse (F64-only columns have no tag column) or a HIP
+ * failure. */
+#define NXG_TAG_BINS 256
+typedef struct NxgTagView {
+    uint64_t cap_rows;
+    uint32_t* rank;
+    uint32_t* row_of;
+    uint64_t* fixed;
+    uint32_t* aux;
+    uint64_t n_rows;                    /* written by the call */
+    uint64_t count[NXG_TAG_BINS];       /* rows per tag value */
+    uint64_t off[NXG_TAG_BINS + 1];     /* exclusive prefix of count */
+} NxgTagView;
+bool nxg_partition_by_tag(NxgCtx* ctx, const NxgColumns* cols, NxgTagView* out, NetidxError* err);
+
 /* ---- publisher commit: replaces UpdateBatch::commit (publisher/mod.rs:776-845) ----------
  * A queued batch (its rows in NxgColumns form: id, tag, fixed, aux, text in `heap`; kind[i] per
  * row; to_client[i] for NXG_PUB_UPDATE_CLIENT rows) becomes per-client batches of

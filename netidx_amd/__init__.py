@@ -11,7 +11,7 @@ from .codec import (BUFFER_SHORT, CAPACITY, DEPTH, HINT_MIXED, INVALID_FORMAT, L
                     PUB_UPDATE_CLIENT, SubTable, columns_from_arrays, frame_header,
                     frame_parse_header, frame_split, lib, Comm, NxgRange, range_link, Session,
                     msg_subscribe, msg_subscribed, msg_heartbeat, msg_parse, msg_update,
-                    TAG_UNSUBSCRIBED, Resolver, ResolverClient)
+                    TAG_UNSUBSCRIBED, Resolver, ResolverClient, TagView, TAG_BINS)
 
 __all__ = ["Codec", "Columns", "PackError", "CodecError", "columns_from_arrays", "lib",
            "frame_split", "frame_header", "frame_parse_header", "LAYOUT_F64", "LAYOUT_MIXED",
@@ -20,4 +20,4 @@ __all__ = ["Codec", "Columns", "PackError", "CodecError", "columns_from_arrays",
            "PubTable", "FrameReader", "PUB_UPDATE", "PUB_UPDATE_CHANGED", "PUB_UPDATE_CLIENT",
            "Comm", "NxgRange", "range_link", "Session", "msg_subscribe", "msg_subscribed",
            "msg_heartbeat", "msg_parse", "msg_update", "TAG_UNSUBSCRIBED", "Resolver",
-           "ResolverClient"]
+           "ResolverClient", "TagView", "TAG_BINS"]

@@ -91,6 +91,15 @@ class NxgDispatch(C.Structure):
                 ("n_unmatched", C.c_uint64)]
 
 
+TAG_BINS = 256
+
+
+class NxgTagView(C.Structure):
+    _fields_ = [("cap_rows", C.c_uint64), ("rank", C.c_void_p), ("row_of", C.c_void_p),
+                ("fixed", C.c_void_p), ("aux", C.c_void_p), ("n_rows", C.c_uint64),
+                ("count", C.c_uint64 * TAG_BINS), ("off", C.c_uint64 * (TAG_BINS + 1))]
+
+
 class NxgPubTable(C.Structure):
     _fields_ = [("n_ids", C.c_uint64), ("slot_of_id", C.c_void_p), ("n_slots", C.c_uint64),
                 ("slot_client_off", C.c_void_p), ("client", C.c_void_p), ("n_clients", C.c_uint32),
@@ -177,6 +186,8 @@ SIGNATURES = {
     "nxg_decode_sharded": (C.c_bool, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64,
                                       C.POINTER(NxgColumns), C.POINTER(C.c_uint64),
                                       C.POINTER(NxgRange), C.POINTER(NetidxError)]),
+    "nxg_partition_by_tag": (C.c_bool, [C.c_void_p, C.c_void_p, C.c_void_p,
+                                        C.POINTER(NetidxError)]),
     "nxg_dispatch_updates": (C.c_bool, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64,
                                         C.c_void_p, C.POINTER(NetidxError)]),
     "nxg_publish_commit": (C.c_bool, [C.c_void_p, C.c_void_p, C.POINTER(NxgColumns), C.c_void_p,
@@ -556,6 +567,25 @@ class Codec:
         return Dispatch(chan_off, ent_sub, ent_row, last_row[: table.slot_sub_id.numel()],
                         out.n_entries, out.n_unmatched)
 
+    def partition_by_tag(self, cols, view=None):
+        """nxg_partition_by_tag: the type-partitioned view of decoded mixed device columns
+        (per-tag dense runs of fixed / aux, the dense index -> row map, the row -> rank map).
+        Returns a TagView (its device tensors are reused when `view` is passed)."""
+        n = int(cols.s.n_rows)
+        if view is None or view.cap < n:
+            view = TagView(max(n, 1), cols.device)
+        v = NxgTagView()
+        v.cap_rows = view.cap
+        v.rank, v.row_of = view.rank.data_ptr(), view.row_of.data_ptr()
+        v.fixed, v.aux = view.fixed.data_ptr(), view.aux.data_ptr()
+        err = NetidxError()
+        _check(lib().nxg_partition_by_tag(self.ctx, C.byref(cols.s), C.byref(v), C.byref(err)),
+               err)
+        view.n_rows = int(v.n_rows)
+        view.count = np.frombuffer(bytes(v.count), np.uint64).copy()
+        view.off = np.frombuffer(bytes(v.off), np.uint64).copy()
+        return view
+
     def publish_commit(self, table, batch, kind, to_client=None, heap=None, cap=None):
         """UpdateBatch::commit on device columns: `batch` (Columns: id, tag, fixed, aux and the
         children of its Array/Map/Error(Value) values), per-row
@@ -713,6 +743,29 @@ class SubTable:
                            self.slot_sub_id.numel(), self.slot_sub_id.data_ptr(),
                            self.slot_stream_off.data_ptr(), self.stream_chan.data_ptr(),
                            self.slot_has_last.data_ptr(), self.n_chans)
+
+
+class TagView:
+    """Device tensors of the type-partitioned view (include/nxg_codec.h NxgTagView): tag t's rows
+    are the dense indices [off[t], off[t+1]): row_of (int32 holding u32), fixed (int64), aux
+    (int32); rank[i] is row i's index among its tag's rows."""
+
+    def __init__(self, cap, device="cuda"):
+        import torch
+        self.cap = cap
+        self.rank = torch.empty(cap, dtype=torch.int32, device=device)
+        self.row_of = torch.empty(cap, dtype=torch.int32, device=device)
+        self.fixed = torch.empty(cap, dtype=torch.int64, device=device)
+        self.aux = torch.empty(cap, dtype=torch.int32, device=device)
+        self.n_rows, self.count, self.off = 0, None, None
+
+    def numpy(self):
+        n = self.n_rows
+        return {"rank": self.rank[:n].cpu().numpy().view(np.uint32),
+                "row_of": self.row_of[:n].cpu().numpy().view(np.uint32),
+                "fixed": self.fixed[:n].cpu().numpy().view(np.uint64),
+                "aux": self.aux[:n].cpu().numpy().view(np.uint32),
+                "count": self.count, "off": self.off}
 
 
 class Dispatch:

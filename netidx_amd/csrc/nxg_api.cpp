@@ -83,6 +83,8 @@ struct NxgCtx {
     // the sequential-id f64 encoder (nxg_encode_f64_seq.hip): after it declines a batch (ids not
     // counting up by one) it is skipped for the next kSeqSkipCalls f64 encodes; NXG_F64_ENC=tile
     // skips it always
+    uint8_t* pscratch = nullptr;  // the type-partitioned view's counts and offsets
+    size_t pscratch_cap = 0;
     uint32_t enc_seq_left = 0;
     uint32_t last_enc_kernel = 0;  // the last f64 encode: 1 sequential-id kernel, 2 tiled (debug)
     bool no_enc_seq = false;
@@ -828,6 +830,7 @@ void nxg_ctx_destroy(NxgCtx* c) {
     if (c->glws) (void)hipFree(c->glws);
     if (c->gruns) (void)hipFree(c->gruns);
     if (c->dscratch) (void)hipFree(c->dscratch);
+    if (c->pscratch) (void)hipFree(c->pscratch);
     if (c->dframe) (void)hipFree(c->dframe);
     if (c->escratch) (void)hipFree(c->escratch);
     if (c->rdesc) (void)hipFree(c->rdesc);
@@ -1594,6 +1597,55 @@ bool nxg_decode_archive_batch(NxgCtx* c, const uint8_t* buf, uint64_t len, NxgCo
     out->layout = NXG_LAYOUT_MIXED;
     if (ust) *ust = s;
     if (consumed) *consumed = r.consumed;
+    return true;
+}
+
+// ---- type-partitioned view ------------------------------------------------------
+bool nxg_partition_by_tag(NxgCtx* c, const NxgColumns* cols, NxgTagView* out, NetidxError* err) {
+    if (!c || !cols || !out) {
+        set_err(err, "null argument");
+        return false;
+    }
+    const uint64_t n = cols->n_rows;
+    if (cols->layout != NXG_LAYOUT_MIXED || !cols->tag || !cols->fixed || !cols->aux) {
+        set_err(err, "the type-partitioned view needs mixed-layout columns (a tag column)");
+        return false;
+    }
+    if (n && (!out->rank || !out->row_of || !out->fixed || !out->aux)) {
+        set_err(err, "null output array");
+        return false;
+    }
+    if (n > out->cap_rows || n > 0xffffffffull) {
+        set_err(err, "%llu rows: the view's capacity is %llu (and rows must be < 2^32)",
+                (unsigned long long)n, (unsigned long long)out->cap_rows);
+        return false;
+    }
+    if (n && (!is_device_ptr(cols->tag) || !is_device_ptr(out->rank))) {
+        set_err(err, "the type-partitioned view needs device columns and device outputs");
+        return false;
+    }
+    if (!c->pending.empty()) {
+        set_err(err, "an async operation is pending on this ctx; call nxg_ctx_sync first");
+        return false;
+    }
+    if (!set_device(c, err)) return false;
+    const size_t need = nxg_part_scratch_bytes(n);
+    if (need > c->pscratch_cap) {
+        HIPCHK(hipStreamSynchronize(c->stream));
+        if (c->pscratch) HIPCHK(hipFree(c->pscratch));
+        c->pscratch = nullptr;
+        const size_t m = std::max(need, c->pscratch_cap * 2);
+        HIPCHK(hipMalloc(&c->pscratch, m));
+        c->pscratch_cap = m;
+    }
+    uint64_t* doff = nullptr;
+    HIPCHK(nxg_launch_partition(cols->tag, cols->fixed, cols->aux, n, c->pscratch, out->rank,
+                                out->row_of, out->fixed, out->aux, &doff, c->stream));
+    HIPCHK(hipMemcpyAsync(out->off, doff, sizeof(uint64_t) * (NXG_TAG_BINS + 1),
+                          hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    for (int t = 0; t < NXG_TAG_BINS; t++) out->count[t] = out->off[t + 1] - out->off[t];
+    out->n_rows = n;
     return true;
 }
 

@@ -151,6 +151,13 @@ hipError_t nxg_launch_enc_f64(const uint64_t* id, const uint64_t* val, uint64_t 
 uint64_t nxg_enc_f64s_groups(uint64_t n);
 hipError_t nxg_launch_enc_f64s(const uint64_t* id, const uint64_t* val, uint64_t n, uint8_t* out,
                                uint64_t cap, DevStatus* st, hipStream_t s);
+// the type-partitioned view (nxg_partition.hip): count + scan + offsets + place launches;
+// `scratch` holds nxg_part_scratch_bytes(n) bytes; *off_out = the per-tag offsets (device, 257)
+uint64_t nxg_part_scratch_bytes(uint64_t n);
+hipError_t nxg_launch_partition(const uint8_t* tag, const uint64_t* fixed, const uint32_t* aux,
+                                uint64_t n, uint8_t* scratch, uint32_t* rank, uint32_t* row_of,
+                                uint64_t* dfixed, uint32_t* daux, uint64_t** off_out,
+                                hipStream_t s);
 uint64_t nxg_enc_general_tiles(uint64_t n);  // tiles (and tstat words) of a general encode
 // arch_base > 0: archive-batch rows after an arch_base-byte count header (nxg_encode_general.hip)
 hipError_t nxg_launch_enc_general(const ColsDesc& cols, const uint8_t* heap, uint8_t* out,

@@ -318,3 +318,19 @@ def share(o, k, shares):
     }
     out["n_heartbeat"] = int((out["ctl_variant"] == 5).sum())
     return r0, out
+
+
+def partition_by_tag(tag, fixed, aux, bins=256):
+    """Checker for nxg_partition_by_tag (the type-partitioned view): the rows grouped
+    by tag with a stable sort (record order within a tag), as numpy restates it -- integer
+    bookkeeping only, no codec rule involved. Returns {count, off, row_of, fixed, aux, rank}."""
+    tag = np.asarray(tag, np.uint8)
+    n = len(tag)
+    row_of = np.argsort(tag, kind="stable").astype(np.uint32)
+    count = np.bincount(tag, minlength=bins).astype(np.uint64)
+    off = np.zeros(bins + 1, np.uint64)
+    off[1:] = np.cumsum(count)
+    rank = np.empty(n, np.uint32)
+    rank[row_of] = (np.arange(n, dtype=np.uint64) - off[tag[row_of]]).astype(np.uint32)
+    return {"count": count, "off": off, "row_of": row_of, "fixed": np.asarray(fixed)[row_of],
+            "aux": np.asarray(aux)[row_of], "rank": rank}
