@@ -607,7 +607,7 @@ def extras_single_gpu(codec, stream, steps, warmup):
         heap = torch.from_numpy(m.heap.copy()).cuda()
         wire = codec.encode_batch(mc, heap)
         out = Columns(n + 1, len(m.ctag) + 1, 1, netidx_amd.LAYOUT_MIXED, "cuda")
-        wall, kms, st = time_decode(codec, wire, out, n, max(3, steps // 4), 1, 1, stream,
+        wall, kms, st = time_decode(codec, wire, out, n, max(20, steps // 2), 2, 1, stream,
                                     flags=netidx_amd.HINT_MIXED)
         assert st.path == 4 and st.n_rows == n and st.err_kind == 0
         checked = oracle_check_decode(wire, out, n, len(m.ctag))
@@ -700,7 +700,7 @@ def extras_single_gpu(codec, stream, steps, warmup):
         heap = torch.from_numpy(m.heap.copy()).cuda()
         wire = codec.encode_batch(mc, heap)
         out = Columns(n + 1, len(m.ctag) + 1, len(cr) + 1, netidx_amd.LAYOUT_MIXED, "cuda")
-        wall, kms, st = time_decode(codec, wire, out, n, max(3, steps // 4), 1, 1, stream,
+        wall, kms, st = time_decode(codec, wire, out, n, max(20, steps // 2), 2, 1, stream,
                                     flags=netidx_amd.HINT_MIXED)
         assert st.path == 4 and st.n_rows == n and st.err_kind == 0, st
         assert st.n_heartbeat == len(cr)

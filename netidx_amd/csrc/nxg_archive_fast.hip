@@ -745,7 +745,10 @@ __global__ __launch_bounds__(TPB) void nxg_fa_resolve_kernel(
 }
 
 // emit: one wave per tile that holds rows < count
-__global__ __launch_bounds__(TPB) void nxg_fa_emit_kernel(
+#ifndef NXG_FA_EOCC
+#define NXG_FA_EOCC 1  // waves per SIMD asked of the emit's register allocation (LDS allows 5)
+#endif
+__global__ __launch_bounds__(TPB, NXG_FA_EOCC) void nxg_fa_emit_kernel(
     const uint8_t* __restrict__ buf, uint64_t W, uint64_t nt, uint32_t p0, uint64_t count,
     const FaDesc* __restrict__ td, const uint64_t* __restrict__ tloc,
     const uint64_t* __restrict__ bpre, const uint64_t* __restrict__ starts, ColsDesc cols,

@@ -825,7 +825,10 @@ __global__ __launch_bounds__(TPB) void nxg_fmx_resolve_kernel(
 // after the tag), the value by val_decode; then the text of the round (ASCII per lane, the rest
 // by the wave), the rows (64 consecutive per store), and the array elements: their starts by a
 // walk per lane (by size), then one element per lane.
-__global__ __launch_bounds__(TPB) void nxg_fmx_emit_kernel(
+#ifndef NXG_FMX_EOCC
+#define NXG_FMX_EOCC 5  // waves per SIMD asked of the emit's register allocation (LDS allows 5; A/B 0.258 vs 0.273 ms)
+#endif
+__global__ __launch_bounds__(TPB, NXG_FMX_EOCC) void nxg_fmx_emit_kernel(
     const uint8_t* __restrict__ wire, FRange rg, uint64_t nt, const TileDesc* __restrict__ td,
     const uint64_t* __restrict__ tloc, const uint64_t* __restrict__ bpre,
     const uint64_t* __restrict__ starts, ColsDesc cols, bool ctl_on, DevStatus* __restrict__ st) {

@@ -114,7 +114,10 @@ NXG_DEV uint32_t wave_min(uint32_t v) { return wave_min_u32(v); }
 }  // namespace
 
 // ---- pass 1: per (channel, segment) entry counts ---------------------------------------------
-__global__ __launch_bounds__(TPB) void nxg_disp_count_kernel(
+#ifndef NXG_DISP_COCC
+#define NXG_DISP_COCC 1  // waves per SIMD asked of the register allocation (A/B)
+#endif
+__global__ __launch_bounds__(TPB, NXG_DISP_COCC) void nxg_disp_count_kernel(
     NxgSubTable tb, Route rt, const uint64_t* __restrict__ id, uint64_t n, uint64_t seg_rows,
     uint64_t n_seg,
     uint32_t* __restrict__ hist, uint64_t* __restrict__ last_row, uint64_t* __restrict__ unmatched) {
@@ -233,7 +236,10 @@ __global__ __launch_bounds__(TPB) void nxg_disp_scan_add_kernel(
 }
 
 // ---- pass 3: entries --------------------------------------------------------------------------
-__global__ __launch_bounds__(TPB) void nxg_disp_scatter_kernel(
+#ifndef NXG_DISP_SOCC
+#define NXG_DISP_SOCC 1  // waves per SIMD asked of the register allocation (A/B)
+#endif
+__global__ __launch_bounds__(TPB, NXG_DISP_SOCC) void nxg_disp_scatter_kernel(
     NxgSubTable tb, Route rt, const uint64_t* __restrict__ id, uint64_t n, uint64_t seg_rows,
     uint64_t n_seg,
     uint64_t* __restrict__ off, uint64_t* __restrict__ ent_sub, uint64_t* __restrict__ ent_row,
