@@ -36,6 +36,10 @@
 #ifndef NXG_ENC_PF
 #define NXG_ENC_PF 1  // the sizing and staging loops load their next entry's columns ahead
 #endif
+#ifndef NXG_ENC_KEEP
+#define NXG_ENC_KEEP 1  // the thread's entries' columns loaded once, all together, and kept in
+#endif                  // registers from the sizing pass to the staging pass (config 3 at 10^7:
+                        // 0.2265 vs 0.2428 ms with the one-ahead loads of NXG_ENC_PF)
 #ifndef NXG_ENC_CLS2
 #define NXG_ENC_CLS2 1  // class buckets from per-wave ballot counts (no LDS atomics)
 #endif
@@ -575,24 +579,8 @@ __global__ __launch_bounds__(TPB, NXG_ENC_OCC) void nxg_enc_rows_kernel(
         const uint32_t ne = cls_b[NCLS];
         // 2. message lengths, class by class. Each thread's next entry's slot and id are loaded
         //    while it sizes the current one (NXG_ENC_PF: two memory round trips in flight)
-        uint32_t p_rl = 0;
-        Slot p_v{0, 0, 0};
-        uint64_t p_id = 0;
-        if (NXG_ENC_PF && tid < ne) {
-            p_rl = lst_row[tid];
-            p_v = get_slot(c, true, rt + p_rl);
-            p_id = c.id[rt + p_rl];
-        }
-        for (uint32_t e = tid; e < ne; e += TPB) {
-            const uint32_t rl = NXG_ENC_PF ? p_rl : lst_row[e];
+        auto size_one = [&](uint32_t rl, Slot v, uint64_t idv) {
             const uint64_t r = rt + rl;
-            const Slot v = NXG_ENC_PF ? p_v : get_slot(c, true, r);
-            const uint64_t idv = NXG_ENC_PF ? p_id : c.id[r];
-            if (NXG_ENC_PF && e + TPB < ne) {
-                p_rl = lst_row[e + TPB];
-                p_v = get_slot(c, true, rt + p_rl);
-                p_id = c.id[rt + p_rl];
-            }
             uint64_t vlen = 0;
             uint32_t err = 0;
             bool gen = false;
@@ -628,7 +616,50 @@ __global__ __launch_bounds__(TPB, NXG_ENC_OCC) void nxg_enc_rows_kernel(
             if (!err && ml > (arch ? 0xFFFFFFFFull : 0x3FFFFFFFull)) err = NXG_TOO_BIG;
             if (err) atomicMax(&st->err_kind, err);
             len_lds[rl] = err ? 0u : (uint32_t)ml;
+        };
+#if NXG_ENC_KEEP
+        uint32_t k_rl[4];
+        Slot k_v[4];
+        uint64_t k_id[4];
+#pragma unroll
+        for (int j = 0; j < GRPT; j++) {
+            const uint32_t e = tid + (uint32_t)j * TPB;
+            k_rl[j] = e < ne ? lst_row[e] : 0u;
+            k_v[j] = e < ne ? get_slot(c, true, rt + k_rl[j]) : Slot{0, 0, 0};
+            k_id[j] = e < ne ? c.id[rt + k_rl[j]] : 0ull;
         }
+        // (spelled out: a loop the compiler leaves rolled would index the arrays dynamically,
+        // i.e. put them in scratch memory)
+        static_assert(GRPT <= 4, "NXG_ENC_KEEP keeps at most 4 rows per thread");
+#define NXG_KEEP_CALL(F, j) \
+    if ((j) < GRPT && tid + (uint32_t)(j) * TPB < ne) F(k_rl[j], k_v[j], k_id[j])
+        NXG_KEEP_CALL(size_one, 0);
+        NXG_KEEP_CALL(size_one, 1);
+        NXG_KEEP_CALL(size_one, 2);
+        NXG_KEEP_CALL(size_one, 3);
+#else
+        {
+            uint32_t p_rl = 0;
+            Slot p_v{0, 0, 0};
+            uint64_t p_id = 0;
+            if (NXG_ENC_PF && tid < ne) {
+                p_rl = lst_row[tid];
+                p_v = get_slot(c, true, rt + p_rl);
+                p_id = c.id[rt + p_rl];
+            }
+            for (uint32_t e = tid; e < ne; e += TPB) {
+                const uint32_t rl = NXG_ENC_PF ? p_rl : lst_row[e];
+                const Slot v = NXG_ENC_PF ? p_v : get_slot(c, true, rt + rl);
+                const uint64_t idv = NXG_ENC_PF ? p_id : c.id[rt + rl];
+                if (NXG_ENC_PF && e + TPB < ne) {
+                    p_rl = lst_row[e + TPB];
+                    p_v = get_slot(c, true, rt + p_rl);
+                    p_id = c.id[rt + p_rl];
+                }
+                size_one(rl, v, idv);
+            }
+        }
+#endif
         __syncthreads();
         ESTAMP(2);
         // 3. the tile's byte offsets: block scan, then look-back over the tiles' byte counts
@@ -681,27 +712,10 @@ __global__ __launch_bounds__(TPB, NXG_ENC_OCC) void nxg_enc_rows_kernel(
                 }
             }
             __syncthreads();
-            const uint32_t e0 = tid, es = TPB;
-            uint32_t q_rl = 0;
-            Slot q_v{0, 0, 0};
-            uint64_t q_id = 0;
-            if (NXG_ENC_PF && e0 < ne) {
-                q_rl = lst_row[e0];
-                q_v = get_slot(c, true, rt + q_rl);
-                q_id = c.id[rt + q_rl];
-            }
-            for (uint32_t e = e0; e < ne; e += es) {
-                const uint32_t rl = NXG_ENC_PF ? q_rl : lst_row[e];
+            auto stage_one = [&](uint32_t rl, Slot v, uint64_t idv) {
                 const uint64_t r = rt + rl;
-                const Slot v = NXG_ENC_PF ? q_v : get_slot(c, true, r);
-                const uint64_t idv = NXG_ENC_PF ? q_id : c.id[r];
-                if (NXG_ENC_PF && e + es < ne) {
-                    q_rl = lst_row[e + es];
-                    q_v = get_slot(c, true, rt + q_rl);
-                    q_id = c.id[rt + q_rl];
-                }
                 const uint32_t len = len_lds[rl];
-                if (!len) continue;
+                if (!len) return;
                 Out w{stg, off_lds[rl]};
                 if (arch) {
                     w.var((uint32_t)idv);
@@ -731,7 +745,34 @@ __global__ __launch_bounds__(TPB, NXG_ENC_OCC) void nxg_enc_rows_kernel(
                 }
                 one_lane_at_a_time(cls_lds[rl] == CLS_GEN,
                                    [&] { value_write(c, heap, true, r, w, stk); });
+            };
+#if NXG_ENC_KEEP
+            NXG_KEEP_CALL(stage_one, 0);
+            NXG_KEEP_CALL(stage_one, 1);
+            NXG_KEEP_CALL(stage_one, 2);
+            NXG_KEEP_CALL(stage_one, 3);
+#else
+            const uint32_t e0 = tid, es = TPB;
+            uint32_t q_rl = 0;
+            Slot q_v{0, 0, 0};
+            uint64_t q_id = 0;
+            if (NXG_ENC_PF && e0 < ne) {
+                q_rl = lst_row[e0];
+                q_v = get_slot(c, true, rt + q_rl);
+                q_id = c.id[rt + q_rl];
             }
+            for (uint32_t e = e0; e < ne; e += es) {
+                const uint32_t rl = NXG_ENC_PF ? q_rl : lst_row[e];
+                const Slot v = NXG_ENC_PF ? q_v : get_slot(c, true, rt + rl);
+                const uint64_t idv = NXG_ENC_PF ? q_id : c.id[rt + rl];
+                if (NXG_ENC_PF && e + es < ne) {
+                    q_rl = lst_row[e + es];
+                    q_v = get_slot(c, true, rt + q_rl);
+                    q_id = c.id[rt + q_rl];
+                }
+                stage_one(rl, v, idv);
+            }
+#endif
         }
         if (NXG_ENC_PF) {  // the next tile's tags: their round trip overlaps the look-back
             const uint64_t rn = (uint64_t)(tile + gridDim.x) * GTILE + (uint64_t)tid * GRPT;
