@@ -28,6 +28,34 @@ constexpr uint32_t WROWS = TROWS / WAVES;   // rows per wave: 16 rounds of 64
 constexpr uint32_t ROUNDS = WROWS / 64;
 constexpr uint32_t NB = 256;                // tag bins (the tag column is u8)
 constexpr uint32_t NOTAG = 0x100;           // a lane past the last row
+constexpr int KU = 8;                       // distinct tags per round handled unrolled
+
+// The round's distinct tags one after another (readfirstlane of the first unclaimed lane, a ballot
+// of the lanes holding that tag): f(k, leader lane, tag, lane mask) for each. The first KU are
+// unrolled (each LDS operation f issues gets its own registers, so nothing waits between them);
+// more than KU distinct tags in one round of 64 rows take the rolled loop.
+template <typename F>
+NXG_DEV void each_tag(uint32_t t, F&& f) {
+    uint64_t rem = __ballot(t != NOTAG);
+#pragma unroll
+    for (int k = 0; k < KU; k++) {
+        if (rem) {
+            const uint32_t l = (uint32_t)__builtin_ctzll(rem);
+            const uint32_t tv = (uint32_t)__builtin_amdgcn_readlane((int)t, (int)l);
+            const uint64_t m = __ballot(t == tv);
+            f(k, l, tv, m);
+            rem &= ~m;
+        }
+    }
+#pragma unroll 1
+    while (rem) {
+        const uint32_t l = (uint32_t)__builtin_ctzll(rem);
+        const uint32_t tv = (uint32_t)__builtin_amdgcn_readlane((int)t, (int)l);
+        const uint64_t m = __ballot(t == tv);
+        f(KU, l, tv, m);
+        rem &= ~m;
+    }
+}
 
 // the wave's rows' tags (16 rounds of 64; NOTAG past n), all loads in flight together
 NXG_DEV void load_tags(const uint8_t* __restrict__ tag, uint64_t r0, uint64_t n, uint32_t lane,
@@ -43,17 +71,10 @@ NXG_DEV void load_tags(const uint8_t* __restrict__ tag, uint64_t r0, uint64_t n,
 // distinct tag of a round, with no return (nothing waits on it)
 NXG_DEV void wave_hist(const uint32_t (&t)[ROUNDS], uint32_t* h, uint32_t lane) {
 #pragma unroll
-    for (uint32_t r = 0; r < ROUNDS; r++) {
-        uint64_t rem = __ballot(t[r] != NOTAG);
-#pragma unroll 1
-        while (rem) {
-            const uint32_t l = (uint32_t)__builtin_ctzll(rem);
-            const uint32_t tv = (uint32_t)__builtin_amdgcn_readlane((int)t[r], (int)l);
-            const uint64_t m = __ballot(t[r] == tv);
+    for (uint32_t r = 0; r < ROUNDS; r++)
+        each_tag(t[r], [&](int, uint32_t l, uint32_t tv, uint64_t m) {
             if (lane == l) atomicAdd(&h[tv], (uint32_t)__popcll(m));
-            rem &= ~m;
-        }
-    }
+        });
 }
 }  // namespace part
 
@@ -115,10 +136,12 @@ __global__ __launch_bounds__(TPB) void nxg_part_place_kernel(
     uint32_t* __restrict__ rank, uint32_t* __restrict__ row_of, uint64_t* __restrict__ dfixed,
     uint32_t* __restrict__ daux) {
     __shared__ uint32_t hist[WAVES][NB];  // then: each wave's next slot per bin
+    __shared__ uint32_t offl[NB];         // the per-tag offsets (rows < 2^32)
     const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const uint32_t tile = blockIdx.x;
 #pragma unroll
     for (uint32_t b = tid; b < WAVES * NB; b += TPB) (&hist[0][0])[b] = 0;
+    offl[tid] = (uint32_t)off[tid];
     __syncthreads();
     const uint64_t r0 = (uint64_t)tile * TROWS + (uint64_t)w * WROWS;
     uint32_t t[ROUNDS];
@@ -152,29 +175,33 @@ __global__ __launch_bounds__(TPB) void nxg_part_place_kernel(
         const uint64_t row = r0 + r * 64 + lane;
         const bool in = t[r] != NOTAG;
         // per distinct tag of the round: its leader lane takes the tag's slots with one LDS
-        // fetch-and-add (the adds of a round issue back to back; LDS applies them in order),
-        // each lane notes its leader and its tag's lane mask; then one ds_bpermute hands every
-        // lane its leader's base
-        uint32_t b = 0, ldr = 0;
+        // fetch-and-add into a register of its own (the adds of a round issue back to back; LDS
+        // applies them in order), each lane notes its leader and its tag's lane mask; then one
+        // ds_bpermute hands every lane its leader's base
+        uint32_t bk[KU + 1];
+#pragma unroll
+        for (int k = 0; k <= KU; k++) bk[k] = 0;
+        uint32_t ldr = 0;
         uint64_t mine = 0;
-        uint64_t rem = __ballot(in);
-#pragma unroll 1
-        while (rem) {
-            const uint32_t l = (uint32_t)__builtin_ctzll(rem);
-            const uint32_t tv = (uint32_t)__builtin_amdgcn_readlane((int)t[r], (int)l);
-            const uint64_t m = __ballot(t[r] == tv);
-            if (lane == l) b = atomicAdd(&nx[tv], (uint32_t)__popcll(m));
+        each_tag(t[r], [&](int k, uint32_t l, uint32_t tv, uint64_t m) {
+            if (lane == l) {
+                const uint32_t v = atomicAdd(&nx[tv], (uint32_t)__popcll(m));
+                if (k < KU) bk[k] = v;
+                else bk[KU] = v;  // (the rolled loop: its adds wait on each other)
+            }
             if (t[r] == tv) {
                 ldr = l;
                 mine = m;
             }
-            rem &= ~m;
-        }
+        });
+        uint32_t b = 0;
+#pragma unroll
+        for (int k = 0; k <= KU; k++) b |= bk[k];  // (each lane leads at most one tag)
         const uint32_t base = (uint32_t)__shfl((int)b, (int)ldr, 64);
         const uint32_t rk = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(mine >> 32),
                                                              __builtin_amdgcn_mbcnt_lo((uint32_t)mine, 0u));
         if (in) {
-            const uint64_t dest = off[t[r]] + rk;
+            const uint64_t dest = (uint64_t)offl[t[r]] + rk;
             rank[row] = rk;
             row_of[dest] = (uint32_t)row;
             dfixed[dest] = fv[r];
