@@ -628,6 +628,56 @@ __global__ __launch_bounds__(TPB) void nxg_fmx_count_kernel(const uint8_t* __res
     if (lane == 0) td[t] = d;
 }
 
+// The fix pass with a lane per tile (NXG_FMX_FIXW): a wave checks 64 tiles -- entry against the
+// predecessor's counted exit, as MODE 2 does per wave -- and recounts the ones that disagree one
+// after another, so a frame that needs few recounts (42 at config 3's 10^7 records) launches 64x
+// fewer waves than tiles. The same recount as MODE 2 (from the predecessor's exit when known,
+// else every candidate kind); the resolve pass checks whatever still disagrees.
+#ifndef NXG_FMX_FIXW
+#define NXG_FMX_FIXW 1  // (A/B at 10^7: plain 0.2564-0.2578 vs 0.2577-0.2604 ms, the frame with control equal)
+#endif
+__global__ __launch_bounds__(TPB) void nxg_fmx_fix_kernel(const uint8_t* __restrict__ wire, FRange rg,
+                                                          uint64_t nt, TileDesc* __restrict__ td,
+                                                          uint64_t* __restrict__ starts,
+                                                          DevStatus* sz) {
+    __shared__ __attribute__((aligned(16))) CountLds lds[TPB / 64];
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint64_t t0 = ((uint64_t)blockIdx.x * (TPB / 64) + w) * 64;
+    if (t0 >= nt) return;
+    const uint64_t tl = t0 + lane;
+    uint32_t pe = FAIL;
+    bool redo = false;
+    if (tl < nt) {
+        const uint32_t e = td[tl].entry;
+        if (tl > 0) {
+            const uint32_t px = td[tl - 1].exit;
+            if (px != FAIL && px - TILE < TILE) pe = px - TILE;
+        }
+        redo = !(e != FAIL && (pe == FAIL || pe == e));
+    }
+    uint8_t* img = lds[w].img;
+#pragma unroll 1
+    for (uint64_t m = __ballot(redo); m; m &= m - 1) {
+        const uint32_t j = (uint32_t)__builtin_ctzll(m);
+        const uint64_t t = t0 + j;
+        const uint32_t pj = (uint32_t)__builtin_amdgcn_readlane((int)pe, (int)j);
+        if (lane == 0) atomicAdd(&sz->diag[5], 1ull);
+        TileRegs g;
+        tile_load(g, wire, t * TILE, rg.W, lane);
+        tile_store(img, g, lane);
+        uint64_t bits;
+        TileDesc d;
+        if (pj != FAIL) {
+            const Cands cd = lane_cands<true>(img, lane, rg.lim(t));
+            d = count_from(img, cd, pj, rg.lim(t), rg.last(t, nt), lane, bits);
+        } else {
+            d = count_tile<true>(img, t, nt, rg, lane, bits);
+        }
+        starts[t * 64 + lane] = bits;
+        if (lane == 0) td[t] = d;
+    }
+}
+
 // The exit at which the chain leaves tile t - 1 (t >= 1), by the whole wave (uniform), from the
 // count pass's descriptors: the last tile before t whose entry is its predecessor's exit keeps
 // its exit; each tile after it passes the chain on -- a tile one long message covers entirely
@@ -1062,13 +1112,21 @@ hipError_t nxg_launch_dec_fmx_range(const uint8_t* wire, uint64_t W, uint64_t be
     if (lean_count) {
         hipLaunchKernelGGL(nxg_fmx_count_kernel<0>, dim3(gc), dim3(TPB), 0, s, wire, rg, nt, td,
                            starts, nxg_take_zero_slot());
-        hipLaunchKernelGGL(nxg_fmx_count_kernel<2>, dim3(gc), dim3(TPB), 0, s, wire, rg, nt, td,
-                           starts, st);
+        if (NXG_FMX_FIXW)
+            hipLaunchKernelGGL(nxg_fmx_fix_kernel, dim3((uint32_t)((nt + 64 * WV - 1) / (64 * WV))),
+                               dim3(TPB), 0, s, wire, rg, nt, td, starts, st);
+        else
+            hipLaunchKernelGGL(nxg_fmx_count_kernel<2>, dim3(gc), dim3(TPB), 0, s, wire, rg, nt,
+                               td, starts, st);
     } else {
         hipLaunchKernelGGL(nxg_fmx_count_kernel<1>, dim3(gc), dim3(TPB), 0, s, wire, rg, nt, td,
                            starts, nxg_take_zero_slot());
-        hipLaunchKernelGGL(nxg_fmx_count_kernel<2>, dim3(gc), dim3(TPB), 0, s, wire, rg, nt, td,
-                           starts, st);
+        if (NXG_FMX_FIXW)
+            hipLaunchKernelGGL(nxg_fmx_fix_kernel, dim3((uint32_t)((nt + 64 * WV - 1) / (64 * WV))),
+                               dim3(TPB), 0, s, wire, rg, nt, td, starts, st);
+        else
+            hipLaunchKernelGGL(nxg_fmx_count_kernel<2>, dim3(gc), dim3(TPB), 0, s, wire, rg, nt,
+                               td, starts, st);
     }
     const bool ctl_on = cols.ctl_row && cols.ctl_off && cols.ctl_len && cols.ctl_variant;
     hipLaunchKernelGGL(nxg_fmx_resolve_kernel, dim3((uint32_t)nb), dim3(TPB), 0, s, wire, rg, nt,
