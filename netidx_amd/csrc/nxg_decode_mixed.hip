@@ -459,6 +459,49 @@ NXG_DEV bool chunk_msgs(const uint8_t* img, uint32_t ce, uint32_t lane, uint32_t
     return true;
 }
 
+#ifndef NXG_FMX_LEANMSGS
+#define NXG_FMX_LEANMSGS 1
+#endif
+// chunk_msgs for a chain of the lean count: every position on it is a lean candidate (a one-byte
+// prefix in [4, 127], then the Update variant), so no Heartbeat and no two-byte prefix; each
+// message's length, id varint, tag and next byte come from one 12-byte window (two ds_read2_b32)
+// instead of a byte read, a 20-byte window and another byte read. The same checks as msg_kids.
+NXG_DEV bool chunk_msgs_lean(const uint8_t* img, uint32_t ce, uint32_t lane, uint32_t lim,
+                             uint32_t& n, uint32_t& kids, uint64_t& bits) {
+    n = 0;
+    kids = 0;
+    bits = 0;
+    if (ce == NONE) return true;
+    uint32_t x = ce;
+    const uint32_t c = lane * CH, end = min(c + CH, lim);
+#pragma unroll 1
+    while (x < end) {
+        uint32_t q[3];
+        win_words<3>((lds_bytes)img, x, q);  // bytes x .. x + 11
+        const uint32_t L = q[0] & 0xffu;
+        // bytes x + 2 .. x + 9: the id varint (at most 5 bytes here), the tag, the byte after
+        const uint64_t w = (uint64_t)__builtin_amdgcn_alignbyte(q[1], q[0], 2) |
+                           ((uint64_t)__builtin_amdgcn_alignbyte(q[2], q[1], 2) << 32);
+        const uint64_t stop = ~w & 0x8080808080808080ull;
+        const uint32_t k = stop ? (uint32_t)__builtin_ctzll(stop) >> 3 : 8u;
+        if (k >= 5) return false;  // ids wider than 35 bits: the general decoder
+        const uint32_t t = (uint32_t)(w >> (8 * k + 8)) & 0xffu;
+        const uint32_t cb = (uint32_t)(w >> (8 * k + 16)) & 0xffu;
+        uint32_t kk = 0;
+        if (t == 19u) {
+            if (cb >= 0x80u) return false;
+            kk = cb;
+        } else if (t == 21u || t >= 28u || (t == 22u && cb != 12u)) {
+            return false;
+        }
+        bits |= 1ull << (x - c);
+        n++;
+        kids += kk;
+        x += L;
+    }
+    return true;
+}
+
 // The decoded range: `wire` is its first byte, W the bytes from there to the frame's end, R <= W
 // the range's length (messages that START before R are the range's; the rest is read as
 // look-ahead), base = the range's offset in the frame (text / control offsets are frame
@@ -488,6 +531,7 @@ NXG_DEV bool lean_tile(const TileDesc& d) { return (d.rows >> 16) == 0 && !(d.ki
 // The tile's descriptor for the chain from entry e: exit, messages, child slots (FAIL entry and
 // exit when the chain breaks, or does not end exactly at the frame end in the last tile).
 // `bits`: the lane's message starts (chunk_msgs).
+template <bool FULL = true>
 NXG_DEV TileDesc count_from(const uint8_t* img, const Cands& cd, uint32_t e, uint32_t lim,
                             bool last, uint32_t lane, uint64_t& bits) {
     uint32_t ce;
@@ -497,7 +541,10 @@ NXG_DEV TileDesc count_from(const uint8_t* img, const Cands& cd, uint32_t e, uin
     uint32_t n = 0, h = 0, k = 0;
     bool two = false;
     bits = 0;
-    if (!bad) bad = !chunk_msgs(img, ce, lane, lim, n, h, k, bits, two);
+    if (!bad) {
+        if (!FULL && NXG_FMX_LEANMSGS) bad = !chunk_msgs_lean(img, ce, lane, lim, n, k, bits);
+        else bad = !chunk_msgs(img, ce, lane, lim, n, h, k, bits, two);
+    }
     bad = __any(bad);
     if (bad) return TileDesc{FAIL, FAIL, 0, 0};
     const uint32_t nh = wave_sum<uint32_t>(n | (h << 16));
@@ -521,7 +568,7 @@ NXG_DEV TileDesc count_tile(const uint8_t* img, uint64_t t, uint64_t nt, const F
     const Cands cd = lane_cands<FULL>(img, lane, lim);
     TileDesc d{FAIL, FAIL, 0, 0};
     bits = 0;
-    if (t == 0 && rg.first) return count_from(img, cd, 0, lim, last, lane, bits);
+    if (t == 0 && rg.first) return count_from<FULL>(img, cd, 0, lim, last, lane, bits);
     // the guesses: the first one-byte / Heartbeat candidates of chunks 0 and 1 (c0, c1)
     const uint32_t g00 = (uint32_t)__builtin_amdgcn_readlane((int)cd.c0, 0);
     const uint32_t g01 = (uint32_t)__builtin_amdgcn_readlane((int)cd.c1, 0);
@@ -539,7 +586,7 @@ NXG_DEV TileDesc count_tile(const uint8_t* img, uint64_t t, uint64_t nt, const F
             g = CH + (uint32_t)__builtin_ctzll(m1);
             m1 &= m1 - 1;
         }
-        d = count_from(img, cd, g, lim, last, lane, bits);
+        d = count_from<FULL>(img, cd, g, lim, last, lane, bits);
     }
     if (d.entry == FAIL) {
         // chunks 0 and 1 hold no candidate (the tile starts inside a long text): the first
@@ -547,7 +594,7 @@ NXG_DEV TileDesc count_tile(const uint8_t* img, uint64_t t, uint64_t nt, const F
         const uint64_t cm = __ballot(cd.c0 != FAIL) & ~3ull;
         if (cm) {
             const uint32_t g = (uint32_t)__builtin_amdgcn_readlane((int)cd.c0, (int)__builtin_ctzll(cm));
-            d = count_from(img, cd, g, lim, last, lane, bits);
+            d = count_from<FULL>(img, cd, g, lim, last, lane, bits);
         }
     }
     if (FULL && d.entry != FAIL) {
