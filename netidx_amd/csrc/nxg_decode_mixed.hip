@@ -78,12 +78,26 @@ using namespace nxgmsg;
 struct CountLds {  // count / fix passes
     uint8_t img[IMG];
 };
+#ifndef NXG_FMX_DEFER
+#define NXG_FMX_DEFER 0  // 1: the emit gathers Array elements over rounds (defer_flush). Measured slower
+// (config 3 at 10^7: 0.290-0.303 ms with the walk inlined, 0.54 ms out of line, against 0.253-0.268
+// ms per round): the batch state spills the emit at 96 VGPRs (scratch 8 -> 52 bytes per lane)
+#endif
+constexpr uint32_t DMAXA = 64;  // deferred arrays per batch (a round's arrays fit one)
 struct EmitLds {
     uint8_t img[IMG];
     uint16_t msg[MAXM];  // the tile's message starts
     uint32_t el[MAXC];   // a round's array elements: position | (message end - position) << 13
     uint8_t mark[256];   // utf8_packed
+#if NXG_FMX_DEFER
+    uint8_t emark[MAXC];    // deferred elements: array index + 1 at each array's first element
+    // deferred arrays: first element | (message end - first element) << 13 | element size << 20
+    // | batch index of the first element << 24
+    uint32_t adesc[DMAXA];
+#endif
 };
+// a workgroup's EmitLds in 32 KB: 5 workgroups per CU (NXG_FMX_EOCC)
+static_assert(sizeof(EmitLds) * (TPB / 64) <= 32768, "emit LDS");
 
 // candidate message starts in the lane's chunk: bit i = byte c+i starts an Update with a one-byte
 // prefix (a byte in [4, 127], then 4) or a Heartbeat (02 05): the return value; or an Update with
@@ -916,6 +930,100 @@ __global__ __launch_bounds__(TPB) void nxg_fmx_resolve_kernel(
     }
 }
 
+#if NXG_FMX_DEFER
+// defer_flush's fallback, out of line (rare; its registers kept out of the emit's): lane a walks
+// array a by val_decode, with the UTF-8 check per element. Returns this lane's ok.
+#ifndef NXG_FMX_DWALK_NI
+#define NXG_FMX_DWALK_NI 1
+#endif
+#if NXG_FMX_DWALK_NI
+__device__ __noinline__
+#else
+NXG_DEV
+#endif
+bool defer_walk(EmitLds& L, uint32_t ne, uint32_t na, uint64_t cpend,
+                                        const ColsDesc& cols, uint64_t t0f, uint32_t lane) {
+    const lds_bytes limg = (lds_bytes)L.img;
+    bool ok = true;
+    if (lane < na) {
+        const uint32_t dsc = L.adesc[lane], k0 = dsc >> 24;
+        const uint32_t k1 = lane + 1u < na ? L.adesc[lane + 1u] >> 24 : ne;
+        uint32_t ep = dsc & 0x1fffu;
+        const uint32_t lim = ep + ((dsc >> 13) & 127u);
+#pragma unroll 1
+        for (uint32_t c = k0; ok && c < k1; c++) {
+            ok = ep < lim;
+            if (!ok) break;
+            const uint32_t et = L.img[ep];
+            uint32_t q[3];
+            win_words<3>(limg, ep + 1, q);
+            const FV e = val_decode(et, q[0], q[1], q[2], ep + 1, lim, false, t0f);
+            ok = e.ok && (!e.slen || utf8_ok(LdsSrc{limg, t0f}, t0f + e.soff, e.slen));
+            const uint64_t slot = cpend + c;
+            if (ok && slot < cols.cap_children) {
+                col_st(&cols.ctag[slot], (uint8_t)e.tag);
+                col_st(&cols.cfixed[slot], (uint64_t)e.fixed);
+                col_st(&cols.caux[slot], (uint32_t)e.aux);
+            }
+            ep = e.end;
+        }
+    }
+    return ok;
+}
+
+// The deferred Array elements of a tile: ne elements of na arrays gathered over rounds (each
+// array's first element of a fixed size), batch element j in slot cpend + j, one element per
+// lane: its array from a max-scan over emark, its position from the array's stride, checked by
+// its own tag (as round_elements' stride path, over up to 256 elements of several rounds instead
+// of one round's). An array whose elements differ in size sends the batch to a walk per lane
+// (lane a: array a, val_decode and the UTF-8 check per element). emark is left zero. Returns
+// true (uniform) on a decode error.
+NXG_DEV bool defer_flush(EmitLds& L, uint32_t ne, uint32_t na, uint64_t cpend,
+                         const ColsDesc& cols, uint64_t t0f, uint32_t lane) {
+    const lds_bytes limg = (lds_bytes)L.img;
+    bool bad = false, strided = true;
+    uint32_t carry = 0;
+    wave_lds_order();
+#pragma unroll 1
+    for (uint32_t j0 = 0; j0 < ne; j0 += 64) {
+        const uint32_t j = j0 + lane;
+        const bool he = j < ne;
+        // emark[0] is set (the batch's first array starts it): a1 >= 1 on every lane
+        const uint32_t a1 = max(wave_max_scan(he ? (uint32_t)L.emark[j] : 0u), carry);
+        carry = wave_last<uint32_t>(a1);
+        const uint32_t dsc = L.adesc[a1 - 1u];
+        const uint32_t fa = (dsc >> 20) & 15u, k0 = dsc >> 24, ep = dsc & 0x1fffu;
+        const uint32_t e0 = he ? ep + (j - k0) * fa : 8u;
+        const uint32_t elim = he ? ep + ((dsc >> 13) & 127u) : 16u;
+        uint32_t q[4];
+        win_words<4>(limg, e0, q);
+        const uint32_t et = q[0] & 0xffu;
+        if (!__all(!he || (e0 < elim && fixed_size1(et) == fa))) {
+            strided = false;
+            break;
+        }
+        FV e;
+        if (__all(!he || simple_fixed(et))) e = fixed_elem(q, e0, elim);  // scalars only
+        else  // DateTime / Duration elements
+            e = val_decode(et, alignbyte(q[1], q[0], 1), alignbyte(q[2], q[1], 1),
+                           alignbyte(q[3], q[2], 1), e0 + 1, elim, false, t0f);
+        bad = __any(he && !e.ok);
+        if (bad) break;
+        const uint64_t slot = cpend + j;
+        if (he && slot < cols.cap_children) {
+            col_st(&cols.ctag[slot], (uint8_t)e.tag);
+            col_st(&cols.cfixed[slot], (uint64_t)e.fixed);
+            col_st(&cols.caux[slot], (uint32_t)e.aux);
+        }
+    }
+    if (!strided) bad = __any(!defer_walk(L, ne, na, cpend, cols, t0f, lane));
+    wave_lds_order();
+    if (lane < na) L.emark[L.adesc[lane] >> 24] = 0;
+    wave_lds_order();
+    return bad;
+}
+#endif
+
 // emit: one wave per tile. The message starts come from the count / fix passes (bits per
 // chunk), so the emit pass does not walk the chain again. Per round of 64 messages each lane
 // decodes one: the header from 20 bytes at its start (length, id varint, tag and the 12 bytes
@@ -969,6 +1077,10 @@ __global__ __launch_bounds__(TPB, NXG_FMX_EOCC) void nxg_fmx_emit_kernel(
     // agent-scope load per wave on one address)
     if (NXG_FF_CHECK && st->fast_fail) return;
     tile_store(img, g, lane);
+#if NXG_FMX_DEFER
+    reinterpret_cast<uint32_t*>(lds[w].emark)[lane] = 0u;
+    static_assert(MAXC == 256, "emark: a word per lane");
+#endif
     // the message list in wire order
     const uint32_t n0 = (uint32_t)__popcll(bits);
     uint32_t at = wave_incl_scan<uint32_t>(n0) - n0;
@@ -986,6 +1098,8 @@ __global__ __launch_bounds__(TPB, NXG_FMX_EOCC) void nxg_fmx_emit_kernel(
     auto rounds = [&](auto lean_c) {
         constexpr bool LEAN = decltype(lean_c)::value;
         uint32_t ntxt = 0;  // deferred text checks in el[0, ntxt)
+        uint32_t pe = 0, pa = 0;  // deferred elements and arrays (NXG_FMX_DEFER)
+        uint64_t cpend = 0;       // the first deferred element's slot
     #pragma unroll 1
         for (uint32_t k = 0; k < nm && !bad; k += 64) {
             const uint32_t i = k + lane;
@@ -1073,10 +1187,56 @@ __global__ __launch_bounds__(TPB, NXG_FMX_EOCC) void nxg_fmx_emit_kernel(
                 col_st(&cols.aux[row], (uint32_t)o.aux);
             }
             PMARK(3);
+#if NXG_FMX_DEFER
+            if (NXG_FMX_SKIP & 1) {
+                cnext += rk;
+                continue;
+            }
+            {
+                // a round whose every array starts with a fixed-size element joins the batch (a
+                // round without arrays too); the batch is flushed before a round that does not fit
+                // or join it and after the tile's last round (one call site: defer_flush inlined
+                // once)
+                const uint32_t f1a = kd && o.end < lim ? fixed_size1(img[o.end]) : 0u;
+                const uint64_t am = __ballot(kd != 0u);
+                const uint32_t narr = (uint32_t)__popcll(am);
+                const bool join = !__any(kd && (f1a == 0u || lim - o.end > 127u || o.end > 0x1fffu)) && rk <= MAXC;
+                const bool last = k + 64u >= nm;
+                bool app = false;
+    #pragma unroll 1
+                for (;;) {
+                    if (pe && (app ? last : (!join || pe + rk > MAXC || pa + narr > DMAXA))) {
+                        bad = defer_flush(lds[w], pe, pa, cpend, cols, t0f, lane);
+                        pe = pa = 0;
+                        if (bad) break;
+                    }
+                    if (app || !join) break;
+                    if (pe == 0) cpend = cnext;
+                    if (kd) {
+                        const uint32_t ai = pa + __builtin_amdgcn_mbcnt_hi(
+                                                     (uint32_t)(am >> 32),
+                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)am, 0u));
+                        lds[w].adesc[ai] = o.end | ((lim - o.end) << 13) | (f1a << 20) |
+                                           ((pe + kpre) << 24);
+                        lds[w].emark[pe + kpre] = (uint8_t)(ai + 1u);
+                    }
+                    pe += rk;
+                    pa += narr;
+                    app = true;
+                }
+                if (bad) break;
+                if (join) {
+                    cnext += rk;
+                    PMARK(5);
+                    continue;
+                }
+            }
+#else
             if (rk == 0 || (NXG_FMX_SKIP & 1)) {
                 cnext += rk;
                 continue;
             }
+#endif
             bad = round_elements(img, lds[w].mark, el, kd, kpre, rk, o.end, lim, cnext, cols, t0f, lane,
                                  ntxt, st);
             if (bad) break;

@@ -251,6 +251,43 @@ def test_fast_long_arrays(codec):
     assert reencode(codec, cols, wire) == wire
 
 
+@pytest.mark.parametrize("mix", [0.0, 0.02, 0.3])
+def test_fast_deferred_array_batches(codec, mix):
+    """Arrays of one fixed-size element tag each (the emit gathers their elements over rounds, up
+    to 256 elements of 64 arrays a batch), DateTime / Duration arrays among them, and a share
+    `mix` of arrays whose later elements differ in size (a fixed size of another length, a varint
+    or text: the batch's walk per array), between scalars and Arrays without elements."""
+    mg = _mg()
+    rng = random.Random(int(mix * 1000) + 17)
+    fixed_tags = [0, 2, 4, 6, 8, 9, 10, 11, 14, 15, 16, 20, 23, 24, 25, 26]
+    msgs = []
+    for i in range(20_000):
+        u = rng.random()
+        if u < 0.15:
+            msgs.append(("u", i, (9, rng.getrandbits(64))))
+            continue
+        if u < 0.18:
+            msgs.append(("u", i, (19, [])))
+            continue
+        t = rng.choice(fixed_tags)
+        while True:  # (rand_value draws every tag at depth 0)
+            v = mg.rand_value(rng)
+            if v[0] == t:
+                break
+        els = [v] * rng.randrange(1, 12)
+        if len(els) > 1 and rng.random() < mix:
+            els[rng.randrange(1, len(els))] = rng.choice(
+                [(1, rng.getrandbits(14)), (12, "é€".encode()), (24, -5), (9, 7), (10, (5, 6)),
+                 (11, (3, 4))])
+        if len(mg.update(i, (19, els))) < 128:
+            msgs.append(("u", i, (19, els)))
+    wire, _ = mg.batch(msgs)
+    cols, st = gpu_decode(codec, wire, flags=hint())
+    assert st.err_kind == 0 and st.path == 4, (st.path, st.err_kind)
+    assert_same_as_oracle(cols, st, wire)
+    assert reencode(codec, cols, wire) == wire
+
+
 UTF8_VALID = [
     b"", b"a", b"\x7f", "\u0080".encode(), "߿".encode(), "ࠀ".encode(),
     "퟿".encode(), "".encode(), "￿".encode(), "\U00010000".encode(),
