@@ -33,7 +33,9 @@ constexpr uint32_t SCAN_B = TPB * SCAN_K;
 
 constexpr uint32_t RF = 4;  // streams per row held in registers (more: read from memory)
 #ifndef NXG_DISP_U
-#define NXG_DISP_U 4  // (1 / 2 / 4 at 10^7, 16 channels: 0.433 / 0.415 / 0.401-0.418 ms)
+#define NXG_DISP_U 2  // (round 5, 1024-row segments: 1 / 2 / 4 steps 0.433 / 0.415 / 0.401-0.418 ms;
+// round 6, one segment per wave: 128 rows x 2 steps 0.346-0.351, 256 x 4 0.337-0.360, 256 x 2
+// 0.365-0.369, 512 x 8 0.418-0.422 ms, 1024 x 4 on a capped grid 0.366-0.384 ms)
 #endif
 constexpr int DU = NXG_DISP_U;  // 64-row steps whose lookups are in flight together
 // (entries stored nontemporal measured 0.56 vs 0.40 ms: scattered 8-byte stores need the L2 to
@@ -111,6 +113,51 @@ NXG_DEV uint32_t count_chan(const NxgSubTable& tb, const Row& r, uint32_t d) {
 
 NXG_DEV uint32_t wave_min(uint32_t v) { return wave_min_u32(v); }
 
+// The count pass's lookups kept for the scatter (NXG_DISP_CACHE): per row its slot and the
+// channels of up to two streams (a 16-bit half each, kNoChan: none; kLookup in the low half: more
+// streams, the scatter looks the row up again), so the scatter's chain of dependent loads is the
+// cache and the SubId instead of Id -> slot -> stream offsets -> channel. Null pointers: no cache
+// (kLookup channels or more). `narrow` (fewer than 254 channels): the two channels in the bytes
+// of a 16-bit word (0xff none, 0xfe look up), 6 bytes per row instead of 8.
+#ifndef NXG_DISP_CACHE
+#define NXG_DISP_CACHE 1
+#endif
+constexpr uint16_t kNoChan = 0xffff, kLookup = 0xfffe;
+struct RowCache {
+    uint32_t* slot;
+    void* ch;
+    bool narrow;
+};
+NXG_DEV void cache_put(const RowCache& rc, uint64_t i, uint32_t slot, uint32_t ns, uint32_t c0,
+                       uint32_t c1) {  // c0, c1: channels or NONE
+    rc.slot[i] = slot;
+    if (rc.narrow)
+        static_cast<uint16_t*>(rc.ch)[i] =
+            ns > 2u ? 0xfeu : (c0 == NONE ? 0xffu : c0) | ((c1 == NONE ? 0xffu : c1) << 8);
+    else
+        static_cast<uint32_t*>(rc.ch)[i] =
+            ns > 2u ? kLookup : (c0 == NONE ? kNoChan : c0) | ((c1 == NONE ? kNoChan : c1) << 16);
+}
+// false: look the row up again; else its two channels (NONE: none)
+NXG_DEV bool cache_get(const RowCache& rc, uint64_t i, uint32_t& c0, uint32_t& c1) {
+    if (rc.narrow) {
+        const uint32_t w = static_cast<const uint16_t*>(rc.ch)[i];
+        c0 = w & 0xffu;
+        c1 = w >> 8;
+        if (c0 == 0xfeu) return false;
+        c0 = c0 == 0xffu ? NONE : c0;
+        c1 = c1 == 0xffu ? NONE : c1;
+    } else {
+        const uint32_t w = static_cast<const uint32_t*>(rc.ch)[i];
+        c0 = w & 0xffffu;
+        c1 = w >> 16;
+        if (c0 == kLookup) return false;
+        c0 = c0 == kNoChan ? NONE : c0;
+        c1 = c1 == kNoChan ? NONE : c1;
+    }
+    return true;
+}
+
 }  // namespace
 
 // ---- pass 1: per (channel, segment) entry counts ---------------------------------------------
@@ -120,7 +167,8 @@ NXG_DEV uint32_t wave_min(uint32_t v) { return wave_min_u32(v); }
 __global__ __launch_bounds__(TPB, NXG_DISP_COCC) void nxg_disp_count_kernel(
     NxgSubTable tb, Route rt, const uint64_t* __restrict__ id, uint64_t n, uint64_t seg_rows,
     uint64_t n_seg,
-    uint32_t* __restrict__ hist, uint64_t* __restrict__ last_row, uint64_t* __restrict__ unmatched) {
+    uint32_t* __restrict__ hist, uint64_t* __restrict__ last_row, uint64_t* __restrict__ unmatched,
+    RowCache rc) {
     // (dynamic LDS: n_chans counters per wave, sized at launch, so that few channels leave room
     // for more workgroups per CU)
     extern __shared__ __attribute__((aligned(16))) uint64_t dyn_lds[];
@@ -149,6 +197,10 @@ __global__ __launch_bounds__(TPB, NXG_DISP_COCC) void nxg_disp_count_kernel(
             const bool unm = unms[u];
             const Row& r = rows[u];
             um += unm;
+            if (rc.slot && i < r1) {
+                const uint32_t ns = r.k1 - r.k0;
+                cache_put(rc, i, r.slot, ns, ns >= 1u ? r.c[0] : NONE, ns >= 2u ? r.c[1] : NONE);
+            }
             if (r.slot != NONE && (!tb.slot_has_last || tb.slot_has_last[r.slot]))
                 atomicMax((unsigned long long*)&last_row[r.slot], (unsigned long long)(i + 1));
             // order-free: one atomic per (row, stream)
@@ -243,7 +295,7 @@ __global__ __launch_bounds__(TPB, NXG_DISP_SOCC) void nxg_disp_scatter_kernel(
     NxgSubTable tb, Route rt, const uint64_t* __restrict__ id, uint64_t n, uint64_t seg_rows,
     uint64_t n_seg,
     uint64_t* __restrict__ off, uint64_t* __restrict__ ent_sub, uint64_t* __restrict__ ent_row,
-    uint64_t cap) {
+    uint64_t cap, RowCache rc) {
     // (dynamic LDS: a cursor and a lane mask per channel and wave, sized at launch)
     extern __shared__ __attribute__((aligned(16))) uint64_t dyn_lds[];
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -271,7 +323,13 @@ __global__ __launch_bounds__(TPB, NXG_DISP_SOCC) void nxg_disp_scatter_kernel(
           for (int u = 0; u < DU; u++) {
             const uint64_t i = b0 + 64 * u + lane;
             bool unm;
-            rows[u] = row_of(tb, rt, id, i, r1, unm);
+            if (rc.slot) {
+                uint32_t c0 = NONE, c1 = NONE;
+                if (i < r1 && !cache_get(rc, i, c0, c1)) rows[u] = row_of(tb, rt, id, i, r1, unm);
+                else rows[u] = Row{0u, 2u, i < r1 ? rc.slot[i] : NONE, {c0, c1, NONE, NONE}};
+            } else {
+                rows[u] = row_of(tb, rt, id, i, r1, unm);
+            }
             // the entry's tag: the subscription's SubId, or (no SubId table) the row's own Id
             subs[u] = !tb.slot_sub_id ? (i < r1 ? id[i] : 0)
                       : (rows[u].slot != NONE ? tb.slot_sub_id[rows[u].slot] : 0);
@@ -359,8 +417,14 @@ namespace {
 constexpr uint64_t MAX_M = 1ull << 26;  // (channel, segment) counters
 }
 
+#ifndef NXG_DISP_SEG
+#define NXG_DISP_SEG 128  // rows per segment (one group of NXG_DISP_U 64-row steps)
+#endif
+#ifndef NXG_DISP_GCAP
+#define NXG_DISP_GCAP 0  // workgroups per CU at most (0: one segment per wave, no grid-stride)
+#endif
 uint64_t nxg_disp_seg_rows(uint64_t n, uint32_t n_chans) {
-    uint64_t seg = 1024;
+    uint64_t seg = NXG_DISP_SEG;
     const uint64_t ch = n_chans ? n_chans : 1;
     while (((n + seg - 1) / seg) * ch > MAX_M) seg *= 2;
     return seg;
@@ -370,7 +434,7 @@ uint64_t nxg_disp_scratch_bytes(uint64_t n, uint32_t n_chans) {
     const uint64_t seg = nxg_disp_seg_rows(n, n_chans);
     const uint64_t M = ((n + seg - 1) / seg) * (uint64_t)n_chans;
     const uint64_t nb = (M + SCAN_B - 1) / SCAN_B;
-    return M * 4 + M * 8 + (nb + 1) * 8 + 64;
+    return M * 4 + M * 8 + (nb + 1) * 8 + 64 + (NXG_DISP_CACHE ? n * 8 + 16 : 0);
 }
 
 hipError_t nxg_launch_dispatch(const NxgSubTable& tb, const uint64_t* id, uint64_t n,
@@ -386,19 +450,32 @@ hipError_t nxg_launch_dispatch(const NxgSubTable& tb, const uint64_t* id, uint64
     uint32_t* hist = reinterpret_cast<uint32_t*>(scratch);
     uint64_t* off = reinterpret_cast<uint64_t*>(scratch + ((M * 4 + 7) & ~7ull));
     uint64_t* bsum = off + M;
+#ifndef NXG_DISP_NARROW
+#define NXG_DISP_NARROW 1
+#endif
+    RowCache rc{nullptr, nullptr, NXG_DISP_NARROW && tb.n_chans < 0xfeu};
+    if (NXG_DISP_CACHE && tb.n_chans < kLookup) {
+        rc.slot = reinterpret_cast<uint32_t*>(bsum + nb + 1);
+        rc.ch = rc.slot + n;
+    }
     hipError_t e;
     if ((e = hipMemsetAsync(unmatched, 0, 8, s)) != hipSuccess) return e;
     if (tb.n_slots && (e = hipMemsetAsync(last_row, 0, tb.n_slots * 8, s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(chan_off, 0, ((uint64_t)tb.n_chans + 1) * 8, s)) != hipSuccess) return e;
     if (n == 0) return hipSuccess;
     if (tb.n_chans > LCH && (e = hipMemsetAsync(hist, 0, M * 4, s)) != hipSuccess) return e;
+    // one segment per wave: the hardware hands workgroups to CUs as they free up, so a wave's
+    // chain of dependent lookups (Id -> slot -> streams -> channel) does not leave a tail of CUs
+    // working a second segment while the others idle (round 6: 1024-row segments on a grid of
+    // 8 workgroups per CU measured count 127 / scatter 185 us at 10^7 rows, 16 channels)
     const uint64_t want = (n_seg + WAVES - 1) / WAVES;
-    const uint32_t g = (uint32_t)(want < (uint64_t)ncu * 8 ? want : (uint64_t)ncu * 8);
+    const uint64_t gcap = NXG_DISP_GCAP ? (uint64_t)ncu * NXG_DISP_GCAP : 0x7fffffffull;
+    const uint32_t g = (uint32_t)(want < gcap ? want : gcap);
     const bool in_lds = tb.n_chans <= LCH;
     const size_t lds_count = in_lds ? (size_t)WAVES * tb.n_chans * 4 : 0;
     const size_t lds_scatter = in_lds ? (size_t)WAVES * tb.n_chans * 16 : 0;
     hipLaunchKernelGGL(nxg_disp_count_kernel, dim3(g), dim3(TPB), lds_count, s, tb, rt, id, n, seg,
-                       n_seg, hist, last_row, unmatched);
+                       n_seg, hist, last_row, unmatched, rc);
     if (M) {
         hipLaunchKernelGGL(nxg_disp_scan_block_kernel, dim3((uint32_t)nb), dim3(TPB), 0, s, hist, M,
                            off, bsum);
@@ -406,7 +483,7 @@ hipError_t nxg_launch_dispatch(const NxgSubTable& tb, const uint64_t* id, uint64
         hipLaunchKernelGGL(nxg_disp_scan_add_kernel, dim3((uint32_t)((M + TPB - 1) / TPB)),
                            dim3(TPB), 0, s, off, M, bsum, nb, n_seg, tb.n_chans, chan_off);
         hipLaunchKernelGGL(nxg_disp_scatter_kernel, dim3(g), dim3(TPB), lds_scatter, s, tb, rt, id,
-                           n, seg, n_seg, off, ent_sub, ent_row, cap);
+                           n, seg, n_seg, off, ent_sub, ent_row, cap, rc);
     }
     return hipGetLastError();
 }

@@ -54,6 +54,8 @@ def run_both(codec, ids, subs, n_ids, n_chans):
     (18, 30000, 3000, 1025, 3),  # global-memory counters
     (19, 20000, 20000, 5000, 2),
     (20, 100000, 1000, 64, 8),  # repeated ids: last = the final occurrence
+    (21, 129, 100, 5, 2),       # one row past a 128-row segment
+    (22, 5000, 3000, 70000, 2),  # more channels than the count pass's row cache names
 ])
 def test_dispatch_matches_oracle(codec, seed, n_rows, n_ids, n_chans, max_fan):
     rng = random.Random(seed)
