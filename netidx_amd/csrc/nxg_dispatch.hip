@@ -9,7 +9,8 @@
 // launches, deterministic (no atomics decide an order):
 //   count    one wave per segment of SEG rows (64 rows per step); one counter increment per
 //            (row, stream), order-free. Counters end in hist[chan * n_seg + seg] (channel-major).
-//            Also: last_row (atomicMax of row + 1), unmatched rows.
+//            Also: last_row (atomicMax of row + 1), unmatched rows. (NXG_DISP_LASTP: a plain store
+//            that the scatter raises to the slot's last row, measured slower.)
 //   scan     exclusive scan of hist in that order: the first entry of every (channel, segment)
 //            pair; chan_off[c] is the (c, 0) value.
 //   scatter  the rows again; an entry's position is the wave's running count for its channel
@@ -161,6 +162,13 @@ NXG_DEV bool cache_get(const RowCache& rc, uint64_t i, uint32_t& c0, uint32_t& c
 }  // namespace
 
 // ---- pass 1: per (channel, segment) entry counts ---------------------------------------------
+#ifndef NXG_DISP_SKIP
+#define NXG_DISP_SKIP 0  // timing experiments only: 1 last_row, 2 counters, 4 the row cache
+#endif
+#ifndef NXG_DISP_LASTP
+#define NXG_DISP_LASTP 0  // 1: plain last_row stores finished by the scatter (measured slower: 0.353-0.363
+// vs 0.337-0.350 ms sequential, 1.40-1.42 vs 1.10 ms random Ids at 10^7, 16 channels)
+#endif
 #ifndef NXG_DISP_COCC
 #define NXG_DISP_COCC 1  // waves per SIMD asked of the register allocation (A/B)
 #endif
@@ -168,7 +176,7 @@ __global__ __launch_bounds__(TPB, NXG_DISP_COCC) void nxg_disp_count_kernel(
     NxgSubTable tb, Route rt, const uint64_t* __restrict__ id, uint64_t n, uint64_t seg_rows,
     uint64_t n_seg,
     uint32_t* __restrict__ hist, uint64_t* __restrict__ last_row, uint64_t* __restrict__ unmatched,
-    RowCache rc) {
+    RowCache rc, bool plain_last) {
     // (dynamic LDS: n_chans counters per wave, sized at launch, so that few channels leave room
     // for more workgroups per CU)
     extern __shared__ __attribute__((aligned(16))) uint64_t dyn_lds[];
@@ -197,14 +205,17 @@ __global__ __launch_bounds__(TPB, NXG_DISP_COCC) void nxg_disp_count_kernel(
             const bool unm = unms[u];
             const Row& r = rows[u];
             um += unm;
-            if (rc.slot && i < r1) {
+            if (!(NXG_DISP_SKIP & 4) && rc.slot && i < r1) {
                 const uint32_t ns = r.k1 - r.k0;
                 cache_put(rc, i, r.slot, ns, ns >= 1u ? r.c[0] : NONE, ns >= 2u ? r.c[1] : NONE);
             }
-            if (r.slot != NONE && (!tb.slot_has_last || tb.slot_has_last[r.slot]))
-                atomicMax((unsigned long long*)&last_row[r.slot], (unsigned long long)(i + 1));
+            if (!(NXG_DISP_SKIP & 1) && r.slot != NONE && (!tb.slot_has_last || tb.slot_has_last[r.slot])) {
+                if (plain_last) last_row[r.slot] = i + 1;
+                else atomicMax((unsigned long long*)&last_row[r.slot], (unsigned long long)(i + 1));
+            }
             // order-free: one atomic per (row, stream)
-            if (r.k1 - r.k0 <= RF) {
+            if (NXG_DISP_SKIP & 2) {
+            } else if (r.k1 - r.k0 <= RF) {
 #pragma unroll
                 for (uint32_t j = 0; j < RF; j++) {
                     if (r.c[j] == NONE) continue;
@@ -295,7 +306,7 @@ __global__ __launch_bounds__(TPB, NXG_DISP_SOCC) void nxg_disp_scatter_kernel(
     NxgSubTable tb, Route rt, const uint64_t* __restrict__ id, uint64_t n, uint64_t seg_rows,
     uint64_t n_seg,
     uint64_t* __restrict__ off, uint64_t* __restrict__ ent_sub, uint64_t* __restrict__ ent_row,
-    uint64_t cap, RowCache rc) {
+    uint64_t cap, RowCache rc, uint64_t* __restrict__ last_row, bool plain_last) {
     // (dynamic LDS: a cursor and a lane mask per channel and wave, sized at launch)
     extern __shared__ __attribute__((aligned(16))) uint64_t dyn_lds[];
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -318,7 +329,7 @@ __global__ __launch_bounds__(TPB, NXG_DISP_SOCC) void nxg_disp_scatter_kernel(
         for (uint64_t b0 = r0; b0 < r1; b0 += 64 * DU) {
           // DU steps' rows and SubIds looked up together, then the steps in order
           Row rows[DU];
-          uint64_t subs[DU];
+          uint64_t subs[DU], lastv[DU];
 #pragma unroll
           for (int u = 0; u < DU; u++) {
             const uint64_t i = b0 + 64 * u + lane;
@@ -333,12 +344,19 @@ __global__ __launch_bounds__(TPB, NXG_DISP_SOCC) void nxg_disp_scatter_kernel(
             // the entry's tag: the subscription's SubId, or (no SubId table) the row's own Id
             subs[u] = !tb.slot_sub_id ? (i < r1 ? id[i] : 0)
                       : (rows[u].slot != NONE ? tb.slot_sub_id[rows[u].slot] : 0);
+            // the count pass's last_row of a kept slot (~0: none to check)
+            lastv[u] = ~0ull;
+            if (plain_last && rows[u].slot != NONE &&
+                (!tb.slot_has_last || tb.slot_has_last[rows[u].slot]))
+                lastv[u] = last_row[rows[u].slot];
           }
 #pragma unroll
           for (int u = 0; u < DU; u++) {
             const uint64_t i = b0 + 64 * u + lane;
             const Row& r = rows[u];
             const uint64_t sub = subs[u];
+            if (lastv[u] < i + 1)  // a later row of the slot than the count pass's store
+                atomicMax((unsigned long long*)&last_row[r.slot], (unsigned long long)(i + 1));
             const bool dup = (r.c[0] != NONE && (r.c[0] == r.c[1] || r.c[0] == r.c[2] ||
                                                  r.c[0] == r.c[3])) ||
                              (r.c[1] != NONE && (r.c[1] == r.c[2] || r.c[1] == r.c[3])) ||
@@ -472,10 +490,12 @@ hipError_t nxg_launch_dispatch(const NxgSubTable& tb, const uint64_t* id, uint64
     const uint64_t gcap = NXG_DISP_GCAP ? (uint64_t)ncu * NXG_DISP_GCAP : 0x7fffffffull;
     const uint32_t g = (uint32_t)(want < gcap ? want : gcap);
     const bool in_lds = tb.n_chans <= LCH;
+    // (no channels: no scatter to finish last_row, the count pass takes the atomics)
+    const bool plain_last = NXG_DISP_LASTP && M != 0;
     const size_t lds_count = in_lds ? (size_t)WAVES * tb.n_chans * 4 : 0;
     const size_t lds_scatter = in_lds ? (size_t)WAVES * tb.n_chans * 16 : 0;
     hipLaunchKernelGGL(nxg_disp_count_kernel, dim3(g), dim3(TPB), lds_count, s, tb, rt, id, n, seg,
-                       n_seg, hist, last_row, unmatched, rc);
+                       n_seg, hist, last_row, unmatched, rc, plain_last);
     if (M) {
         hipLaunchKernelGGL(nxg_disp_scan_block_kernel, dim3((uint32_t)nb), dim3(TPB), 0, s, hist, M,
                            off, bsum);
@@ -483,7 +503,7 @@ hipError_t nxg_launch_dispatch(const NxgSubTable& tb, const uint64_t* id, uint64
         hipLaunchKernelGGL(nxg_disp_scan_add_kernel, dim3((uint32_t)((M + TPB - 1) / TPB)),
                            dim3(TPB), 0, s, off, M, bsum, nb, n_seg, tb.n_chans, chan_off);
         hipLaunchKernelGGL(nxg_disp_scatter_kernel, dim3(g), dim3(TPB), lds_scatter, s, tb, rt, id,
-                           n, seg, n_seg, off, ent_sub, ent_row, cap, rc);
+                           n, seg, n_seg, off, ent_sub, ent_row, cap, rc, last_row, plain_last);
     }
     return hipGetLastError();
 }
