@@ -175,6 +175,9 @@ NXG_DEV bool cache_get(const RowCache& rc, uint64_t i, uint32_t& c0, uint32_t& c
 #ifndef NXG_DISP_SKIP
 #define NXG_DISP_SKIP 0  // timing experiments only: 1 last_row, 2 counters, 4 the row cache
 #endif
+#ifndef NXG_DISP_A32
+#define NXG_DISP_A32 0  // 1: last_row's atomicMax on its low 32-bit word while rows fit 32 bits
+#endif
 #ifndef NXG_DISP_LASTP
 #define NXG_DISP_LASTP 0  // 1: plain last_row stores finished by the scatter (measured slower: 0.353-0.363
 // vs 0.337-0.350 ms sequential, 1.40-1.42 vs 1.10 ms random Ids at 10^7, 16 channels)
@@ -221,6 +224,8 @@ __global__ __launch_bounds__(TPB, NXG_DISP_COCC) void nxg_disp_count_kernel(
             }
             if (!(NXG_DISP_SKIP & 1) && r.slot != NONE && (!tb.slot_has_last || tb.slot_has_last[r.slot])) {
                 if (plain_last) last_row[r.slot] = i + 1;
+                else if (NXG_DISP_A32 && n < 0xffffffffull)  // the low word (high words are 0)
+                    atomicMax(reinterpret_cast<unsigned*>(&last_row[r.slot]), (unsigned)(i + 1));
                 else atomicMax((unsigned long long*)&last_row[r.slot], (unsigned long long)(i + 1));
             }
             // order-free: one atomic per (row, stream)
