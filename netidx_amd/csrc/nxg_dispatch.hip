@@ -177,6 +177,7 @@ NXG_DEV bool cache_get(const RowCache& rc, uint64_t i, uint32_t& c0, uint32_t& c
 #endif
 #ifndef NXG_DISP_A32
 #define NXG_DISP_A32 0  // 1: last_row's atomicMax on its low 32-bit word while rows fit 32 bits
+// (A/B at 10^7, 16 channels: 0.316-0.321 vs 0.317-0.328 ms, equal)
 #endif
 #ifndef NXG_DISP_LASTP
 #define NXG_DISP_LASTP 0  // 1: plain last_row stores finished by the scatter (measured slower: 0.353-0.363
