@@ -697,6 +697,11 @@ __global__ __launch_bounds__(TPB) void nxg_fmx_count_kernel(const uint8_t* __res
 #ifndef NXG_FMX_FIXW
 #define NXG_FMX_FIXW 1  // (A/B at 10^7: plain 0.2564-0.2578 vs 0.2577-0.2604 ms, the frame with control equal)
 #endif
+#ifndef NXG_FMX_FIXC
+#define NXG_FMX_FIXC 0  // 1: the fix wave follows a recount's new exit into the tiles after it (measured
+// slower: plain 0.261-0.262 vs 0.251-0.255, control 0.343-0.346 vs 0.337-0.338 ms; the recounts
+// were 42 / 55 either way, no cascades)
+#endif
 __global__ __launch_bounds__(TPB) void nxg_fmx_fix_kernel(const uint8_t* __restrict__ wire, FRange rg,
                                                           uint64_t nt, TileDesc* __restrict__ td,
                                                           uint64_t* __restrict__ starts,
@@ -717,11 +722,40 @@ __global__ __launch_bounds__(TPB) void nxg_fmx_fix_kernel(const uint8_t* __restr
         redo = !(e != FAIL && (pe == FAIL || pe == e));
     }
     uint8_t* img = lds[w].img;
+#if NXG_FMX_FIXC
+    // in tile order from the first tile to redo: a tile after a recounted one is recounted too
+    // when its entry is not the new exit (the cascade the resolve pass would otherwise walk)
+    const uint64_t m = __ballot(redo);
+    uint32_t ex = tl < nt ? td[tl].exit : FAIL, en = tl < nt ? td[tl].entry : FAIL;
+    bool chain = false;  // (uniform) the previous tile was recounted here
+#pragma unroll 1
+    for (uint32_t j = m ? (uint32_t)__builtin_ctzll(m) : 64u; j < 64u && t0 + j < nt; j++) {
+        const uint64_t t = t0 + j;
+        uint32_t pj = (uint32_t)__builtin_amdgcn_readlane((int)pe, (int)j);
+        if (chain) {
+            const uint32_t px = (uint32_t)__builtin_amdgcn_readlane((int)ex, (int)(j - 1));
+            const uint32_t ej = (uint32_t)__builtin_amdgcn_readlane((int)en, (int)j);
+            if (px != FAIL && px - TILE < TILE) {
+                if (px - TILE == ej && !((m >> j) & 1ull)) {
+                    chain = false;
+                    continue;
+                }
+                pj = px - TILE;
+            } else if (!((m >> j) & 1ull)) {
+                chain = false;
+                continue;
+            }
+        } else if (!((m >> j) & 1ull)) {
+            continue;
+        }
+        chain = true;
+#else
 #pragma unroll 1
     for (uint64_t m = __ballot(redo); m; m &= m - 1) {
         const uint32_t j = (uint32_t)__builtin_ctzll(m);
         const uint64_t t = t0 + j;
         const uint32_t pj = (uint32_t)__builtin_amdgcn_readlane((int)pe, (int)j);
+#endif
         if (lane == 0) atomicAdd(&sz->diag[5], 1ull);
         TileRegs g;
         tile_load(g, wire, t * TILE, rg.W, lane);
@@ -736,6 +770,12 @@ __global__ __launch_bounds__(TPB) void nxg_fmx_fix_kernel(const uint8_t* __restr
         }
         starts[t * 64 + lane] = bits;
         if (lane == 0) td[t] = d;
+#if NXG_FMX_FIXC
+        if (lane == j) {
+            ex = d.exit;
+            en = d.entry;
+        }
+#endif
     }
 }
 
