@@ -23,8 +23,11 @@
 namespace part {
 constexpr int TPB = 256;
 constexpr int WAVES = TPB / 64;
-constexpr uint32_t TROWS = 4096;            // rows per tile
-constexpr uint32_t WROWS = TROWS / WAVES;   // rows per wave: 16 rounds of 64
+#ifndef NXG_PART_TROWS
+#define NXG_PART_TROWS 4096  // (A/B at 10^7: 4096 0.149-0.150, 2048 0.156-0.158, 1024 0.169-0.171 ms)
+#endif
+constexpr uint32_t TROWS = NXG_PART_TROWS;  // rows per tile
+constexpr uint32_t WROWS = TROWS / WAVES;   // rows per wave (4096: 16 rounds of 64)
 constexpr uint32_t ROUNDS = WROWS / 64;
 constexpr uint32_t NB = 256;                // tag bins (the tag column is u8)
 constexpr uint32_t NOTAG = 0x100;           // a lane past the last row
