@@ -302,6 +302,41 @@ __global__ __launch_bounds__(1024) void nxg_disp_scan_top_kernel(uint64_t* __res
     if (threadIdx.x == 0) bsum[nb] = carry;
 }
 
+// NXG_DISP_FUSE: the top scan also writes chan_off (each channel's first entry: its segment 0's
+// block-local offset plus its block's prefix), and the scatter adds the block prefixes itself, so
+// neither the scan_add launch nor chan_off's memset runs (LDS counters only; more channels keep
+// the global cursors, which the scatter rewrites, and the add pass)
+#ifndef NXG_DISP_FUSE
+#define NXG_DISP_FUSE 1
+#endif
+__global__ __launch_bounds__(1024) void nxg_disp_scan_top_chan_kernel(
+    uint64_t* __restrict__ bsum, uint64_t nb, const uint64_t* __restrict__ off, uint64_t n_seg,
+    uint32_t n_chans, uint64_t* __restrict__ chan_off) {
+    __shared__ uint64_t tmp[16];
+    __shared__ uint64_t carry;
+    if (threadIdx.x == 0) carry = 0;
+    __syncthreads();
+#pragma unroll 1
+    for (uint64_t b0 = 0; b0 < nb; b0 += 1024) {
+        const uint64_t i = b0 + threadIdx.x;
+        const uint64_t v = i < nb ? bsum[i] : 0;
+        uint64_t total;
+        const uint64_t p = block_excl_scan<uint64_t, 1024>(v, tmp, &total);
+        const uint64_t c = carry;
+        if (i < nb) bsum[i] = c + p;
+        __syncthreads();
+        if (threadIdx.x == 0) carry = c + total;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) bsum[nb] = carry;
+#pragma unroll 1
+    for (uint32_t c = threadIdx.x; c < n_chans; c += 1024) {
+        const uint64_t i = (uint64_t)c * n_seg;
+        chan_off[c] = off[i] + bsum[i / SCAN_B];
+    }
+    if (threadIdx.x == 0) chan_off[n_chans] = carry;
+}
+
 __global__ __launch_bounds__(TPB) void nxg_disp_scan_add_kernel(
     uint64_t* __restrict__ off, uint64_t M, const uint64_t* __restrict__ bsum, uint64_t nb,
     uint64_t n_seg, uint32_t n_chans, uint64_t* __restrict__ chan_off) {
@@ -322,7 +357,8 @@ __global__ __launch_bounds__(TPB, NXG_DISP_SOCC) void nxg_disp_scatter_kernel(
     NxgSubTable tb, Route rt, const uint64_t* __restrict__ id, uint64_t n, uint64_t seg_rows,
     uint64_t n_seg,
     uint64_t* __restrict__ off, uint64_t* __restrict__ ent_sub, uint64_t* __restrict__ ent_row,
-    uint64_t cap, RowCache rc, uint64_t* __restrict__ last_row, bool plain_last) {
+    uint64_t cap, RowCache rc, uint64_t* __restrict__ last_row, bool plain_last,
+    const uint64_t* __restrict__ bpre) {
     // (dynamic LDS: a cursor and a lane mask per channel and wave, sized at launch)
     extern __shared__ __attribute__((aligned(16))) uint64_t dyn_lds[];
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -335,7 +371,8 @@ __global__ __launch_bounds__(TPB, NXG_DISP_SOCC) void nxg_disp_scatter_kernel(
          seg += (uint64_t)gridDim.x * WAVES) {
         if (lds) {
             for (uint32_t c = lane; c < tb.n_chans; c += 64) {
-                cur[c] = off[(uint64_t)c * n_seg + seg];
+                const uint64_t i = (uint64_t)c * n_seg + seg;
+                cur[c] = off[i] + (bpre ? bpre[i / SCAN_B] : 0ull);  // (bpre: the add pass skipped)
                 mask[c] = 0;
             }
             wave_lds_order();
@@ -495,7 +532,9 @@ hipError_t nxg_launch_dispatch(const NxgSubTable& tb, const uint64_t* id, uint64
     hipError_t e;
     if ((e = hipMemsetAsync(unmatched, 0, 8, s)) != hipSuccess) return e;
     if (tb.n_slots && (e = hipMemsetAsync(last_row, 0, tb.n_slots * 8, s)) != hipSuccess) return e;
-    if ((e = hipMemsetAsync(chan_off, 0, ((uint64_t)tb.n_chans + 1) * 8, s)) != hipSuccess) return e;
+    const bool fuse = NXG_DISP_FUSE && M != 0 && tb.n_chans <= LCH;
+    if (!fuse && (e = hipMemsetAsync(chan_off, 0, ((uint64_t)tb.n_chans + 1) * 8, s)) != hipSuccess)
+        return e;
     if (n == 0) return hipSuccess;
     if (tb.n_chans > LCH && (e = hipMemsetAsync(hist, 0, M * 4, s)) != hipSuccess) return e;
     // one segment per wave: the hardware hands workgroups to CUs as they free up, so a wave's
@@ -515,11 +554,17 @@ hipError_t nxg_launch_dispatch(const NxgSubTable& tb, const uint64_t* id, uint64
     if (M) {
         hipLaunchKernelGGL(nxg_disp_scan_block_kernel, dim3((uint32_t)nb), dim3(TPB), 0, s, hist, M,
                            off, bsum);
-        hipLaunchKernelGGL(nxg_disp_scan_top_kernel, dim3(1), dim3(1024), 0, s, bsum, nb);
-        hipLaunchKernelGGL(nxg_disp_scan_add_kernel, dim3((uint32_t)((M + TPB - 1) / TPB)),
-                           dim3(TPB), 0, s, off, M, bsum, nb, n_seg, tb.n_chans, chan_off);
+        if (fuse) {
+            hipLaunchKernelGGL(nxg_disp_scan_top_chan_kernel, dim3(1), dim3(1024), 0, s, bsum, nb,
+                               off, n_seg, tb.n_chans, chan_off);
+        } else {
+            hipLaunchKernelGGL(nxg_disp_scan_top_kernel, dim3(1), dim3(1024), 0, s, bsum, nb);
+            hipLaunchKernelGGL(nxg_disp_scan_add_kernel, dim3((uint32_t)((M + TPB - 1) / TPB)),
+                               dim3(TPB), 0, s, off, M, bsum, nb, n_seg, tb.n_chans, chan_off);
+        }
         hipLaunchKernelGGL(nxg_disp_scatter_kernel, dim3(g), dim3(TPB), lds_scatter, s, tb, rt, id,
-                           n, seg, n_seg, off, ent_sub, ent_row, cap, rc, last_row, plain_last);
+                           n, seg, n_seg, off, ent_sub, ent_row, cap, rc, last_row, plain_last,
+                           fuse ? (const uint64_t*)bsum : nullptr);
     }
     return hipGetLastError();
 }
