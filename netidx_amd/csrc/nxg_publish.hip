@@ -493,6 +493,10 @@ static PubScratch pub_layout(uint8_t* p, uint64_t n, uint64_t n_slots) {
     return sc;
 }
 
+#ifndef NXG_PUB_GCAP
+#define NXG_PUB_GCAP 8  // the repeated-Id check's workgroups per CU (a bounded grid striding over rows;
+// A/B of the commit at 10^7: 4 0.550-0.556, 8 0.508-0.515, 16 0.504-0.514 ms)
+#endif
 hipError_t nxg_launch_pub_stage1(const NxgPubTable& tb, const NxgPubBatch& b, uint8_t* scratch,
                                  int ncu, hipStream_t s) {
     PubScratch sc = pub_layout(scratch, b.n_rows, tb.n_slots);
@@ -504,7 +508,7 @@ hipError_t nxg_launch_pub_stage1(const NxgPubTable& tb, const NxgPubBatch& b, ui
     if (b.n_rows)
         hipLaunchKernelGGL(nxg_pub_count_kernel,
                            dim3((uint32_t)std::min<uint64_t>((b.n_rows + TPB - 1) / TPB,
-                                                             (uint64_t)ncu * 8)),
+                                                             (uint64_t)ncu * NXG_PUB_GCAP)),
                            dim3(TPB), 0, s, tb, in, sc.cnt, sc.flags);
     return hipGetLastError();
 }
